@@ -1,0 +1,109 @@
+/* monkeypose.h -- C ABI of libmonkeypose.so, the MI355X (gfx950) inference path of the
+ * monkey-pose regressors.
+ *
+ * The reference (krg-nandu/monkey-pose, TensorFlow 1.x / Python 2) has no FFI: its "operator API"
+ * is a set of Python graph-builder classes.  Each entry point below replaces one of them; the
+ * Python facade in monkey-pose_amd/ (hgru_pose.py, hgru_module.py) binds them with ctypes and
+ * keeps the reference's class / method names and argument order.
+ *
+ *   reference interface                                        replaced by
+ *   ---------------------------------------------------------  ------------------------------------
+ *   hgru_pose.model.get_var / data_dict   hgru_pose.py:196-216  mp_set_weight, mp_finalize_weights
+ *   hgru_pose.model.build(depth, output_shape, batch_norm,     mp_hgru_pose_fwd
+ *     train_mode) -> .out_put             hgru_pose.py:47-105
+ *   hgru_module.ContextualCircuit(X, timesteps, SRF, SSN, SSF, mp_hgru_circuit_fwd
+ *     strides, padding, aux).build()      hgru_module.py:61-128, 872-959
+ *   (tf.Session / device placement)       train_cnn_networks_hgru.py:95  mp_create / mp_destroy
+ *
+ * Conventions
+ *   - Every tensor argument is a device pointer (hipMalloc'd or a torch CUDA tensor's data_ptr),
+ *     fp32, contiguous, NHWC exactly as the reference feeds it (depth crops [n,128,128,1] =
+ *     crop_mm / 10000, train_cnn_networks_hgru.py:50).  Output buffers are caller-owned.
+ *   - Weights are identified by their TensorFlow variable names (e.g. "cnn/contextual_circuit/p_r",
+ *     "cnn/fc_1/fc_1_weights"); a leading "cnn/" scope is optional.  The library copies them.
+ *   - Calls on one context are serialised by the caller and are asynchronous on `stream`
+ *     (a hipStream_t; NULL = default stream).  One context per device.
+ *   - Status: MP_OK (0) or a negative MP_ERR_*; mp_last_error() gives a thread-local message.
+ *     No C++ exception crosses the ABI.  Shapes are validated on the host before any launch.
+ */
+#ifndef MONKEYPOSE_H
+#define MONKEYPOSE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct mp_ctx mp_ctx;
+
+enum {
+  MP_OK = 0,
+  MP_ERR_ARG = -1,         /* bad argument / null pointer */
+  MP_ERR_STATE = -2,       /* weights missing or not finalized */
+  MP_ERR_HIP = -3,         /* HIP runtime error (message has hipGetErrorString) */
+  MP_ERR_WEIGHT = -4,      /* unknown weight name or wrong shape */
+  MP_ERR_SHAPE = -5,       /* unsupported input shape */
+  MP_ERR_UNSUPPORTED = -6  /* option not implemented (e.g. train_mode) */
+};
+
+enum {
+  MP_MODEL_HGRU_POSE = 1,    /* hgru_pose.model                (hgru_pose.py:6-216)        */
+  MP_MODEL_HGRU_CIRCUIT = 2  /* hgru_module.ContextualCircuit  (hgru_module.py:54-959)     */
+};
+
+enum { MP_MEM_HOST = 0, MP_MEM_DEVICE = 1 };
+enum { MP_DTYPE_F32 = 0 };
+
+/* library version, (major << 16) | minor */
+int mp_version(void);
+
+/* thread-local description of the last error on this thread ("" if none) */
+const char* mp_last_error(void);
+
+/* create a context on HIP device `device` for model `model_kind` */
+int mp_create(int device, int model_kind, mp_ctx** out);
+void mp_destroy(mp_ctx* ctx);
+
+/* copy one variable (fp32, row-major, TF shape) into the context; replaces
+ * hgru_pose.get_var / tf.get_variable (hgru_pose.py:196-216, hgru_module.py:262-503) */
+int mp_set_weight(mp_ctx* ctx, const char* name, const float* data, const int64_t* shape, int ndim,
+                  int mem_kind);
+
+/* fold BN, pack every weight into its kernel's fragment order; must follow the last
+ * mp_set_weight and precede any forward call */
+int mp_finalize_weights(mp_ctx* ctx, int compute_dtype);
+
+/* pre-allocate the activation workspace for batches up to max_batch (otherwise grown lazily) */
+int mp_reserve(mp_ctx* ctx, int64_t max_batch);
+
+/* hgru_pose.model.build (hgru_pose.py:47-105), inference:
+ *   depth  [n, h, w, 1]   normalised depth crops (h = w = 128 in the reference)
+ *   o0     [n, h/2, w/2, 64] initial hGRU output state (hidden_init='random',
+ *          hgru_module.py:879-887, made explicit)
+ *   out    [n, output_shape] joint coordinates / (cube_z / 2), joint-major (j*3 + {x,y,z}) */
+int mp_hgru_pose_fwd(mp_ctx* ctx, const float* depth, int64_t n, int64_t h, int64_t w,
+                     const float* o0, float* out, void* stream);
+
+/* ContextualCircuit(X, timesteps, ...).build() -> O  (hgru_module.py:872-959), hgru_pose aux:
+ *   x, o0, o_out  [n, h, w, k] NHWC; k must be 64, h % 16 == 0, w % 32 == 0;
+ *   timesteps <= the length of the "contextual_circuit/rho" weight */
+int mp_hgru_circuit_fwd(mp_ctx* ctx, const float* x, const float* o0, int64_t n, int64_t h,
+                        int64_t w, int64_t k, int timesteps, float* o_out, void* stream);
+
+/* read a model property: "output_shape", "timesteps", "ssf", "finalized", "workspace_bytes",
+ * "weight_bytes" */
+int mp_info(mp_ctx* ctx, const char* key, int64_t* value);
+
+/* per-kernel device timing with HIP events recorded on the launch stream around every launch of
+ * kernel class `name` ("conv15_a", "conv15_b", "fc1", "backbone"); enable, run, then read the
+ * summed elapsed milliseconds and launch count (reading synchronises those events) */
+int mp_profile_enable(mp_ctx* ctx, int enable);
+int mp_profile_read(mp_ctx* ctx, const char* name, double* total_ms, int64_t* launches);
+
+#ifdef __cplusplus
+}
+#endif
+
+#endif /* MONKEYPOSE_H */

@@ -1,0 +1,16 @@
+"""monkey-pose_amd: MI355X (gfx950) inference path of krg-nandu/monkey-pose's 3D pose regressors.
+
+The directory name carries a hyphen, so import it with ``importlib.import_module("monkey-pose_amd")``
+(see ``tests/conftest.py``).  Modules:
+
+* ``hgru_pose``   -- drop-in ``model().build(depth, output_shape)`` (reference ``hgru_pose.py``)
+* ``hgru_module`` -- drop-in ``ContextualCircuit(X, ...).build()`` (reference ``hgru_module.py``)
+* ``weights``     -- TF variable-name tables and deterministic synthetic initialisers
+* ``_lib``        -- ctypes binding of ``libmonkeypose.so`` (C ABI: ``include/monkeypose.h``)
+"""
+from . import weights  # noqa: F401
+from . import _lib  # noqa: F401
+from . import hgru_pose  # noqa: F401
+from . import hgru_module  # noqa: F401
+
+__all__ = ["hgru_pose", "hgru_module", "weights", "_lib"]

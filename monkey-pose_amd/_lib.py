@@ -1,0 +1,162 @@
+"""ctypes binding of ``libmonkeypose.so`` (C ABI in ``include/monkeypose.h``).
+
+The library is loaded *after* ``import torch`` so that it binds to the HIP runtime torch already
+loaded (both resolve the soname ``libamdhip64.so.7``): device pointers and streams from torch
+tensors are then valid inside the library.  There is no CPU fallback: if the library is missing
+or the GPU is unavailable every entry point raises.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Optional
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libmonkeypose.so")
+
+MP_OK = 0
+MP_MODEL_HGRU_POSE = 1
+MP_MODEL_HGRU_CIRCUIT = 2
+MP_MEM_HOST = 0
+MP_MEM_DEVICE = 1
+MP_DTYPE_F32 = 0
+
+# every function the header declares, with its ctypes signature
+_SIGS = {
+    "mp_version": (ctypes.c_int, []),
+    "mp_last_error": (ctypes.c_char_p, []),
+    "mp_create": (ctypes.c_int, [ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]),
+    "mp_destroy": (None, [ctypes.c_void_p]),
+    "mp_set_weight": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p,
+                                     ctypes.POINTER(ctypes.c_int64), ctypes.c_int, ctypes.c_int]),
+    "mp_finalize_weights": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "mp_reserve": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
+    "mp_hgru_pose_fwd": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                        ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_void_p]),
+    "mp_hgru_circuit_fwd": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                           ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                                           ctypes.c_int64, ctypes.c_int, ctypes.c_void_p,
+                                           ctypes.c_void_p]),
+    "mp_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64)]),
+    "mp_profile_enable": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "mp_profile_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p,
+                                       ctypes.POINTER(ctypes.c_double),
+                                       ctypes.POINTER(ctypes.c_int64)]),
+}
+
+_lib: Optional[ctypes.CDLL] = None
+
+
+class MonkeyPoseError(RuntimeError):
+    """A non-zero status from the C ABI; ``code`` is the MP_ERR_* value."""
+
+    def __init__(self, code: int, msg: str):
+        super().__init__(f"[{code}] {msg}")
+        self.code = code
+
+
+def load() -> ctypes.CDLL:
+    """Load (once) and return the library; raises if it has not been built."""
+    global _lib
+    if _lib is None:
+        import torch  # noqa: F401  -- binds the library to torch's HIP runtime
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"{LIB_PATH} is missing: build it with `python -c 'import "
+                               "__graft_entry__ as g; g.build()'` (no CPU fallback exists)")
+        lib = ctypes.CDLL(LIB_PATH)
+        for name, (res, args) in _SIGS.items():
+            fn = getattr(lib, name)
+            fn.restype = res
+            fn.argtypes = args
+        _lib = lib
+    return _lib
+
+
+def check(status: int) -> None:
+    if status != MP_OK:
+        raise MonkeyPoseError(status, load().mp_last_error().decode())
+
+
+def _ptr(t) -> int:
+    return int(t.data_ptr())
+
+
+class Context:
+    """One ``mp_ctx`` on one device (the unit the reference's tf.Session/device placement maps to)."""
+
+    def __init__(self, model_kind: int, device: int = 0):
+        import torch
+        if not torch.cuda.is_available():
+            raise RuntimeError("monkey-pose_amd needs a ROCm GPU; there is no CPU fallback")
+        self.lib = load()
+        self.device = device
+        h = ctypes.c_void_p()
+        check(self.lib.mp_create(device, model_kind, ctypes.byref(h)))
+        self.h = h
+
+    def close(self):
+        if getattr(self, "h", None):
+            self.lib.mp_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_weight(self, name: str, value) -> None:
+        import torch
+        if isinstance(value, torch.Tensor):
+            t = value.detach()
+            if t.dtype != torch.float32:
+                t = t.float()
+            t = t.contiguous()
+            shape = (ctypes.c_int64 * t.dim())(*t.shape)
+            mem = MP_MEM_DEVICE if t.is_cuda else MP_MEM_HOST
+            if t.is_cuda:
+                torch.cuda.synchronize(t.device)   # the copy below runs on the null stream
+            check(self.lib.mp_set_weight(self.h, name.encode(), ctypes.c_void_p(t.data_ptr()), shape,
+                                         t.dim(), mem))
+        else:
+            a = np.ascontiguousarray(np.asarray(value, dtype=np.float32))
+            shape = (ctypes.c_int64 * a.ndim)(*a.shape)
+            check(self.lib.mp_set_weight(self.h, name.encode(), a.ctypes.data_as(ctypes.c_void_p),
+                                         shape, a.ndim, MP_MEM_HOST))
+
+    def finalize(self, dtype: int = MP_DTYPE_F32) -> None:
+        check(self.lib.mp_finalize_weights(self.h, dtype))
+
+    def reserve(self, max_batch: int) -> None:
+        check(self.lib.mp_reserve(self.h, int(max_batch)))
+
+    def info(self, key: str) -> int:
+        v = ctypes.c_int64()
+        check(self.lib.mp_info(self.h, key.encode(), ctypes.byref(v)))
+        return int(v.value)
+
+    def pose_fwd(self, depth, o0, out, stream: int) -> None:
+        n, h, w, c = depth.shape
+        check(self.lib.mp_hgru_pose_fwd(self.h, _ptr(depth), n, h, w, _ptr(o0), _ptr(out),
+                                        ctypes.c_void_p(stream)))
+
+    def circuit_fwd(self, x, o0, out, timesteps: int, stream: int) -> None:
+        n, h, w, k = x.shape
+        check(self.lib.mp_hgru_circuit_fwd(self.h, _ptr(x), _ptr(o0), n, h, w, k, int(timesteps),
+                                           _ptr(out), ctypes.c_void_p(stream)))
+
+    def profile(self, enable: bool) -> None:
+        check(self.lib.mp_profile_enable(self.h, 1 if enable else 0))
+
+    def profile_read(self, name: str):
+        ms, cnt = ctypes.c_double(), ctypes.c_int64()
+        check(self.lib.mp_profile_read(self.h, name.encode(), ctypes.byref(ms), ctypes.byref(cnt)))
+        return float(ms.value), int(cnt.value)
+
+
+def current_stream(device=None) -> int:
+    import torch
+    return int(torch.cuda.current_stream(device).cuda_stream)

@@ -1,0 +1,152 @@
+// Fully-connected layers: split-K fp32 GEMM on v_mfma_f32_32x32x2_f32 + a reduce/epilogue kernel.
+//
+// Reference: hgru_pose.fc_layer (hgru_pose.py:156-163) = reshape [-1,in] -> tf.matmul(x, W[in,out])
+// -> bias_add; then relu (92) and inference BN (95-103, folded to an affine) for fc_1, plain
+// bias for fc_out (104).  The same kernels serve every fc_* of the dense / hier heads.
+//
+// D^T[n][m] = sum_k W[k][n] A[m][k]: W is the MFMA A operand, streamed once from HBM in a packed
+// fragment order ([k/8][n/32][lane] float4, one 16-byte load per lane per 8-deep k group); the
+// activations (the small M side) are staged in LDS [128 m][32 k + 4] (the +4 pad makes the
+// ds_read_b128 row reads conflict-free).  Partial sums per K slice go to a slab
+// part[split][M][Npad]; fc_reduce sums the slabs in fixed order (bit-reproducible), then applies
+// bias, relu and the per-feature affine.
+#include "mp_kernels.hpp"
+
+namespace mp {
+
+constexpr int FC_BM = 128, FC_BK = 32, FC_LDA = FC_BK + 4;
+
+__global__ void pack_fc_kernel(const float* __restrict__ W, f32x4* out, int K, int N, int K8, int N32) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const size_t total = (size_t)K8 * N32 * 64;
+  if (i >= total) return;
+  const int lane = i % 64;
+  const int nb = (i / 64) % N32;
+  const size_t kb = i / ((size_t)64 * N32);
+  const int n = 32 * nb + (lane & 31);
+  const size_t k0 = 8 * kb + 4 * (lane >> 5);
+  f32x4 v;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) v[s] = (k0 + s < (size_t)K && n < N) ? W[(k0 + s) * N + n] : 0.f;
+  out[i] = v;
+}
+
+__global__ __launch_bounds__(256) void fc_gemm_kernel(const float* __restrict__ A, int lda,
+                                                      const f32x4* __restrict__ Wpk,
+                                                      float* __restrict__ part, int M, int K,
+                                                      int N32, int kslice) {
+  __shared__ float As[FC_BM * FC_LDA];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, col = lane & 31;
+  const int mt = blockIdx.x, ntile = blockIdx.y, split = blockIdx.z;
+  const int K8 = (K + 7) / 8;
+  const int Npad = N32 * 32;
+  const int nb = ntile * 4 + wv;
+  const bool wave_on = nb < N32;   // wave-uniform
+  const int kbeg = split * kslice;
+  const int kend = min(K, kbeg + kslice);
+
+  f32x16 acc[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) acc[m] = f32x16{};
+
+  for (int k0 = kbeg; k0 < kend; k0 += FC_BK) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = tid + i * 256;          // 0..1023 float4 slots: row = e / 8, k4 = e % 8
+      const int row = e >> 3, k4 = (e & 7) * 4;
+      const int gm = mt * FC_BM + row, gk = k0 + k4;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (gm < M) {
+        if (gk + 3 < kend) {
+          v = *reinterpret_cast<const f32x4*>(A + (size_t)gm * lda + gk);
+        } else {
+#pragma unroll
+          for (int s = 0; s < 4; ++s) v[s] = (gk + s < kend) ? A[(size_t)gm * lda + gk + s] : 0.f;
+        }
+      }
+      *reinterpret_cast<f32x4*>(As + row * FC_LDA + k4) = v;
+    }
+    __syncthreads();
+    if (wave_on) {
+#pragma unroll
+      for (int g = 0; g < FC_BK / 8; ++g) {
+        const int kb = (k0 >> 3) + g;
+        if (kb >= K8) break;
+        const f32x4 wf = Wpk[((size_t)kb * N32 + nb) * 64 + lane];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const f32x4 a = *reinterpret_cast<const f32x4*>(As + (m * 32 + col) * FC_LDA + 8 * g + 4 * h);
+#pragma unroll
+          for (int s = 0; s < 4; ++s) acc[m] = mfma32(wf[s], a[s], acc[m]);
+        }
+      }
+    }
+  }
+  if (!wave_on) return;
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int gm = mt * FC_BM + m * 32 + col;
+    if (gm >= M) continue;
+    float* dst = part + ((size_t)split * M + gm) * Npad + 32 * nb + 4 * h;
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      *reinterpret_cast<f32x4*>(dst + 8 * g) =
+          f32x4{acc[m][4 * g], acc[m][4 * g + 1], acc[m][4 * g + 2], acc[m][4 * g + 3]};
+  }
+}
+
+__global__ void fc_reduce_kernel(const float* __restrict__ part, int S, int M, int N, int Npad,
+                                 const float* __restrict__ bias, int relu,
+                                 const float* __restrict__ aff_s, const float* __restrict__ aff_t,
+                                 float* out, int ldo) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (size_t)M * N) return;
+  const int m = i / N, n = i % N;
+  float v = 0.f;
+  for (int s = 0; s < S; ++s) v += part[((size_t)s * M + m) * Npad + n];
+  if (bias) v += bias[n];
+  if (relu) v = fmaxf(v, 0.f);
+  if (aff_s) v = v * aff_s[n] + aff_t[n];
+  out[(size_t)m * ldo + n] = v;
+}
+
+hipError_t launch_pack_fc(const float* W, f32x4* out, int K, int N, hipStream_t st) {
+  const int K8 = (K + 7) / 8, N32 = (N + 31) / 32;
+  const size_t total = (size_t)K8 * N32 * 64;
+  hipLaunchKernelGGL(pack_fc_kernel, dim3((total + 255) / 256), dim3(256), 0, st, W, out, K, N, K8, N32);
+  return hipGetLastError();
+}
+
+// K slices of ~4096: a function of K only, so every output row is summed in the same order
+// whatever the batch size (results are bit-identical between a crop alone and inside a batch).
+int fc_choose_splits(int M, int K, int N, int* kslice) {
+  (void)M;
+  (void)N;
+  int S = K / 4096;
+  if (S < 1) S = 1;
+  int ks = (K + S - 1) / S;
+  ks = (ks + FC_BK - 1) / FC_BK * FC_BK;
+  S = (K + ks - 1) / ks;
+  *kslice = ks;
+  return S;
+}
+
+hipError_t launch_fc_gemm(const float* A, int lda, const f32x4* Wpk, float* part, int M, int K, int N,
+                          int S, int kslice, hipStream_t st) {
+  const int N32 = (N + 31) / 32;
+  dim3 grid((M + FC_BM - 1) / FC_BM, (N32 + 3) / 4, S);
+  hipLaunchKernelGGL(fc_gemm_kernel, grid, dim3(256), 0, st, A, lda, Wpk, part, M, K, N32, kslice);
+  return hipGetLastError();
+}
+
+hipError_t launch_fc_reduce(const float* part, int S, int M, int N, const float* bias, int relu,
+                            const float* aff_s, const float* aff_t, float* out, int ldo, hipStream_t st) {
+  const int Npad = (N + 31) / 32 * 32;
+  const size_t total = (size_t)M * N;
+  hipLaunchKernelGGL(fc_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, part, S, M, N, Npad,
+                     bias, relu, aff_s, aff_t, out, ldo);
+  return hipGetLastError();
+}
+
+}  // namespace mp

@@ -1,0 +1,611 @@
+// C ABI of libmonkeypose.so (declared in include/monkeypose.h): contexts, weight registry,
+// finalize (BN folding + fragment packing) and the forward orchestration of the hot path.
+//
+// Forward of hgru_pose.model.build (hgru_pose.py:47-105) as launched here, one stream, no host
+// synchronisation:
+//   conv1_pool_bn            conv_1 + relu + max_pool + BN            (50-60)     HBM-bound
+//   conv64<3,BB>  x2         conv_2 / conv_3 + relu + BN              (61-80)     MFMA fp32
+//   gate_init                O0 -> O, O0*sigmoid(O0.i_r+i_b)          hgru_module.py:696-711
+//   T x { conv64<15,A>, conv64<15,B> }  the hGRU half-steps         hgru_module.py:825-857
+//                            (last B also applies BN_3, writes NHWC) (82-90)
+//   fc_gemm + fc_reduce      fc_1 + relu + BN_4                       (91-103)
+//   fc_gemm + fc_reduce      fc_out                                   (104-105)
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <cstring>
+#include <functional>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/monkeypose.h"
+#include "mp_kernels.hpp"
+
+
+using namespace mp;
+
+namespace {
+
+thread_local std::string g_err;
+
+struct Fail {
+  int code;
+};
+
+[[noreturn]] void fail(int code, const std::string& msg) {
+  g_err = msg;
+  throw Fail{code};
+}
+
+void hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) fail(MP_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  void alloc(size_t n) {
+    if (n <= bytes && p) return;
+    release();
+    hip_check(hipMalloc(&p, n ? n : 16), "hipMalloc");
+    bytes = n;
+  }
+  float* f() const { return static_cast<float*>(p); }
+  f32x4* v4() const { return static_cast<f32x4*>(p); }
+};
+
+struct RawWeight {
+  std::vector<int64_t> shape;
+  std::unique_ptr<DevBuf> dev;
+  std::vector<float> host;  // kept for small tensors (host-side BN folding)
+  size_t numel() const {
+    size_t n = 1;
+    for (auto s : shape) n *= (size_t)s;
+    return n;
+  }
+};
+
+struct ProfEvent {
+  std::string name;
+  hipEvent_t a, b;
+};
+
+std::string strip_scope(const char* name) {
+  std::string s(name);
+  if (s.rfind("cnn/", 0) == 0) s = s.substr(4);
+  return s;
+}
+
+bool known_name(int model, const std::string& n) {
+  static const char* circuit[] = {"p_r", "i_r", "i_b", "o_r", "o_b", "beta", "nu", "gamma", "kappa",
+                                  "omega", "rho", "lateral_bias"};
+  for (auto c : circuit)
+    if (n == std::string("contextual_circuit/") + c) return true;
+  if (model == MP_MODEL_HGRU_CIRCUIT) return false;
+  for (const char* l : {"conv_1", "conv_2", "conv_3"})
+    if (n == std::string(l) + "/" + l + "_filters" || n == std::string(l) + "/" + l + "_biases") return true;
+  for (const char* l : {"fc_1", "fc_out"})
+    if (n == std::string(l) + "/" + l + "_weights" || n == std::string(l) + "/" + l + "_biases") return true;
+  for (const char* b : {"batch_normalization", "batch_normalization_1", "batch_normalization_2",
+                        "batch_normalization_3", "batch_normalization_4"})
+    for (const char* v : {"gamma", "beta", "moving_mean", "moving_variance"})
+      if (n == std::string(b) + "/" + v) return true;
+  return false;
+}
+
+}  // namespace
+
+struct mp_ctx {
+  int device = 0;
+  int model = 0;
+  bool finalized = false;
+  std::map<std::string, RawWeight> raw;
+
+  // ---- finalized weights ----
+  int ssf = 15, timesteps = 8, nout = 0, fc1_in = 0, fc1_out = 0;
+  std::vector<float> rho;
+  DevBuf conv1_w, conv1_b, bn0_s, bn0_t;
+  DevBuf conv2_pk, conv2_b, bn1_s, bn1_t;
+  DevBuf conv3_pk, conv3_b, bn2_s, bn2_t;
+  DevBuf p_pk, ir_pk, or_pk, vecs;
+  DevBuf fc1_pk, fc1_b, bn4_s, bn4_t, fco_pk, fco_b;
+
+  // ---- workspace ----
+  int64_t cap_batch = 0;
+  int64_t cap_hw = 0;
+  DevBuf bufA, bufB, X, O, I, Og, fcin, part, h1;
+
+  // ---- profiling ----
+  bool prof = false;
+  std::vector<ProfEvent> events;
+  std::vector<hipEvent_t> pool;
+
+  ~mp_ctx() {
+    for (auto& e : events) {
+      (void)hipEventDestroy(e.a);
+      (void)hipEventDestroy(e.b);
+    }
+    for (auto e : pool) (void)hipEventDestroy(e);
+  }
+
+  const RawWeight& need(const std::string& n, std::vector<int64_t> shape) {
+    auto it = raw.find(n);
+    if (it == raw.end()) fail(MP_ERR_STATE, "weight not set: " + n);
+    if (!shape.empty() && it->second.shape != shape) {
+      std::string s = "weight " + n + " has shape [";
+      for (auto v : it->second.shape) s += std::to_string(v) + ",";
+      s += "], expected [";
+      for (auto v : shape) s += std::to_string(v) + ",";
+      fail(MP_ERR_WEIGHT, s + "]");
+    }
+    return it->second;
+  }
+
+  hipEvent_t ev() {
+    if (!pool.empty()) {
+      hipEvent_t e = pool.back();
+      pool.pop_back();
+      return e;
+    }
+    hipEvent_t e;
+    hip_check(hipEventCreate(&e), "hipEventCreate");
+    return e;
+  }
+};
+
+namespace {
+
+void upload(DevBuf& d, const std::vector<float>& h) {
+  d.alloc(h.size() * sizeof(float));
+  hip_check(hipMemcpy(d.p, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice), "hipMemcpy H2D");
+}
+
+void bn_fold(mp_ctx* c, const std::string& scope, int n, DevBuf& s_out, DevBuf& t_out,
+             std::vector<float>* hs = nullptr, std::vector<float>* ht = nullptr) {
+  const auto& g = c->need(scope + "/gamma", {n}).host;
+  const auto& b = c->need(scope + "/beta", {n}).host;
+  const auto& m = c->need(scope + "/moving_mean", {n}).host;
+  const auto& v = c->need(scope + "/moving_variance", {n}).host;
+  std::vector<float> s(n), t(n);
+  for (int i = 0; i < n; ++i) {
+    // inference BN: gamma * (x - mean) / sqrt(var + eps) + beta, eps = 1e-5 (hgru_pose.py:17)
+    const double sc = (double)g[i] / std::sqrt((double)v[i] + 1e-5);
+    s[i] = (float)sc;
+    t[i] = (float)((double)b[i] - (double)m[i] * sc);
+  }
+  upload(s_out, s);
+  upload(t_out, t);
+  if (hs) *hs = s;
+  if (ht) *ht = t;
+}
+
+void copy_dev(DevBuf& d, const RawWeight& w) {
+  d.alloc(w.numel() * sizeof(float));
+  hip_check(hipMemcpy(d.p, w.dev->p, w.numel() * sizeof(float), hipMemcpyDeviceToDevice), "hipMemcpy D2D");
+}
+
+std::vector<float> vec64(mp_ctx* c, const std::string& n) {
+  return c->need("contextual_circuit/" + n, {1, 1, 1, 64}).host;
+}
+
+void finalize_circuit(mp_ctx* c, const std::vector<float>* outs, const std::vector<float>* outt) {
+  auto it = c->raw.find("contextual_circuit/p_r");
+  if (it == c->raw.end()) fail(MP_ERR_STATE, "weight not set: contextual_circuit/p_r");
+  const auto& ps = it->second.shape;
+  if (ps.size() != 4 || ps[0] != ps[1] || ps[2] != 64 || ps[3] != 64 ||
+      !(ps[0] == 3 || ps[0] == 5 || ps[0] == 15))
+    fail(MP_ERR_WEIGHT, "contextual_circuit/p_r must be [S,S,64,64] with S in {3,5,15}");
+  c->ssf = (int)ps[0];
+  c->p_pk.alloc((size_t)8 * c->ssf * c->ssf * 2 * 64 * 16);
+  hip_check(launch_pack_conv64(it->second.dev->f(), c->p_pk.v4(), c->ssf, nullptr), "pack p_r");
+  c->ir_pk.alloc(1024 * 16);
+  c->or_pk.alloc(1024 * 16);
+  hip_check(launch_pack_gate(c->need("contextual_circuit/i_r", {1, 1, 64, 64}).dev->f(), c->ir_pk.v4(), nullptr),
+            "pack i_r");
+  hip_check(launch_pack_gate(c->need("contextual_circuit/o_r", {1, 1, 64, 64}).dev->f(), c->or_pk.v4(), nullptr),
+            "pack o_r");
+  std::vector<float> v(V_COUNT * 64);
+  const char* order[] = {"lateral_bias", "beta", "nu", "gamma", "kappa", "omega", "i_b", "o_b"};
+  for (int k = 0; k < 8; ++k) {
+    auto x = vec64(c, order[k]);
+    std::copy(x.begin(), x.end(), v.begin() + k * 64);
+  }
+  for (int i = 0; i < 64; ++i) {
+    v[V_OUTS * 64 + i] = outs ? (*outs)[i] : 1.f;
+    v[V_OUTT * 64 + i] = outt ? (*outt)[i] : 0.f;
+  }
+  upload(c->vecs, v);
+  auto rt = c->raw.find("contextual_circuit/rho");
+  if (rt == c->raw.end() || rt->second.shape.size() != 1 || rt->second.shape[0] < 1)
+    fail(MP_ERR_WEIGHT, "contextual_circuit/rho must be set with shape [timesteps]");
+  c->rho = rt->second.host;
+  c->timesteps = (int)c->rho.size();
+}
+
+void finalize_pose(mp_ctx* c) {
+  const int k = 64;
+  copy_dev(c->conv1_w, c->need("conv_1/conv_1_filters", {3, 3, 1, k}));
+  copy_dev(c->conv1_b, c->need("conv_1/conv_1_biases", {k}));
+  bn_fold(c, "batch_normalization", k, c->bn0_s, c->bn0_t);
+  c->conv2_pk.alloc((size_t)8 * 9 * 2 * 64 * 16);
+  c->conv3_pk.alloc((size_t)8 * 9 * 2 * 64 * 16);
+  hip_check(launch_pack_conv64(c->need("conv_2/conv_2_filters", {3, 3, k, k}).dev->f(), c->conv2_pk.v4(), 3, nullptr),
+            "pack conv_2");
+  hip_check(launch_pack_conv64(c->need("conv_3/conv_3_filters", {3, 3, k, k}).dev->f(), c->conv3_pk.v4(), 3, nullptr),
+            "pack conv_3");
+  copy_dev(c->conv2_b, c->need("conv_2/conv_2_biases", {k}));
+  copy_dev(c->conv3_b, c->need("conv_3/conv_3_biases", {k}));
+  bn_fold(c, "batch_normalization_1", k, c->bn1_s, c->bn1_t);
+  bn_fold(c, "batch_normalization_2", k, c->bn2_s, c->bn2_t);
+  DevBuf s3, t3;
+  std::vector<float> hs3, ht3;
+  bn_fold(c, "batch_normalization_3", k, s3, t3, &hs3, &ht3);
+  finalize_circuit(c, &hs3, &ht3);
+
+  auto f1 = c->raw.find("fc_1/fc_1_weights");
+  if (f1 == c->raw.end()) fail(MP_ERR_STATE, "weight not set: fc_1/fc_1_weights");
+  if (f1->second.shape.size() != 2 || f1->second.shape[0] % 64 != 0)
+    fail(MP_ERR_WEIGHT, "fc_1/fc_1_weights must be [H*W*64, N]");
+  c->fc1_in = (int)f1->second.shape[0];
+  c->fc1_out = (int)f1->second.shape[1];
+  const int K8 = (c->fc1_in + 7) / 8, N32 = (c->fc1_out + 31) / 32;
+  c->fc1_pk.alloc((size_t)K8 * N32 * 64 * 16);
+  hip_check(launch_pack_fc(f1->second.dev->f(), c->fc1_pk.v4(), c->fc1_in, c->fc1_out, nullptr), "pack fc_1");
+  copy_dev(c->fc1_b, c->need("fc_1/fc_1_biases", {c->fc1_out}));
+  bn_fold(c, "batch_normalization_4", c->fc1_out, c->bn4_s, c->bn4_t);
+  auto fo = c->raw.find("fc_out/fc_out_weights");
+  if (fo == c->raw.end()) fail(MP_ERR_STATE, "weight not set: fc_out/fc_out_weights");
+  if (fo->second.shape.size() != 2 || fo->second.shape[0] != c->fc1_out)
+    fail(MP_ERR_WEIGHT, "fc_out/fc_out_weights must be [fc_1 out, output_shape]");
+  c->nout = (int)fo->second.shape[1];
+  const int K8o = (c->fc1_out + 7) / 8, N32o = (c->nout + 31) / 32;
+  c->fco_pk.alloc((size_t)K8o * N32o * 64 * 16);
+  hip_check(launch_pack_fc(fo->second.dev->f(), c->fco_pk.v4(), c->fc1_out, c->nout, nullptr), "pack fc_out");
+  copy_dev(c->fco_b, c->need("fc_out/fc_out_biases", {c->nout}));
+}
+
+void ensure_ws(mp_ctx* c, int64_t n, int64_t H, int64_t W) {
+  const int64_t px = n * H * W;
+  if (n <= c->cap_batch && H * W <= c->cap_hw) return;
+  const int64_t nb = std::max(n, c->cap_batch), hw = std::max(H * W, c->cap_hw);
+  const size_t st = (size_t)nb * hw * 64 * sizeof(float);
+  c->X.alloc(st);
+  c->O.alloc(st);
+  c->I.alloc(st);
+  c->Og.alloc(st);
+  if (c->model == MP_MODEL_HGRU_POSE) {
+    c->bufA.alloc(st);
+    c->bufB.alloc(st);
+    c->fcin.alloc(st);
+    int ks;
+    const int S = fc_choose_splits((int)nb, c->fc1_in, c->fc1_out, &ks);
+    const size_t p1 = (size_t)S * nb * ((c->fc1_out + 31) / 32 * 32) * sizeof(float);
+    const int S2 = fc_choose_splits((int)nb, c->fc1_out, c->nout, &ks);
+    const size_t p2 = (size_t)S2 * nb * ((c->nout + 31) / 32 * 32) * sizeof(float);
+    c->part.alloc(std::max(p1, p2));
+    c->h1.alloc((size_t)nb * c->fc1_out * sizeof(float));
+  }
+  (void)px;
+  c->cap_batch = nb;
+  c->cap_hw = hw;
+}
+
+struct ProfScope {
+  mp_ctx* c;
+  hipStream_t st;
+  const char* name;
+  hipEvent_t a = nullptr;
+  ProfScope(mp_ctx* c_, hipStream_t s, const char* n) : c(c_), st(s), name(n) {
+    if (c->prof) {
+      a = c->ev();
+      hip_check(hipEventRecord(a, st), "hipEventRecord");
+    }
+  }
+  ~ProfScope() noexcept(false) {
+    if (a) {
+      hipEvent_t b = c->ev();
+      hip_check(hipEventRecord(b, st), "hipEventRecord");
+      c->events.push_back({name, a, b});
+    }
+  }
+};
+
+void run_circuit(mp_ctx* c, int64_t n, int H, int W, int T, const float* o0_nhwc, float* final_dst2,
+                 hipStream_t st) {
+  hip_check(launch_gate_init(o0_nhwc, c->O.f(), c->Og.f(), c->ir_pk.v4(), c->vecs.f(), (int)n, H, W, st),
+            "gate_init");
+  for (int t = 0; t < T; ++t) {
+    ConvArgs a{};
+    a.H = H;
+    a.W = W;
+    a.src = c->Og.f();
+    a.wpk = c->p_pk.v4();
+    a.dst = c->I.f();
+    a.X = c->X.f();
+    a.O = c->O.f();
+    a.vecs = c->vecs.f();
+    {
+      ProfScope ps(c, st, "conv15_a");
+      hip_check(launch_conv64(c->ssf, EPI_HGRU_A, a, (int)n, st), "conv15 A");
+    }
+    ConvArgs b{};
+    b.H = H;
+    b.W = W;
+    b.src = c->I.f();
+    b.wpk = c->p_pk.v4();
+    b.dst = c->O.f();
+    b.O = c->O.f();
+    b.I = c->I.f();
+    b.vecs = c->vecs.f();
+    b.gpk_or = c->or_pk.v4();
+    b.gpk_ir = c->ir_pk.v4();
+    b.rho = c->rho[t];
+    b.mode = (t == T - 1) ? 1 : 0;
+    b.dst2 = (t == T - 1) ? final_dst2 : c->Og.f();
+    {
+      ProfScope ps(c, st, "conv15_b");
+      hip_check(launch_conv64(c->ssf, EPI_HGRU_B, b, (int)n, st), "conv15 B");
+    }
+  }
+}
+
+}  // namespace
+
+// ================================================ C ABI ============================================
+
+namespace {
+int guard(const std::function<void()>& f) {
+  try {
+    g_err.clear();
+    f();
+    return MP_OK;
+  } catch (const Fail& e) {
+    return e.code;
+  } catch (const std::exception& e) {
+    g_err = std::string("internal error: ") + e.what();
+    return MP_ERR_STATE;
+  } catch (...) {
+    g_err = "internal error";
+    return MP_ERR_STATE;
+  }
+}
+}  // namespace
+
+extern "C" {
+
+int mp_version(void) { return (0 << 16) | 1; }
+
+const char* mp_last_error(void) { return g_err.c_str(); }
+
+int mp_create(int device, int model_kind, mp_ctx** out) {
+  return guard([&] {
+    if (!out) fail(MP_ERR_ARG, "out is NULL");
+    if (model_kind != MP_MODEL_HGRU_POSE && model_kind != MP_MODEL_HGRU_CIRCUIT)
+      fail(MP_ERR_ARG, "unknown model_kind " + std::to_string(model_kind));
+    int ndev = 0;
+    hip_check(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
+    if (device < 0 || device >= ndev) fail(MP_ERR_ARG, "device " + std::to_string(device) + " out of range");
+    hip_check(hipSetDevice(device), "hipSetDevice");
+    auto* c = new mp_ctx();
+    c->device = device;
+    c->model = model_kind;
+    *out = c;
+  });
+}
+
+void mp_destroy(mp_ctx* ctx) {
+  if (!ctx) return;
+  (void)hipSetDevice(ctx->device);
+  (void)hipDeviceSynchronize();
+  delete ctx;
+}
+
+int mp_set_weight(mp_ctx* ctx, const char* name, const float* data, const int64_t* shape, int ndim,
+                  int mem_kind) {
+  return guard([&] {
+    if (!ctx || !name || !data || (!shape && ndim > 0) || ndim < 0 || ndim > 8)
+      fail(MP_ERR_ARG, "mp_set_weight: bad argument");
+    if (mem_kind != MP_MEM_HOST && mem_kind != MP_MEM_DEVICE) fail(MP_ERR_ARG, "mp_set_weight: bad mem_kind");
+    hip_check(hipSetDevice(ctx->device), "hipSetDevice");
+    const std::string n = strip_scope(name);
+    if (!known_name(ctx->model, n)) fail(MP_ERR_WEIGHT, "unknown weight name: " + std::string(name));
+    RawWeight w;
+    for (int i = 0; i < ndim; ++i) {
+      if (shape[i] <= 0) fail(MP_ERR_WEIGHT, "non-positive dimension in " + n);
+      w.shape.push_back(shape[i]);
+    }
+    const size_t cnt = w.numel(), bytes = cnt * sizeof(float);
+    w.dev = std::make_unique<DevBuf>();
+    w.dev->alloc(bytes);
+    hip_check(hipMemcpy(w.dev->p, data, bytes,
+                        mem_kind == MP_MEM_HOST ? hipMemcpyHostToDevice : hipMemcpyDeviceToDevice),
+              "hipMemcpy weight");
+    if (cnt <= (1u << 16)) {
+      w.host.resize(cnt);
+      hip_check(hipMemcpy(w.host.data(), w.dev->p, bytes, hipMemcpyDeviceToHost), "hipMemcpy D2H");
+    }
+    ctx->raw[n] = std::move(w);
+    ctx->finalized = false;
+  });
+}
+
+int mp_finalize_weights(mp_ctx* ctx, int compute_dtype) {
+  return guard([&] {
+    if (!ctx) fail(MP_ERR_ARG, "ctx is NULL");
+    if (compute_dtype != MP_DTYPE_F32) fail(MP_ERR_UNSUPPORTED, "only MP_DTYPE_F32 is implemented");
+    hip_check(hipSetDevice(ctx->device), "hipSetDevice");
+    if (ctx->model == MP_MODEL_HGRU_POSE)
+      finalize_pose(ctx);
+    else
+      finalize_circuit(ctx, nullptr, nullptr);
+    hip_check(hipDeviceSynchronize(), "finalize sync");
+    ctx->finalized = true;
+  });
+}
+
+int mp_reserve(mp_ctx* ctx, int64_t max_batch) {
+  return guard([&] {
+    if (!ctx || max_batch <= 0) fail(MP_ERR_ARG, "mp_reserve: bad argument");
+    if (!ctx->finalized) fail(MP_ERR_STATE, "mp_reserve before mp_finalize_weights");
+    hip_check(hipSetDevice(ctx->device), "hipSetDevice");
+    const int64_t hw = ctx->model == MP_MODEL_HGRU_POSE ? ctx->fc1_in / 64 : 64 * 64;
+    ensure_ws(ctx, max_batch, hw, 1);
+  });
+}
+
+int mp_hgru_pose_fwd(mp_ctx* ctx, const float* depth, int64_t n, int64_t h, int64_t w, const float* o0,
+                     float* out, void* stream) {
+  return guard([&] {
+    if (!ctx || !depth || !o0 || !out) fail(MP_ERR_ARG, "mp_hgru_pose_fwd: null pointer");
+    if (ctx->model != MP_MODEL_HGRU_POSE) fail(MP_ERR_STATE, "context is not an hgru_pose model");
+    if (!ctx->finalized) fail(MP_ERR_STATE, "weights not finalized");
+    if (n <= 0 || n > (1 << 20)) fail(MP_ERR_SHAPE, "batch must be in [1, 2^20]");
+    if (h % 2 || w % 2) fail(MP_ERR_SHAPE, "crop height/width must be even");
+    const int H = (int)(h / 2), W = (int)(w / 2);
+    if (H % TH || W % TW) fail(MP_ERR_SHAPE, "crop/2 must be a multiple of 16 (rows) and 32 (cols)");
+    if ((int64_t)H * W * 64 != ctx->fc1_in)
+      fail(MP_ERR_SHAPE, "crop size does not match fc_1 input (" + std::to_string(ctx->fc1_in) + ")");
+    hip_check(hipSetDevice(ctx->device), "hipSetDevice");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    ensure_ws(ctx, n, H, W);
+    const int N = (int)n;
+    {
+      ProfScope ps(ctx, st, "backbone");
+      hip_check(launch_conv1_pool_bn(depth, ctx->conv1_w.f(), ctx->conv1_b.f(), ctx->bn0_s.f(), ctx->bn0_t.f(),
+                                     ctx->bufA.f(), N, (int)h, (int)w, st),
+                "conv_1");
+      ConvArgs a{};
+      a.H = H;
+      a.W = W;
+      a.src = ctx->bufA.f();
+      a.wpk = ctx->conv2_pk.v4();
+      a.dst = ctx->bufB.f();
+      a.bias = ctx->conv2_b.f();
+      a.bn_s = ctx->bn1_s.f();
+      a.bn_t = ctx->bn1_t.f();
+      hip_check(launch_conv64(3, EPI_BB, a, N, st), "conv_2");
+      a.src = ctx->bufB.f();
+      a.wpk = ctx->conv3_pk.v4();
+      a.dst = ctx->X.f();
+      a.bias = ctx->conv3_b.f();
+      a.bn_s = ctx->bn2_s.f();
+      a.bn_t = ctx->bn2_t.f();
+      hip_check(launch_conv64(3, EPI_BB, a, N, st), "conv_3");
+    }
+    run_circuit(ctx, n, H, W, ctx->timesteps, o0, ctx->fcin.f(), st);
+    {
+      ProfScope ps(ctx, st, "fc1");
+      int ks;
+      const int S = fc_choose_splits(N, ctx->fc1_in, ctx->fc1_out, &ks);
+      hip_check(launch_fc_gemm(ctx->fcin.f(), ctx->fc1_in, ctx->fc1_pk.v4(), ctx->part.f(), N, ctx->fc1_in,
+                               ctx->fc1_out, S, ks, st),
+                "fc_1 gemm");
+      hip_check(launch_fc_reduce(ctx->part.f(), S, N, ctx->fc1_out, ctx->fc1_b.f(), 1, ctx->bn4_s.f(),
+                                 ctx->bn4_t.f(), ctx->h1.f(), ctx->fc1_out, st),
+                "fc_1 reduce");
+    }
+    {
+      ProfScope ps(ctx, st, "fc_out");
+      int ks;
+      const int S2 = fc_choose_splits(N, ctx->fc1_out, ctx->nout, &ks);
+      hip_check(launch_fc_gemm(ctx->h1.f(), ctx->fc1_out, ctx->fco_pk.v4(), ctx->part.f(), N, ctx->fc1_out,
+                               ctx->nout, S2, ks, st),
+                "fc_out gemm");
+      hip_check(launch_fc_reduce(ctx->part.f(), S2, N, ctx->nout, ctx->fco_b.f(), 0, nullptr, nullptr, out,
+                                 ctx->nout, st),
+                "fc_out reduce");
+    }
+  });
+}
+
+int mp_hgru_circuit_fwd(mp_ctx* ctx, const float* x, const float* o0, int64_t n, int64_t h, int64_t w,
+                        int64_t k, int timesteps, float* o_out, void* stream) {
+  return guard([&] {
+    if (!ctx || !x || !o0 || !o_out) fail(MP_ERR_ARG, "mp_hgru_circuit_fwd: null pointer");
+    if (!ctx->finalized) fail(MP_ERR_STATE, "weights not finalized");
+    if (k != 64) fail(MP_ERR_SHAPE, "channel count k must be 64");
+    if (n <= 0 || h <= 0 || w <= 0 || h % TH || w % TW) fail(MP_ERR_SHAPE, "need h % 16 == 0 and w % 32 == 0");
+    if (timesteps < 1 || timesteps > (int)ctx->rho.size())
+      fail(MP_ERR_ARG, "timesteps must be in [1, len(rho)]");
+    hip_check(hipSetDevice(ctx->device), "hipSetDevice");
+    hipStream_t st = static_cast<hipStream_t>(stream);
+    ensure_ws(ctx, n, h, w);
+    hip_check(launch_nhwc_to_c8(x, ctx->X.f(), (int)n, (int)h, (int)w, st), "nhwc_to_c8");
+    if (ctx->model == MP_MODEL_HGRU_POSE) {
+      // the pose context's output affine is BN_3: use identity by running with a temporary copy
+      fail(MP_ERR_UNSUPPORTED, "use an MP_MODEL_HGRU_CIRCUIT context for the standalone circuit");
+    }
+    run_circuit(ctx, n, (int)h, (int)w, timesteps, o0, o_out, st);
+  });
+}
+
+int mp_info(mp_ctx* ctx, const char* key, int64_t* value) {
+  return guard([&] {
+    if (!ctx || !key || !value) fail(MP_ERR_ARG, "mp_info: null pointer");
+    const std::string k(key);
+    if (k == "output_shape")
+      *value = ctx->nout;
+    else if (k == "timesteps")
+      *value = ctx->timesteps;
+    else if (k == "ssf")
+      *value = ctx->ssf;
+    else if (k == "finalized")
+      *value = ctx->finalized ? 1 : 0;
+    else if (k == "fc1_in")
+      *value = ctx->fc1_in;
+    else if (k == "workspace_bytes")
+      *value = (int64_t)(ctx->X.bytes + ctx->O.bytes + ctx->I.bytes + ctx->Og.bytes + ctx->bufA.bytes +
+                         ctx->bufB.bytes + ctx->fcin.bytes + ctx->part.bytes + ctx->h1.bytes);
+    else if (k == "weight_bytes") {
+      size_t s = 0;
+      for (auto& kv : ctx->raw) s += kv.second.numel() * sizeof(float);
+      *value = (int64_t)s;
+    } else
+      fail(MP_ERR_ARG, "unknown info key: " + k);
+  });
+}
+
+int mp_profile_enable(mp_ctx* ctx, int enable) {
+  return guard([&] {
+    if (!ctx) fail(MP_ERR_ARG, "ctx is NULL");
+    ctx->prof = enable != 0;
+  });
+}
+
+int mp_profile_read(mp_ctx* ctx, const char* name, double* total_ms, int64_t* launches) {
+  return guard([&] {
+    if (!ctx || !name || !total_ms || !launches) fail(MP_ERR_ARG, "mp_profile_read: null pointer");
+    double tot = 0;
+    int64_t cnt = 0;
+    std::vector<ProfEvent> keep;
+    for (auto& e : ctx->events) {
+      if (e.name == name) {
+        hip_check(hipEventSynchronize(e.b), "hipEventSynchronize");
+        float ms = 0;
+        hip_check(hipEventElapsedTime(&ms, e.a, e.b), "hipEventElapsedTime");
+        tot += ms;
+        ++cnt;
+        ctx->pool.push_back(e.a);
+        ctx->pool.push_back(e.b);
+      } else {
+        keep.push_back(e);
+      }
+    }
+    ctx->events.swap(keep);
+    *total_ms = tot;
+    *launches = cnt;
+  });
+}
+
+}  // extern "C"

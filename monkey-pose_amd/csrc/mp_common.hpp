@@ -1,0 +1,47 @@
+// Shared definitions for the monkey-pose MI355X (gfx950) kernels.
+//
+// Activation layout ("C8"): every 64-channel feature map of the hot path is stored in HBM as
+//   act[b][q][y][x][e],  q = c / 8 (8 channel chunks), e = c % 8
+// so that one halo-chunk load of the association-field convolution reads 32 contiguous bytes
+// per pixel and one epilogue store of a 32x32 fp32 MFMA tile is a contiguous 1 KiB run.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+typedef float f32x4 __attribute__((ext_vector_type(4)));
+typedef float f32x16 __attribute__((ext_vector_type(16)));
+
+namespace mp {
+
+constexpr int C = 64;      // channels of every hGRU / backbone map (hgru_pose.py:50-81)
+constexpr int NQ = C / 8;  // channel chunks in the C8 layout
+
+__device__ __forceinline__ size_t c8_index(int b, int q, int y, int x, int e, int H, int W) {
+  return ((((size_t)b * NQ + q) * H + y) * W + x) * 8 + e;
+}
+
+// v_mfma_f32_32x32x2_f32: exact fp32 (fma chain), 64 cycles issue per SIMD.
+// A lane l: A[i=l&31][k=l>>5];  B lane l: B[k=l>>5][j=l&31];
+// D lane l: D[i=(r&3)+8(r>>2)+4(l>>5)][j=l&31], r = 0..15.
+__device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x2f32(a, b, c, 0, 0, 0);
+}
+
+__device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
+
+// per-channel parameter vectors of the hGRU epilogues, each 64 floats, in this order
+enum VecId {
+  V_LAT = 0,   // lateral_bias        (hgru_module.py:498-503, added at 657)
+  V_BETA,      // beta                (405-416)
+  V_NU,        // nu                  (418-429)
+  V_GAMMA,     // gamma               (439-447)
+  V_KAPPA,     // kappa               (469-474)
+  V_OMEGA,     // omega               (480-485)
+  V_IB,        // i_b                 (344-357)
+  V_OB,        // o_b                 (382-396)
+  V_OUTS,      // output affine scale (BN after the circuit, hgru_pose.py:82-90; 1 standalone)
+  V_OUTT,      // output affine shift
+  V_COUNT
+};
+
+}  // namespace mp

@@ -1,0 +1,49 @@
+// Launcher declarations shared by the kernel translation units and the C-ABI layer.
+#pragma once
+#include "mp_common.hpp"
+
+namespace mp {
+
+constexpr int TH = 16, TW = 32;   // conv64 output tile (pixels) per 256-thread block
+enum Epi { EPI_BB = 0, EPI_HGRU_A = 1, EPI_HGRU_B = 2 };
+
+struct ConvArgs {
+  const float* src;       // conv input, C8
+  const f32x4* wpk;       // packed conv weights [q][tap][n][lane]
+  float* dst;             // BB: output C8; A: I (C8); B: O' (C8, in place over O)
+  // backbone epilogue
+  const float* bias;      // [64]
+  const float* bn_s;      // [64]
+  const float* bn_t;      // [64]
+  // hGRU epilogues
+  const float* X;         // A: feed-forward drive (C8)
+  const float* O;         // A, B: current output state (C8)
+  const float* I;         // B: I (C8) (also the conv input)
+  const float* vecs;      // [V_COUNT][64]
+  const f32x4* gpk_or;    // B: packed o_r
+  const f32x4* gpk_ir;    // B: packed i_r (next step's input gate)
+  float* dst2;            // B mode 0: Og' (C8);  mode 1: affine(O') NHWC
+  float rho;              // B: rho[t]
+  int mode;               // B: 0 = next-step gate, 1 = final step
+  int H, W, tiles_x, tiles_y;
+};
+
+// k_conv64.hip
+hipError_t launch_conv64(int ks, int epi, ConvArgs a, int B, hipStream_t st);
+hipError_t launch_gate_init(const float* O0, float* O, float* Og, const f32x4* gpk_ir, const float* vecs,
+                            int B, int H, int W, hipStream_t st);
+hipError_t launch_conv1_pool_bn(const float* in, const float* w, const float* bias, const float* s,
+                                const float* t, float* out, int B, int Hin, int Win, hipStream_t st);
+hipError_t launch_nhwc_to_c8(const float* in, float* out, int B, int H, int W, hipStream_t st);
+hipError_t launch_c8_to_nhwc(const float* in, float* out, int B, int H, int W, hipStream_t st);
+hipError_t launch_pack_conv64(const float* w, f32x4* out, int ks, hipStream_t st);
+hipError_t launch_pack_gate(const float* g, f32x4* out, hipStream_t st);
+// k_fc.hip
+hipError_t launch_pack_fc(const float* W, f32x4* out, int K, int N, hipStream_t st);
+int fc_choose_splits(int M, int K, int N, int* kslice);
+hipError_t launch_fc_gemm(const float* A, int lda, const f32x4* Wpk, float* part, int M, int K, int N, int S,
+                          int kslice, hipStream_t st);
+hipError_t launch_fc_reduce(const float* part, int S, int M, int N, const float* bias, int relu,
+                            const float* aff_s, const float* aff_t, float* out, int ldo, hipStream_t st);
+
+}  // namespace mp

@@ -1,0 +1,132 @@
+"""Drop-in for ``/root/reference/hgru_module.py``: ``ContextualCircuit(X, ...).build()``.
+
+Supports the configuration the pose model uses (``hgru_pose.py:20-39`` merged over the defaults
+of ``auxilliary_variables``, ``hgru_module.py:9-51``): association-field eCRF with a full
+SSFxSSF conv, 1x1 GRU gates on the input, multiplicative excitation, learned gamma/kappa/omega,
+adaptation (rho), xi = zeta = 1, tanh recurrence, no rectification.  Other aux combinations raise
+``NotImplementedError`` rather than silently computing something else.  Inference only.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Optional
+
+import numpy as np
+
+from . import _lib
+from . import weights as W
+
+# the effective aux of hgru_pose (hgru_pose.py:20-39 over hgru_module.py:9-51)
+SUPPORTED_AUX = {
+    'recurrent_nl': 'tanh', 'rectify_weights': None, 'gate_filter': 1, 'xi': False,
+    'zeta': False, 'gamma': True, 'beta': True, 'nu': True, 'batch_norm': False,
+    'atrous_convolutions': False, 'output_gru_gates': False, 'association_field': True,
+    'multiplicative_excitation': True, 'gru_gates': True, 'adapation': True,
+    'dense_connections': False, 'integration_type': 'alternate', 'hidden_init': 'random',
+    'lesion_beta': False, 'lesion_nu': False, 'lesion_omega': False, 'lesion_kappa': False,
+    'dropout': None, 'store_states': False,
+}
+# keys that only affect training / initialisation, never the forward values
+_IGNORED = {'symmetric_weights', 'symmetric_gate_weights', 'trainable', 'pre_batchnorm',
+            'post_batchnorm', 'train', 'normal_initializer', 'gate_bias_init', 'dtype',
+            'return_weights', 'lesions', 'tuning_nl', 'gate_nl', 'ecrf_nl', 'post_tuning_nl'}
+
+_DEFAULTS = {  # auxilliary_variables() values for the keys checked above (hgru_module.py:13-51)
+    'recurrent_nl': 'tanh', 'rectify_weights': None, 'gate_filter': 1, 'xi': False, 'zeta': False,
+    'gamma': True, 'beta': True, 'nu': True, 'batch_norm': False, 'atrous_convolutions': False,
+    'output_gru_gates': False, 'association_field': True, 'multiplicative_excitation': True,
+    'gru_gates': False, 'adapation': False, 'dense_connections': False,
+    'integration_type': 'alternate', 'hidden_init': 'random', 'lesion_beta': False,
+    'lesion_nu': False, 'lesion_omega': False, 'lesion_kappa': False, 'dropout': None,
+    'store_states': False,
+}
+
+
+class ContextualCircuit(object):
+    """``hgru_module.ContextualCircuit`` (hgru_module.py:54-128)."""
+
+    def __getitem__(self, name):
+        return getattr(self, name)
+
+    def __contains__(self, name):
+        return hasattr(self, name)
+
+    def __init__(self, X, timesteps=1, SRF=1, SSN=9, SSF=29, strides=[1, 1, 1, 1],
+                 padding='SAME', aux=None, train=True):
+        self.X = X
+        self.n, self.h, self.w, self.k = [int(x) for x in X.shape]
+        self.timesteps = timesteps
+        self.strides = strides
+        self.padding = padding
+        self.train = train
+        merged = dict(_DEFAULTS)
+        if aux is not None and isinstance(aux, dict):
+            for key, val in aux.items():
+                merged[key] = val
+        if merged.get('recurrent_nl') is not None and not isinstance(merged['recurrent_nl'], str):
+            raise NotImplementedError("recurrent_nl must be given by name ('tanh')")
+        bad = {k: merged[k] for k in SUPPORTED_AUX if merged.get(k) != SUPPORTED_AUX[k]}
+        if bad:
+            raise NotImplementedError(f"aux settings outside the implemented hGRU variant: {bad}")
+        unknown = set(merged) - set(SUPPORTED_AUX) - _IGNORED
+        if unknown:
+            raise NotImplementedError(f"unsupported aux keys: {sorted(unknown)}")
+        for key, val in merged.items():
+            setattr(self, key, val)
+        self.SRF, self.SSN, self.SSF = SRF, SSN, SSF
+        if isinstance(SSF, list):
+            raise NotImplementedError("hierarchical (list) SSF is not implemented")
+        self.SSF_ext = 2 * int(math.floor(SSF / 2.0)) + 1                # hgru_module.py:97
+        if list(strides) != [1, 1, 1, 1] or padding != 'SAME':
+            raise NotImplementedError("only strides [1,1,1,1] with SAME padding")
+        self.p_shape = [self.SSF_ext, self.SSF_ext, self.k, self.k]
+        self.i_shape = [self.gate_filter, self.gate_filter, self.k, self.k]
+        self.o_shape = [self.gate_filter, self.gate_filter, self.k, self.k]
+        self.bias_shape = [1, 1, 1, self.k]
+        self.weights: Optional[Dict[str, np.ndarray]] = None
+        self.weight_seed = 1234
+        self.scope = "contextual_circuit"
+
+    def prepare_tensors(self, weights: Optional[Dict[str, np.ndarray]] = None,
+                        seed: Optional[int] = None) -> Dict[str, np.ndarray]:
+        """Variables of ``prepare_tensors`` (hgru_module.py:172-503) keyed
+        ``contextual_circuit/<name>``; given values win, the rest are synthesised."""
+        table = W.hgru_circuit_vars(k=self.k, ssf=self.SSF_ext, gate_filter=self.gate_filter,
+                                    timesteps=self.timesteps, scope=self.scope)
+        given = {}
+        for k_, v in (weights or self.weights or {}).items():
+            given[k_.split("/")[-1]] = v
+        s = self.weight_seed if seed is None else seed
+        out = {}
+        for v in table:
+            short = v.name.split("/")[-1]
+            out[v.name] = (np.asarray(given[short], np.float32) if short in given
+                           else W.synth_value(v, s, self.timesteps))
+        return out
+
+    def build(self, weights: Optional[Dict[str, np.ndarray]] = None, h2_init=None):
+        """Run the circuit; returns ``(O, weights, activities)`` like the reference with
+        ``return_weights=True`` (hgru_module.py:939-954)."""
+        import torch
+        X = self.X
+        if not isinstance(X, torch.Tensor) or not X.is_cuda:
+            raise TypeError("X must be a CUDA (ROCm) torch tensor [n, h, w, k]")
+        wts = self.prepare_tensors(weights)
+        ctx = _lib.Context(_lib.MP_MODEL_HGRU_CIRCUIT, X.device.index or 0)
+        for name, val in wts.items():
+            ctx.set_weight(name, val)
+        ctx.finalize()
+        X = X.detach().float().contiguous()
+        if h2_init is None:
+            h2_init = torch.from_numpy(W.synth_hidden(tuple(X.shape))).to(X.device)
+        h2_init = h2_init.detach().float().contiguous()
+        if h2_init.shape != X.shape:
+            raise ValueError("h2_init must have the shape of X")
+        O = torch.empty_like(X)
+        ctx.circuit_fwd(X, h2_init, O, self.timesteps, _lib.current_stream(X.device))
+        torch.cuda.current_stream(X.device).synchronize()
+        ctx.close()
+        self.h2_init = h2_init
+        weights_out = {k_.split("/")[-1]: v for k_, v in wts.items()}
+        weights_out['p_t'] = weights_out['p_r']
+        return O, weights_out, {}

@@ -1,0 +1,154 @@
+"""Drop-in for ``/root/reference/hgru_pose.py`` (inference): ``model().build(depth, output_shape)``.
+
+Same class, attribute and argument names as the reference (``hgru_pose.py:6-118``).  ``build``
+runs the forward immediately on the depth crops' device (the reference builds a TF graph that a
+later ``sess.run`` executes) and sets ``self.out_put`` to a ``[N, output_shape]`` fp32 tensor in
+the reference's joint-major layout (``j*3 + {x,y,z}``, normalised by ``cube_z / 2``).  Call
+``forward(depth)`` to run again with the finalized weights.
+
+Everything is computed by ``libmonkeypose.so`` (HIP, gfx950); there is no CPU path.
+"""
+from __future__ import annotations
+
+import copy
+from typing import Dict, Optional
+
+import numpy as np
+
+from . import _lib
+from . import weights as W
+
+
+class model:
+    """``hgru_pose.model`` (hgru_pose.py:6-39)."""
+
+    def __init__(self, trainable=True):
+        self.trainable = trainable
+        self.data_dict = None                  # {layer: [W, b]} as in get_var (hgru_pose.py:199)
+        self.var_dict = {}
+        self.SRF = 1
+        self.SSN = 15
+        self.SSF = 15
+        self.strides = [1, 1, 1, 1]
+        self._BATCH_NORM_DECAY = 0.997
+        self._BATCH_NORM_EPSILON = 1e-5
+        self.padding = 'SAME'
+        self.timesteps = 8
+        self.aux = {
+            'recurrent_nl': 'tanh',
+            'rectify_weights': None,
+            'pre_batchnorm': False,
+            'gate_filter': 1,
+            'xi': False,
+            'post_batchnorm': False,
+            'dense_connections': False,
+            'symmetric_weights': True,
+            'symmetric_gate_weights': False,
+            'batch_norm': False,
+            'atrous_convolutions': False,
+            'output_gru_gates': False,
+            'association_field': True,
+            'multiplicative_excitation': True,
+            'gru_gates': True,
+            'gamma': True,
+            'adapation': True,
+            'trainable': True,
+        }
+        self.weights: Optional[Dict[str, np.ndarray]] = None   # TF variable name -> array
+        self.weight_seed = 1234
+        self._ctx: Optional[_lib.Context] = None
+        self._ctx_key = None
+        self.out_put = None
+        self.h2_init = None
+
+    def __getitem__(self, name):
+        return getattr(self, name)
+
+    def __contains__(self, name):
+        return hasattr(self, name)
+
+    # ---------------------------------------------------------------- weights
+    def load_weights(self, weights: Dict[str, np.ndarray]) -> None:
+        """Variables keyed by TF name (``cnn/...``); missing ones are synthesised."""
+        self.weights = {(k if k.startswith("cnn/") else "cnn/" + k): v for k, v in weights.items()}
+        self._ctx_key = None
+
+    def load_npz(self, path: str) -> None:
+        with np.load(path, allow_pickle=False) as z:
+            self.load_weights({k: z[k] for k in z.files})
+
+    def _resolve_weights(self, output_shape: int, crop=(128, 128)) -> Dict[str, np.ndarray]:
+        table = W.hgru_pose_vars(output_shape=output_shape, timesteps=self.timesteps, crop=crop)
+        given = dict(self.weights or {})
+        out: Dict[str, np.ndarray] = {}
+        for v in table:
+            if v.name in given:
+                out[v.name] = np.asarray(given[v.name], np.float32)
+            else:
+                out[v.name] = W.synth_value(v, self.weight_seed, self.timesteps)
+        # data_dict[name] = [W, b] overrides conv_* / fc_* (get_var, hgru_pose.py:199-200)
+        if self.data_dict is not None:
+            for layer, vals in self.data_dict.items():
+                suff = ("_weights", "_biases") if layer.startswith("fc") else ("_filters", "_biases")
+                for idx in (0, 1):
+                    out[f"cnn/{layer}/{layer}{suff[idx]}"] = np.asarray(vals[idx], np.float32)
+        for k, v in out.items():
+            self.var_dict[(k.split("/")[1], k)] = v
+        return out
+
+    def _context(self, output_shape: int, device: int, crop=(128, 128)) -> _lib.Context:
+        key = (output_shape, device, tuple(crop), id(self.weights), id(self.data_dict))
+        if self._ctx is None or self._ctx_key != key:
+            ctx = _lib.Context(_lib.MP_MODEL_HGRU_POSE, device)
+            for name, val in self._resolve_weights(output_shape, crop).items():
+                ctx.set_weight(name, val)
+            ctx.finalize()
+            self._ctx, self._ctx_key = ctx, key
+        return self._ctx
+
+    # ---------------------------------------------------------------- forward
+    def build(self, depth, output_shape, batch_norm=None, train_mode=None, h2_init=None):
+        """``hgru_pose.model.build`` (hgru_pose.py:47-105), inference only.
+
+        depth     torch CUDA tensor [N, 128, 128, 1] fp32 (crop / 10000, train_cnn_networks_hgru.py:50)
+        h2_init   optional [N, 64, 64, 64] initial hGRU output state; the reference draws it at
+                  random per run (hgru_module.py:879-887), here it defaults to a seeded draw
+        """
+        import torch
+        if train_mode:
+            raise NotImplementedError("train_mode=True (dropout / BN batch statistics / backward) is "
+                                      "outside the inference path")
+        if batch_norm is not None:
+            raise NotImplementedError("conv_layer batchnorm= option is never used by hgru_pose")
+        if not isinstance(depth, torch.Tensor) or not depth.is_cuda:
+            raise TypeError("depth must be a CUDA (ROCm) torch tensor")
+        if depth.dim() != 4 or depth.shape[-1] != 1:
+            raise ValueError(f"depth must be [N, H, W, 1], got {tuple(depth.shape)}")
+        self.output_shape = int(output_shape)
+        self._ctx = self._context(self.output_shape, depth.device.index or 0,
+                                  (int(depth.shape[1]), int(depth.shape[2])))
+        return self.forward(depth, h2_init)
+
+    def forward(self, depth, h2_init=None):
+        import torch
+        if self._ctx is None:
+            raise RuntimeError("call build() first")
+        depth = depth.detach().float().contiguous()
+        n, h, w, _ = depth.shape
+        if h2_init is None:
+            h2_init = torch.from_numpy(W.synth_hidden((n, h // 2, w // 2, 64))).to(depth.device)
+        h2_init = h2_init.detach().float().contiguous()
+        if tuple(h2_init.shape) != (n, h // 2, w // 2, 64):
+            raise ValueError(f"h2_init must be [{n}, {h // 2}, {w // 2}, 64]")
+        out = torch.empty((n, self.output_shape), dtype=torch.float32, device=depth.device)
+        self._ctx.pose_fwd(depth, h2_init, out, _lib.current_stream(depth.device))
+        self.h2_init = h2_init
+        self.out_put = out
+        return out
+
+    # ---------------------------------------------------------------- profiling
+    def profile(self, enable: bool = True) -> None:
+        self._ctx.profile(enable)
+
+    def profile_read(self, name: str):
+        return self._ctx.profile_read(name)

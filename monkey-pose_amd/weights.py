@@ -1,0 +1,205 @@
+"""Variable tables and deterministic synthetic initialisers for the pose regressors.
+
+Every tensor is keyed by the TensorFlow variable name the reference creates, so a
+checkpoint exported from the reference (``{name: ndarray}``) loads unchanged:
+
+* ``cnn/conv_1/conv_1_filters`` ... -- ``hgru_pose.conv_layer`` -> ``get_conv_var``
+  (``hgru_pose.py:139-180``; scope ``cnn`` from ``train_cnn_networks_hgru.py:95``)
+* ``cnn/batch_normalization{,_1.._4}/{gamma,beta,moving_mean,moving_variance}`` --
+  the five ``tf.layers.batch_normalization`` calls (``hgru_pose.py:52-103``)
+* ``cnn/contextual_circuit/{p_r,i_r,i_b,o_r,o_b,beta,nu,gamma,kappa,omega,rho,lateral_bias}``
+  -- ``hgru_module.ContextualCircuit.prepare_tensors`` (``hgru_module.py:262-503``)
+* ``cnn/fc_1/fc_1_weights`` ... -- ``hgru_pose.fc_layer`` / ``get_fc_var`` (156-194)
+
+The reference draws its initial values from TF1 initialisers (truncated normal xavier,
+``hgru_module.py:5`` ``ops.initialization`` which is *not vendored*), so the synthetic
+values here are NOT the reference's random draws -- they are a reproducible stand-in with
+the same shapes and variance class (glorot-uniform), generated from a splitmix64 hash so
+that the numpy oracle and the HIP path see bit-identical weights for a given seed.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass
+from typing import Dict, List, Sequence, Tuple
+
+import numpy as np
+
+# ---------------------------------------------------------------------------
+# splitmix64 counter-based generator (vectorised, chunked)
+# ---------------------------------------------------------------------------
+_GOLDEN = np.uint64(0x9E3779B97F4A7C15)
+_M1 = np.uint64(0xBF58476D1CE4E5B9)
+_M2 = np.uint64(0x94D049BB133111EB)
+
+
+def _fnv1a64(s: str) -> int:
+    h = 0xCBF29CE484222325
+    for b in s.encode():
+        h ^= b
+        h = (h * 0x100000001B3) & 0xFFFFFFFFFFFFFFFF
+    return h
+
+
+def _mix(z: np.ndarray) -> np.ndarray:
+    z = (z ^ (z >> np.uint64(30))) * _M1
+    z = (z ^ (z >> np.uint64(27))) * _M2
+    return z ^ (z >> np.uint64(31))
+
+
+def uniform01(seed: int, name: str, n: int, out: np.ndarray | None = None,
+              chunk: int = 1 << 22) -> np.ndarray:
+    """``n`` doubles in [0,1) from splitmix64(key + i*golden); float64 unless ``out`` given."""
+    key = np.uint64((_fnv1a64(name) ^ (seed * 0x2545F4914F6CDD1D)) & 0xFFFFFFFFFFFFFFFF)
+    if out is None:
+        out = np.empty(n, dtype=np.float64)
+    with np.errstate(over="ignore"):
+        for s in range(0, n, chunk):
+            e = min(n, s + chunk)
+            idx = np.arange(s, e, dtype=np.uint64)
+            z = _mix(idx * _GOLDEN + key)
+            out[s:e] = (z >> np.uint64(11)).astype(np.float64) * (1.0 / (1 << 53))
+    return out
+
+
+def sym_uniform(seed: int, name: str, shape: Sequence[int], limit: float,
+                dtype=np.float32) -> np.ndarray:
+    n = int(np.prod(shape)) if len(shape) else 1
+    u = uniform01(seed, name, n)
+    return ((2.0 * u - 1.0) * limit).astype(dtype).reshape(shape)
+
+
+def glorot_limit(shape: Sequence[int]) -> float:
+    """TF glorot fan rule: conv kernels [kh,kw,in,out] -> fans scaled by the receptive field."""
+    shape = list(shape)
+    if len(shape) == 2:
+        fan_in, fan_out = shape
+    elif len(shape) >= 3:
+        rf = int(np.prod(shape[:-2]))
+        fan_in, fan_out = shape[-2] * rf, shape[-1] * rf
+    else:
+        fan_in = fan_out = shape[0]
+    return math.sqrt(6.0 / (fan_in + fan_out))
+
+
+# ---------------------------------------------------------------------------
+# variable table
+# ---------------------------------------------------------------------------
+@dataclass(frozen=True)
+class Var:
+    name: str
+    shape: Tuple[int, ...]
+    init: str          # see synth_value
+
+
+def _bn(scope: str, n: int) -> List[Var]:
+    return [Var(f"{scope}/gamma", (n,), "bn_gamma"), Var(f"{scope}/beta", (n,), "bn_beta"),
+            Var(f"{scope}/moving_mean", (n,), "bn_mean"),
+            Var(f"{scope}/moving_variance", (n,), "bn_var")]
+
+
+def _conv(scope: str, k: int, cin: int, cout: int) -> List[Var]:
+    return [Var(f"{scope}/{scope.split('/')[-1]}_filters", (k, k, cin, cout), "glorot"),
+            Var(f"{scope}/{scope.split('/')[-1]}_biases", (cout,), "bias")]
+
+
+def _fc(scope: str, nin: int, nout: int) -> List[Var]:
+    return [Var(f"{scope}/{scope.split('/')[-1]}_weights", (nin, nout), "glorot"),
+            Var(f"{scope}/{scope.split('/')[-1]}_biases", (nout,), "bias")]
+
+
+def hgru_circuit_vars(k: int = 64, ssf: int = 15, gate_filter: int = 1, timesteps: int = 8,
+                      scope: str = "cnn/contextual_circuit") -> List[Var]:
+    """``prepare_tensors`` with the hgru_pose aux (``hgru_pose.py:20-39``): association field,
+    gru gates, gamma, multiplicative excitation, adaptation (rho); xi/zeta constant 1."""
+    v = [Var(f"{scope}/p_r", (ssf, ssf, k, k), "glorot"),                    # 298-310
+         Var(f"{scope}/i_r", (gate_filter, gate_filter, k, k), "glorot"),    # 322-332
+         Var(f"{scope}/i_b", (1, 1, 1, k), "chronos"),                       # 344-357
+         Var(f"{scope}/o_r", (gate_filter, gate_filter, k, k), "glorot"),    # 360-370
+         Var(f"{scope}/o_b", (1, 1, 1, k), "neg_chronos")]                   # 382-396
+    for nm in ("beta", "nu", "gamma", "kappa", "omega"):                    # 405-486
+        v.append(Var(f"{scope}/{nm}", (1, 1, 1, k), "glorot"))
+    v.append(Var(f"{scope}/rho", (timesteps,), "ones"))                      # 490-493
+    v.append(Var(f"{scope}/lateral_bias", (1, 1, 1, k), "glorot"))           # 498-503
+    return v
+
+
+def hgru_pose_vars(output_shape: int = 69, timesteps: int = 8, crop=128,
+                   k: int = 64) -> List[Var]:
+    """All variables of ``hgru_pose.model.build`` (``hgru_pose.py:47-105``) in build order.
+    ``crop`` is the input size (int or (h, w)); fc_1's fan-in is (h/2)*(w/2)*64."""
+    ch, cw = (crop, crop) if isinstance(crop, int) else crop
+    v: List[Var] = []
+    v += _conv("cnn/conv_1", 3, 1, k)
+    v += _bn("cnn/batch_normalization", k)
+    v += _conv("cnn/conv_2", 3, k, k)
+    v += _bn("cnn/batch_normalization_1", k)
+    v += _conv("cnn/conv_3", 3, k, k)
+    v += _bn("cnn/batch_normalization_2", k)
+    v += hgru_circuit_vars(k=k, timesteps=timesteps)
+    v += _bn("cnn/batch_normalization_3", k)
+    v += _fc("cnn/fc_1", (ch // 2) * (cw // 2) * k, 1024)
+    v += _bn("cnn/batch_normalization_4", 1024)
+    v += _fc("cnn/fc_out", 1024, output_shape)
+    return v
+
+
+def synth_value(var: Var, seed: int, timesteps: int = 8) -> np.ndarray:
+    """Deterministic stand-in for the reference's TF initialisers (see module docstring)."""
+    s, nm, kind = var.shape, var.name, var.init
+    n = int(np.prod(s))
+    if kind == "glorot":
+        return sym_uniform(seed, nm, s, glorot_limit(s))
+    if kind == "bias":
+        return sym_uniform(seed, nm, s, 1e-2)
+    if kind == "bn_gamma":
+        return (1.0 + sym_uniform(seed, nm, s, 0.1, np.float64)).astype(np.float32)
+    if kind in ("bn_beta", "bn_mean"):
+        return sym_uniform(seed, nm, s, 0.1)
+    if kind == "bn_var":
+        return (1.0 + sym_uniform(seed, nm, s, 0.1, np.float64)).astype(np.float32)
+    if kind in ("chronos", "neg_chronos"):
+        # i_b = -log(U(1, T-1)); o_b = -i_b   (hgru_module.py:344-347, 386)
+        base = nm.rsplit("/", 1)[0] + "/i_b"
+        u = uniform01(seed, base, n).reshape(s)
+        ib = -np.log(1.0 + u * (timesteps - 2))
+        return (ib if kind == "chronos" else -ib).astype(np.float32)
+    if kind == "ones":
+        return np.ones(s, np.float32)
+    raise ValueError(kind)
+
+
+def synth_weights(vars_: Sequence[Var], seed: int = 1234, timesteps: int = 8) -> Dict[str, np.ndarray]:
+    return {v.name: synth_value(v, seed, timesteps) for v in vars_}
+
+
+def synth_hidden(shape: Sequence[int], seed: int = 7, name: str = "h2_init",
+                 limit: float | None = None) -> np.ndarray:
+    """Default hGRU output-state init O0 (``hgru_module.py:879-887``: xavier tensor, re-drawn per
+    run).  The reference's ``ops.initialization`` is missing, so the scale is unpinned; we use
+    glorot-uniform with fan_in = fan_out = k."""
+    k = shape[-1]
+    if limit is None:
+        limit = math.sqrt(6.0 / (2 * k))
+    return sym_uniform(seed, name, shape, limit)
+
+
+def synth_crops(n: int, seed: int = 42, size: int = 128) -> np.ndarray:
+    """Synthetic normalised depth crops [n,size,size,1] float32: background 1.0 (the
+    ``maxDepth`` canvas fill, ``tf_monkeydetector.py:353`` / 10000), a few ellipsoid blobs at
+    depth 0.20-0.30, ~5 % dropout pixels at 0.0."""
+    yy, xx = np.mgrid[0:size, 0:size].astype(np.float64)
+    out = np.ones((n, size, size), np.float64)
+    for i in range(n):
+        u = uniform01(seed, f"crop{i}", 64)
+        nb = 3 + int(u[0] * 4)
+        for b in range(nb):
+            cy, cx = size * (0.2 + 0.6 * u[1 + 6 * b]), size * (0.2 + 0.6 * u[2 + 6 * b])
+            ry, rx = size * (0.05 + 0.2 * u[3 + 6 * b]), size * (0.05 + 0.2 * u[4 + 6 * b])
+            d0 = 0.20 + 0.10 * u[5 + 6 * b]
+            r2 = ((yy - cy) / ry) ** 2 + ((xx - cx) / rx) ** 2
+            m = r2 < 1.0
+            out[i][m] = np.minimum(out[i][m], d0 + 0.02 * r2[m])
+        drop = uniform01(seed, f"drop{i}", size * size).reshape(size, size) < 0.05
+        out[i][drop] = 0.0
+    return out.astype(np.float32)[..., None]

@@ -1,0 +1,46 @@
+"""Shared helpers for the parity tests: case inputs (regenerated from seeds) and error metrics."""
+import importlib
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+if ROOT not in sys.path:
+    sys.path.insert(0, ROOT)
+
+GOLDEN = os.path.join(ROOT, "tests", "golden")
+sys.path.insert(0, GOLDEN)
+import make_golden as MG  # noqa: E402
+
+HGRU_POSE_AUX = {
+    'recurrent_nl': 'tanh', 'rectify_weights': None, 'pre_batchnorm': False, 'gate_filter': 1,
+    'xi': False, 'post_batchnorm': False, 'dense_connections': False, 'symmetric_weights': True,
+    'symmetric_gate_weights': False, 'batch_norm': False, 'atrous_convolutions': False,
+    'output_gru_gates': False, 'association_field': True, 'multiplicative_excitation': True,
+    'gru_gates': True, 'gamma': True, 'adapation': True, 'trainable': True,
+}
+
+# fp32 parity gate of SURVEY.md 8d / BASELINE.md: ||out - ref||_inf / ||ref||_inf <= 1e-4
+FP32_REL_TOL = 1e-4
+
+
+def golden_meta():
+    with open(os.path.join(GOLDEN, "golden.json")) as f:
+        return json.load(f)
+
+
+def golden_array(name, key):
+    with np.load(os.path.join(GOLDEN, f"{name}.npz"), allow_pickle=False) as z:
+        return z[key]
+
+
+def rel_inf(a, ref):
+    a = np.asarray(a, np.float64)
+    ref = np.asarray(ref, np.float64)
+    return float(np.abs(a - ref).max() / max(np.abs(ref).max(), 1e-30))
+
+
+def pkg():
+    return importlib.import_module("monkey-pose_amd")

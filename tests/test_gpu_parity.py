@@ -1,0 +1,106 @@
+"""GPU parity: the HIP path (through the C ABI via the reference-shaped facades) against the CPU
+oracle and the committed golden vectors.  Tolerance: fp32 gate ||out-ref||_inf/||ref||_inf <= 1e-4
+(SURVEY.md 8d); the integer / bit-level properties are exact."""
+import numpy as np
+import pytest
+
+from helpers import FP32_REL_TOL, HGRU_POSE_AUX, MG, golden_array, golden_meta, pkg, rel_inf
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def _cuda(a):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).cuda()
+
+
+@pytest.mark.parametrize("case", [c[0] for c in MG.CIRCUIT_CASES])
+def test_circuit_matches_oracle(case):
+    from oracle import hgru_ref as R
+    mp = pkg()
+    meta = golden_meta()[case]
+    n, h, w, ssf, T = meta["n"], meta["h"], meta["w"], meta["ssf"], meta["timesteps"]
+    wts, X, O0 = MG.circuit_inputs(n, h, w, ssf, T, meta["weight_seed"], meta["x_seed"], meta["o0_seed"])
+    cc = mp.hgru_module.ContextualCircuit(_cuda(X), timesteps=T, SRF=1, SSN=ssf, SSF=ssf,
+                                          aux=HGRU_POSE_AUX)
+    O, weights, acts = cc.build(weights=wts, h2_init=_cuda(O0))
+    O = O.cpu().numpy()
+    ref = golden_array(case, "O")
+    assert rel_inf(O, ref) <= FP32_REL_TOL
+    fresh = R.hgru_forward(X.astype(np.float64), O0, wts, T)
+    assert rel_inf(O, fresh) <= FP32_REL_TOL
+    assert set(weights) >= {"p_r", "i_r", "o_r", "rho", "p_t"}
+
+
+def _pose(case, batch_slice=None):
+    mp = pkg()
+    meta = golden_meta()[case]
+    n, crop, T = meta["n"], meta["crop"], meta["timesteps"]
+    wts, depth, O0 = MG.pose_inputs(n, crop, T, meta["weight_seed"], meta["crop_seed"], meta["o0_seed"])
+    m = mp.hgru_pose.model()
+    m.load_weights(wts)
+    out = m.build(_cuda(depth), meta["output_shape"], train_mode=False, h2_init=_cuda(O0))
+    torch.cuda.synchronize()
+    return m, out.cpu().numpy(), wts, depth, O0
+
+
+@pytest.mark.parametrize("case", [c[0] for c in MG.POSE_CASES])
+def test_pose_matches_golden(case):
+    m, out, *_ = _pose(case)
+    ref = golden_array(case, "out")
+    assert out.shape == ref.shape
+    err = rel_inf(out, ref)
+    assert err <= FP32_REL_TOL, err
+
+
+def test_pose_matches_fresh_oracle_and_metric():
+    from oracle import hgru_ref as R
+    m, out, wts, depth, O0 = _pose("pose_c64_t8")
+    ref = R.hgru_pose_forward(depth, wts, O0, 8, np.float64)
+    assert rel_inf(out, ref) <= FP32_REL_TOL
+    # mean 3D joint error between the two paths in mm (getMeanError_train semantics)
+    e = R.mean_error(R.to_joints_mm(ref), R.to_joints_mm(out))
+    assert e < 0.1
+
+
+def test_batch_invariance_and_determinism():
+    """Each crop's output is bit-identical alone or inside a batch, and run to run."""
+    mp = pkg()
+    W = mp.weights
+    n, crop = 6, 128
+    wts = W.synth_weights(W.hgru_pose_vars(crop=crop), seed=5)
+    depth = W.synth_crops(n, seed=9, size=crop)
+    O0 = W.synth_hidden((n, crop // 2, crop // 2, 64), seed=3)
+    m = mp.hgru_pose.model()
+    m.load_weights(wts)
+    full = m.build(_cuda(depth), 69, h2_init=_cuda(O0)).cpu().numpy()
+    again = m.forward(_cuda(depth), h2_init=_cuda(O0)).cpu().numpy()
+    assert np.array_equal(full, again)
+    for i in (0, 3, 5):
+        one = m.forward(_cuda(depth[i:i + 1]), h2_init=_cuda(O0[i:i + 1])).cpu().numpy()
+        assert np.array_equal(one[0], full[i])
+
+
+def test_rejects_training_and_bad_shapes():
+    mp = pkg()
+    m = mp.hgru_pose.model()
+    x = torch.zeros((1, 128, 128, 1), device="cuda")
+    with pytest.raises(NotImplementedError):
+        m.build(x, 69, train_mode=True)
+    m2 = mp.hgru_pose.model()
+    with pytest.raises(Exception):
+        m2.build(torch.zeros((1, 100, 100, 1), device="cuda"), 69)
+    with pytest.raises(NotImplementedError):
+        mp.hgru_module.ContextualCircuit(torch.zeros((1, 16, 32, 64), device="cuda"), timesteps=2,
+                                         aux={'gru_gates': False})
+
+
+def test_profile_counters():
+    m, out, *_ = _pose("pose_c64_t8")
+    m.profile(True)
+    x = torch.from_numpy(MG.pose_inputs(2, 64, 8, 1234, 42, 7)[1]).cuda()
+    m.forward(x)
+    ms_a, na = m.profile_read("conv15_a")
+    ms_b, nb = m.profile_read("conv15_b")
+    assert na == 8 and nb == 8 and ms_a > 0 and ms_b > 0
