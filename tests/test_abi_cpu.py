@@ -1,0 +1,83 @@
+"""CPU: the C-ABI library loads, exports every function include/monkeypose.h declares, the ctypes
+table matches the header, and the facades reject bad input before touching a GPU.  No compute
+call is made here (there is no GPU in the build container)."""
+import ctypes
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+from helpers import HGRU_POSE_AUX, ROOT, pkg
+
+HEADER = os.path.join(ROOT, "include", "monkeypose.h")
+
+
+def header_functions():
+    txt = open(HEADER).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(mp_[a-z_]+)\s*\(", txt)))
+
+
+def test_header_lists_entry_points():
+    fns = header_functions()
+    for f in ("mp_create", "mp_set_weight", "mp_finalize_weights", "mp_hgru_pose_fwd",
+              "mp_hgru_circuit_fwd", "mp_last_error", "mp_destroy"):
+        assert f in fns
+
+
+def test_library_exports_every_declared_symbol():
+    mp = pkg()
+    path = mp._lib.LIB_PATH
+    assert os.path.exists(path), "build first: python -c 'import __graft_entry__ as g; g.build()'"
+    out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True,
+                         check=True).stdout
+    exported = set(re.findall(r" T (mp_[a-z_]+)", out))
+    missing = set(header_functions()) - exported
+    assert not missing, missing
+
+
+def test_ctypes_table_matches_header():
+    mp = pkg()
+    assert sorted(mp._lib._SIGS) == header_functions()
+
+
+def test_library_loads_and_reports():
+    mp = pkg()
+    lib = mp._lib.load()
+    assert lib.mp_version() == 1
+    assert lib.mp_last_error() == b""
+    assert lib.mp_create(0, 99, ctypes.byref(ctypes.c_void_p())) < 0    # bad model kind
+    assert b"model_kind" in lib.mp_last_error()
+
+
+def test_header_compiles_as_c():
+    src = '#include "monkeypose.h"\nint main(void){ return MP_OK; }\n'
+    p = subprocess.run(["gcc", "-x", "c", "-std=c99", "-Wall", "-Werror", "-fsyntax-only",
+                        "-I", os.path.dirname(HEADER), "-"], input=src, text=True, capture_output=True)
+    assert p.returncode == 0, p.stderr
+
+
+def test_facades_validate_before_gpu():
+    import torch
+    mp = pkg()
+    m = mp.hgru_pose.model()
+    with pytest.raises(NotImplementedError):
+        m.build(torch.zeros((1, 128, 128, 1)), 69, train_mode=True)
+    with pytest.raises(TypeError):
+        m.build(torch.zeros((1, 128, 128, 1)), 69)           # CPU tensor: no CPU fallback
+    with pytest.raises(NotImplementedError):
+        mp.hgru_module.ContextualCircuit(torch.zeros((1, 16, 32, 64)), timesteps=2)   # default aux
+    cc = mp.hgru_module.ContextualCircuit(torch.zeros((1, 16, 32, 64)), timesteps=2, SSF=15,
+                                          aux=HGRU_POSE_AUX)
+    assert cc.SSF_ext == 15 and cc.p_shape == [15, 15, 64, 64]
+    with pytest.raises(TypeError):
+        cc.build()
+
+
+def test_reference_defaults_preserved():
+    mp = pkg()
+    m = mp.hgru_pose.model()
+    assert (m.SRF, m.SSN, m.SSF, m.timesteps, m._BATCH_NORM_EPSILON) == (1, 15, 15, 8, 1e-5)
+    assert m.aux == {k: v for k, v in HGRU_POSE_AUX.items()}
