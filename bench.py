@@ -36,6 +36,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample", type=int, default=8, help="crops timed on the CPU oracle")
     p.add_argument("--no-parity", action="store_true")
+    p.add_argument("--dtype", default="f32_split", choices=["f32", "f32_split"],
+                   help="hGRU eCRF conv precision: exact fp32 MFMA or fp32-accurate f16x3 split")
     return p.parse_args()
 
 
@@ -84,7 +86,7 @@ def main():
     for v, s in zip(table, sizes):
         ctx.set_weight(v.name, flat[o:o + s].view(*v.shape))
         o += s
-    ctx.finalize()
+    ctx.finalize(mp._lib.dtype_code(args.dtype))
     del flat
     ctx.reserve(B)
 
@@ -135,7 +137,7 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32",
+        "dtype": "f32" if args.dtype == "f32" else "f32 (f16x3 split MFMA, fp32 accumulate)",
         "data": "synthetic crops + synthetic weights (splitmix64 stand-ins; reference publishes none)",
         "config": {"workload": f"hgru_pose.model.build fwd, T={T}, {crop}x{crop} crops, "
                                f"batch {B} per GPU", "global_batch": world * B, "crop": crop,

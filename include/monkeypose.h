@@ -54,7 +54,13 @@ enum {
 };
 
 enum { MP_MEM_HOST = 0, MP_MEM_DEVICE = 1 };
-enum { MP_DTYPE_F32 = 0 };
+/* compute precision of the hGRU association-field convolutions (the rest of the path is fp32):
+ *   MP_DTYPE_F32        exact fp32 (v_mfma_f32_32x32x2_f32, an fmaf chain)
+ *   MP_DTYPE_F32_SPLIT  fp32-accurate "f16x3": each fp32 operand split into two power-of-two
+ *                       scaled f16 halves (22 mantissa bits), three f16 MFMAs per product with fp32
+ *                       accumulation; errors within a few fp32 ulps of the F32 path, 5.3x fewer
+ *                       matrix-core cycles.  Needs map height and width multiples of 32. */
+enum { MP_DTYPE_F32 = 0, MP_DTYPE_F32_SPLIT = 1 };
 
 /* library version, (major << 16) | minor */
 int mp_version(void);

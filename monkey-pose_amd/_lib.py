@@ -22,6 +22,15 @@ MP_MODEL_HGRU_CIRCUIT = 2
 MP_MEM_HOST = 0
 MP_MEM_DEVICE = 1
 MP_DTYPE_F32 = 0
+MP_DTYPE_F32_SPLIT = 1
+DTYPES = {'fp32': MP_DTYPE_F32, 'f32': MP_DTYPE_F32, 'fp32_split': MP_DTYPE_F32_SPLIT,
+          'f32_split': MP_DTYPE_F32_SPLIT}
+
+
+def dtype_code(name: str) -> int:
+    if name not in DTYPES:
+        raise ValueError(f"compute dtype must be one of {sorted(DTYPES)}, got {name!r}")
+    return DTYPES[name]
 
 # every function the header declares, with its ctypes signature
 _SIGS = {

@@ -114,6 +114,8 @@ struct mp_ctx {
 
   // ---- finalized weights ----
   int ssf = 15, timesteps = 8, nout = 0, fc1_in = 0, fc1_out = 0;
+  int dtype = MP_DTYPE_F32;
+  float p_unscale = 1.f;   // MP_DTYPE_F32_SPLIT: 1 / (weight scale * activation scale)
   std::vector<float> rho;
   DevBuf conv1_w, conv1_b, bn0_s, bn0_t;
   DevBuf conv2_pk, conv2_b, bn1_s, bn1_t;
@@ -208,7 +210,21 @@ void finalize_circuit(mp_ctx* c, const std::vector<float>* outs, const std::vect
     fail(MP_ERR_WEIGHT, "contextual_circuit/p_r must be [S,S,64,64] with S in {3,5,15}");
   c->ssf = (int)ps[0];
   c->p_pk.alloc((size_t)8 * c->ssf * c->ssf * 2 * 64 * 16);
-  hip_check(launch_pack_conv64(it->second.dev->f(), c->p_pk.v4(), c->ssf, nullptr), "pack p_r");
+  if (c->dtype == MP_DTYPE_F32_SPLIT) {
+    // power-of-two weight scale putting max|p_r| at 2^13..2^14 (f16 max is 65504)
+    std::vector<float> hw(it->second.numel());
+    hip_check(hipMemcpy(hw.data(), it->second.dev->p, hw.size() * sizeof(float), hipMemcpyDeviceToHost),
+              "hipMemcpy p_r");
+    float mx = 0.f;
+    for (float v : hw) mx = std::max(mx, std::fabs(v));
+    int e = 0;
+    if (mx > 0.f) std::frexp(mx, &e);   // mx = f * 2^e, f in [0.5, 1)
+    const float wscale = std::ldexp(1.0f, 14 - e);
+    c->p_unscale = 1.0f / (wscale * 1024.0f);   // activations are scaled by 2^10 in the kernel
+    hip_check(launch_pack_conv64x3(it->second.dev->f(), c->p_pk.p, c->ssf, wscale, nullptr), "pack p_r (f16x3)");
+  } else {
+    hip_check(launch_pack_conv64(it->second.dev->f(), c->p_pk.v4(), c->ssf, nullptr), "pack p_r");
+  }
   c->ir_pk.alloc(1024 * 16);
   c->or_pk.alloc(1024 * 16);
   hip_check(launch_pack_gate(c->need("contextual_circuit/i_r", {1, 1, 64, 64}).dev->f(), c->ir_pk.v4(), nullptr),
@@ -337,7 +353,10 @@ void run_circuit(mp_ctx* c, int64_t n, int H, int W, int T, const float* o0_nhwc
     a.vecs = c->vecs.f();
     {
       ProfScope ps(c, st, "conv15_a");
-      hip_check(launch_conv64(c->ssf, EPI_HGRU_A, a, (int)n, st), "conv15 A");
+      hip_check(c->dtype == MP_DTYPE_F32_SPLIT
+                    ? launch_conv64x3(c->ssf, EPI_HGRU_A, a, c->p_pk.p, c->p_unscale, (int)n, st)
+                    : launch_conv64(c->ssf, EPI_HGRU_A, a, (int)n, st),
+                "conv15 A");
     }
     ConvArgs b{};
     b.H = H;
@@ -355,7 +374,10 @@ void run_circuit(mp_ctx* c, int64_t n, int H, int W, int T, const float* o0_nhwc
     b.dst2 = (t == T - 1) ? final_dst2 : c->Og.f();
     {
       ProfScope ps(c, st, "conv15_b");
-      hip_check(launch_conv64(c->ssf, EPI_HGRU_B, b, (int)n, st), "conv15 B");
+      hip_check(c->dtype == MP_DTYPE_F32_SPLIT
+                    ? launch_conv64x3(c->ssf, EPI_HGRU_B, b, c->p_pk.p, c->p_unscale, (int)n, st)
+                    : launch_conv64(c->ssf, EPI_HGRU_B, b, (int)n, st),
+                "conv15 B");
     }
   }
 }
@@ -443,7 +465,9 @@ int mp_set_weight(mp_ctx* ctx, const char* name, const float* data, const int64_
 int mp_finalize_weights(mp_ctx* ctx, int compute_dtype) {
   return guard([&] {
     if (!ctx) fail(MP_ERR_ARG, "ctx is NULL");
-    if (compute_dtype != MP_DTYPE_F32) fail(MP_ERR_UNSUPPORTED, "only MP_DTYPE_F32 is implemented");
+    if (compute_dtype != MP_DTYPE_F32 && compute_dtype != MP_DTYPE_F32_SPLIT)
+      fail(MP_ERR_UNSUPPORTED, "compute_dtype must be MP_DTYPE_F32 or MP_DTYPE_F32_SPLIT");
+    ctx->dtype = compute_dtype;
     hip_check(hipSetDevice(ctx->device), "hipSetDevice");
     if (ctx->model == MP_MODEL_HGRU_POSE)
       finalize_pose(ctx);
@@ -473,7 +497,9 @@ int mp_hgru_pose_fwd(mp_ctx* ctx, const float* depth, int64_t n, int64_t h, int6
     if (n <= 0 || n > (1 << 20)) fail(MP_ERR_SHAPE, "batch must be in [1, 2^20]");
     if (h % 2 || w % 2) fail(MP_ERR_SHAPE, "crop height/width must be even");
     const int H = (int)(h / 2), W = (int)(w / 2);
-    if (H % TH || W % TW) fail(MP_ERR_SHAPE, "crop/2 must be a multiple of 16 (rows) and 32 (cols)");
+    const int th = ctx->dtype == MP_DTYPE_F32_SPLIT ? TH3 : TH;
+    if (H % th || W % TW)
+      fail(MP_ERR_SHAPE, "crop/2 must be a multiple of " + std::to_string(th) + " (rows) and 32 (cols)");
     if ((int64_t)H * W * 64 != ctx->fc1_in)
       fail(MP_ERR_SHAPE, "crop size does not match fc_1 input (" + std::to_string(ctx->fc1_in) + ")");
     hip_check(hipSetDevice(ctx->device), "hipSetDevice");
@@ -535,7 +561,9 @@ int mp_hgru_circuit_fwd(mp_ctx* ctx, const float* x, const float* o0, int64_t n,
     if (!ctx || !x || !o0 || !o_out) fail(MP_ERR_ARG, "mp_hgru_circuit_fwd: null pointer");
     if (!ctx->finalized) fail(MP_ERR_STATE, "weights not finalized");
     if (k != 64) fail(MP_ERR_SHAPE, "channel count k must be 64");
-    if (n <= 0 || h <= 0 || w <= 0 || h % TH || w % TW) fail(MP_ERR_SHAPE, "need h % 16 == 0 and w % 32 == 0");
+    const int th = ctx->dtype == MP_DTYPE_F32_SPLIT ? TH3 : TH;
+    if (n <= 0 || h <= 0 || w <= 0 || h % th || w % TW)
+      fail(MP_ERR_SHAPE, "need h % " + std::to_string(th) + " == 0 and w % 32 == 0");
     if (timesteps < 1 || timesteps > (int)ctx->rho.size())
       fail(MP_ERR_ARG, "timesteps must be in [1, len(rho)]");
     hip_check(hipSetDevice(ctx->device), "hipSetDevice");

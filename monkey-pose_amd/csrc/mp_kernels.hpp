@@ -38,6 +38,10 @@ hipError_t launch_nhwc_to_c8(const float* in, float* out, int B, int H, int W, h
 hipError_t launch_c8_to_nhwc(const float* in, float* out, int B, int H, int W, hipStream_t st);
 hipError_t launch_pack_conv64(const float* w, f32x4* out, int ks, hipStream_t st);
 hipError_t launch_pack_gate(const float* g, f32x4* out, hipStream_t st);
+// k_conv64x3.hip (fp32-accurate split-f16 MFMA path)
+constexpr int TH3 = 32;
+hipError_t launch_conv64x3(int ks, int epi, ConvArgs a, const void* wpk, float unscale, int B, hipStream_t st);
+hipError_t launch_pack_conv64x3(const float* w, void* out, int ks, float wscale, hipStream_t st);
 // k_fc.hip
 hipError_t launch_pack_fc(const float* W, f32x4* out, int K, int N, hipStream_t st);
 int fc_choose_splits(int M, int K, int N, int* kslice);

@@ -104,9 +104,11 @@ class ContextualCircuit(object):
                            else W.synth_value(v, s, self.timesteps))
         return out
 
-    def build(self, weights: Optional[Dict[str, np.ndarray]] = None, h2_init=None):
+    def build(self, weights: Optional[Dict[str, np.ndarray]] = None, h2_init=None,
+              compute_dtype: str = 'fp32'):
         """Run the circuit; returns ``(O, weights, activities)`` like the reference with
-        ``return_weights=True`` (hgru_module.py:939-954)."""
+        ``return_weights=True`` (hgru_module.py:939-954).  ``compute_dtype``: 'fp32' or
+        'fp32_split' (see include/monkeypose.h)."""
         import torch
         X = self.X
         if not isinstance(X, torch.Tensor) or not X.is_cuda:
@@ -115,7 +117,7 @@ class ContextualCircuit(object):
         ctx = _lib.Context(_lib.MP_MODEL_HGRU_CIRCUIT, X.device.index or 0)
         for name, val in wts.items():
             ctx.set_weight(name, val)
-        ctx.finalize()
+        ctx.finalize(_lib.dtype_code(compute_dtype))
         X = X.detach().float().contiguous()
         if h2_init is None:
             h2_init = torch.from_numpy(W.synth_hidden(tuple(X.shape))).to(X.device)

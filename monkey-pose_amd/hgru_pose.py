@@ -56,6 +56,8 @@ class model:
         }
         self.weights: Optional[Dict[str, np.ndarray]] = None   # TF variable name -> array
         self.weight_seed = 1234
+        # precision of the hGRU eCRF convs: 'fp32' (exact fp32 MFMA) or 'fp32_split' (f16x3)
+        self.compute_dtype = 'fp32'
         self._ctx: Optional[_lib.Context] = None
         self._ctx_key = None
         self.out_put = None
@@ -97,12 +99,13 @@ class model:
         return out
 
     def _context(self, output_shape: int, device: int, crop=(128, 128)) -> _lib.Context:
-        key = (output_shape, device, tuple(crop), id(self.weights), id(self.data_dict))
+        key = (output_shape, device, tuple(crop), id(self.weights), id(self.data_dict),
+               self.compute_dtype)
         if self._ctx is None or self._ctx_key != key:
             ctx = _lib.Context(_lib.MP_MODEL_HGRU_POSE, device)
             for name, val in self._resolve_weights(output_shape, crop).items():
                 ctx.set_weight(name, val)
-            ctx.finalize()
+            ctx.finalize(_lib.dtype_code(self.compute_dtype))
             self._ctx, self._ctx_key = ctx, key
         return self._ctx
 

@@ -15,16 +15,26 @@ def _cuda(a):
     return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).cuda()
 
 
+DTYPES = ["fp32", "fp32_split"]
+
+
+def _split_ok(h, w):
+    return h % 32 == 0 and w % 32 == 0
+
+
+@pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("case", [c[0] for c in MG.CIRCUIT_CASES])
-def test_circuit_matches_oracle(case):
+def test_circuit_matches_oracle(case, dtype):
     from oracle import hgru_ref as R
     mp = pkg()
     meta = golden_meta()[case]
     n, h, w, ssf, T = meta["n"], meta["h"], meta["w"], meta["ssf"], meta["timesteps"]
+    if dtype == "fp32_split" and not _split_ok(h, w):
+        pytest.skip("split path tiles 32x32")
     wts, X, O0 = MG.circuit_inputs(n, h, w, ssf, T, meta["weight_seed"], meta["x_seed"], meta["o0_seed"])
     cc = mp.hgru_module.ContextualCircuit(_cuda(X), timesteps=T, SRF=1, SSN=ssf, SSF=ssf,
                                           aux=HGRU_POSE_AUX)
-    O, weights, acts = cc.build(weights=wts, h2_init=_cuda(O0))
+    O, weights, acts = cc.build(weights=wts, h2_init=_cuda(O0), compute_dtype=dtype)
     O = O.cpu().numpy()
     ref = golden_array(case, "O")
     assert rel_inf(O, ref) <= FP32_REL_TOL
@@ -33,21 +43,23 @@ def test_circuit_matches_oracle(case):
     assert set(weights) >= {"p_r", "i_r", "o_r", "rho", "p_t"}
 
 
-def _pose(case, batch_slice=None):
+def _pose(case, dtype="fp32"):
     mp = pkg()
     meta = golden_meta()[case]
     n, crop, T = meta["n"], meta["crop"], meta["timesteps"]
     wts, depth, O0 = MG.pose_inputs(n, crop, T, meta["weight_seed"], meta["crop_seed"], meta["o0_seed"])
     m = mp.hgru_pose.model()
+    m.compute_dtype = dtype
     m.load_weights(wts)
     out = m.build(_cuda(depth), meta["output_shape"], train_mode=False, h2_init=_cuda(O0))
     torch.cuda.synchronize()
     return m, out.cpu().numpy(), wts, depth, O0
 
 
+@pytest.mark.parametrize("dtype", DTYPES)
 @pytest.mark.parametrize("case", [c[0] for c in MG.POSE_CASES])
-def test_pose_matches_golden(case):
-    m, out, *_ = _pose(case)
+def test_pose_matches_golden(case, dtype):
+    m, out, *_ = _pose(case, dtype)
     ref = golden_array(case, "out")
     assert out.shape == ref.shape
     err = rel_inf(out, ref)
@@ -64,7 +76,8 @@ def test_pose_matches_fresh_oracle_and_metric():
     assert e < 0.1
 
 
-def test_batch_invariance_and_determinism():
+@pytest.mark.parametrize("dtype", DTYPES)
+def test_batch_invariance_and_determinism(dtype):
     """Each crop's output is bit-identical alone or inside a batch, and run to run."""
     mp = pkg()
     W = mp.weights
@@ -73,6 +86,7 @@ def test_batch_invariance_and_determinism():
     depth = W.synth_crops(n, seed=9, size=crop)
     O0 = W.synth_hidden((n, crop // 2, crop // 2, 64), seed=3)
     m = mp.hgru_pose.model()
+    m.compute_dtype = dtype
     m.load_weights(wts)
     full = m.build(_cuda(depth), 69, h2_init=_cuda(O0)).cpu().numpy()
     again = m.forward(_cuda(depth), h2_init=_cuda(O0)).cpu().numpy()
@@ -104,3 +118,13 @@ def test_profile_counters():
     ms_a, na = m.profile_read("conv15_a")
     ms_b, nb = m.profile_read("conv15_b")
     assert na == 8 and nb == 8 and ms_a > 0 and ms_b > 0
+
+
+def test_split_precision_is_fp32_class():
+    """The f16x3 split path stays within a few fp32 ulps of the exact fp32 path."""
+    _, a, *_ = _pose("pose_c128_t8", "fp32")
+    _, b, *_ = _pose("pose_c128_t8", "fp32_split")
+    ref = golden_array("pose_c128_t8", "out")
+    ea, eb = rel_inf(a, ref), rel_inf(b, ref)
+    print(f"rel_inf err: fp32 {ea:.3e}  fp32_split {eb:.3e}  (split vs fp32 {rel_inf(b, a):.3e})")
+    assert eb <= max(10 * ea, 2e-6)
