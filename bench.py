@@ -22,7 +22,28 @@ ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
 PEAK_FP32_TFLOPS = 157.3   # MI355X dense fp32 (MFMA = vector), MI355X_MICROARCH.md chip table
+PEAK_F16_TFLOPS = 2516.6   # MI355X dense f16/bf16 MFMA (no sparsity)
 PEAK_HBM_GBS = 8000.0
+
+
+def roofline(dtype, achieved_tf, launch_ms, launches, flop_per_launch):
+    """Roofline of the dominant kernel (the hGRU eCRF conv, both half-step variants).
+    achieved = ALGORITHMIC conv FLOPs per launch (2*px*15*15*64*64*B) / avg launch time.
+    For the f16x3 split path every fp32 multiply-add costs three f16 MFMA products, so its
+    fp32-accurate ceiling is the dense f16 MFMA peak / 3; the executed f16 rate is also given."""
+    r = {"bound": "mfma", "kernel": "conv64<15> (hGRU eCRF conv, A+B half-steps)",
+         "achieved": round(achieved_tf, 3), "unit": "TFLOP/s", "traffic": None,
+         "avg_launch_ms": round(launch_ms, 4), "launches": launches,
+         "flop_per_launch": flop_per_launch}
+    if dtype == "f32":
+        r.update(peak=PEAK_FP32_TFLOPS, peak_basis="dense fp32 MFMA (v_mfma_f32_32x32x2_f32)")
+    else:
+        r.update(peak=round(PEAK_F16_TFLOPS / 3, 1),
+                 peak_basis="dense f16 MFMA peak 2516.6 / 3 products per fp32-accurate MAC",
+                 executed_f16_tflops=round(3 * achieved_tf, 3),
+                 executed_frac_of_f16_peak=round(3 * achieved_tf / PEAK_F16_TFLOPS, 4))
+    r["frac"] = round(achieved_tf / r["peak"], 4)
+    return r
 
 
 def parse():
@@ -142,11 +163,7 @@ def main():
         "config": {"workload": f"hgru_pose.model.build fwd, T={T}, {crop}x{crop} crops, "
                                f"batch {B} per GPU", "global_batch": world * B, "crop": crop,
                    "timesteps": T, "parallelism": f"dp{world} (batch shards, RCCL weight broadcast)"},
-        "roofline": {"bound": "mfma", "kernel": "conv64<15> (hGRU eCRF conv, A+B half-steps)",
-                     "achieved": round(achieved_tf, 3), "peak": PEAK_FP32_TFLOPS, "unit": "TFLOP/s",
-                     "frac": round(achieved_tf / PEAK_FP32_TFLOPS, 4), "traffic": None,
-                     "avg_launch_ms": round(conv_launch_ms, 4), "launches": na + nb,
-                     "flop_per_launch": conv15_flop},
+        "roofline": roofline(args.dtype, achieved_tf, conv_launch_ms, na + nb, conv15_flop),
         "breakdown_ms_per_step": {"conv15": round((ms_a + ms_b) / args.steps, 3),
                                   "fc1": round(ms_fc / max(1, nfc) if nfc else 0.0, 3),
                                   "backbone": round(ms_bb / max(1, nbb) if nbb else 0.0, 3)},

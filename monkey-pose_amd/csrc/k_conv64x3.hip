@@ -29,13 +29,19 @@ __device__ __forceinline__ f32x16 mfma16(f16x8 a, f16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
 
-template <int KS, int EPI>
-__global__ __launch_bounds__(256, 1) void conv64x3_kernel(ConvArgs p, const f16x8* __restrict__ wpk,
-                                                          float unscale) {
+// NW waves per block (4: one wave per SIMD, 8 M-blocks each; 8: two waves per SIMD, 4 M-blocks
+// each).  SCHED selects the tap-loop schedule: 0 = fragments loaded at the top of each tap and
+// left to the compiler; 1 = one-tap-ahead prefetch with the halo reads of M-block m pinned right
+// after its MFMAs (sched_group_barrier).
+template <int KS, int EPI, int NW, int SCHED>
+__global__ __launch_bounds__(NW * 64, 1) void conv64x3_kernel(ConvArgs p, const f16x8* __restrict__ wpk,
+                                                              float unscale) {
   constexpr int R = KS / 2;
   constexpr int HY = TH3 + KS - 1, HX = TW + KS - 1;
   constexpr int KK = KS * KS;
   constexpr int NQ16 = 4;                // 16-channel chunks
+  constexpr int MB = TH3 / NW;           // M-blocks (rows of 32 pixels) per wave
+  constexpr int NT = NW * 64;
   __shared__ f16x8 halo[HY * 4 * HX];
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, col = lane & 31;
@@ -47,16 +53,16 @@ __global__ __launch_bounds__(256, 1) void conv64x3_kernel(ConvArgs p, const f16x
   const int b = bid / p.tiles_y;
   const int y0 = ty * TH3, x0 = tx * TW;
 
-  f32x16 acc[2][8];
+  f32x16 acc[2][MB];
 #pragma unroll
   for (int n = 0; n < 2; ++n)
 #pragma unroll
-    for (int m = 0; m < 8; ++m) acc[n][m] = f32x16{};
+    for (int m = 0; m < MB; ++m) acc[n][m] = f32x16{};
 
   for (int Q = 0; Q < NQ16; ++Q) {
     __syncthreads();
     // ---- stage + split the 16-channel halo chunk (zero outside the image = SAME padding) ----
-    for (int it = tid; it < HY * HX * 2; it += 256) {
+    for (int it = tid; it < HY * HX * 2; it += NT) {
       const int hh = it & 1;
       const int pix = it >> 1;
       const int hy = pix / HX, hx = pix - hy * HX;
@@ -78,58 +84,81 @@ __global__ __launch_bounds__(256, 1) void conv64x3_kernel(ConvArgs p, const f16x
     }
     __syncthreads();
 
-    // software pipeline, one tap ahead: the next tap's 4 weight fragments (L2) and 16 halo
-    // fragments (LDS) are in flight while this tap's 48 MFMAs issue (1 wave per SIMD here).
-    const f16x8* wt = wpk + (size_t)Q * KK * 4 * 64 + lane;
-    const f16x8* hb = halo + ((wv * 8) * 4 + h) * HX + col;
-    f16x8 w[4], bh[8], bl[8];
+    const f16x8* wq = wpk + (size_t)Q * KK * 4 * 64 + lane;
+    const f16x8* hb = halo + ((wv * MB) * 4 + h) * HX + col;
+    if constexpr (SCHED == 0) {
+      for (int ky = 0; ky < KS; ++ky) {
+        const f16x8* hrow = hb + ky * 4 * HX;
+#pragma unroll 1
+        for (int kx = 0; kx < KS; ++kx) {
+          const f16x8* wt = wq + (ky * KS + kx) * 4 * 64;
+          const f16x8 w0 = wt[0], w1 = wt[64], w2 = wt[128], w3 = wt[192];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) w[i] = wt[i * 64];
-#pragma unroll
-    for (int m = 0; m < 8; ++m) {
-      bh[m] = hb[m * 4 * HX];
-      bl[m] = hb[m * 4 * HX + 2 * HX];
-    }
-    int ky = 0, kx = 0;
-    for (int tap = 0; tap < KK; ++tap) {
-      f16x8 cw[4], ch[8], cl[8];
-#pragma unroll
-      for (int i = 0; i < 4; ++i) cw[i] = w[i];
-#pragma unroll
-      for (int m = 0; m < 8; ++m) {
-        ch[m] = bh[m];
-        cl[m] = bl[m];
-      }
-      if (++kx == KS) {
-        kx = 0;
-        ++ky;
-      }
-      if (tap + 1 < KK) {
-        wt += 4 * 64;
-#pragma unroll
-        for (int i = 0; i < 4; ++i) w[i] = wt[i * 64];
-        const f16x8* hn = hb + ky * 4 * HX + kx;
-#pragma unroll
-        for (int m = 0; m < 8; ++m) {
-          bh[m] = hn[m * 4 * HX];
-          bl[m] = hn[m * 4 * HX + 2 * HX];
+          for (int m = 0; m < MB; ++m) {
+            const f16x8 ch = hrow[m * 4 * HX + kx];
+            const f16x8 cl = hrow[m * 4 * HX + 2 * HX + kx];
+            acc[0][m] = mfma16(w0, cl, acc[0][m]);
+            acc[1][m] = mfma16(w2, cl, acc[1][m]);
+            acc[0][m] = mfma16(w1, ch, acc[0][m]);
+            acc[1][m] = mfma16(w3, ch, acc[1][m]);
+            acc[0][m] = mfma16(w0, ch, acc[0][m]);
+            acc[1][m] = mfma16(w2, ch, acc[1][m]);
+          }
         }
       }
+    } else {
+      // one-tap-ahead prefetch: the weights of tap t+1 are requested at the top of tap t, the
+      // halo fragments of M-block m for tap t+1 right after M-block m's MFMAs of tap t.  The "next
+      // tap" of the last tap wraps to tap 0 so every address stays in bounds.
+      f16x8 w[4], bh[MB], bl[MB];
 #pragma unroll
-      for (int m = 0; m < 8; ++m) {
-        acc[0][m] = mfma16(cw[0], cl[m], acc[0][m]);
-        acc[1][m] = mfma16(cw[2], cl[m], acc[1][m]);
-        acc[0][m] = mfma16(cw[1], ch[m], acc[0][m]);
-        acc[1][m] = mfma16(cw[3], ch[m], acc[1][m]);
-        acc[0][m] = mfma16(cw[0], ch[m], acc[0][m]);
-        acc[1][m] = mfma16(cw[2], ch[m], acc[1][m]);
+      for (int i = 0; i < 4; ++i) w[i] = wq[i * 64];
+#pragma unroll
+      for (int m = 0; m < MB; ++m) {
+        bh[m] = hb[m * 4 * HX];
+        bl[m] = hb[m * 4 * HX + 2 * HX];
+      }
+      int nky = 0, nkx = 0;
+      for (int tap = 0; tap < KK; ++tap) {
+        const int ntap = (tap + 1 < KK) ? tap + 1 : 0;
+        if (++nkx == KS) {
+          nkx = 0;
+          nky = (nky + 1 == KS) ? 0 : nky + 1;
+        }
+        f16x8 cw[4];
+#pragma unroll
+        for (int i = 0; i < 4; ++i) cw[i] = w[i];
+        const f16x8* wn = wq + ntap * 4 * 64;
+#pragma unroll
+        for (int i = 0; i < 4; ++i) w[i] = wn[i * 64];
+        const f16x8* hn = hb + nky * 4 * HX + nkx;
+#pragma unroll
+        for (int m = 0; m < MB; ++m) {
+          const f16x8 ch = bh[m], cl = bl[m];
+          acc[0][m] = mfma16(cw[0], cl, acc[0][m]);
+          acc[1][m] = mfma16(cw[2], cl, acc[1][m]);
+          acc[0][m] = mfma16(cw[1], ch, acc[0][m]);
+          acc[1][m] = mfma16(cw[3], ch, acc[1][m]);
+          acc[0][m] = mfma16(cw[0], ch, acc[0][m]);
+          acc[1][m] = mfma16(cw[2], ch, acc[1][m]);
+          bh[m] = hn[m * 4 * HX];
+          bl[m] = hn[m * 4 * HX + 2 * HX];
+          if (m == 0) __builtin_amdgcn_sched_group_barrier(0x020, 4, 0);   // the 4 weight loads
+          __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);               // 6 MFMA
+          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);               // 2 ds_read
+        }
       }
     }
   }
 
   const int x = x0 + col;
 #pragma unroll
-  for (int m = 0; m < 8; ++m) conv_epilogue<EPI>(p, acc[0][m], acc[1][m], b, y0 + wv * 8 + m, x, h, lane, unscale);
+  for (int m = 0; m < MB; ++m) {
+    // one M-block at a time: keeps the scheduler from hoisting every block's epilogue loads
+    // beside the live accumulators
+    __builtin_amdgcn_sched_barrier(0);
+    conv_epilogue<EPI>(p, acc[0][m], acc[1][m], b, y0 + wv * MB + m, x, h, lane, unscale);
+  }
 }
 
 // HWIO [KS][KS][64][64] fp32 -> [Q][tap][n][hi|lo][lane] f16x8:
@@ -154,19 +183,22 @@ __global__ void pack_conv64x3_kernel(const float* __restrict__ w, f16x8* out, in
   dst[64] = lv;
 }
 
-template <int KS, int EPI>
+template <int KS, int EPI, int NW, int SCHED>
 static hipError_t launch_x3_t(const ConvArgs& a, const void* wpk, float unscale, int B, hipStream_t st) {
   const int nblk = B * a.tiles_x * a.tiles_y;
-  hipLaunchKernelGGL((conv64x3_kernel<KS, EPI>), dim3(nblk), dim3(256), 0, st, a,
+  hipLaunchKernelGGL((conv64x3_kernel<KS, EPI, NW, SCHED>), dim3(nblk), dim3(NW * 64), 0, st, a,
                      static_cast<const f16x8*>(wpk), unscale);
   return hipGetLastError();
 }
+
+// the production variant per kernel size (chosen with tools/bench_conv.hip)
+constexpr int X3_NW = 8, X3_SCHED = 1;
 
 hipError_t launch_conv64x3(int ks, int epi, ConvArgs a, const void* wpk, float unscale, int B, hipStream_t st) {
   a.tiles_x = a.W / TW;
   a.tiles_y = a.H / TH3;
 #define MP_CASE(K, E) \
-  if (ks == K && epi == E) return launch_x3_t<K, E>(a, wpk, unscale, B, st);
+  if (ks == K && epi == E) return launch_x3_t<K, E, X3_NW, X3_SCHED>(a, wpk, unscale, B, st);
   MP_CASE(15, EPI_HGRU_A)
   MP_CASE(15, EPI_HGRU_B)
   MP_CASE(5, EPI_HGRU_A)
