@@ -50,7 +50,9 @@ enum {
 
 enum {
   MP_MODEL_HGRU_POSE = 1,    /* hgru_pose.model                (hgru_pose.py:6-216)        */
-  MP_MODEL_HGRU_CIRCUIT = 2  /* hgru_module.ContextualCircuit  (hgru_module.py:54-959)     */
+  MP_MODEL_HGRU_CIRCUIT = 2, /* hgru_module.ContextualCircuit  (hgru_module.py:54-959)     */
+  MP_MODEL_DENSE = 3,        /* dense_model_struct  (train_dense_networks.py:211-509)      */
+  MP_MODEL_HIER = 4          /* hier_model_struct   (train_hier_networks.py:327-631)       */
 };
 
 enum { MP_MEM_HOST = 0, MP_MEM_DEVICE = 1 };
@@ -97,6 +99,17 @@ int mp_hgru_pose_fwd(mp_ctx* ctx, const float* depth, int64_t n, int64_t h, int6
  *   timesteps <= the length of the "contextual_circuit/rho" weight */
 int mp_hgru_circuit_fwd(mp_ctx* ctx, const float* x, const float* o0, int64_t n, int64_t h,
                         int64_t w, int64_t k, int timesteps, float* o_out, void* stream);
+
+/* dense_model_struct.build(depth, output_shape) -> .output  (train_dense_networks.py:223-408):
+ *   depth [n, h, w, 1] (h, w multiples of 32 in the reference's 128x128), out [n, output_shape] */
+int mp_dense_fwd(mp_ctx* ctx, const float* depth, int64_t n, int64_t h, int64_t w, float* out,
+                 void* stream);
+
+/* hier_model_struct.build(depth, output_shape, P_shape, R_shape, M_shape, I_shape, T_shape)
+ * (train_hier_networks.py:338-530): outs[0] = .output [n, output_shape], outs[1..5] =
+ * .p_output .r_output .m_output .i_output .t_output [n, *_shape] (sizes = the fc_3 widths) */
+int mp_hier_fwd(mp_ctx* ctx, const float* depth, int64_t n, int64_t h, int64_t w, float* const* outs,
+                void* stream);
 
 /* read a model property: "output_shape", "timesteps", "ssf", "finalized", "workspace_bytes",
  * "weight_bytes" */

@@ -5,6 +5,8 @@ The directory name carries a hyphen, so import it with ``importlib.import_module
 
 * ``hgru_pose``   -- drop-in ``model().build(depth, output_shape)`` (reference ``hgru_pose.py``)
 * ``hgru_module`` -- drop-in ``ContextualCircuit(X, ...).build()`` (reference ``hgru_module.py``)
+* ``train_dense_networks.dense_model_struct`` / ``train_hier_networks.hier_model_struct`` --
+  drop-ins for the dense and hierarchical regressor heads
 * ``weights``     -- TF variable-name tables and deterministic synthetic initialisers
 * ``_lib``        -- ctypes binding of ``libmonkeypose.so`` (C ABI: ``include/monkeypose.h``)
 """
@@ -12,5 +14,7 @@ from . import weights  # noqa: F401
 from . import _lib  # noqa: F401
 from . import hgru_pose  # noqa: F401
 from . import hgru_module  # noqa: F401
+from . import train_dense_networks  # noqa: F401
+from . import train_hier_networks  # noqa: F401
 
-__all__ = ["hgru_pose", "hgru_module", "weights", "_lib"]
+__all__ = ["hgru_pose", "hgru_module", "train_dense_networks", "train_hier_networks", "weights", "_lib"]

@@ -19,6 +19,8 @@ LIB_PATH = os.path.join(_HERE, "libmonkeypose.so")
 MP_OK = 0
 MP_MODEL_HGRU_POSE = 1
 MP_MODEL_HGRU_CIRCUIT = 2
+MP_MODEL_DENSE = 3
+MP_MODEL_HIER = 4
 MP_MEM_HOST = 0
 MP_MEM_DEVICE = 1
 MP_DTYPE_F32 = 0
@@ -49,6 +51,10 @@ _SIGS = {
                                            ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
                                            ctypes.c_int64, ctypes.c_int, ctypes.c_void_p,
                                            ctypes.c_void_p]),
+    "mp_dense_fwd": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                                    ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
+    "mp_hier_fwd": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                                   ctypes.c_int64, ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p]),
     "mp_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64)]),
     "mp_profile_enable": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "mp_profile_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p,
@@ -156,6 +162,15 @@ class Context:
         n, h, w, k = x.shape
         check(self.lib.mp_hgru_circuit_fwd(self.h, _ptr(x), _ptr(o0), n, h, w, k, int(timesteps),
                                            _ptr(out), ctypes.c_void_p(stream)))
+
+    def dense_fwd(self, depth, out, stream: int) -> None:
+        n, h, w, c = depth.shape
+        check(self.lib.mp_dense_fwd(self.h, _ptr(depth), n, h, w, _ptr(out), ctypes.c_void_p(stream)))
+
+    def hier_fwd(self, depth, outs, stream: int) -> None:
+        n, h, w, c = depth.shape
+        arr = (ctypes.c_void_p * 6)(*[_ptr(o) for o in outs])
+        check(self.lib.mp_hier_fwd(self.h, _ptr(depth), n, h, w, arr, ctypes.c_void_p(stream)))
 
     def profile(self, enable: bool) -> None:
         check(self.lib.mp_profile_enable(self.h, 1 if enable else 0))

@@ -1,0 +1,174 @@
+// Generic NHWC convolution (any Cin/Cout, KxK, stride, TF SAME padding) as an implicit GEMM on
+// exact-fp32 MFMA, plus 2x2/2 SAME max/avg pooling -- the op vocabulary of the dense and the
+// hierarchical regressors (train_dense_networks.py:414-448, train_hier_networks.py:535-569:
+// conv_layer = relu(conv2d(x, W, stride, 'SAME') + b); max_pool / avg_pool 2x2/2 SAME).
+//
+// Tensors are "views": a base pointer, a row stride `ld` (channels per pixel of the underlying
+// buffer) and a channel offset, so tf.concat along channels is free: producers write their
+// channel range of one wide buffer and consumers read a channel prefix of it.
+//
+// GEMM: D[cout][pixel] = sum_k W[k][cout] * im2col[pixel][k], k = (ky*KS + kx)*Cin + ci, i.e. the
+// HWIO filter read as a [K][Cout] matrix, packed like an FC weight ([k/8][cout/32][lane] float4).
+// Block = 4 waves = 128 output pixels (one 32-pixel M-block per wave) x NB*32 output channels;
+// the im2col tile [128][32 k] is gathered into LDS (+4 float row pad: conflict-free b128 reads).
+#include "mp_kernels.hpp"
+
+namespace mp {
+
+constexpr int IG_BM = 128, IG_BK = 32, IG_LDA = IG_BK + 4;
+
+template <int NB>
+__global__ __launch_bounds__(256) void igemm_conv_kernel(IgemmArgs p) {
+  __shared__ float As[IG_BM * IG_LDA];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, col = lane & 31;
+  const int HWo = p.Ho * p.Wo;
+  const int M = p.N * HWo;
+  const int m0 = blockIdx.x * IG_BM;
+  const int nb0 = blockIdx.y * NB;
+  const int N32 = (p.Cout + 31) / 32;
+  const int K8 = (p.K + 7) / 8;
+  const bool vec = (p.Cin % 4 == 0) && (p.cix % 4 == 0) && (p.ldx % 4 == 0);
+
+  // the 4 staging slots of this thread keep their pixel for the whole K loop
+  int sn[4], sy[4], sx[4];
+  bool sok[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int gm = m0 + (tid >> 3) + 32 * i;
+    sok[i] = gm < M;
+    const int g = sok[i] ? gm : 0;
+    sn[i] = g / HWo;
+    const int r = g - sn[i] * HWo;
+    sy[i] = (r / p.Wo) * p.stride - p.pad_t;
+    sx[i] = (r % p.Wo) * p.stride - p.pad_l;
+  }
+  const int k4 = (tid & 7) * 4;
+
+  f32x16 acc[NB];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) acc[nb] = f32x16{};
+
+  for (int k0 = 0; k0 < p.K; k0 += IG_BK) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      const int kk = k0 + k4;
+      if (sok[i]) {
+        if (vec) {
+          if (kk < p.K) {
+            const int tap = kk / p.Cin, ci = kk - tap * p.Cin;
+            const int iy = sy[i] + tap / p.KS, ix = sx[i] + tap % p.KS;
+            if (iy >= 0 && iy < p.H && ix >= 0 && ix < p.W)
+              v = *reinterpret_cast<const f32x4*>(p.x + (((size_t)sn[i] * p.H + iy) * p.W + ix) * p.ldx + p.cix + ci);
+          }
+        } else {
+#pragma unroll
+          for (int s = 0; s < 4; ++s) {
+            const int k = kk + s;
+            if (k < p.K) {
+              const int tap = k / p.Cin, ci = k - tap * p.Cin;
+              const int iy = sy[i] + tap / p.KS, ix = sx[i] + tap % p.KS;
+              if (iy >= 0 && iy < p.H && ix >= 0 && ix < p.W)
+                v[s] = p.x[(((size_t)sn[i] * p.H + iy) * p.W + ix) * p.ldx + p.cix + ci];
+            }
+          }
+        }
+      }
+      *reinterpret_cast<f32x4*>(As + ((tid >> 3) + 32 * i) * IG_LDA + k4) = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int g = 0; g < IG_BK / 8; ++g) {
+      const int kb = (k0 >> 3) + g;
+      if (kb >= K8) break;
+      const f32x4 a = *reinterpret_cast<const f32x4*>(As + (wv * 32 + col) * IG_LDA + 8 * g + 4 * h);
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        if (nb0 + nb >= N32) break;   // block-uniform
+        const f32x4 wf = p.wpk[((size_t)kb * N32 + nb0 + nb) * 64 + lane];
+#pragma unroll
+        for (int s = 0; s < 4; ++s) acc[nb] = mfma32(wf[s], a[s], acc[nb]);
+      }
+    }
+  }
+
+  const int gm = m0 + wv * 32 + col;
+  if (gm >= M) return;
+  float* dst = p.out + (size_t)gm * p.ldo + p.coff;
+  const bool vst = (p.ldo % 4 == 0) && (p.coff % 4 == 0) && (p.Cout % 4 == 0);
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) {
+    if (nb0 + nb >= N32) break;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int c = (nb0 + nb) * 32 + 8 * g + 4 * h;
+      f32x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        float v = acc[nb][4 * g + j] + (c + j < p.Cout ? p.bias[c + j] : 0.f);
+        o[j] = p.relu ? fmaxf(v, 0.f) : v;
+      }
+      if (vst) {
+        if (c < p.Cout) *reinterpret_cast<f32x4*>(dst + c) = o;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (c + j < p.Cout) dst[c + j] = o[j];
+      }
+    }
+  }
+}
+
+// 2x2 / stride 2, TF SAME (odd sizes pad one row/column after; max ignores it, avg divides by the
+// in-image count).  One thread per output element; C innermost for coalescing.
+__global__ void pool2_kernel(const float* __restrict__ x, int ldx, int cix, int N, int H, int W, int C,
+                             float* out, int ldo, int coff, int mode) {
+  const int Ho = (H + 1) / 2, Wo = (W + 1) / 2;
+  const size_t total = (size_t)N * Ho * Wo * C;
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int c = i % C;
+  const size_t pix = i / C;
+  const int ox = pix % Wo, oy = (pix / Wo) % Ho;
+  const int n = pix / ((size_t)Wo * Ho);
+  float best = -INFINITY, sum = 0.f;
+  int cnt = 0;
+#pragma unroll
+  for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+    for (int dx = 0; dx < 2; ++dx) {
+      const int iy = 2 * oy + dy, ix = 2 * ox + dx;
+      if (iy < H && ix < W) {
+        const float v = x[(((size_t)n * H + iy) * W + ix) * ldx + cix + c];
+        best = fmaxf(best, v);
+        sum += v;
+        ++cnt;
+      }
+    }
+  out[pix * ldo + coff + c] = mode == 0 ? best : sum / (float)cnt;
+}
+
+hipError_t launch_igemm_conv(const IgemmArgs& a, hipStream_t st) {
+  const int M = a.N * a.Ho * a.Wo;
+  const int N32 = (a.Cout + 31) / 32;
+  const int nb = N32 >= 4 ? 4 : (N32 >= 2 ? 2 : 1);
+  dim3 grid((M + IG_BM - 1) / IG_BM, (N32 + nb - 1) / nb);
+  if (nb == 4)
+    hipLaunchKernelGGL(igemm_conv_kernel<4>, grid, dim3(256), 0, st, a);
+  else if (nb == 2)
+    hipLaunchKernelGGL(igemm_conv_kernel<2>, grid, dim3(256), 0, st, a);
+  else
+    hipLaunchKernelGGL(igemm_conv_kernel<1>, grid, dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_pool2(const float* x, int ldx, int cix, int N, int H, int W, int C, float* out, int ldo,
+                        int coff, int mode, hipStream_t st) {
+  const size_t total = (size_t)N * ((H + 1) / 2) * ((W + 1) / 2) * C;
+  hipLaunchKernelGGL(pool2_kernel, dim3((total + 255) / 256), dim3(256), 0, st, x, ldx, cix, N, H, W, C, out,
+                     ldo, coff, mode);
+  return hipGetLastError();
+}
+
+}  // namespace mp

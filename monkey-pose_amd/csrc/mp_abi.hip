@@ -21,150 +21,15 @@
 #include <vector>
 
 #include "../../include/monkeypose.h"
-#include "mp_kernels.hpp"
+#include "mp_runtime.hpp"
 
 
 using namespace mp;
 
-namespace {
-
+namespace mpr {
 thread_local std::string g_err;
-
-struct Fail {
-  int code;
-};
-
-[[noreturn]] void fail(int code, const std::string& msg) {
-  g_err = msg;
-  throw Fail{code};
 }
 
-void hip_check(hipError_t e, const char* what) {
-  if (e != hipSuccess) fail(MP_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
-}
-
-struct DevBuf {
-  void* p = nullptr;
-  size_t bytes = 0;
-  DevBuf() = default;
-  DevBuf(const DevBuf&) = delete;
-  DevBuf& operator=(const DevBuf&) = delete;
-  ~DevBuf() { release(); }
-  void release() {
-    if (p) (void)hipFree(p);
-    p = nullptr;
-    bytes = 0;
-  }
-  void alloc(size_t n) {
-    if (n <= bytes && p) return;
-    release();
-    hip_check(hipMalloc(&p, n ? n : 16), "hipMalloc");
-    bytes = n;
-  }
-  float* f() const { return static_cast<float*>(p); }
-  f32x4* v4() const { return static_cast<f32x4*>(p); }
-};
-
-struct RawWeight {
-  std::vector<int64_t> shape;
-  std::unique_ptr<DevBuf> dev;
-  std::vector<float> host;  // kept for small tensors (host-side BN folding)
-  size_t numel() const {
-    size_t n = 1;
-    for (auto s : shape) n *= (size_t)s;
-    return n;
-  }
-};
-
-struct ProfEvent {
-  std::string name;
-  hipEvent_t a, b;
-};
-
-std::string strip_scope(const char* name) {
-  std::string s(name);
-  if (s.rfind("cnn/", 0) == 0) s = s.substr(4);
-  return s;
-}
-
-bool known_name(int model, const std::string& n) {
-  static const char* circuit[] = {"p_r", "i_r", "i_b", "o_r", "o_b", "beta", "nu", "gamma", "kappa",
-                                  "omega", "rho", "lateral_bias"};
-  for (auto c : circuit)
-    if (n == std::string("contextual_circuit/") + c) return true;
-  if (model == MP_MODEL_HGRU_CIRCUIT) return false;
-  for (const char* l : {"conv_1", "conv_2", "conv_3"})
-    if (n == std::string(l) + "/" + l + "_filters" || n == std::string(l) + "/" + l + "_biases") return true;
-  for (const char* l : {"fc_1", "fc_out"})
-    if (n == std::string(l) + "/" + l + "_weights" || n == std::string(l) + "/" + l + "_biases") return true;
-  for (const char* b : {"batch_normalization", "batch_normalization_1", "batch_normalization_2",
-                        "batch_normalization_3", "batch_normalization_4"})
-    for (const char* v : {"gamma", "beta", "moving_mean", "moving_variance"})
-      if (n == std::string(b) + "/" + v) return true;
-  return false;
-}
-
-}  // namespace
-
-struct mp_ctx {
-  int device = 0;
-  int model = 0;
-  bool finalized = false;
-  std::map<std::string, RawWeight> raw;
-
-  // ---- finalized weights ----
-  int ssf = 15, timesteps = 8, nout = 0, fc1_in = 0, fc1_out = 0;
-  int dtype = MP_DTYPE_F32;
-  float p_unscale = 1.f;   // MP_DTYPE_F32_SPLIT: 1 / (weight scale * activation scale)
-  std::vector<float> rho;
-  DevBuf conv1_w, conv1_b, bn0_s, bn0_t;
-  DevBuf conv2_pk, conv2_b, bn1_s, bn1_t;
-  DevBuf conv3_pk, conv3_b, bn2_s, bn2_t;
-  DevBuf p_pk, ir_pk, or_pk, vecs;
-  DevBuf fc1_pk, fc1_b, bn4_s, bn4_t, fco_pk, fco_b;
-
-  // ---- workspace ----
-  int64_t cap_batch = 0;
-  int64_t cap_hw = 0;
-  DevBuf bufA, bufB, X, O, I, Og, fcin, part, h1;
-
-  // ---- profiling ----
-  bool prof = false;
-  std::vector<ProfEvent> events;
-  std::vector<hipEvent_t> pool;
-
-  ~mp_ctx() {
-    for (auto& e : events) {
-      (void)hipEventDestroy(e.a);
-      (void)hipEventDestroy(e.b);
-    }
-    for (auto e : pool) (void)hipEventDestroy(e);
-  }
-
-  const RawWeight& need(const std::string& n, std::vector<int64_t> shape) {
-    auto it = raw.find(n);
-    if (it == raw.end()) fail(MP_ERR_STATE, "weight not set: " + n);
-    if (!shape.empty() && it->second.shape != shape) {
-      std::string s = "weight " + n + " has shape [";
-      for (auto v : it->second.shape) s += std::to_string(v) + ",";
-      s += "], expected [";
-      for (auto v : shape) s += std::to_string(v) + ",";
-      fail(MP_ERR_WEIGHT, s + "]");
-    }
-    return it->second;
-  }
-
-  hipEvent_t ev() {
-    if (!pool.empty()) {
-      hipEvent_t e = pool.back();
-      pool.pop_back();
-      return e;
-    }
-    hipEvent_t e;
-    hip_check(hipEventCreate(&e), "hipEventCreate");
-    return e;
-  }
-};
 
 namespace {
 
@@ -317,25 +182,6 @@ void ensure_ws(mp_ctx* c, int64_t n, int64_t H, int64_t W) {
   c->cap_hw = hw;
 }
 
-struct ProfScope {
-  mp_ctx* c;
-  hipStream_t st;
-  const char* name;
-  hipEvent_t a = nullptr;
-  ProfScope(mp_ctx* c_, hipStream_t s, const char* n) : c(c_), st(s), name(n) {
-    if (c->prof) {
-      a = c->ev();
-      hip_check(hipEventRecord(a, st), "hipEventRecord");
-    }
-  }
-  ~ProfScope() noexcept(false) {
-    if (a) {
-      hipEvent_t b = c->ev();
-      hip_check(hipEventRecord(b, st), "hipEventRecord");
-      c->events.push_back({name, a, b});
-    }
-  }
-};
 
 void run_circuit(mp_ctx* c, int64_t n, int H, int W, int T, const float* o0_nhwc, float* final_dst2,
                  hipStream_t st) {
@@ -386,23 +232,6 @@ void run_circuit(mp_ctx* c, int64_t n, int H, int W, int T, const float* o0_nhwc
 
 // ================================================ C ABI ============================================
 
-namespace {
-int guard(const std::function<void()>& f) {
-  try {
-    g_err.clear();
-    f();
-    return MP_OK;
-  } catch (const Fail& e) {
-    return e.code;
-  } catch (const std::exception& e) {
-    g_err = std::string("internal error: ") + e.what();
-    return MP_ERR_STATE;
-  } catch (...) {
-    g_err = "internal error";
-    return MP_ERR_STATE;
-  }
-}
-}  // namespace
 
 extern "C" {
 
@@ -413,7 +242,7 @@ const char* mp_last_error(void) { return g_err.c_str(); }
 int mp_create(int device, int model_kind, mp_ctx** out) {
   return guard([&] {
     if (!out) fail(MP_ERR_ARG, "out is NULL");
-    if (model_kind != MP_MODEL_HGRU_POSE && model_kind != MP_MODEL_HGRU_CIRCUIT)
+    if (model_kind < MP_MODEL_HGRU_POSE || model_kind > MP_MODEL_HIER)
       fail(MP_ERR_ARG, "unknown model_kind " + std::to_string(model_kind));
     int ndev = 0;
     hip_check(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
@@ -471,8 +300,10 @@ int mp_finalize_weights(mp_ctx* ctx, int compute_dtype) {
     hip_check(hipSetDevice(ctx->device), "hipSetDevice");
     if (ctx->model == MP_MODEL_HGRU_POSE)
       finalize_pose(ctx);
-    else
+    else if (ctx->model == MP_MODEL_HGRU_CIRCUIT)
       finalize_circuit(ctx, nullptr, nullptr);
+    else
+      finalize_regressor(ctx);
     hip_check(hipDeviceSynchronize(), "finalize sync");
     ctx->finalized = true;
   });
@@ -483,6 +314,7 @@ int mp_reserve(mp_ctx* ctx, int64_t max_batch) {
     if (!ctx || max_batch <= 0) fail(MP_ERR_ARG, "mp_reserve: bad argument");
     if (!ctx->finalized) fail(MP_ERR_STATE, "mp_reserve before mp_finalize_weights");
     hip_check(hipSetDevice(ctx->device), "hipSetDevice");
+    if (ctx->model == MP_MODEL_DENSE || ctx->model == MP_MODEL_HIER) return;   // sized at first call
     const int64_t hw = ctx->model == MP_MODEL_HGRU_POSE ? ctx->fc1_in / 64 : 64 * 64;
     ensure_ws(ctx, max_batch, hw, 1);
   });

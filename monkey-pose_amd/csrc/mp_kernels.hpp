@@ -42,6 +42,22 @@ hipError_t launch_pack_gate(const float* g, f32x4* out, hipStream_t st);
 constexpr int TH3 = 32;
 hipError_t launch_conv64x3(int ks, int epi, ConvArgs a, const void* wpk, float unscale, int B, hipStream_t st);
 hipError_t launch_pack_conv64x3(const float* w, void* out, int ks, float wscale, hipStream_t st);
+// k_igemm.hip (dense / hierarchical regressors)
+struct IgemmArgs {
+  const float* x;      // input view: pixel (n,y,x) channel ci at x[((n*H+y)*W+x)*ldx + cix + ci]
+  int ldx, cix;
+  int N, H, W, Cin;
+  const f32x4* wpk;    // HWIO filter as [K][Cout], packed like an FC weight
+  int K;               // KS*KS*Cin
+  const float* bias;
+  float* out;          // output view: out[(pixel)*ldo + coff + co]
+  int ldo, coff, Cout;
+  int Ho, Wo, KS, stride, pad_t, pad_l;
+  int relu;
+};
+hipError_t launch_igemm_conv(const IgemmArgs& a, hipStream_t st);
+hipError_t launch_pool2(const float* x, int ldx, int cix, int N, int H, int W, int C, float* out, int ldo,
+                        int coff, int mode, hipStream_t st);
 // k_fc.hip
 hipError_t launch_pack_fc(const float* W, f32x4* out, int K, int N, hipStream_t st);
 int fc_choose_splits(int M, int K, int N, int* kslice);

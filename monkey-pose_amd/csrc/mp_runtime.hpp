@@ -1,0 +1,220 @@
+// Internal runtime types shared by the C-ABI translation units (not part of the ABI).
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cmath>
+#include <functional>
+#include <map>
+#include <memory>
+#include <string>
+#include <vector>
+
+#include "../../include/monkeypose.h"
+#include "mp_kernels.hpp"
+
+using namespace mp;
+
+namespace mpr {
+
+extern thread_local std::string g_err;
+
+struct Fail {
+  int code;
+};
+
+[[noreturn]] inline void fail(int code, const std::string& msg) {
+  g_err = msg;
+  throw Fail{code};
+}
+
+inline void hip_check(hipError_t e, const char* what) {
+  if (e != hipSuccess) fail(MP_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+struct DevBuf {
+  void* p = nullptr;
+  size_t bytes = 0;
+  DevBuf() = default;
+  DevBuf(const DevBuf&) = delete;
+  DevBuf& operator=(const DevBuf&) = delete;
+  ~DevBuf() { release(); }
+  void release() {
+    if (p) (void)hipFree(p);
+    p = nullptr;
+    bytes = 0;
+  }
+  void alloc(size_t n) {
+    if (n <= bytes && p) return;
+    release();
+    hip_check(hipMalloc(&p, n ? n : 16), "hipMalloc");
+    bytes = n;
+  }
+  float* f() const { return static_cast<float*>(p); }
+  f32x4* v4() const { return static_cast<f32x4*>(p); }
+};
+
+struct RawWeight {
+  std::vector<int64_t> shape;
+  std::unique_ptr<DevBuf> dev;
+  std::vector<float> host;  // kept for small tensors (host-side BN folding)
+  size_t numel() const {
+    size_t n = 1;
+    for (auto s : shape) n *= (size_t)s;
+    return n;
+  }
+};
+
+struct ProfEvent {
+  std::string name;
+  hipEvent_t a, b;
+};
+
+inline std::string strip_scope(const char* name) {
+  std::string s(name);
+  if (s.rfind("cnn/", 0) == 0) s = s.substr(4);
+  return s;
+}
+
+inline bool known_name_hgru(int model, const std::string& n) {
+  static const char* circuit[] = {"p_r", "i_r", "i_b", "o_r", "o_b", "beta", "nu", "gamma", "kappa",
+                                  "omega", "rho", "lateral_bias"};
+  for (auto c : circuit)
+    if (n == std::string("contextual_circuit/") + c) return true;
+  if (model == MP_MODEL_HGRU_CIRCUIT) return false;
+  for (const char* l : {"conv_1", "conv_2", "conv_3"})
+    if (n == std::string(l) + "/" + l + "_filters" || n == std::string(l) + "/" + l + "_biases") return true;
+  for (const char* l : {"fc_1", "fc_out"})
+    if (n == std::string(l) + "/" + l + "_weights" || n == std::string(l) + "/" + l + "_biases") return true;
+  for (const char* b : {"batch_normalization", "batch_normalization_1", "batch_normalization_2",
+                        "batch_normalization_3", "batch_normalization_4"})
+    for (const char* v : {"gamma", "beta", "moving_mean", "moving_variance"})
+      if (n == std::string(b) + "/" + v) return true;
+  return false;
+}
+
+// dense / hierarchical regressor variable names (mp_regressors.hip)
+bool known_name_regressor(int model, const std::string& n);
+
+inline bool known_name(int model, const std::string& n) {
+  return (model == MP_MODEL_HGRU_POSE || model == MP_MODEL_HGRU_CIRCUIT) ? known_name_hgru(model, n)
+                                                                         : known_name_regressor(model, n);
+}
+
+}  // namespace mpr
+
+using namespace mpr;
+
+struct mp_ctx {
+  int device = 0;
+  int model = 0;
+  bool finalized = false;
+  std::map<std::string, RawWeight> raw;
+
+  // ---- finalized weights ----
+  int ssf = 15, timesteps = 8, nout = 0, fc1_in = 0, fc1_out = 0;
+  int dtype = MP_DTYPE_F32;
+  float p_unscale = 1.f;   // MP_DTYPE_F32_SPLIT: 1 / (weight scale * activation scale)
+  std::vector<float> rho;
+  DevBuf conv1_w, conv1_b, bn0_s, bn0_t;
+  DevBuf conv2_pk, conv2_b, bn1_s, bn1_t;
+  DevBuf conv3_pk, conv3_b, bn2_s, bn2_t;
+  DevBuf p_pk, ir_pk, or_pk, vecs;
+  DevBuf fc1_pk, fc1_b, bn4_s, bn4_t, fco_pk, fco_b;
+
+  // ---- workspace ----
+  int64_t cap_batch = 0;
+  int64_t cap_hw = 0;
+  DevBuf bufA, bufB, X, O, I, Og, fcin, part, h1;
+
+  // ---- dense / hierarchical regressors (mp_regressors.hip) ----
+  struct PackedLayer {
+    DevBuf w, b;          // conv: HWIO as [K][Cout] packed like an FC weight; fc: [in][out] packed
+    int k = 0, cin = 0, cout = 0, K = 0;
+  };
+  std::map<std::string, PackedLayer> layers;   // keyed by layer name ("conv_3_1", "p_fc_2", ...)
+  std::map<std::string, DevBuf> ws;            // named activation buffers
+  int64_t ws_batch = 0, ws_h = 0, ws_w = 0;
+  std::vector<int> head_sizes;                 // outputs: dense {out}; hier {out, P, R, M, I, T}
+
+  // ---- profiling ----
+  bool prof = false;
+  std::vector<ProfEvent> events;
+  std::vector<hipEvent_t> pool;
+
+  ~mp_ctx() {
+    for (auto& e : events) {
+      (void)hipEventDestroy(e.a);
+      (void)hipEventDestroy(e.b);
+    }
+    for (auto e : pool) (void)hipEventDestroy(e);
+  }
+
+  const RawWeight& need(const std::string& n, std::vector<int64_t> shape) {
+    auto it = raw.find(n);
+    if (it == raw.end()) fail(MP_ERR_STATE, "weight not set: " + n);
+    if (!shape.empty() && it->second.shape != shape) {
+      std::string s = "weight " + n + " has shape [";
+      for (auto v : it->second.shape) s += std::to_string(v) + ",";
+      s += "], expected [";
+      for (auto v : shape) s += std::to_string(v) + ",";
+      fail(MP_ERR_WEIGHT, s + "]");
+    }
+    return it->second;
+  }
+
+  hipEvent_t ev() {
+    if (!pool.empty()) {
+      hipEvent_t e = pool.back();
+      pool.pop_back();
+      return e;
+    }
+    hipEvent_t e;
+    hip_check(hipEventCreate(&e), "hipEventCreate");
+    return e;
+  }
+};
+
+namespace mpr {
+
+// run f, converting a Fail / exception into a status code + thread-local message
+inline int guard(const std::function<void()>& f) {
+  try {
+    g_err.clear();
+    f();
+    return MP_OK;
+  } catch (const Fail& e) {
+    return e.code;
+  } catch (const std::exception& e) {
+    g_err = std::string("internal error: ") + e.what();
+    return MP_ERR_STATE;
+  } catch (...) {
+    g_err = "internal error";
+    return MP_ERR_STATE;
+  }
+}
+
+// HIP events around a launch sequence on its stream (mp_profile_*)
+struct ProfScope {
+  mp_ctx* c;
+  hipStream_t st;
+  const char* name;
+  hipEvent_t a = nullptr;
+  ProfScope(mp_ctx* c_, hipStream_t s, const char* n) : c(c_), st(s), name(n) {
+    if (c->prof) {
+      a = c->ev();
+      hip_check(hipEventRecord(a, st), "hipEventRecord");
+    }
+  }
+  ~ProfScope() noexcept(false) {
+    if (a) {
+      hipEvent_t b = c->ev();
+      hip_check(hipEventRecord(b, st), "hipEventRecord");
+      c->events.push_back({name, a, b});
+    }
+  }
+};
+
+// mp_regressors.hip
+void finalize_regressor(mp_ctx* c);
+
+}  // namespace mpr

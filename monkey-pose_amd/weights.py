@@ -144,6 +144,81 @@ def hgru_pose_vars(output_shape: int = 69, timesteps: int = 8, crop=128,
     return v
 
 
+def _conv_b(name: str, k: int, cin: int, cout: int) -> List[Var]:
+    return _conv(f"cnn/{name}", k, cin, cout)
+
+
+# dense_model_struct widths per layer 3..6 (train_dense_networks.py:250-373):
+# (scale-1 1x1, scale-1 3x3, s2-from-s1 1x1, s2 3x3/2, s2 1x1, s2 3x3, s3-from-s2 1x1, s3 3x3/2,
+#  s3 1x1, s3 3x3)
+DENSE_WIDTHS = {3: (24, 32, 32, 48, 32, 48, 48, 64, 48, 64),
+                4: (32, 48, 48, 64, 48, 64, 64, 96, 64, 96),
+                5: (48, 64, 64, 96, 64, 96, 96, 128, 96, 128),
+                6: (64, 96, 96, 128, 96, 128, 128, 144, 128, 144)}
+
+
+def dense_conv_specs():
+    """[(name, k, stride, cin, cout)] of dense_model_struct.build in call order (49 convs)."""
+    s = [("conv_0", 3, 1, 1, 12), ("conv_1_1", 3, 1, 12, 16), ("conv_1_2", 3, 2, 16, 24),
+         ("conv_1_3", 3, 2, 24, 32), ("conv_2_1", 3, 1, 16, 24), ("conv_2_2_1", 3, 2, 16, 24),
+         ("conv_2_2_2", 3, 1, 24, 32), ("conv_2_3_2", 3, 2, 24, 32), ("conv_2_3_3", 3, 1, 32, 48)]
+    w1, w2, w3 = 16 + 24, 24 + 56, 32 + 80          # widths of conv{3}_{1,2,3}_in
+    for L in (3, 4, 5, 6):
+        a, b, c, d, e, f, g, h, i, j = DENSE_WIDTHS[L]
+        s += [(f"conv_{L}_1_1x1", 1, 1, w1, a), (f"conv_{L}_1", 3, 1, a, b),
+              (f"conv_{L}_2_1x1_1", 1, 1, w1, c), (f"conv_{L}_2_1", 3, 2, c, d),
+              (f"conv_{L}_2_1x1_2", 1, 1, w2, e), (f"conv_{L}_2_2", 3, 1, e, f),
+              (f"conv_{L}_3_1x1_2", 1, 1, w2, g), (f"conv_{L}_3_2", 3, 2, g, h),
+              (f"conv_{L}_3_1x1_3", 1, 1, w3, i), (f"conv_{L}_3_3", 3, 1, i, j)]
+        w1, w2, w3 = w1 + b, w2 + d + f, w3 + h + j
+    return s
+
+
+def dense_vars(output_shape: int = 69, crop: int = 128) -> List[Var]:
+    """All variables of ``dense_model_struct.build`` (train_dense_networks.py:223-408)."""
+    v: List[Var] = []
+    for name, k, _, cin, cout in dense_conv_specs():
+        v += _conv_b(name, k, cin, cout)
+    q = crop // 4   # conv6_1 is at crop/2, avg-pooled to crop/4
+    v += _fc("cnn/fc_1_1", q * q * 96, 512)
+    v += _fc("cnn/fc_1_2", (q // 2) * (q // 2) * 256, 512)
+    v += _fc("cnn/fc_1_3", (q // 4) * (q // 4) * 288, 512)
+    v += _fc("cnn/fc_2", 1536, 1024)
+    v += _fc("cnn/fc_3", 1024, 512)
+    v += _fc("cnn/fc_4", 512, output_shape)
+    return v
+
+
+HIER_FINGERS = ("p", "r", "m", "i", "t")
+
+
+def hier_conv_specs():
+    """[(name, k, stride, cin, cout)] of hier_model_struct.build (train_hier_networks.py:341-469)."""
+    s = [("conv_1", 3, 1, 1, 64), ("conv_2", 3, 1, 64, 128)]
+    for br in ("pr", "mi", "t"):
+        s += [(f"{br}_con_3", 3, 1, 128, 256), (f"{br}_con_4", 3, 1, 256, 512)]
+    for f in HIER_FINGERS:
+        s += [(f"{f}_con_5", 3, 1, 512, 512), (f"{f}_con_6", 5, 1, 512, 1024)]
+    return s
+
+
+def hier_vars(output_shape: int = 108, part_shapes=(39, 39, 39, 39, 36), crop: int = 128) -> List[Var]:
+    """All variables of ``hier_model_struct.build``; head sizes as at its call site
+    (train_hier_networks.py:263: num_classes, 13*3, 13*3, 13*3, 13*3, 12*3)."""
+    v: List[Var] = []
+    for name, k, _, cin, cout in hier_conv_specs():
+        v += _conv_b(name, k, cin, cout)
+    q = crop // 64                  # six 2x2 pools
+    flat = q * q * 1024
+    for f, ps in zip(HIER_FINGERS, part_shapes):
+        v += _fc(f"cnn/{f}_fc_1", flat, 1024) + _fc(f"cnn/{f}_fc_2", 1024, 1024)
+        v += _fc(f"cnn/{f}_fc_3", 1024, ps)
+    for f in HIER_FINGERS:
+        v += _fc(f"cnn/{f}h_fc_1", flat, 1024) + _fc(f"cnn/{f}h_fc_2", 1024, 1024)
+    v += _fc("cnn/final_fc_1", 5120, 1024) + _fc("cnn/final_fc_2", 1024, output_shape)
+    return v
+
+
 def synth_value(var: Var, seed: int, timesteps: int = 8) -> np.ndarray:
     """Deterministic stand-in for the reference's TF initialisers (see module docstring)."""
     s, nm, kind = var.shape, var.name, var.init

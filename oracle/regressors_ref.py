@@ -1,0 +1,123 @@
+"""CPU ORACLE (test infrastructure only; see oracle/hgru_ref.py for the import rule and the
+"parity unpinned" statement, which applies here too).
+
+NumPy restatements of the two other pose regressors on the north-star path, call for call:
+
+* ``dense_model_struct.build``  -- /root/reference/train_dense_networks.py:223-408
+  (helpers conv_layer 433-448 = relu(conv2d SAME + b), max_pool/avg_pool 2x2/2 SAME 414-426,
+  fc_layer 450-457)
+* ``hier_model_struct.build``   -- /root/reference/train_hier_networks.py:338-530
+  (helpers 535-579, same semantics)
+
+Inference only (train_mode falsy: no dropout); ``batchnorm=None`` at every call site the
+reference's test paths use, so the conv_layer batch-moment branch is never taken.
+"""
+from __future__ import annotations
+
+from typing import Dict
+
+import numpy as np
+
+from .hgru_ref import avg_pool_same, conv2d_same, fc, max_pool_same
+
+
+def _conv(wts, x, name, stride=1):
+    """conv_layer(bottom, ..., name, filter_size, stride): relu(conv2d(x, W, SAME) + b)."""
+    w = wts[f"cnn/{name}/{name}_filters"].astype(x.dtype)
+    b = wts[f"cnn/{name}/{name}_biases"].astype(x.dtype)
+    return np.maximum(conv2d_same(x, w, stride) + b, 0)
+
+
+def _fc(wts, x, name):
+    return fc(x, wts[f"cnn/{name}/{name}_weights"], wts[f"cnn/{name}/{name}_biases"])
+
+
+def _cat(*xs):
+    return np.concatenate(xs, axis=-1)
+
+
+def dense_forward(depth: np.ndarray, wts: Dict[str, np.ndarray], dtype=np.float64, keep=False):
+    """train_dense_networks.py:223-408, line for line."""
+    x = depth.astype(dtype)
+    t = {}
+    t["conv0"] = _conv(wts, x, "conv_0")                                          # 226
+    t["pool0"] = max_pool_same(t["conv0"])                                        # 227
+    # layer 1 (230-232)
+    t["conv1_1"] = _conv(wts, t["pool0"], "conv_1_1")
+    t["conv1_2"] = _conv(wts, t["conv1_1"], "conv_1_2", 2)
+    t["conv1_3"] = _conv(wts, t["conv1_2"], "conv_1_3", 2)
+    # layer 2 (236-245)
+    t["conv2_1"] = _conv(wts, t["conv1_1"], "conv_2_1")
+    t["conv2_2_1"] = _conv(wts, t["conv1_1"], "conv_2_2_1", 2)
+    t["conv2_2_2"] = _conv(wts, t["conv1_2"], "conv_2_2_2")
+    t["conv2_2"] = _cat(t["conv2_2_1"], t["conv2_2_2"])
+    t["conv2_3_2"] = _conv(wts, t["conv1_2"], "conv_2_3_2", 2)
+    t["conv2_3_3"] = _conv(wts, t["conv1_3"], "conv_2_3_3")
+    t["conv2_3"] = _cat(t["conv2_3_2"], t["conv2_3_3"])
+    # layers 3-6 share one pattern (250-373): per scale s, a 1x1 bottleneck then a 3x3 conv at the
+    # same scale, and a 1x1 + stride-2 3x3 from the finer scale's dense input
+    prev = {1: [t["conv1_1"], t["conv2_1"]], 2: [t["conv1_2"], t["conv2_2"]],
+            3: [t["conv1_3"], t["conv2_3"]]}
+    for L in (3, 4, 5, 6):
+        in1 = _cat(*prev[1])                                   # conv{L}_1_in
+        b1 = _conv(wts, in1, f"conv_{L}_1_1x1")
+        o1 = _conv(wts, b1, f"conv_{L}_1")
+        d21 = _conv(wts, _conv(wts, in1, f"conv_{L}_2_1x1_1"), f"conv_{L}_2_1", 2)
+        in2 = _cat(*prev[2])                                   # conv{L}_2_in
+        d22 = _conv(wts, _conv(wts, in2, f"conv_{L}_2_1x1_2"), f"conv_{L}_2_2")
+        o2 = _cat(d21, d22)
+        d32 = _conv(wts, _conv(wts, in2, f"conv_{L}_3_1x1_2"), f"conv_{L}_3_2", 2)
+        in3 = _cat(*prev[3])                                   # conv{L}_3_in
+        d33 = _conv(wts, _conv(wts, in3, f"conv_{L}_3_1x1_3"), f"conv_{L}_3_3")
+        o3 = _cat(d32, d33)
+        t[f"conv{L}_1"], t[f"conv{L}_2"], t[f"conv{L}_3"] = o1, o2, o3
+        prev[1].append(o1)
+        prev[2].append(o2)
+        prev[3].append(o3)
+    # pooling + fc (376-408)
+    p1 = avg_pool_same(t["conv6_1"])
+    p2 = avg_pool_same(t["conv6_2"])
+    p3 = avg_pool_same(t["conv6_3"])
+    r11 = np.maximum(_fc(wts, p1, "fc_1_1"), 0)
+    r12 = np.maximum(_fc(wts, p2, "fc_1_2"), 0)
+    r13 = np.maximum(_fc(wts, p3, "fc_1_3"), 0)
+    r2 = np.maximum(_fc(wts, _cat(r11, r12, r13), "fc_2"), 0)
+    r3 = np.maximum(_fc(wts, r2, "fc_3"), 0)
+    out = _fc(wts, r3, "fc_4")
+    if keep:
+        t.update(pool1=p1, pool2=p2, pool3=p3, relu2=r2, relu3=r3)
+        return out, t
+    return out
+
+
+FINGERS = ("p", "r", "m", "i", "t")
+
+
+def hier_forward(depth: np.ndarray, wts: Dict[str, np.ndarray], dtype=np.float64):
+    """train_hier_networks.py:338-530.  Returns (output, {p,r,m,i,t}_output)."""
+    x = depth.astype(dtype)
+    c1 = _conv(wts, x, "conv_1")                                       # 341
+    p1 = max_pool_same(c1)
+    c2 = _conv(wts, p1, "conv_2")                                      # 344
+    p2 = max_pool_same(c2)
+    trunk = {}
+    for br in ("pr", "mi"):                                            # 347-352, 395-400
+        a = max_pool_same(_conv(wts, p2, f"{br}_con_3"))
+        trunk[br] = max_pool_same(_conv(wts, a, f"{br}_con_4"))
+    a = max_pool_same(_conv(wts, p2, "t_con_3"))                       # 444-449
+    t4 = max_pool_same(_conv(wts, a, "t_con_4"))
+    src5 = {"p": trunk["pr"], "r": trunk["pr"], "m": trunk["mi"], "i": trunk["mi"], "t": t4}
+    pool6, outs = {}, {}
+    for f in FINGERS:                                                  # 354-469
+        c5 = max_pool_same(_conv(wts, src5[f], f"{f}_con_5"))
+        pool6[f] = max_pool_same(_conv(wts, c5, f"{f}_con_6"))
+        r1 = np.maximum(_fc(wts, pool6[f], f"{f}_fc_1"), 0)
+        r2 = np.maximum(_fc(wts, r1, f"{f}_fc_2"), 0)
+        outs[f] = _fc(wts, r2, f"{f}_fc_3")
+    hand = []
+    for f in FINGERS:                                                  # 473-523
+        r1 = np.maximum(_fc(wts, pool6[f], f"{f}h_fc_1"), 0)
+        hand.append(np.maximum(_fc(wts, r1, f"{f}h_fc_2"), 0))
+    f1 = np.maximum(_fc(wts, _cat(*hand), "final_fc_1"), 0)            # 525-528 (dropout ignored)
+    out = _fc(wts, f1, "final_fc_2")                                   # 529-530
+    return out, outs

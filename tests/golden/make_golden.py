@@ -50,6 +50,20 @@ def pose_inputs(n, crop, T, ws, cs, os_):
     return wts, depth, O0
 
 
+# (name, kind, n, crop, weight seed, crop seed)
+REGRESSOR_CASES = [
+    ("dense_c128", "dense", 2, 128, 77, 43),
+    ("hier_c128", "hier", 2, 128, 78, 44),
+]
+HIER_HEADS = (108, 39, 39, 39, 39, 36)     # train_hier_networks.py:263 with 36 joints
+
+
+def regressor_inputs(kind, n, crop, ws, cs):
+    table = (W.dense_vars(output_shape=69, crop=crop) if kind == "dense"
+             else W.hier_vars(output_shape=HIER_HEADS[0], part_shapes=HIER_HEADS[1:], crop=crop))
+    return W.synth_weights(table, seed=ws), W.synth_crops(n, seed=cs, size=crop)
+
+
 def checksums(a):
     a = np.asarray(a, np.float64)
     return [float(a.sum()), float((a * a).sum()), float(np.abs(a).max())]
@@ -78,6 +92,20 @@ def main(which=None):
                           hgru_bn_checksum=checksums(inter["hgru_bn"]),
                           fc1_checksum=checksums(inter["fc1"]))
         print(name, out[:, :6])
+    from oracle import regressors_ref as RR
+    for (name, kind, n, crop, ws, cs) in REGRESSOR_CASES:
+        if which and name not in which:
+            continue
+        wts, depth = regressor_inputs(kind, n, crop, ws, cs)
+        if kind == "dense":
+            out = RR.dense_forward(depth, wts)
+            np.savez_compressed(os.path.join(HERE, f"{name}.npz"), out=out)
+        else:
+            out, parts = RR.hier_forward(depth, wts)
+            np.savez_compressed(os.path.join(HERE, f"{name}.npz"), out=out,
+                                **{f"{k}_out": v for k, v in parts.items()})
+        meta[name] = dict(kind=kind, n=n, crop=crop, weight_seed=ws, crop_seed=cs)
+        print(name, out[:, :4])
     path = os.path.join(HERE, "golden.json")
     old = json.load(open(path)) if os.path.exists(path) else {}
     old.update(meta)

@@ -1,0 +1,72 @@
+"""Dense (train_dense_networks.py:223-408) and hierarchical (train_hier_networks.py:338-530)
+regressors: CPU oracle pinned to the golden vectors, GPU path (C ABI) against oracle + golden."""
+import numpy as np
+import pytest
+
+from helpers import FP32_REL_TOL, MG, golden_array, golden_meta, pkg, rel_inf
+from oracle import regressors_ref as RR
+
+
+def _inputs(case):
+    m = golden_meta()[case]
+    return m, MG.regressor_inputs(m["kind"], m["n"], m["crop"], m["weight_seed"], m["crop_seed"])
+
+
+def test_dense_oracle_matches_golden():
+    m, (wts, depth) = _inputs("dense_c128")
+    out, t = RR.dense_forward(depth, wts, keep=True)
+    assert rel_inf(out, golden_array("dense_c128", "out")) < 1e-9
+    # the concat widths the reference builds: pool1/2/3 flatten to 98304/65536/18432
+    assert t["pool1"][0].size == 98304 and t["pool2"][0].size == 65536 and t["pool3"][0].size == 18432
+
+
+def test_hier_oracle_matches_golden():
+    m, (wts, depth) = _inputs("hier_c128")
+    out, parts = RR.hier_forward(depth, wts)
+    assert rel_inf(out, golden_array("hier_c128", "out")) < 1e-9
+    for f in RR.FINGERS:
+        assert rel_inf(parts[f], golden_array("hier_c128", f"{f}_out")) < 1e-9
+
+
+def test_dense_conv_table_is_consistent():
+    W = pkg().weights
+    specs = W.dense_conv_specs()
+    assert len(specs) == 49
+    assert sum(1 for s in specs if s[1] == 3) == 29 and sum(1 for s in specs if s[1] == 1) == 20
+
+
+@pytest.mark.gpu
+def test_dense_gpu_matches_golden_and_oracle():
+    torch = pytest.importorskip("torch")
+    m, (wts, depth) = _inputs("dense_c128")
+    model = pkg().train_dense_networks.dense_model_struct()
+    model.load_weights(wts)
+    out = model.build(torch.from_numpy(depth).cuda(), 69, train_mode=False).cpu().numpy()
+    assert rel_inf(out, golden_array("dense_c128", "out")) <= FP32_REL_TOL
+    again = model.forward(torch.from_numpy(depth).cuda()).cpu().numpy()
+    assert np.array_equal(out, again)
+    one = model.forward(torch.from_numpy(depth[1:2]).cuda()).cpu().numpy()
+    assert np.array_equal(one[0], out[1])
+
+
+@pytest.mark.gpu
+def test_hier_gpu_matches_golden_and_oracle():
+    torch = pytest.importorskip("torch")
+    m, (wts, depth) = _inputs("hier_c128")
+    model = pkg().train_hier_networks.hier_model_struct()
+    model.load_weights(wts)
+    out = model.build(torch.from_numpy(depth).cuda(), *MG.HIER_HEADS, train_mode=False).cpu().numpy()
+    assert rel_inf(out, golden_array("hier_c128", "out")) <= FP32_REL_TOL
+    for f in RR.FINGERS:
+        got = getattr(model, f"{f}_output").cpu().numpy()
+        assert rel_inf(got, golden_array("hier_c128", f"{f}_out")) <= FP32_REL_TOL
+
+
+@pytest.mark.gpu
+def test_regressors_reject_training():
+    torch = pytest.importorskip("torch")
+    x = torch.zeros((1, 128, 128, 1), device="cuda")
+    with pytest.raises(NotImplementedError):
+        pkg().train_dense_networks.dense_model_struct().build(x, 69, train_mode=True)
+    with pytest.raises(NotImplementedError):
+        pkg().train_hier_networks.hier_model_struct().build(x, 108, 39, 39, 39, 39, 36, batch_norm=["conv_1"])
