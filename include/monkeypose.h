@@ -111,6 +111,42 @@ int mp_dense_fwd(mp_ctx* ctx, const float* depth, int64_t n, int64_t h, int64_t 
 int mp_hier_fwd(mp_ctx* ctx, const float* depth, int64_t n, int64_t h, int64_t w, float* const* outs,
                 void* stream);
 
+/* ---- host-side 3D CoM crop (no GPU; the pre-step of every regressor) -------------------------
+ * MonkeyDetector(fx, fy, ux, uy, cube, d1, d2) (monkeydetector.py:31-63, tf_monkeydetector.py),
+ * constructed in the reference as (365.456, 365.456, 256, 212, [800,800,1200], 200, 10000)
+ * (train_cnn_networks_hgru.py:77). */
+typedef struct {
+  double fx, fy, ux, uy; /* focal lengths, principal point (pixels) */
+  double cube[3];        /* crop volume (x, y, z) in mm */
+  double min_depth;      /* d1: near plane, mm */
+  double max_depth;      /* d2: far plane, mm (also the canvas fill of the crop) */
+} mp_camera;
+
+/* depth frame element type: float32 mm (the hGRU caller: image * 10000, train_cnn_networks_hgru.py:47)
+ * or uint16 mm (Kinect PNG, sample_pipeline.py:21); numpy semantics differ and are kept: the CoM
+ * depth sum is float32-pairwise vs exact, the near-plane clamp rounds vs truncates */
+enum { MP_DEPTH_F32 = 0, MP_DEPTH_U16 = 1 };
+
+/* MonkeyDetector.calculateCoM (monkeydetector.py:66-83): com = (mean col, mean row, sum(d)/count)
+ * over pixels with min_depth <= d <= max_depth of a float32 [h][w] frame in mm; (0,0,0) if none */
+int mp_center_of_mass(const mp_camera* cam, const void* depth, int depth_dtype, int64_t h, int64_t w,
+                      double com[3]);
+
+/* MonkeyDetector.cropArea3D(dpt, com, dsize=(dsize, dsize)) (monkeydetector.py:261-334):
+ *   com     (u, v, d) in pixels / mm, or NULL to use mp_center_of_mass
+ *   out     [dsize][dsize] float32 crop in mm, canvas filled with max_depth
+ *   M       3x3 row-major crop transform (off * scale * trans), com_out: the CoM used
+ *   info    optional {xstart, xend, ystart, yend, sz_w, sz_h, off_x, off_y} (integers of the crop) */
+int mp_crop3d(const mp_camera* cam, const void* depth, int depth_dtype, int64_t h, int64_t w, const double* com,
+              int64_t dsize, float* out, double M[9], double com_out[3], int32_t info[8]);
+
+/* prepare_data_test (train_cnn_networks_hgru.py:61-74) for n frames [n][h][w]: patches
+ * [n][dsize][dsize][1] = crop / max_depth (the model input), Ms [n][9], coms_out [n][3];
+ * coms [n][3] or NULL; frames are processed by up to nthreads host threads */
+int mp_crop3d_batch(const mp_camera* cam, const void* frames, int depth_dtype, int64_t n, int64_t h, int64_t w,
+                    const double* coms, int64_t dsize, float* patches, double* Ms, double* coms_out,
+                    int nthreads);
+
 /* read a model property: "output_shape", "timesteps", "ssf", "finalized", "workspace_bytes",
  * "weight_bytes" */
 int mp_info(mp_ctx* ctx, const char* key, int64_t* value);
