@@ -17,7 +17,7 @@ HEADER = os.path.join(ROOT, "include", "monkeypose.h")
 def header_functions():
     txt = open(HEADER).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    return sorted(set(re.findall(r"\b(mp_[a-z_]+)\s*\(", txt)))
+    return sorted(set(re.findall(r"\b(mp_[a-z0-9_]+)\s*\(", txt)))
 
 
 def test_header_lists_entry_points():
@@ -33,7 +33,7 @@ def test_library_exports_every_declared_symbol():
     assert os.path.exists(path), "build first: python -c 'import __graft_entry__ as g; g.build()'"
     out = subprocess.run(["nm", "-D", "--defined-only", path], capture_output=True, text=True,
                          check=True).stdout
-    exported = set(re.findall(r" T (mp_[a-z_]+)", out))
+    exported = set(re.findall(r" T (mp_[a-z0-9_]+)", out))
     missing = set(header_functions()) - exported
     assert not missing, missing
 
