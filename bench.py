@@ -1,13 +1,16 @@
 """Benchmark: depth-crops/s of the hGRU-8T pose forward (hgru_pose.model.build, 128x128 crops,
 batch 256 per GPU), one process per GPU, weak scaling (batch shards, no data-path collective).
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--no-cpu-baseline]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--dtype f32|f32_split]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
 A step = one forward of the whole hot path (conv_1 ... hGRU x8 ... fc_out) over B synthetic crops
 already resident in HBM.  Weights: synthetic (splitmix64 glorot stand-ins), generated on rank 0
 and broadcast ONCE over RCCL (xGMI) as one flat fp32 blob before timing.  Rank 0 prints one JSON
-line; value = all ranks' crops / max-over-ranks elapsed.
+line; value = all ranks' crops / max-over-ranks elapsed.  At N=1 the line also carries the parity
+of the measured path vs the float64 oracle, the CPU baseline, and "extras" (the other BASELINE
+configs: hierarchical regressor at batch 256, dense regressor, batch-1 end-to-end latency with the
+host CoM crop).
 """
 import argparse
 import importlib
@@ -23,7 +26,23 @@ sys.path.insert(0, ROOT)
 
 PEAK_FP32_TFLOPS = 157.3   # MI355X dense fp32 (MFMA = vector), MI355X_MICROARCH.md chip table
 PEAK_F16_TFLOPS = 2516.6   # MI355X dense f16/bf16 MFMA (no sparsity)
-PEAK_HBM_GBS = 8000.0
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=10)
+    p.add_argument("--warmup", type=int, default=2)
+    p.add_argument("--batch", type=int, default=256, help="crops per GPU")
+    p.add_argument("--crop", type=int, default=128)
+    p.add_argument("--timesteps", type=int, default=8)
+    p.add_argument("--dtype", default="f32_split", choices=["f32", "f32_split"],
+                   help="hGRU eCRF conv precision: exact fp32 MFMA or fp32-accurate f16x3 split")
+    p.add_argument("--no-cpu-baseline", action="store_true")
+    p.add_argument("--cpu-sample", type=int, default=8, help="crops timed on the CPU oracle")
+    p.add_argument("--no-parity", action="store_true")
+    p.add_argument("--no-extras", action="store_true")
+    return p.parse_args()
 
 
 def roofline(dtype, achieved_tf, launch_ms, launches, flop_per_launch):
@@ -46,20 +65,78 @@ def roofline(dtype, achieved_tf, launch_ms, launches, flop_per_launch):
     return r
 
 
-def parse():
-    p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
-    p.add_argument("--steps", type=int, default=10)
-    p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--batch", type=int, default=256, help="crops per GPU")
-    p.add_argument("--crop", type=int, default=128)
-    p.add_argument("--timesteps", type=int, default=8)
-    p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-sample", type=int, default=8, help="crops timed on the CPU oracle")
-    p.add_argument("--no-parity", action="store_true")
-    p.add_argument("--dtype", default="f32_split", choices=["f32", "f32_split"],
-                   help="hGRU eCRF conv precision: exact fp32 MFMA or fp32-accurate f16x3 split")
-    return p.parse_args()
+def time_gpu(fn, steps, warmup):
+    import torch
+    for _ in range(warmup):
+        fn()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        fn()
+    torch.cuda.synchronize()
+    return (time.perf_counter() - t0) / steps
+
+
+def extras(mp, dev, args):
+    """The other BASELINE.json configs, measured on this GPU (not the headline)."""
+    import torch
+    W = mp.weights
+    out = {}
+    B = args.batch
+    depth = torch.from_numpy(W.synth_crops(B, seed=99, size=128)).to(dev)
+    stream = mp._lib.current_stream(dev)
+    try:   # config 3: hierarchical cascade, batch 256
+        ctx = mp._lib.Context(mp._lib.MP_MODEL_HIER, dev.index)
+        for v in W.hier_vars():
+            ctx.set_weight(v.name, W.synth_value(v, 5))
+        ctx.finalize()
+        heads = [torch.empty((B, s), device=dev) for s in (108, 39, 39, 39, 39, 36)]
+        t = time_gpu(lambda: ctx.hier_fwd(depth, heads, stream), 5, 1)
+        out["hier_b256"] = {"crops_per_s": round(B / t, 2), "ms_per_batch": round(t * 1e3, 3),
+                            "gflop_per_crop": 7.97, "tflops": round(7.97e9 * B / t / 1e12, 2)}
+        ctx.close()
+    except Exception as e:  # noqa: BLE001
+        out["hier_b256"] = {"error": repr(e)}
+    try:   # config 1 plumbing model, measured on the GPU at batch 256
+        ctx = mp._lib.Context(mp._lib.MP_MODEL_DENSE, dev.index)
+        for v in W.dense_vars():
+            ctx.set_weight(v.name, W.synth_value(v, 6))
+        ctx.finalize()
+        o = torch.empty((B, 69), device=dev)
+        t = time_gpu(lambda: ctx.dense_fwd(depth, o, stream), 5, 1)
+        out["dense_b256"] = {"crops_per_s": round(B / t, 2), "ms_per_batch": round(t * 1e3, 3),
+                             "gflop_per_crop": 3.22, "tflops": round(3.22e9 * B / t / 1e12, 2)}
+        ctx.close()
+    except Exception as e:  # noqa: BLE001
+        out["dense_b256"] = {"error": repr(e)}
+    return out
+
+
+def e2e_latency(mp, ctx, dev, T, frames=40):
+    """Config 5: one 424x512 float32 depth frame per call -> native host CoM crop -> H2D -> hGRU pose
+    forward at batch 1 -> D2H -> absolute joints; p50 / p99 wall latency."""
+    import torch
+    sys.path.insert(0, ROOT)
+    from oracle.crop_ref import synth_frame   # synthetic frames only (the measured path is native)
+    md = mp.monkeydetector.MonkeyDetector(365.456, 365.456, 256, 212, [800, 800, 1200], 200, 10000)
+    W = mp.weights
+    o0 = torch.from_numpy(W.synth_hidden((1, 64, 64, 64), seed=3)).to(dev)
+    out = torch.empty((1, 69), device=dev)
+    stream = mp._lib.current_stream(dev)
+    fr = [synth_frame(i) for i in range(8)]
+    lat = []
+    for i in range(frames):
+        t0 = time.perf_counter()
+        patch, M, com = md.crop_batch(fr[i % 8][None], None, nthreads=1)
+        x = torch.from_numpy(patch).to(dev, non_blocking=False)
+        ctx.pose_fwd(x, o0, out, stream)
+        rel = out.cpu().numpy().reshape(23, 3) * 600.0
+        md.getAbsoluteCoordinates(rel, com[0])
+        lat.append(time.perf_counter() - t0)
+    lat = np.array(lat[5:]) * 1e3
+    return {"p50_ms": round(float(np.percentile(lat, 50)), 3), "p99_ms": round(float(np.percentile(lat, 99)), 3),
+            "frames": len(lat), "fps_capacity": round(1000.0 / float(np.percentile(lat, 50)), 1),
+            "path": "native host crop (mp_crop3d_batch) + H2D + hgru_pose fwd B=1 + D2H"}
 
 
 def main():
@@ -78,40 +155,20 @@ def main():
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
     mp = importlib.import_module("monkey-pose_amd")
-    W = mp.weights
+    W, par = mp.weights, mp.parallel
     B, crop, T = args.batch, args.crop, args.timesteps
 
-    # ---- weights: generate on rank 0, one RCCL broadcast of the flat blob ----
+    # ---- weights: generated on rank 0, ONE RCCL broadcast of the flat blob, packed per rank ----
     table = W.hgru_pose_vars(output_shape=69, timesteps=T, crop=crop)
-    sizes = [int(np.prod(v.shape)) for v in table]
-    total = int(sum(sizes))
-    flat = torch.empty(total, dtype=torch.float32, device=dev)
-    if rank == 0:
-        host = np.empty(total, np.float32)
-        o = 0
-        for v, s in zip(table, sizes):
-            host[o:o + s] = W.synth_value(v, 1234, T).reshape(-1)
-            o += s
-        flat.copy_(torch.from_numpy(host))
-        del host
-    bcast_ms = 0.0
-    if world > 1:
-        torch.cuda.synchronize()
-        dist.barrier()
-        t0 = time.perf_counter()
-        dist.broadcast(flat, src=0)
-        torch.cuda.synchronize()
-        bcast_ms = (time.perf_counter() - t0) * 1e3
+    wts = {v.name: W.synth_value(v, 1234, T) for v in table} if rank == 0 else None
+    flat, layout, bcast_s = par.broadcast_weights(table, wts, dev, rank, world)
     ctx = mp._lib.Context(mp._lib.MP_MODEL_HGRU_POSE, dev.index)
-    o = 0
-    for v, s in zip(table, sizes):
-        ctx.set_weight(v.name, flat[o:o + s].view(*v.shape))
-        o += s
+    par.load_context(ctx, flat, layout)
     ctx.finalize(mp._lib.dtype_code(args.dtype))
     del flat
     ctx.reserve(B)
 
-    # ---- synthetic inputs resident in HBM (per-rank shard) ----
+    # ---- synthetic inputs resident in HBM (this rank's shard of the global batch) ----
     depth = torch.from_numpy(W.synth_crops(B, seed=42 + rank, size=crop)).to(dev)
     o0 = torch.from_numpy(W.synth_hidden((B, crop // 2, crop // 2, 64), seed=7 + rank)).to(dev)
     out = torch.empty((B, 69), dtype=torch.float32, device=dev)
@@ -148,7 +205,7 @@ def main():
 
     value = world * B * args.steps / elapsed
     rec = {
-        "metric": "depth-crops/sec hGRU-8T fwd @batch256 per GPU (128x128 crops, fp32)",
+        "metric": "depth-crops/sec hGRU-8T fwd @batch256 per GPU (128x128 crops)",
         "value": round(value, 3),
         "unit": "crops/s",
         "n_gpus": world,
@@ -165,38 +222,43 @@ def main():
                    "timesteps": T, "parallelism": f"dp{world} (batch shards, RCCL weight broadcast)"},
         "roofline": roofline(args.dtype, achieved_tf, conv_launch_ms, na + nb, conv15_flop),
         "breakdown_ms_per_step": {"conv15": round((ms_a + ms_b) / args.steps, 3),
-                                  "fc1": round(ms_fc / max(1, nfc) if nfc else 0.0, 3),
-                                  "backbone": round(ms_bb / max(1, nbb) if nbb else 0.0, 3)},
-        "weight_bcast_ms": round(bcast_ms, 3),
+                                  "fc1": round(ms_fc / max(1, nfc), 3),
+                                  "backbone": round(ms_bb / max(1, nbb), 3)},
+        "weight_bcast_ms": round(bcast_s * 1e3, 3),
     }
 
     if rank == 0 and world == 1:
         from oracle import hgru_ref as R
         if not args.no_parity:
             # parity of the measured path on its first 2 crops vs the float64 oracle
-            wts = {v.name: W.synth_value(v, 1234, T) for v in table}
             d2 = depth[:2].cpu().numpy()
             o2 = o0[:2].cpu().numpy()
             ref = R.hgru_pose_forward(d2, wts, o2, T, np.float64)
             got = out[:2].cpu().numpy()
             rec["parity"] = {"rel_inf_err": float(np.abs(got - ref).max() / np.abs(ref).max()),
                              "mean_joint_err_mm": R.mean_error(R.to_joints_mm(ref), R.to_joints_mm(got)),
-                             "crops": 2, "oracle": "oracle/hgru_ref.py float64"}
+                             "crops": 2, "oracle": "oracle/hgru_ref.py float64", "gate": 1e-4}
         if not args.no_cpu_baseline:
             from threadpoolctl import threadpool_info
-            wts32 = {v.name: W.synth_value(v, 1234, T) for v in table}
             nc = args.cpu_sample
             d = depth[:nc].cpu().numpy()
             oo = o0[:nc].cpu().numpy()
             t0 = time.perf_counter()
             for i in range(0, nc, 4):
-                R.hgru_pose_forward(d[i:i + 4], wts32, oo[i:i + 4], T, np.float32)
+                R.hgru_pose_forward(d[i:i + 4], wts, oo[i:i + 4], T, np.float32)
             cpu_s = time.perf_counter() - t0
             threads = max([t["num_threads"] for t in threadpool_info() if t["user_api"] == "blas"] or [1])
             rec["cpu_baseline"] = {"value": round(nc / cpu_s, 4), "unit": "crops/s", "cores": threads,
                                    "kind": "port",
                                    "sample": f"{nc} crops of the same workload (numpy fp32 oracle, "
                                              f"OpenBLAS, batches of 4), {cpu_s:.1f} s"}
+        if not args.no_extras:
+            try:
+                rec["extras"] = {"e2e_batch1_latency": e2e_latency(mp, ctx, dev, T)}
+            except Exception as e:  # noqa: BLE001
+                rec["extras"] = {"e2e_batch1_latency": {"error": repr(e)}}
+            ctx.close()
+            rec["extras"].update(extras(mp, dev, args))
     if rank == 0:
         print(json.dumps(rec), flush=True)
     if world > 1:

@@ -17,5 +17,6 @@ from . import hgru_module  # noqa: F401
 from . import train_dense_networks  # noqa: F401
 from . import train_hier_networks  # noqa: F401
 from . import monkeydetector  # noqa: F401
+from . import parallel  # noqa: F401
 
 __all__ = ["hgru_pose", "hgru_module", "train_dense_networks", "train_hier_networks", "weights", "_lib"]
