@@ -39,7 +39,7 @@ def parse():
     p.add_argument("--dtype", default="f32_split", choices=["f32", "f32_split"],
                    help="hGRU eCRF conv precision: exact fp32 MFMA or fp32-accurate f16x3 split")
     p.add_argument("--no-cpu-baseline", action="store_true")
-    p.add_argument("--cpu-sample", type=int, default=8, help="crops timed on the CPU oracle")
+    p.add_argument("--cpu-sample", type=int, default=16, help="crops timed on the CPU oracle")
     p.add_argument("--no-parity", action="store_true")
     p.add_argument("--no-extras", action="store_true")
     return p.parse_args()
