@@ -26,6 +26,7 @@ sys.path.insert(0, ROOT)
 
 PEAK_FP32_TFLOPS = 157.3   # MI355X dense fp32 (MFMA = vector), MI355X_MICROARCH.md chip table
 PEAK_F16_TFLOPS = 2516.6   # MI355X dense f16/bf16 MFMA (no sparsity)
+PEAK_HBM_GBPS = 8000.0     # MI355X HBM3E
 
 
 def parse():
@@ -36,8 +37,9 @@ def parse():
     p.add_argument("--batch", type=int, default=256, help="crops per GPU")
     p.add_argument("--crop", type=int, default=128)
     p.add_argument("--timesteps", type=int, default=8)
-    p.add_argument("--dtype", default="f32_split", choices=["f32", "f32_split"],
-                   help="hGRU eCRF conv precision: exact fp32 MFMA or fp32-accurate f16x3 split")
+    p.add_argument("--dtype", default="f32_fft", choices=["f32", "f32_split", "f32_fft"],
+                   help="hGRU eCRF conv path: exact fp32 MFMA direct, fp32-accurate f16x3 split "
+                        "direct, or fp32 FFT convolution")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--cpu-sample", type=int, default=16, help="crops timed on the CPU oracle")
     p.add_argument("--no-parity", action="store_true")
@@ -62,6 +64,51 @@ def roofline(dtype, achieved_tf, launch_ms, launches, flop_per_launch):
                  executed_f16_tflops=round(3 * achieved_tf, 3),
                  executed_frac_of_f16_peak=round(3 * achieved_tf / PEAK_F16_TFLOPS, 4))
     r["frac"] = round(achieved_tf / r["peak"], 4)
+    return r
+
+
+def fft_kernels(ctx, B, hw, steps):
+    """Per-kernel time / algorithmic traffic of the FFT conv path (k_fft.hip), per launch."""
+    NF, act = 72 * 37, B * 64 * hw * 4                 # frequencies; one fp32 C8 activation map
+    spec = B * 16 * NF * 32                            # one spectrum buffer [b][cq][f][4] complex64
+    algo = {   # name: (bytes, flops) per launch
+        "fft_fwd": (act + spec, 0.0),
+        "spec_gemm": (2 * spec + NF * 64 * 1024, 8.0 * B * NF * 64 * 64),
+        "fft_inv": (spec + act, 0.0),
+        "epi_a": (4 * act, 0.0),                       # P, X, O in; I out
+        "epi_b": (6 * act, 0.0),                       # P, I, O in; O', Og' out (+ rereads of O)
+    }
+    out = {}
+    for name, (byt, flop) in algo.items():
+        ms, n = ctx.profile_read(name)
+        if n == 0:
+            continue
+        t = ms / n * 1e-3
+        hbm = byt / t / 1e9
+        k = {"ms_per_step": round(ms / steps, 3), "avg_launch_ms": round(ms / n, 4), "launches": n,
+             "algo_bytes": byt, "achieved_GBps": round(hbm, 1), "hbm_frac": round(hbm / PEAK_HBM_GBPS, 4)}
+        if flop:
+            k.update(algo_flop=flop, achieved_tflops=round(flop / t / 1e12, 2),
+                     mfma_frac=round(flop / t / 1e12 / PEAK_FP32_TFLOPS, 4))
+        out[name] = k
+    return out
+
+
+def fft_roofline(kern):
+    """Roofline of the dominant FFT-path kernel: its binding roof (HBM bytes or fp32 MFMA FLOPs,
+    whichever bounds it tighter at peak) against its measured average launch time."""
+    name = max(kern, key=lambda k: kern[k]["ms_per_step"])
+    k = kern[name]
+    r = {"kernel": name + " (k_fft.hip)", "avg_launch_ms": k["avg_launch_ms"], "launches": k["launches"],
+         "traffic": None}
+    t_hbm = k["algo_bytes"] / (PEAK_HBM_GBPS * 1e9)
+    t_mfma = k.get("algo_flop", 0.0) / (PEAK_FP32_TFLOPS * 1e12)
+    if t_mfma > t_hbm:
+        r.update(bound="mfma", achieved=k["achieved_tflops"], peak=PEAK_FP32_TFLOPS, unit="TFLOP/s",
+                 peak_basis="dense fp32 MFMA (v_mfma_f32_32x32x2_f32)", frac=k["mfma_frac"])
+    else:
+        r.update(bound="hbm", achieved=k["achieved_GBps"], peak=PEAK_HBM_GBPS, unit="GB/s",
+                 peak_basis="HBM3E 8 TB/s", frac=k["hbm_frac"])
     return r
 
 
@@ -203,6 +250,7 @@ def main():
     conv15_flop = 2.0 * px * 15 * 15 * 64 * 64 * B            # algorithmic, per launch
     achieved_tf = conv15_flop / (conv_launch_ms * 1e-3) / 1e12
 
+    kern = fft_kernels(ctx, B, px, args.steps) if args.dtype == "f32_fft" else None
     value = world * B * args.steps / elapsed
     rec = {
         "metric": "depth-crops/sec hGRU-8T fwd @batch256 per GPU (128x128 crops)",
@@ -215,17 +263,22 @@ def main():
         "higher_is_better": True,
         "scaling": "weak",
         "vs_baseline": None,
-        "dtype": "f32" if args.dtype == "f32" else "f32 (f16x3 split MFMA, fp32 accumulate)",
+        "dtype": {"f32": "f32", "f32_split": "f32 (f16x3 split MFMA, fp32 accumulate)",
+                  "f32_fft": "f32 (fp32 FFT convolution, fp32 MFMA spectral GEMM)"}[args.dtype],
         "data": "synthetic crops + synthetic weights (splitmix64 stand-ins; reference publishes none)",
         "config": {"workload": f"hgru_pose.model.build fwd, T={T}, {crop}x{crop} crops, "
                                f"batch {B} per GPU", "global_batch": world * B, "crop": crop,
                    "timesteps": T, "parallelism": f"dp{world} (batch shards, RCCL weight broadcast)"},
-        "roofline": roofline(args.dtype, achieved_tf, conv_launch_ms, na + nb, conv15_flop),
+        "roofline": (fft_roofline(kern) if args.dtype == "f32_fft" else
+                     roofline(args.dtype, achieved_tf, conv_launch_ms, na + nb, conv15_flop)),
         "breakdown_ms_per_step": {"conv15": round((ms_a + ms_b) / args.steps, 3),
                                   "fc1": round(ms_fc / max(1, nfc), 3),
                                   "backbone": round(ms_bb / max(1, nbb), 3)},
         "weight_bcast_ms": round(bcast_s * 1e3, 3),
     }
+    if kern:
+        rec["fft_kernels"] = kern
+        rec["eCRF_conv_equiv_tflops"] = round(achieved_tf, 2)   # direct-conv FLOPs / FFT-conv time
 
     if rank == 0 and world == 1:
         from oracle import hgru_ref as R

@@ -25,8 +25,9 @@ MP_MEM_HOST = 0
 MP_MEM_DEVICE = 1
 MP_DTYPE_F32 = 0
 MP_DTYPE_F32_SPLIT = 1
+MP_DTYPE_F32_FFT = 2
 DTYPES = {'fp32': MP_DTYPE_F32, 'f32': MP_DTYPE_F32, 'fp32_split': MP_DTYPE_F32_SPLIT,
-          'f32_split': MP_DTYPE_F32_SPLIT}
+          'f32_split': MP_DTYPE_F32_SPLIT, 'fp32_fft': MP_DTYPE_F32_FFT, 'f32_fft': MP_DTYPE_F32_FFT}
 
 
 def dtype_code(name: str) -> int:

@@ -87,6 +87,9 @@ void finalize_circuit(mp_ctx* c, const std::vector<float>* outs, const std::vect
     const float wscale = std::ldexp(1.0f, 14 - e);
     c->p_unscale = 1.0f / (wscale * 1024.0f);   // activations are scaled by 2^10 in the kernel
     hip_check(launch_pack_conv64x3(it->second.dev->f(), c->p_pk.p, c->ssf, wscale, nullptr), "pack p_r (f16x3)");
+  } else if (c->dtype == MP_DTYPE_F32_FFT) {
+    c->spec_g.alloc(fft_weight_bytes());
+    hip_check(launch_spec_weights(it->second.dev->f(), c->spec_g.f(), c->ssf, nullptr), "p_r spectrum");
   } else {
     hip_check(launch_pack_conv64(it->second.dev->f(), c->p_pk.v4(), c->ssf, nullptr), "pack p_r");
   }
@@ -165,6 +168,11 @@ void ensure_ws(mp_ctx* c, int64_t n, int64_t H, int64_t W) {
   c->O.alloc(st);
   c->I.alloc(st);
   c->Og.alloc(st);
+  if (c->dtype == MP_DTYPE_F32_FFT) {
+    c->specS.alloc(fft_spec_bytes((int)nb));
+    c->specY.alloc(fft_spec_bytes((int)nb));
+    c->specP.alloc(st);
+  }
   if (c->model == MP_MODEL_HGRU_POSE) {
     c->bufA.alloc(st);
     c->bufB.alloc(st);
@@ -183,6 +191,43 @@ void ensure_ws(mp_ctx* c, int64_t n, int64_t H, int64_t W) {
 }
 
 
+// one association-field conv p_r * a.src with its fused hGRU epilogue, in the context's precision
+void eCRF_conv(mp_ctx* c, int epi, const ConvArgs& a, int n, hipStream_t st) {
+  if (c->dtype == MP_DTYPE_F32_FFT) {
+    {
+      ProfScope ps(c, st, "fft_fwd");
+      hip_check(launch_fft_fwd(a.src, c->specS.p, n, a.H, a.W, st), "fft_fwd");
+    }
+    {
+      ProfScope ps(c, st, "spec_gemm");
+      hip_check(launch_spec_gemm(c->specS.p, c->spec_g.f(), c->specY.p, n, st), "spec_gemm");
+    }
+    {
+      ProfScope ps(c, st, "fft_inv");
+      hip_check(launch_fft_inv(c->specY.p, c->specP.f(), n, a.H, a.W, st), "fft_inv");
+    }
+    ProfScope ps(c, st, epi == EPI_HGRU_A ? "epi_a" : "epi_b");
+    hip_check(launch_spec_epi(epi, a, c->specP.f(), n, st), "spectral epilogue");
+  } else if (c->dtype == MP_DTYPE_F32_SPLIT) {
+    hip_check(launch_conv64x3(c->ssf, epi, a, c->p_pk.p, c->p_unscale, n, st), "conv15 (f16x3)");
+  } else {
+    hip_check(launch_conv64(c->ssf, epi, a, n, st), "conv15");
+  }
+}
+
+// map-size rule of the context's association-field conv path (MP_ERR_SHAPE otherwise)
+void check_map(mp_ctx* c, int64_t H, int64_t W, const char* what) {
+  if (c->dtype == MP_DTYPE_F32_FFT) {
+    if (H < 1 || H > FFT_MAX_HW || (W != 32 && W != 64))
+      fail(MP_ERR_SHAPE, std::string(what) + ": the FFT path needs map height in [1, 64] and width 32 or 64");
+    return;
+  }
+  const int th = c->dtype == MP_DTYPE_F32_SPLIT ? TH3 : TH;
+  if (H % th || W % TW)
+    fail(MP_ERR_SHAPE, std::string(what) + ": map height must be a multiple of " + std::to_string(th) +
+                           " and width a multiple of 32");
+}
+
 void run_circuit(mp_ctx* c, int64_t n, int H, int W, int T, const float* o0_nhwc, float* final_dst2,
                  hipStream_t st) {
   hip_check(launch_gate_init(o0_nhwc, c->O.f(), c->Og.f(), c->ir_pk.v4(), c->vecs.f(), (int)n, H, W, st),
@@ -199,10 +244,7 @@ void run_circuit(mp_ctx* c, int64_t n, int H, int W, int T, const float* o0_nhwc
     a.vecs = c->vecs.f();
     {
       ProfScope ps(c, st, "conv15_a");
-      hip_check(c->dtype == MP_DTYPE_F32_SPLIT
-                    ? launch_conv64x3(c->ssf, EPI_HGRU_A, a, c->p_pk.p, c->p_unscale, (int)n, st)
-                    : launch_conv64(c->ssf, EPI_HGRU_A, a, (int)n, st),
-                "conv15 A");
+      eCRF_conv(c, EPI_HGRU_A, a, (int)n, st);
     }
     ConvArgs b{};
     b.H = H;
@@ -220,10 +262,7 @@ void run_circuit(mp_ctx* c, int64_t n, int H, int W, int T, const float* o0_nhwc
     b.dst2 = (t == T - 1) ? final_dst2 : c->Og.f();
     {
       ProfScope ps(c, st, "conv15_b");
-      hip_check(c->dtype == MP_DTYPE_F32_SPLIT
-                    ? launch_conv64x3(c->ssf, EPI_HGRU_B, b, c->p_pk.p, c->p_unscale, (int)n, st)
-                    : launch_conv64(c->ssf, EPI_HGRU_B, b, (int)n, st),
-                "conv15 B");
+      eCRF_conv(c, EPI_HGRU_B, b, (int)n, st);
     }
   }
 }
@@ -294,8 +333,12 @@ int mp_set_weight(mp_ctx* ctx, const char* name, const float* data, const int64_
 int mp_finalize_weights(mp_ctx* ctx, int compute_dtype) {
   return guard([&] {
     if (!ctx) fail(MP_ERR_ARG, "ctx is NULL");
-    if (compute_dtype != MP_DTYPE_F32 && compute_dtype != MP_DTYPE_F32_SPLIT)
-      fail(MP_ERR_UNSUPPORTED, "compute_dtype must be MP_DTYPE_F32 or MP_DTYPE_F32_SPLIT");
+    if (compute_dtype != MP_DTYPE_F32 && compute_dtype != MP_DTYPE_F32_SPLIT && compute_dtype != MP_DTYPE_F32_FFT)
+      fail(MP_ERR_UNSUPPORTED, "compute_dtype must be MP_DTYPE_F32, MP_DTYPE_F32_SPLIT or MP_DTYPE_F32_FFT");
+    if (compute_dtype != ctx->dtype) {   // workspace layout depends on the path
+      ctx->cap_batch = 0;
+      ctx->cap_hw = 0;
+    }
     ctx->dtype = compute_dtype;
     hip_check(hipSetDevice(ctx->device), "hipSetDevice");
     if (ctx->model == MP_MODEL_HGRU_POSE)
@@ -329,9 +372,9 @@ int mp_hgru_pose_fwd(mp_ctx* ctx, const float* depth, int64_t n, int64_t h, int6
     if (n <= 0 || n > (1 << 20)) fail(MP_ERR_SHAPE, "batch must be in [1, 2^20]");
     if (h % 2 || w % 2) fail(MP_ERR_SHAPE, "crop height/width must be even");
     const int H = (int)(h / 2), W = (int)(w / 2);
-    const int th = ctx->dtype == MP_DTYPE_F32_SPLIT ? TH3 : TH;
-    if (H % th || W % TW)
-      fail(MP_ERR_SHAPE, "crop/2 must be a multiple of " + std::to_string(th) + " (rows) and 32 (cols)");
+    if (H % TH || W % TW)
+      fail(MP_ERR_SHAPE, "crop/2 must be a multiple of 16 (rows) and 32 (cols)");   // backbone tiles
+    check_map(ctx, H, W, "crop/2");
     if ((int64_t)H * W * 64 != ctx->fc1_in)
       fail(MP_ERR_SHAPE, "crop size does not match fc_1 input (" + std::to_string(ctx->fc1_in) + ")");
     hip_check(hipSetDevice(ctx->device), "hipSetDevice");
@@ -393,9 +436,8 @@ int mp_hgru_circuit_fwd(mp_ctx* ctx, const float* x, const float* o0, int64_t n,
     if (!ctx || !x || !o0 || !o_out) fail(MP_ERR_ARG, "mp_hgru_circuit_fwd: null pointer");
     if (!ctx->finalized) fail(MP_ERR_STATE, "weights not finalized");
     if (k != 64) fail(MP_ERR_SHAPE, "channel count k must be 64");
-    const int th = ctx->dtype == MP_DTYPE_F32_SPLIT ? TH3 : TH;
-    if (n <= 0 || h <= 0 || w <= 0 || h % th || w % TW)
-      fail(MP_ERR_SHAPE, "need h % " + std::to_string(th) + " == 0 and w % 32 == 0");
+    if (n <= 0 || h <= 0 || w <= 0) fail(MP_ERR_SHAPE, "empty input");
+    check_map(ctx, h, w, "x");
     if (timesteps < 1 || timesteps > (int)ctx->rho.size())
       fail(MP_ERR_ARG, "timesteps must be in [1, len(rho)]");
     hip_check(hipSetDevice(ctx->device), "hipSetDevice");

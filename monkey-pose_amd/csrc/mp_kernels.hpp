@@ -42,6 +42,15 @@ hipError_t launch_pack_gate(const float* g, f32x4* out, hipStream_t st);
 constexpr int TH3 = 32;
 hipError_t launch_conv64x3(int ks, int epi, ConvArgs a, const void* wpk, float unscale, int B, hipStream_t st);
 hipError_t launch_pack_conv64x3(const float* w, void* out, int ks, float wscale, hipStream_t st);
+// k_fft.hip (FFT path of the association-field conv, MP_DTYPE_F32_FFT; maps up to 64x64)
+constexpr int FFT_MAX_HW = 64;
+size_t fft_spec_bytes(int B);      // one spectrum buffer (S or Y) for B images
+size_t fft_weight_bytes();         // expanded spectral weights
+hipError_t launch_spec_weights(const float* w, float* Gx, int ks, hipStream_t st);
+hipError_t launch_fft_fwd(const float* act, void* S, int B, int H, int W, hipStream_t st);
+hipError_t launch_spec_gemm(const void* S, const float* Gx, void* Y, int B, hipStream_t st);
+hipError_t launch_fft_inv(const void* Y, float* P, int B, int H, int W, hipStream_t st);
+hipError_t launch_spec_epi(int epi, const ConvArgs& a, const float* P, int B, hipStream_t st);
 // k_igemm.hip (dense / hierarchical regressors)
 struct IgemmArgs {
   const float* x;      // input view: pixel (n,y,x) channel ci at x[((n*H+y)*W+x)*ldx + cix + ci]

@@ -119,12 +119,14 @@ struct mp_ctx {
   DevBuf conv2_pk, conv2_b, bn1_s, bn1_t;
   DevBuf conv3_pk, conv3_b, bn2_s, bn2_t;
   DevBuf p_pk, ir_pk, or_pk, vecs;
+  DevBuf spec_g;            // MP_DTYPE_F32_FFT: expanded spectral weights of p_r (k_fft.hip)
   DevBuf fc1_pk, fc1_b, bn4_s, bn4_t, fco_pk, fco_b;
 
   // ---- workspace ----
   int64_t cap_batch = 0;
   int64_t cap_hw = 0;
   DevBuf bufA, bufB, X, O, I, Og, fcin, part, h1;
+  DevBuf specS, specY, specP;   // MP_DTYPE_F32_FFT: input / output spectra, spatial conv result
 
   // ---- dense / hierarchical regressors (mp_regressors.hip) ----
   struct PackedLayer {

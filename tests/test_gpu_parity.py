@@ -15,7 +15,7 @@ def _cuda(a):
     return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).cuda()
 
 
-DTYPES = ["fp32", "fp32_split"]
+DTYPES = ["fp32", "fp32_split", "fp32_fft"]
 
 
 def _split_ok(h, w):
@@ -128,3 +128,14 @@ def test_split_precision_is_fp32_class():
     ea, eb = rel_inf(a, ref), rel_inf(b, ref)
     print(f"rel_inf err: fp32 {ea:.3e}  fp32_split {eb:.3e}  (split vs fp32 {rel_inf(b, a):.3e})")
     assert eb <= max(10 * ea, 2e-6)
+
+
+def test_fft_precision_is_fp32_class():
+    """The FFT path (fp32 72-point FFTs + fp32 spectral GEMM) stays fp32-class: its error against
+    the float64 golden output is within a small multiple of the exact fp32 direct path's."""
+    _, a, *_ = _pose("pose_c128_t8", "fp32")
+    _, b, *_ = _pose("pose_c128_t8", "fp32_fft")
+    ref = golden_array("pose_c128_t8", "out")
+    ea, eb = rel_inf(a, ref), rel_inf(b, ref)
+    print(f"rel_inf err: fp32 {ea:.3e}  fp32_fft {eb:.3e}  (fft vs fp32 {rel_inf(b, a):.3e})")
+    assert eb <= max(10 * ea, 1e-5)
