@@ -72,11 +72,11 @@ def fft_kernels(ctx, B, hw, steps):
     NF, act = 72 * 37, B * 64 * hw * 4                 # frequencies; one fp32 C8 activation map
     spec = B * 16 * NF * 32                            # one spectrum buffer [b][cq][f][4] complex64
     algo = {   # name: (bytes, flops) per launch
-        "fft_fwd": (act + spec, 0.0),
-        "spec_gemm": (2 * spec + NF * 64 * 1024, 8.0 * B * NF * 64 * 64),
-        "fft_inv": (spec + act, 0.0),
-        "epi_a": (4 * act, 0.0),                       # P, X, O in; I out
-        "epi_b": (6 * act, 0.0),                       # P, I, O in; O', Og' out (+ rereads of O)
+        "fft_fwd": (act + spec, 0.0),                  # Og in; S out
+        "spec_gemm": (2 * spec + NF * 32 * 1024, 8.0 * B * NF * 64 * 64),   # S in, Y out, weights
+        "inv_a_fwd": (2 * spec + 3 * act, 0.0),        # Y, X, O in; I, S out
+        "fft_inv": (spec + act, 0.0),                  # Y in; P out
+        "epi_b": (5 * act, 0.0),                       # P, I, O in; O', Og' out
     }
     out = {}
     for name, (byt, flop) in algo.items():

@@ -13,21 +13,41 @@
 //
 // G[f][ci][co] = (1/N^2) sum_{ky,kx} w[ky][kx][ci][co] exp(-2 pi i (fy (R-ky) + fx (R-kx)) / N)
 // (cross-correlation written as a convolution with the flipped kernel, inverse-DFT scale folded in)
-// is computed once per weight set in double precision.  Every stage is fp32 (FFT butterflies with
-// fp32 twiddles rounded once from double; the spectral GEMM on v_mfma_f32_32x32x2_f32), so the
-// path is fp32-class: error ~1e-6 of max|output| against the float64 oracle.
+// is computed once per weight set in double precision.  The FFTs are fp32 (twiddles rounded once
+// from double); the spectral GEMM is fp32-accurate "f16x3" (each operand split into power-of-two
+// scaled f16 hi + lo, three f16 MFMA products, fp32 accumulation, as k_conv64x3.hip), so the path
+// is fp32-class: error ~1e-6 of max|output| against the float64 oracle.
 //
 // Frequencies: f = fx * 72 + fy, fy in [0, 72), fx in [0, 37) (the real-input half spectrum), so
 // the 72 values one FFT thread writes / reads sit at a 32-byte stride (immediate offsets).
-// Spectra are stored [b][cq][f][c] (complex, c = channel % 4, cq = channel / 4): every FFT block
-// reads / writes one contiguous 85 KiB run, and a spectral-GEMM lane reads one float4 per group.
+// Spectra live image-major in HBM, [b][cq][f][32 B] (cq = channel / 4, f fastest), so every FFT
+// block reads / writes one contiguous 85 KiB run; the FFT kernels stage that run through LDS in two
+// halves so each wave-instruction moves 1 KiB of consecutive bytes.
+//   S (input spectra): 32 B = 8 f16 hi (re/im of the 4 channels, interleaved) + 8 f16 lo;
+//   Y (output spectra): 32 B = 4 x complex64.
+// The spectral GEMM needs, for ONE frequency, 32 images of one operand half side by side (an MFMA
+// fragment); it loads (4 frequencies x 32 images) tiles whole-line and transposes them in LDS.
 #include "conv_epi.hpp"
 #include "fft_consts.hpp"
+
+#include <cmath>
+#include <cstring>
 
 namespace mp {
 
 constexpr int FX = FFT_N / 2 + 1;      // 37
 constexpr int NF = FFT_N * FX;         // 2664 frequencies
+// scale of the input spectra before the f16 split: |S| <= 4096 max|x|, so activations up to
+// 1023 in magnitude stay inside f16 range (hGRU maps are tanh / sigmoid-gated, |x| <~ 1)
+constexpr float SPEC_SCALE = 1.0f / 64.0f;
+
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f32x16 mfma16(f16x8 a, f16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
 
 struct cpx {
   float x, y;
@@ -126,15 +146,99 @@ __device__ __forceinline__ void fft72(cpx (&v)[72]) {
 }
 
 // ---------------------------------------------------------------------------------------------
-// forward 2-D FFT: one block per (image b, channel group cq); 192 threads.
-//   phase 1 (128 threads): row y, channel pair p: the two real rows packed as one complex FFT,
-//            then separated into their half spectra (fx = 0..36) -> LDS T[fx][c][y]
-//   phase 2 (148 threads): column (fx, c): 72-point FFT over y -> S[b][cq][fx*72+fy][c]
-constexpr int FWD_LD = 65;    // LDS row pitch (complex) of T: conflict-free column reads
-__global__ __launch_bounds__(192, 2) void fft_fwd_kernel(const float* __restrict__ src, cpx* __restrict__ S,
+// 2-D FFT phases.  One block per (image b, channel group cq = 4 channels), 192 threads; the
+// 72 x 72 transform is two passes of 72-point FFTs in registers with one LDS transpose between:
+//   row phase (128 threads): row y, channel pair p -- the two real rows packed as one complex FFT
+//   column phase (148 threads): column (fx, c), fx = 0..36 (the real-input half spectrum)
+constexpr int FWD_LD = 65;        // pitch (complex) of the forward transpose T[fx][c][y]
+constexpr int STG_LD = 296;       // output staging pitch per fx, dwords (36 fy x 8 dwords + 8 pad)
+constexpr int FFT_LDS = FX * 4 * FWD_LD;   // complex elements of the block's LDS (76,960 B)
+
+// forward row phase: the packed row v (a + ib, zero padded) -> half spectra of a and b in T
+__device__ __forceinline__ void fwd_rows_to_T(cpx (&v)[72], int y, int p, cpx* T) {
+  fft72<-1>(v);
+  // Z = FFT(a + i b):  A[k] = (Z[k] + conj Z[-k]) / 2,  B[k] = (Z[k] - conj Z[-k]) / (2i)
+#pragma unroll
+  for (int k = 0; k < FX; ++k) {
+    const cpx zk = v[k], zm = v[(72 - k) % 72];
+    const cpx A = {0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y)};
+    const cpx B = {0.5f * (zk.y + zm.y), -0.5f * (zk.x - zm.x)};
+    T[(k * 4 + 2 * p) * FWD_LD + y] = A;
+    T[(k * 4 + 2 * p + 1) * FWD_LD + y] = B;
+  }
+}
+
+// forward column phase: T -> S[b][cq][fx*72+fy] (scaled, split to f16 hi / lo).  The block's
+// contiguous 85 KiB S run is written through LDS (T's space) in two fy halves, 1 KiB per
+// wave-instruction.  Called by ALL threads (contains barriers); T must be complete on entry.
+__device__ __forceinline__ void fwd_cols_to_S(cpx* T, void* __restrict__ S, int b, int cq, int tid) {
+  const bool col = tid < FX * 4;
+  const int fx = tid >> 2, c = tid & 3;
+  cpx v[72];
+  if (col) {
+#pragma unroll
+    for (int y = 0; y < 72; ++y) v[y] = y < 64 ? T[tid * FWD_LD + y] : cpx{0.f, 0.f};
+    fft72<-1>(v);
+  }
+  uint32_t* stg = reinterpret_cast<uint32_t*>(T);
+  uint4* dst = reinterpret_cast<uint4*>(S) + ((size_t)b * 16 + cq) * NF * 2;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    __syncthreads();   // T (half 0) / the previous half's staging is no longer read
+    if (col) {
+#pragma unroll
+      for (int j = 0; j < 36; ++j) {
+        const cpx z = v[36 * half + j];
+        const float re = z.x * SPEC_SCALE, im = z.y * SPEC_SCALE;
+        const _Float16 hr = (_Float16)re, hi = (_Float16)im;
+        const f16x2 hv = {hr, hi}, lv = {(_Float16)(re - (float)hr), (_Float16)(im - (float)hi)};
+        stg[fx * STG_LD + j * 8 + c] = __builtin_bit_cast(uint32_t, hv);
+        stg[fx * STG_LD + j * 8 + 4 + c] = __builtin_bit_cast(uint32_t, lv);
+      }
+    }
+    __syncthreads();
+    // per fx: 36 groups x 32 B = 72 uint4 at f = fx*72 + 36*half
+    for (int i = tid; i < FX * 72; i += 192) {
+      const int ffx = i / 72, w = i - ffx * 72;
+      dst[(ffx * 72 + 36 * half) * 2 + w] = *reinterpret_cast<const uint4*>(stg + ffx * STG_LD + w * 4);
+    }
+  }
+}
+
+// inverse column phase: Y[b][cq][f] -> T[y][c][fx] (rows y < 64).  Direct per-thread loads (72
+// independent 8-byte loads in flight per thread) measured faster than an LDS-staged read.
+__device__ __forceinline__ void inv_cols_to_T(const cpx* __restrict__ Y, int b, int cq, int tid, cpx* T) {
+  if (tid < FX * 4) {
+    const int fx = tid >> 2, c = tid & 3;
+    const cpx* src = Y + (((size_t)b * 16 + cq) * NF + fx * 72) * 4 + c;
+    cpx v[72];
+#pragma unroll
+    for (int fy = 0; fy < 72; ++fy) v[fy] = src[fy * 4];
+    fft72<1>(v);
+#pragma unroll
+    for (int y = 0; y < 64; ++y) T[(y * 4 + c) * FX + fx] = v[y];   // rows >= H: unused
+  }
+}
+
+// inverse row phase: the Hermitian-extended half spectra of rows (y, 2p) and (y, 2p+1) packed as
+// C = A + iB, one inverse FFT: v[x].x / v[x].y = the two real output rows
+__device__ __forceinline__ void inv_row_from_T(const cpx* T, int y, int p, cpx (&v)[72]) {
+  const cpx* ta = T + (y * 4 + 2 * p) * FX;
+  const cpx* tb = ta + FX;
+#pragma unroll
+  for (int k = 0; k < FX; ++k) {   // C[k] = A[k] + i B[k];  C[72-k] from A[72-k] = conj A[k] etc.
+    const cpx A = ta[k], B = tb[k];
+    v[k] = {A.x - B.y, A.y + B.x};
+    if (k > 0 && k < FX - 1) v[72 - k] = {A.x + B.y, B.x - A.y};
+  }
+  fft72<1>(v);
+}
+
+// forward 2-D FFT of one C8 activation map -> S
+__global__ __launch_bounds__(192, 2) void fft_fwd_kernel(const float* __restrict__ src, void* __restrict__ S,
                                                       int H, int W) {
-  __shared__ cpx T[FX * 4 * FWD_LD];
-  const int cq = blockIdx.x & 15, b = blockIdx.x >> 4;
+  __shared__ cpx T[FFT_LDS];
+  const int b = blockIdx.x >> 4, cq = blockIdx.x & 15;
   const int q = cq >> 1, e0 = 4 * (cq & 1);
   const int tid = threadIdx.x;
   if (tid < 128) {
@@ -150,65 +254,26 @@ __global__ __launch_bounds__(192, 2) void fft_fwd_kernel(const float* __restrict
         v[x] = {0.f, 0.f};
       }
     }
-    fft72<-1>(v);
-    // Z = FFT(a + i b):  A[k] = (Z[k] + conj Z[-k]) / 2,  B[k] = (Z[k] - conj Z[-k]) / (2i)
-#pragma unroll
-    for (int k = 0; k < FX; ++k) {
-      const cpx zk = v[k], zm = v[(72 - k) % 72];
-      const cpx A = {0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y)};
-      const cpx B = {0.5f * (zk.y + zm.y), -0.5f * (zk.x - zm.x)};
-      T[(k * 4 + 2 * p) * FWD_LD + y] = A;
-      T[(k * 4 + 2 * p + 1) * FWD_LD + y] = B;
-    }
+    fwd_rows_to_T(v, y, p, T);
   }
   __syncthreads();
-  if (tid < FX * 4) {
-    const int fx = tid >> 2, c = tid & 3;
-    cpx v[72];
-#pragma unroll
-    for (int y = 0; y < 72; ++y) v[y] = y < 64 ? T[tid * FWD_LD + y] : cpx{0.f, 0.f};
-    fft72<-1>(v);
-    cpx* dst = S + (((size_t)b * 16 + cq) * NF + fx * 72) * 4 + c;
-#pragma unroll
-    for (int fy = 0; fy < 72; ++fy) dst[fy * 4] = v[fy];
-  }
+  fwd_cols_to_S(T, S, b, cq, tid);
 }
 
-// ---------------------------------------------------------------------------------------------
-// inverse 2-D FFT (complex-to-real): one block per (image b, channel group cq); 192 threads.
-//   phase 1 (148 threads): column (fx, c): inverse 72-point FFT over fy, rows y < H -> LDS
-//   phase 2 (128 threads): row y, channel pair p: the Hermitian-extended half spectra of the two
-//            real rows packed as C = A + iB, one inverse FFT, real / imaginary parts = the rows
+// inverse 2-D FFT of Y -> the spatial conv result P (C8)
 __global__ __launch_bounds__(192, 2) void fft_inv_kernel(const cpx* __restrict__ Y, float* __restrict__ P,
                                                       int H, int W) {
-  __shared__ cpx T[64 * 4 * FX];   // [y][c][fx]
-  const int cq = blockIdx.x & 15, b = blockIdx.x >> 4;
+  __shared__ cpx T[FFT_LDS];
+  const int b = blockIdx.x >> 4, cq = blockIdx.x & 15;
   const int q = cq >> 1, e0 = 4 * (cq & 1);
   const int tid = threadIdx.x;
-  if (tid < FX * 4) {
-    const int fx = tid >> 2, c = tid & 3;
-    const cpx* src = Y + (((size_t)b * 16 + cq) * NF + fx * 72) * 4 + c;
-    cpx v[72];
-#pragma unroll
-    for (int fy = 0; fy < 72; ++fy) v[fy] = src[fy * 4];
-    fft72<1>(v);
-#pragma unroll
-    for (int y = 0; y < 64; ++y) T[(y * 4 + c) * FX + fx] = v[y];   // rows >= H: unused
-  }
+  inv_cols_to_T(Y, b, cq, tid, T);
   __syncthreads();
   if (tid < 128) {
     const int y = tid >> 1, p = tid & 1;
     if (y < H) {
-      const cpx* ta = T + (y * 4 + 2 * p) * FX;
-      const cpx* tb = ta + FX;
       cpx v[72];
-#pragma unroll
-      for (int k = 0; k < FX; ++k) {   // C[k] = A[k] + i B[k];  C[72-k] from A[72-k] = conj A[k] etc.
-        const cpx A = ta[k], B = tb[k];
-        v[k] = {A.x - B.y, A.y + B.x};
-        if (k > 0 && k < FX - 1) v[72 - k] = {A.x + B.y, B.x - A.y};
-      }
-      fft72<1>(v);
+      inv_row_from_T(T, y, p, v);
       float* row = P + c8_index(b, q, y, 0, e0 + 2 * p, H, W);
 #pragma unroll
       for (int x = 0; x < 32; ++x) *reinterpret_cast<float2*>(row + 8 * x) = make_float2(v[x].x, v[x].y);
@@ -220,51 +285,150 @@ __global__ __launch_bounds__(192, 2) void fft_inv_kernel(const cpx* __restrict__
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// spectral GEMM: per frequency f, Y[b][co] = sum_ci S[b][ci] G[ci][co] (complex), as one real
-// 128 x 128 x 128 product D[n][b] = sum_k A[n][k] Bm[k][b] on v_mfma_f32_32x32x2_f32:
-//   n = 2 co + (re|im),  k-step s / lane half h  <->  input channel ci = 4 (s>>2) + 2h + ((s&3)>>1),
-//   part (s & 1): each lane's four consecutive k-steps are one float4 of its S group, and each
-//   lane's four accumulator rows 4h..4h+3 of a row group are one float4 of its Y group.
-// A (the expanded spectral weights of f, 64 KiB, fragment order [s][lane][mb]) is staged in LDS;
-// a block = NWV waves x 32 images, blocks of one frequency adjacent in launch order.
-template <int NWV>
-__global__ __launch_bounds__(NWV * 64, 2) void spec_gemm_kernel(const f32x4* __restrict__ S,
-                                                                const f32x4* __restrict__ Gx,
-                                                                f32x4* __restrict__ Y, int B, int groups) {
-  __shared__ f32x4 wl[64 * 64];
-  const int f = blockIdx.x / groups, grp = blockIdx.x - f * groups;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5;
-  const f32x4* gsrc = Gx + (size_t)f * 4096;
-#pragma unroll
-  for (int i = 0; i < 4096 / (NWV * 64); ++i) wl[i * NWV * 64 + tid] = gsrc[i * NWV * 64 + tid];
-  const int b = (grp * NWV + wv) * 32 + (lane & 31);
-  const bool live = b < B;
-  f32x4 sv[16];
-#pragma unroll
-  for (int cq = 0; cq < 16; ++cq)
-    sv[cq] = live ? S[(((size_t)b * 16 + cq) * NF + f) * 2 + h] : f32x4{0.f, 0.f, 0.f, 0.f};
+// The A half-step's tail and the B half-step's head in one pass (hgru_module.py:657, 797-799):
+//   P1 = IFFT(Y)  ->  I = tanh(X - (beta*O + nu) * (P1 + lateral_bias))  ->  S = FFT(I)
+// The inverse row phase leaves each thread with one output row of two channels -- exactly the
+// packed row the forward row phase transforms -- so P1 never leaves registers and I is written
+// once (the B epilogue reads it).  p: the A-epilogue arguments (X, O, vecs; dst = I).
+__global__ __launch_bounds__(192, 2) void fft_inv_a_fwd_kernel(const cpx* __restrict__ Y, ConvArgs p,
+                                                            void* __restrict__ S) {
+  __shared__ cpx T[FFT_LDS];
+  const int H = p.H, W = p.W;
+  const int b = blockIdx.x >> 4, cq = blockIdx.x & 15;
+  const int q = cq >> 1, e0 = 4 * (cq & 1);
+  const int tid = threadIdx.x;
+  inv_cols_to_T(Y, b, cq, tid, T);
   __syncthreads();
-  f32x16 acc[4] = {};
-#pragma unroll 8
-  for (int s = 0; s < 64; ++s) {
-    const f32x4 a = wl[s * 64 + lane];
-    const float bv = sv[s >> 2][s & 3];
-#pragma unroll
-    for (int mb = 0; mb < 4; ++mb) acc[mb] = mfma32(a[mb], bv, acc[mb]);
-  }
+  const int y = tid >> 1, pp = tid & 1;
+  const bool live = tid < 128 && y < H;
+  cpx v[72];
+  if (live) inv_row_from_T(T, y, pp, v);
+  __syncthreads();   // every inverse row has read T
+  // park the row in LDS (own slot, pitch 73) so the epilogue does not hold v[] beside its loads
+  cpx* R = T + tid * 73;
   if (live) {
 #pragma unroll
-    for (int mb = 0; mb < 4; ++mb)
+    for (int x = 0; x < 64; ++x) R[x] = v[x];
+    const int ch = 8 * q + e0 + 2 * pp;
+    const float2 lat = *reinterpret_cast<const float2*>(p.vecs + V_LAT * 64 + ch);
+    const float2 be = *reinterpret_cast<const float2*>(p.vecs + V_BETA * 64 + ch);
+    const float2 nu = *reinterpret_cast<const float2*>(p.vecs + V_NU * 64 + ch);
+    const size_t r0 = c8_index(b, q, y, 0, e0 + 2 * pp, H, W);
+    for (int x = 0; x < W; ++x) {
+      const float2 xv = *reinterpret_cast<const float2*>(p.X + r0 + 8 * x);
+      const float2 ov = *reinterpret_cast<const float2*>(p.O + r0 + 8 * x);
+      const cpx pv = R[x];
+      const float i0 = tanhf(xv.x - (be.x * ov.x + nu.x) * (pv.x + lat.x));
+      const float i1 = tanhf(xv.y - (be.y * ov.y + nu.y) * (pv.y + lat.y));
+      *reinterpret_cast<float2*>(p.dst + r0 + 8 * x) = make_float2(i0, i1);
+      R[x] = {i0, i1};
+    }
 #pragma unroll
-      for (int g = 0; g < 4; ++g)
-        Y[(((size_t)b * 16 + 4 * mb + g) * NF + f) * 2 + h] =
-            f32x4{acc[mb][4 * g], acc[mb][4 * g + 1], acc[mb][4 * g + 2], acc[mb][4 * g + 3]};
+    for (int x = 0; x < 72; ++x) v[x] = x < 64 ? R[x] : cpx{0.f, 0.f};
+    if (W <= 32) {   // uniform; columns >= W of the slot hold stale values
+#pragma unroll
+      for (int x = 32; x < 64; ++x) v[x] = {0.f, 0.f};
+    }
+  } else {
+#pragma unroll
+    for (int x = 0; x < 72; ++x) v[x] = {0.f, 0.f};
+  }
+  __syncthreads();   // every row is back in registers: T's space is free
+  if (tid < 128) fwd_rows_to_T(v, y, pp, T);
+  __syncthreads();
+  fwd_cols_to_S(T, S, b, cq, tid);
+}
+
+// ---------------------------------------------------------------------------------------------
+// spectral GEMM: per frequency f, Y[b][co] = sum_ci S[b][ci] G[ci][co] (complex), as one real
+// 128 x 32 x 128 product per (f, 32 images), D[n][j] = sum_k A[n][k] Bm[k][j] on
+// v_mfma_f32_32x32x16_f16 in the f16x3 split, with n = 64 ro + co (ro = re|im of the output) and
+// k = 2 ci + ri (ri = re|im of the input):
+//   B fragment (lane h, image j; k-step t): k = 16t + 8h + e = the 8 hi (lo) halves of S group
+//     cq = 2t + h of image j;
+//   A fragment (lane h, row i of M-block mb, ro = mb >> 1): re/im pairs of G[ci = 8t+4h..+3][co],
+//     negated imaginary halves for ro = 0 (gr, -gi), swapped halves for ro = 1 (gi, gr), derived in
+//     registers from the compact split weights Gc[f][part][cq][co] (f16x8 = 4 complex), 32 KiB per f.
+// Block = 4 consecutive frequencies (one 128-B line of S / Y per (image, channel group)) x 32
+// images, 4 waves (one frequency each).  The S tile is loaded whole-line (8 lines per
+// wave-instruction) into LDS [cq][part][f][b], the Y tile leaves the same way through LDS
+// [b][cq][f]; the weights stream from L2.  Blocks of one frequency quad are placed on one XCD so its
+// weights are fetched from HBM once.
+constexpr int SG_NI = 32;              // images per block
+constexpr int NQUAD = NF / 4;          // 666 frequency quads
+constexpr int SG_SLD = 33;             // S tile pitch (16-B units) per (cq, part, f) row
+constexpr int SG_YLD = 16 * 4 * 2 + 1; // Y tile pitch (16-B units) per image
+__global__ __launch_bounds__(256, 2) void spec_gemm_kernel(const uint4* __restrict__ S, const uint4* __restrict__ Gc,
+                                                           uint4* __restrict__ Y, int B, int ngrp, float unscale) {
+  __shared__ uint4 tile[16 * 2 * 4 * SG_SLD];   // 67,584 B
+  // block -> (quad, image group): the ngrp groups of quad q run on XCD q % 8 (round-robin dispatch)
+  const int q8 = blockIdx.x / (8 * ngrp), rem = blockIdx.x - q8 * 8 * ngrp;
+  const int grp = rem >> 3, quad = q8 * 8 + (rem & 7);
+  if (quad >= NQUAD) return;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, j = lane & 31;
+  const int img0 = grp * SG_NI;
+  // ---- S tile: 32 images x 16 cq lines of 128 B (4 f x [hi 16 B | lo 16 B]) ----
+#pragma unroll
+  for (int it = 0; it < 16; ++it) {
+    const int idx = it * 256 + tid, line = idx >> 3, piece = idx & 7;
+    const int bl = line >> 4, cq = line & 15, f = piece >> 1, part = piece & 1;
+    const int b = img0 + bl;
+    const uint4 v = b < B ? S[(((size_t)b * 16 + cq) * NF + 4 * quad) * 2 + piece] : uint4{0, 0, 0, 0};
+    tile[((cq * 2 + part) * 4 + f) * SG_SLD + bl] = v;
+  }
+  // ---- weights of frequency f = 4 quad + wv: one f16x8 per (t, h, part, co block) ----
+  const int f = 4 * quad + wv;
+  const uint4* gw = Gc + (size_t)f * 2 * 16 * 64;
+  __syncthreads();
+  f32x16 acc[4] = {};
+  const uint4 m = {0x80000000u, 0x80000000u, 0x80000000u, 0x80000000u};
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const int cq = 2 * t + h;
+    const f16x8 sh = __builtin_bit_cast(f16x8, tile[((cq * 2 + 0) * 4 + wv) * SG_SLD + j]);
+    const f16x8 sl = __builtin_bit_cast(f16x8, tile[((cq * 2 + 1) * 4 + wv) * SG_SLD + j]);
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      const uint4 gh = gw[(0 * 16 + cq) * 64 + 32 * cb + j], gl = gw[(1 * 16 + cq) * 64 + 32 * cb + j];
+      // ro = 0 rows: (gr, -gi) pairs; ro = 1 rows: (gi, gr) pairs
+      const f16x8 ah0 = __builtin_bit_cast(f16x8, gh ^ m), al0 = __builtin_bit_cast(f16x8, gl ^ m);
+      const f16x8 ah1 = __builtin_bit_cast(f16x8, (gh >> 16) | (gh << 16));
+      const f16x8 al1 = __builtin_bit_cast(f16x8, (gl >> 16) | (gl << 16));
+      acc[cb] = mfma16(al0, sh, acc[cb]);
+      acc[cb] = mfma16(ah0, sl, acc[cb]);
+      acc[cb] = mfma16(ah0, sh, acc[cb]);
+      acc[2 + cb] = mfma16(al1, sh, acc[2 + cb]);
+      acc[2 + cb] = mfma16(ah1, sl, acc[2 + cb]);
+      acc[2 + cb] = mfma16(ah1, sh, acc[2 + cb]);
+    }
+  }
+  __syncthreads();   // every wave has read the S tile
+  // ---- Y tile: lane (h, j), co block cb, row group g: channels 32cb + 8g + 4h + e, e < 4 ----
+  f32x4* ytile = reinterpret_cast<f32x4*>(tile);
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int cqo = 8 * cb + 2 * g + h;
+      const f32x16& re = acc[cb];
+      const f32x16& im = acc[2 + cb];
+      const f32x4 lo = f32x4{re[4 * g], im[4 * g], re[4 * g + 1], im[4 * g + 1]} * unscale;
+      const f32x4 hi = f32x4{re[4 * g + 2], im[4 * g + 2], re[4 * g + 3], im[4 * g + 3]} * unscale;
+      ytile[j * SG_YLD + (cqo * 4 + wv) * 2] = lo;
+      ytile[j * SG_YLD + (cqo * 4 + wv) * 2 + 1] = hi;
+    }
+  __syncthreads();
+#pragma unroll
+  for (int it = 0; it < 16; ++it) {
+    const int idx = it * 256 + tid, line = idx >> 3, piece = idx & 7;
+    const int bl = line >> 4, cqo = line & 15, b = img0 + bl;
+    if (b < B) Y[(((size_t)b * 16 + cqo) * NF + 4 * quad) * 2 + piece] = tile[bl * SG_YLD + cqo * 8 + piece];
   }
 }
 
-// spectral weights, once per weight set: one thread per (f, ci, co), float64 accumulation
-__global__ void spec_weights_kernel(const float* __restrict__ w, float* __restrict__ Gx, int KS) {
+// spectral weights, once per weight set: G[f][ci][co] (complex, 1/N^2 folded in), one thread per
+// (f, ci, co), float64 accumulation
+__global__ void spec_weights_kernel(const float* __restrict__ w, cpx* __restrict__ G, int KS) {
   __shared__ double tc[FFT_N], ts[FFT_N];
   for (int m = threadIdx.x; m < FFT_N; m += blockDim.x) {
     double s, c;
@@ -287,16 +451,33 @@ __global__ void spec_weights_kernel(const float* __restrict__ w, float* __restri
       gi -= v * ts[m];
     }
   const double inv = 1.0 / ((double)FFT_N * FFT_N);
-  const float vr = (float)(gr * inv), vi = (float)(gi * inv);
-  // expanded real form: A[(co, ro)][(ci, ri)] = ro == ri ? gr : (ro == 0 ? -gi : gi)
-  const int c = ci & 3, hh = c >> 1, s0 = 4 * (ci >> 2) + 2 * (c & 1);
+  G[idx] = {(float)(gr * inv), (float)(gi * inv)};
+}
+
+__global__ void absmax_kernel(const float* __restrict__ x, size_t n, unsigned* out) {
+  float m = 0.f;
+  for (size_t i = blockIdx.x * (size_t)blockDim.x + threadIdx.x; i < n; i += (size_t)gridDim.x * blockDim.x)
+    m = fmaxf(m, fabsf(x[i]));
+  atomicMax(out, __float_as_uint(m));   // non-negative floats order like their bit patterns
+}
+
+// compact split weights Gc[f][part][cq][co]: one f16x8 = re/im of G[ci = 4cq..4cq+3][co] x wscale,
+// part 0 = hi, 1 = lo; thread = (f, cq, co)
+__global__ void spec_pack_kernel(const cpx* __restrict__ G, f16x8* __restrict__ Gc, float wscale) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= NF * 16 * 64) return;
+  const int co = idx & 63, cq = (idx >> 6) & 15, f = idx >> 10;
+  f16x8 hv, lv;
 #pragma unroll
-  for (int ro = 0; ro < 2; ++ro)
-#pragma unroll
-    for (int ri = 0; ri < 2; ++ri) {
-      const int n = 2 * co + ro, s = s0 + ri, lane = 32 * hh + (n & 31), mb = n >> 5;
-      Gx[(((size_t)f * 64 + s) * 64 + lane) * 4 + mb] = ro == ri ? vr : (ro == 0 ? -vi : vi);
-    }
+  for (int e = 0; e < 8; ++e) {
+    const cpx g = G[((size_t)f * 64 + 4 * cq + (e >> 1)) * 64 + co];
+    const float v = ((e & 1) ? g.y : g.x) * wscale;
+    const _Float16 hh = (_Float16)v;
+    hv[e] = hh;
+    lv[e] = (_Float16)(v - (float)hh);
+  }
+  Gc[(((size_t)f * 2 + 0) * 16 + cq) * 64 + co] = hv;
+  Gc[(((size_t)f * 2 + 1) * 16 + cq) * 64 + co] = lv;
 }
 
 // the fused epilogue on the spatial result P: one wave per 32-pixel row segment, P loaded in the
@@ -323,25 +504,55 @@ __global__ __launch_bounds__(256) void spec_epi_kernel(ConvArgs p, const float* 
 
 // ------------------------------------------------------------------------------------ launchers
 size_t fft_spec_bytes(int B) { return (size_t)B * 16 * NF * 4 * sizeof(cpx); }
-size_t fft_weight_bytes() { return (size_t)NF * 4096 * 4 * sizeof(float); }
+size_t fft_weight_bytes() { return (size_t)NF * 2 * 16 * 64 * sizeof(f16x8); }
 
-hipError_t launch_spec_weights(const float* w, float* Gx, int ks, hipStream_t st) {
-  const int total = NF * 4096;
-  hipLaunchKernelGGL(spec_weights_kernel, dim3((total + 255) / 256), dim3(256), 0, st, w, Gx, ks);
-  return hipGetLastError();
+hipError_t build_spec_weights(const float* w, int ks, void* Gx, float* unscale) {
+  cpx* G = nullptr;
+  unsigned* mx = nullptr;
+  hipError_t e = hipMalloc(&G, (size_t)NF * 4096 * sizeof(cpx));
+  if (e == hipSuccess) e = hipMalloc(&mx, sizeof(unsigned));
+  if (e == hipSuccess) e = hipMemset(mx, 0, sizeof(unsigned));
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(spec_weights_kernel, dim3(NF * 4096 / 256), dim3(256), 0, 0, w, G, ks);
+    hipLaunchKernelGGL(absmax_kernel, dim3(1024), dim3(256), 0, 0, reinterpret_cast<const float*>(G),
+                       (size_t)NF * 4096 * 2, mx);
+    e = hipGetLastError();
+  }
+  unsigned bits = 0;
+  if (e == hipSuccess) e = hipMemcpy(&bits, mx, sizeof(unsigned), hipMemcpyDeviceToHost);
+  if (e == hipSuccess) {
+    // power-of-two weight scale putting max|G| at 2^13..2^14 (f16 max is 65504)
+    float m;
+    std::memcpy(&m, &bits, sizeof m);
+    int ex = 0;
+    if (m > 0.f) std::frexp(m, &ex);
+    const float wscale = std::ldexp(1.0f, 14 - ex);
+    *unscale = 1.0f / (wscale * SPEC_SCALE);
+    hipLaunchKernelGGL(spec_pack_kernel, dim3(NF * 16 * 64 / 256), dim3(256), 0, 0, G,
+                       static_cast<f16x8*>(Gx), wscale);
+    e = hipGetLastError();
+  }
+  if (e == hipSuccess) e = hipDeviceSynchronize();
+  if (G) (void)hipFree(G);
+  if (mx) (void)hipFree(mx);
+  return e;
 }
 
 hipError_t launch_fft_fwd(const float* act, void* S, int B, int H, int W, hipStream_t st) {
-  hipLaunchKernelGGL(fft_fwd_kernel, dim3(B * 16), dim3(192), 0, st, act, static_cast<cpx*>(S), H, W);
+  hipLaunchKernelGGL(fft_fwd_kernel, dim3(B * 16), dim3(192), 0, st, act, S, H, W);
   return hipGetLastError();
 }
 
-hipError_t launch_spec_gemm(const void* S, const float* Gx, void* Y, int B, hipStream_t st) {
-  constexpr int NWV = 4;
-  const int groups = (B + 32 * NWV - 1) / (32 * NWV);
-  hipLaunchKernelGGL((spec_gemm_kernel<NWV>), dim3(NF * groups), dim3(NWV * 64), 0, st,
-                     static_cast<const f32x4*>(S), reinterpret_cast<const f32x4*>(Gx), static_cast<f32x4*>(Y),
-                     B, groups);
+hipError_t launch_fft_inv_a_fwd(const void* Y, const ConvArgs& a, void* S, int B, hipStream_t st) {
+  hipLaunchKernelGGL(fft_inv_a_fwd_kernel, dim3(B * 16), dim3(192), 0, st, static_cast<const cpx*>(Y), a, S);
+  return hipGetLastError();
+}
+
+hipError_t launch_spec_gemm(const void* S, const void* Gx, void* Y, int B, float unscale, hipStream_t st) {
+  const int ngrp = (B + SG_NI - 1) / SG_NI;
+  const int nq8 = (NQUAD + 7) / 8;
+  hipLaunchKernelGGL(spec_gemm_kernel, dim3(nq8 * 8 * ngrp), dim3(256), 0, st, static_cast<const uint4*>(S),
+                     static_cast<const uint4*>(Gx), static_cast<uint4*>(Y), B, ngrp, unscale);
   return hipGetLastError();
 }
 

@@ -89,7 +89,7 @@ void finalize_circuit(mp_ctx* c, const std::vector<float>* outs, const std::vect
     hip_check(launch_pack_conv64x3(it->second.dev->f(), c->p_pk.p, c->ssf, wscale, nullptr), "pack p_r (f16x3)");
   } else if (c->dtype == MP_DTYPE_F32_FFT) {
     c->spec_g.alloc(fft_weight_bytes());
-    hip_check(launch_spec_weights(it->second.dev->f(), c->spec_g.f(), c->ssf, nullptr), "p_r spectrum");
+    hip_check(build_spec_weights(it->second.dev->f(), c->ssf, c->spec_g.p, &c->p_unscale), "p_r spectrum");
   } else {
     hip_check(launch_pack_conv64(it->second.dev->f(), c->p_pk.v4(), c->ssf, nullptr), "pack p_r");
   }
@@ -193,26 +193,41 @@ void ensure_ws(mp_ctx* c, int64_t n, int64_t H, int64_t W) {
 
 // one association-field conv p_r * a.src with its fused hGRU epilogue, in the context's precision
 void eCRF_conv(mp_ctx* c, int epi, const ConvArgs& a, int n, hipStream_t st) {
-  if (c->dtype == MP_DTYPE_F32_FFT) {
+  if (c->dtype == MP_DTYPE_F32_SPLIT)
+    hip_check(launch_conv64x3(c->ssf, epi, a, c->p_pk.p, c->p_unscale, n, st), "conv15 (f16x3)");
+  else
+    hip_check(launch_conv64(c->ssf, epi, a, n, st), "conv15");
+}
+
+// FFT path of one hGRU step (k_fft.hip): the A half-step's inverse transform, its epilogue and the
+// B half-step's forward transform are one kernel, so per step:
+//   fft_fwd(Og) -> S;  spec_gemm -> Y;  inv_a_fwd: I = A-epi(IFFT(Y)), S = FFT(I);
+//   spec_gemm -> Y;  fft_inv -> P2;  epi_b(P2, I, O) -> O', Og'
+void fft_step(mp_ctx* c, const ConvArgs& a, const ConvArgs& b, int n, hipStream_t st) {
+  {
+    ProfScope pa(c, st, "conv15_a");
     {
       ProfScope ps(c, st, "fft_fwd");
       hip_check(launch_fft_fwd(a.src, c->specS.p, n, a.H, a.W, st), "fft_fwd");
     }
     {
       ProfScope ps(c, st, "spec_gemm");
-      hip_check(launch_spec_gemm(c->specS.p, c->spec_g.f(), c->specY.p, n, st), "spec_gemm");
+      hip_check(launch_spec_gemm(c->specS.p, c->spec_g.p, c->specY.p, n, c->p_unscale, st), "spec_gemm");
     }
-    {
-      ProfScope ps(c, st, "fft_inv");
-      hip_check(launch_fft_inv(c->specY.p, c->specP.f(), n, a.H, a.W, st), "fft_inv");
-    }
-    ProfScope ps(c, st, epi == EPI_HGRU_A ? "epi_a" : "epi_b");
-    hip_check(launch_spec_epi(epi, a, c->specP.f(), n, st), "spectral epilogue");
-  } else if (c->dtype == MP_DTYPE_F32_SPLIT) {
-    hip_check(launch_conv64x3(c->ssf, epi, a, c->p_pk.p, c->p_unscale, n, st), "conv15 (f16x3)");
-  } else {
-    hip_check(launch_conv64(c->ssf, epi, a, n, st), "conv15");
+    ProfScope ps(c, st, "inv_a_fwd");
+    hip_check(launch_fft_inv_a_fwd(c->specY.p, a, c->specS.p, n, st), "fft_inv_a_fwd");
   }
+  ProfScope pb(c, st, "conv15_b");
+  {
+    ProfScope ps(c, st, "spec_gemm");
+    hip_check(launch_spec_gemm(c->specS.p, c->spec_g.p, c->specY.p, n, c->p_unscale, st), "spec_gemm");
+  }
+  {
+    ProfScope ps(c, st, "fft_inv");
+    hip_check(launch_fft_inv(c->specY.p, c->specP.f(), n, b.H, b.W, st), "fft_inv");
+  }
+  ProfScope ps(c, st, "epi_b");
+  hip_check(launch_spec_epi(EPI_HGRU_B, b, c->specP.f(), n, st), "spectral epilogue");
 }
 
 // map-size rule of the context's association-field conv path (MP_ERR_SHAPE otherwise)
@@ -242,10 +257,6 @@ void run_circuit(mp_ctx* c, int64_t n, int H, int W, int T, const float* o0_nhwc
     a.X = c->X.f();
     a.O = c->O.f();
     a.vecs = c->vecs.f();
-    {
-      ProfScope ps(c, st, "conv15_a");
-      eCRF_conv(c, EPI_HGRU_A, a, (int)n, st);
-    }
     ConvArgs b{};
     b.H = H;
     b.W = W;
@@ -260,6 +271,14 @@ void run_circuit(mp_ctx* c, int64_t n, int H, int W, int T, const float* o0_nhwc
     b.rho = c->rho[t];
     b.mode = (t == T - 1) ? 1 : 0;
     b.dst2 = (t == T - 1) ? final_dst2 : c->Og.f();
+    if (c->dtype == MP_DTYPE_F32_FFT) {
+      fft_step(c, a, b, (int)n, st);
+      continue;
+    }
+    {
+      ProfScope ps(c, st, "conv15_a");
+      eCRF_conv(c, EPI_HGRU_A, a, (int)n, st);
+    }
     {
       ProfScope ps(c, st, "conv15_b");
       eCRF_conv(c, EPI_HGRU_B, b, (int)n, st);

@@ -45,11 +45,14 @@ hipError_t launch_pack_conv64x3(const float* w, void* out, int ks, float wscale,
 // k_fft.hip (FFT path of the association-field conv, MP_DTYPE_F32_FFT; maps up to 64x64)
 constexpr int FFT_MAX_HW = 64;
 size_t fft_spec_bytes(int B);      // one spectrum buffer (S or Y) for B images
-size_t fft_weight_bytes();         // expanded spectral weights
-hipError_t launch_spec_weights(const float* w, float* Gx, int ks, hipStream_t st);
+size_t fft_weight_bytes();         // expanded split spectral weights
+// HWIO [ks][ks][64][64] -> packed split spectral weights (synchronous, finalize time)
+hipError_t build_spec_weights(const float* w, int ks, void* Gx, float* unscale);
 hipError_t launch_fft_fwd(const float* act, void* S, int B, int H, int W, hipStream_t st);
-hipError_t launch_spec_gemm(const void* S, const float* Gx, void* Y, int B, hipStream_t st);
+hipError_t launch_spec_gemm(const void* S, const void* Gx, void* Y, int B, float unscale, hipStream_t st);
 hipError_t launch_fft_inv(const void* Y, float* P, int B, int H, int W, hipStream_t st);
+// P1 = IFFT(Y); I = A-epilogue(P1) -> a.dst; S = FFT(I)   (the A half-step tail + B half-step head)
+hipError_t launch_fft_inv_a_fwd(const void* Y, const ConvArgs& a, void* S, int B, hipStream_t st);
 hipError_t launch_spec_epi(int epi, const ConvArgs& a, const float* P, int B, hipStream_t st);
 // k_igemm.hip (dense / hierarchical regressors)
 struct IgemmArgs {

@@ -113,7 +113,7 @@ struct mp_ctx {
   // ---- finalized weights ----
   int ssf = 15, timesteps = 8, nout = 0, fc1_in = 0, fc1_out = 0;
   int dtype = MP_DTYPE_F32;
-  float p_unscale = 1.f;   // MP_DTYPE_F32_SPLIT: 1 / (weight scale * activation scale)
+  float p_unscale = 1.f;   // F32_SPLIT / F32_FFT: 1 / (weight scale * activation or spectrum scale)
   std::vector<float> rho;
   DevBuf conv1_w, conv1_b, bn0_s, bn0_t;
   DevBuf conv2_pk, conv2_b, bn1_s, bn1_t;
