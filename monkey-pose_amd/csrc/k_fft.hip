@@ -30,8 +30,10 @@
 #include "conv_epi.hpp"
 #include "fft_consts.hpp"
 
+#include <algorithm>
 #include <cmath>
 #include <cstring>
+#include <vector>
 
 namespace mp {
 
@@ -314,7 +316,8 @@ __global__ __launch_bounds__(192, 2) void fft_inv_a_fwd_kernel(const cpx* __rest
     const float2 be = *reinterpret_cast<const float2*>(p.vecs + V_BETA * 64 + ch);
     const float2 nu = *reinterpret_cast<const float2*>(p.vecs + V_NU * 64 + ch);
     const size_t r0 = c8_index(b, q, y, 0, e0 + 2 * pp, H, W);
-    for (int x = 0; x < W; ++x) {
+#pragma unroll 8
+    for (int x = 0; x < W; ++x) {   // W is 32 or 64: 8 iterations' loads in flight at a time
       const float2 xv = *reinterpret_cast<const float2*>(p.X + r0 + 8 * x);
       const float2 ov = *reinterpret_cast<const float2*>(p.O + r0 + 8 * x);
       const cpx pv = R[x];
@@ -480,6 +483,145 @@ __global__ void spec_pack_kernel(const cpx* __restrict__ G, f16x8* __restrict__ 
   Gc[(((size_t)f * 2 + 1) * 16 + cq) * 64 + co] = lv;
 }
 
+// ---------------------------------------------------------------------------------------------
+// FFT-path B epilogue (hgru_module.py:729-740, 806-849, 696-711) on the spatial conv result P2:
+//   g2 = sigmoid(I . o_r + o_b); e = gamma*(P2 + lat); S = tanh(kappa*(I+e) + omega*(I*e));
+//   O' = (g2*O + (1-g2)*S) * rho[t];  then Og' = O' * sigmoid(O' . i_r + i_b)  (or BN_3(O') NHWC)
+// One wave per 32-pixel row segment, values held in the v_mfma 32x32 accumulator layout
+// (register r of lane (h, x) = channel 32n + 8(r>>2) + 4h + (r&3) of pixel x).  The two 1x1 gate
+// GEMMs run on v_mfma_f32_32x32x16_f16 in the f16x3 split.  Their K order is permuted so that the B
+// fragment of k-step s is accumulator registers 8(s&1)..8(s&1)+7 of block s>>1 as they stand:
+//   k-step s, lane half h, element e  <->  input channel 32(s>>1) + 8(2(s&1) + (e>>2)) + 4h + (e&3)
+// (pack_gate_x3_kernel packs the weights in the same order).  sigmoid / tanh use v_exp_f32 and
+// v_rcp_f32 (abs error ~1e-7).
+constexpr float GATE_VSCALE = 256.0f;   // activations entering a gate: |v| < 255 stays in f16 range
+
+__device__ __forceinline__ float fsigmoid(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+__device__ __forceinline__ float ftanh(float x) { return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __expf(2.f * x)); }
+
+// Y[n2] = sum_cin G[cin][32 n2 + row] V[cin][pixel], f16x3; gpk = [n2][s][hi|lo][lane] f16x8
+__device__ __forceinline__ void gate_x3(const f16x8* __restrict__ gpk, const f32x16 (&V)[2], f32x16 (&Y)[2],
+                                        int lane, float unscale) {
+  f16x8 bh[4], bl[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      const float v = V[s >> 1][8 * (s & 1) + e] * GATE_VSCALE;
+      const _Float16 hv = (_Float16)v;
+      bh[s][e] = hv;
+      bl[s][e] = (_Float16)(v - (float)hv);
+    }
+#pragma unroll
+  for (int n2 = 0; n2 < 2; ++n2) {
+    f32x16 acc = {};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) {
+      const f16x8 ah = gpk[((n2 * 4 + s) * 2) * 64 + lane], al = gpk[((n2 * 4 + s) * 2 + 1) * 64 + lane];
+      acc = mfma16(al, bh[s], acc);
+      acc = mfma16(ah, bl[s], acc);
+      acc = mfma16(ah, bh[s], acc);
+    }
+    Y[n2] = acc * unscale;
+  }
+}
+
+__global__ __launch_bounds__(256) void spec_epi_b_kernel(ConvArgs p, const float* __restrict__ P,
+                                                         const f16x8* __restrict__ or_x3, float or_us,
+                                                         const f16x8* __restrict__ ir_x3, float ir_us, int nseg) {
+  const int lane = threadIdx.x & 63, h = lane >> 5;
+  const int seg = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (seg >= nseg) return;
+  const int H = p.H, W = p.W, xs = W / 32;
+  const int x = (seg % xs) * 32 + (lane & 31);
+  const int y = (seg / xs) % H, b = seg / xs / H;
+  f32x16 Iv[2], Y[2];
+#pragma unroll
+  for (int n = 0; n < 2; ++n)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 iv = *reinterpret_cast<const f32x4*>(p.I + c8_index(b, 4 * n + g, y, x, 4 * h, H, W));
+#pragma unroll
+      for (int j = 0; j < 4; ++j) Iv[n][4 * g + j] = iv[j];
+    }
+  gate_x3(or_x3, Iv, Y, lane, or_us);
+#pragma unroll
+  for (int n = 0; n < 2; ++n)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int c = 32 * n + 8 * g + 4 * h;
+      const size_t idx = c8_index(b, 4 * n + g, y, x, 4 * h, H, W);
+      const f32x4 pv = *reinterpret_cast<const f32x4*>(P + idx);
+      const f32x4 ov = *reinterpret_cast<const f32x4*>(p.O + idx);
+      const f32x4 lat = *reinterpret_cast<const f32x4*>(p.vecs + V_LAT * 64 + c);
+      const f32x4 ga = *reinterpret_cast<const f32x4*>(p.vecs + V_GAMMA * 64 + c);
+      const f32x4 ka = *reinterpret_cast<const f32x4*>(p.vecs + V_KAPPA * 64 + c);
+      const f32x4 om = *reinterpret_cast<const f32x4*>(p.vecs + V_OMEGA * 64 + c);
+      const f32x4 ob = *reinterpret_cast<const f32x4*>(p.vecs + V_OB * 64 + c);
+      f32x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int r = 4 * g + j;
+        const float g2 = fsigmoid(Y[n][r] + ob[j]);
+        const float iv = Iv[n][r];
+        const float e = ga[j] * (pv[j] + lat[j]);
+        const float S = ftanh(ka[j] * (iv + e) + om[j] * (iv * e));
+        const float on = (g2 * ov[j] + (1.f - g2) * S) * p.rho;
+        o[j] = on;
+        Iv[n][r] = on;
+      }
+      *reinterpret_cast<f32x4*>(p.dst + idx) = o;
+    }
+  f32x16 (&Ov)[2] = Iv;
+  if (p.mode == 0) {
+    gate_x3(ir_x3, Ov, Y, lane, ir_us);
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int c = 32 * n + 8 * g + 4 * h;
+        const f32x4 ib = *reinterpret_cast<const f32x4*>(p.vecs + V_IB * 64 + c);
+        f32x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = Ov[n][4 * g + j] * fsigmoid(Y[n][4 * g + j] + ib[j]);
+        *reinterpret_cast<f32x4*>(p.dst2 + c8_index(b, 4 * n + g, y, x, 4 * h, H, W)) = o;
+      }
+  } else {
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int c = 32 * n + 8 * g + 4 * h;
+        const f32x4 ss = *reinterpret_cast<const f32x4*>(p.vecs + V_OUTS * 64 + c);
+        const f32x4 tt = *reinterpret_cast<const f32x4*>(p.vecs + V_OUTT * 64 + c);
+        f32x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) o[j] = Ov[n][4 * g + j] * ss[j] + tt[j];
+        *reinterpret_cast<f32x4*>(p.dst2 + (((size_t)b * H + y) * W + x) * C + c) = o;
+      }
+  }
+}
+
+// 1x1 gate weights [cin][cout] -> [n2][s][hi|lo][lane] f16x8 in gate_x3's K order; thread =
+// (n2, s, lane)
+__global__ void pack_gate_x3_kernel(const float* __restrict__ g, f16x8* __restrict__ out, float wscale) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 2 * 4 * 64) return;
+  const int lane = i & 63, s = (i >> 6) & 3, n2 = i >> 8, h = lane >> 5;
+  const int co = 32 * n2 + (lane & 31);
+  f16x8 hv, lv;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const int ci = 32 * (s >> 1) + 8 * (2 * (s & 1) + (e >> 2)) + 4 * h + (e & 3);
+    const float v = g[ci * 64 + co] * wscale;
+    const _Float16 hh = (_Float16)v;
+    hv[e] = hh;
+    lv[e] = (_Float16)(v - (float)hh);
+  }
+  out[((n2 * 4 + s) * 2) * 64 + lane] = hv;
+  out[((n2 * 4 + s) * 2 + 1) * 64 + lane] = lv;
+}
+
 // the fused epilogue on the spatial result P: one wave per 32-pixel row segment, P loaded in the
 // v_mfma 32x32 accumulator layout conv_epilogue expects (cout 32n + 8g + 4h + j at lane col x)
 template <int EPI>
@@ -558,6 +700,30 @@ hipError_t launch_spec_gemm(const void* S, const void* Gx, void* Y, int B, float
 
 hipError_t launch_fft_inv(const void* Y, float* P, int B, int H, int W, hipStream_t st) {
   hipLaunchKernelGGL(fft_inv_kernel, dim3(B * 16), dim3(192), 0, st, static_cast<const cpx*>(Y), P, H, W);
+  return hipGetLastError();
+}
+
+size_t gate_x3_bytes() { return (size_t)2 * 4 * 2 * 64 * sizeof(f16x8); }
+
+hipError_t pack_gate_x3(const float* g, void* out, float* unscale) {
+  std::vector<float> h(64 * 64);
+  hipError_t e = hipMemcpy(h.data(), g, h.size() * sizeof(float), hipMemcpyDeviceToHost);
+  if (e != hipSuccess) return e;
+  float m = 0.f;
+  for (float v : h) m = std::max(m, std::fabs(v));
+  int ex = 0;
+  if (m > 0.f) std::frexp(m, &ex);
+  const float wscale = std::ldexp(1.0f, 14 - ex);   // max|g| at 2^13..2^14
+  *unscale = 1.0f / (wscale * GATE_VSCALE);
+  hipLaunchKernelGGL(pack_gate_x3_kernel, dim3(2), dim3(256), 0, 0, g, static_cast<f16x8*>(out), wscale);
+  return hipGetLastError();
+}
+
+hipError_t launch_spec_epi_b(const ConvArgs& a, const float* P, const void* or_x3, float or_us, const void* ir_x3,
+                             float ir_us, int B, hipStream_t st) {
+  const int nseg = B * a.H * (a.W / 32);
+  hipLaunchKernelGGL(spec_epi_b_kernel, dim3((nseg + 3) / 4), dim3(256), 0, st, a, P,
+                     static_cast<const f16x8*>(or_x3), or_us, static_cast<const f16x8*>(ir_x3), ir_us, nseg);
   return hipGetLastError();
 }
 

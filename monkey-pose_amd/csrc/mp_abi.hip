@@ -90,6 +90,12 @@ void finalize_circuit(mp_ctx* c, const std::vector<float>* outs, const std::vect
   } else if (c->dtype == MP_DTYPE_F32_FFT) {
     c->spec_g.alloc(fft_weight_bytes());
     hip_check(build_spec_weights(it->second.dev->f(), c->ssf, c->spec_g.p, &c->p_unscale), "p_r spectrum");
+    c->or_x3.alloc(gate_x3_bytes());
+    c->ir_x3.alloc(gate_x3_bytes());
+    hip_check(pack_gate_x3(c->need("contextual_circuit/o_r", {1, 1, 64, 64}).dev->f(), c->or_x3.p, &c->or_us),
+              "pack o_r (f16x3)");
+    hip_check(pack_gate_x3(c->need("contextual_circuit/i_r", {1, 1, 64, 64}).dev->f(), c->ir_x3.p, &c->ir_us),
+              "pack i_r (f16x3)");
   } else {
     hip_check(launch_pack_conv64(it->second.dev->f(), c->p_pk.v4(), c->ssf, nullptr), "pack p_r");
   }
@@ -227,7 +233,7 @@ void fft_step(mp_ctx* c, const ConvArgs& a, const ConvArgs& b, int n, hipStream_
     hip_check(launch_fft_inv(c->specY.p, c->specP.f(), n, b.H, b.W, st), "fft_inv");
   }
   ProfScope ps(c, st, "epi_b");
-  hip_check(launch_spec_epi(EPI_HGRU_B, b, c->specP.f(), n, st), "spectral epilogue");
+  hip_check(launch_spec_epi_b(b, c->specP.f(), c->or_x3.p, c->or_us, c->ir_x3.p, c->ir_us, n, st), "B epilogue");
 }
 
 // map-size rule of the context's association-field conv path (MP_ERR_SHAPE otherwise)

@@ -54,6 +54,11 @@ hipError_t launch_fft_inv(const void* Y, float* P, int B, int H, int W, hipStrea
 // P1 = IFFT(Y); I = A-epilogue(P1) -> a.dst; S = FFT(I)   (the A half-step tail + B half-step head)
 hipError_t launch_fft_inv_a_fwd(const void* Y, const ConvArgs& a, void* S, int B, hipStream_t st);
 hipError_t launch_spec_epi(int epi, const ConvArgs& a, const float* P, int B, hipStream_t st);
+// B epilogue with f16x3 gate GEMMs (FFT path); gate weights packed by pack_gate_x3 (synchronous)
+size_t gate_x3_bytes();
+hipError_t pack_gate_x3(const float* g, void* out, float* unscale);
+hipError_t launch_spec_epi_b(const ConvArgs& a, const float* P, const void* or_x3, float or_us, const void* ir_x3,
+                             float ir_us, int B, hipStream_t st);
 // k_igemm.hip (dense / hierarchical regressors)
 struct IgemmArgs {
   const float* x;      // input view: pixel (n,y,x) channel ci at x[((n*H+y)*W+x)*ldx + cix + ci]
