@@ -23,7 +23,7 @@ typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 namespace mp {
 
-constexpr float ACT_SCALE = 1024.0f;     // 2^10
+constexpr float ACT_SCALE = 1024.0f;     // 2^10, default activation scale (hGRU maps are tanh / sigmoid-bounded)
 
 __device__ __forceinline__ f32x16 mfma16(f16x8 a, f16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
@@ -73,7 +73,7 @@ __global__ __launch_bounds__(NW * 64, 1) void conv64x3_kernel(ConvArgs p, const 
         const f32x4 a0 = src[0], a1 = src[1];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float v = (j < 4 ? a0[j] : a1[j - 4]) * ACT_SCALE;
+          const float v = (j < 4 ? a0[j] : a1[j - 4]) * p.ascale;
           const _Float16 hi = (_Float16)v;
           vh[j] = hi;
           vl[j] = (_Float16)(v - (float)hi);
@@ -197,6 +197,7 @@ constexpr int X3_NW = 8, X3_SCHED = 1;
 hipError_t launch_conv64x3(int ks, int epi, ConvArgs a, const void* wpk, float unscale, int B, hipStream_t st) {
   a.tiles_x = a.W / TW;
   a.tiles_y = a.H / TH3;
+  if (a.ascale == 0.f) a.ascale = ACT_SCALE;
 #define MP_CASE(K, E) \
   if (ks == K && epi == E) return launch_x3_t<K, E, X3_NW, X3_SCHED>(a, wpk, unscale, B, st);
   MP_CASE(15, EPI_HGRU_A)
@@ -205,6 +206,7 @@ hipError_t launch_conv64x3(int ks, int epi, ConvArgs a, const void* wpk, float u
   MP_CASE(5, EPI_HGRU_B)
   MP_CASE(3, EPI_HGRU_A)
   MP_CASE(3, EPI_HGRU_B)
+  MP_CASE(3, EPI_BB)      // backbone conv_2 / conv_3 under MP_DTYPE_F32_SPLIT / _FFT
 #undef MP_CASE
   return hipErrorInvalidValue;
 }

@@ -12,6 +12,10 @@
 // bias, relu and the per-feature affine.
 #include "mp_kernels.hpp"
 
+#include <algorithm>
+#include <cmath>
+#include <vector>
+
 namespace mp {
 
 constexpr int FC_BM = 128, FC_BK = 32, FC_LDA = FC_BK + 4;
@@ -109,6 +113,144 @@ __global__ void fc_reduce_kernel(const float* __restrict__ part, int S, int M, i
   if (relu) v = fmaxf(v, 0.f);
   if (aff_s) v = v * aff_s[n] + aff_t[n];
   out[(size_t)m * ldo + n] = v;
+}
+
+// ---------------------------------------------------------------------------------------------
+// fp32-accurate f16x3 variant (the hGRU pose head's fc_1 under MP_DTYPE_F32_SPLIT / _FFT): the
+// same split-K decomposition and slabs (so the same batch invariance), D^T = W^T A^T on
+// v_mfma_f32_32x32x16_f16 with both operands split into f16 hi + lo (three products per MAC).
+// W is packed [k/16][n/32][hi|lo][lane] f16x8 with a per-tensor power-of-two scale (max|W| at
+// 2^13..2^14, so the lo halves stay normal); activations are split unscaled when staged into LDS
+// (hi / lo planes [128 m][32 k] f16).
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ f32x16 mfma16(f16x8 a, f16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+__global__ void pack_fc_x3_kernel(const float* __restrict__ W, f16x8* out, int K, int N, int N32, size_t total,
+                                  float wscale) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int lane = i % 64;
+  const int nb = (i / 64) % N32;
+  const size_t k16 = i / ((size_t)64 * N32);
+  const int n = 32 * nb + (lane & 31);
+  const size_t k0 = 16 * k16 + 8 * (lane >> 5);
+  f16x8 hv, lv;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float v = (k0 + e < (size_t)K && n < N) ? W[(k0 + e) * N + n] * wscale : 0.f;
+    const _Float16 hh = (_Float16)v;
+    hv[e] = hh;
+    lv[e] = (_Float16)(v - (float)hh);
+  }
+  f16x8* dst = out + ((k16 * N32 + nb) * 2) * 64 + lane;
+  dst[0] = hv;
+  dst[64] = lv;
+}
+
+constexpr int FCX_LD = FC_BK + 8;   // f16 pitch of the hi / lo activation planes (+16 B: conflict-free)
+
+__global__ __launch_bounds__(256) void fc_gemm_x3_kernel(const float* __restrict__ A, int lda,
+                                                         const f16x8* __restrict__ Wpk,
+                                                         float* __restrict__ part, int M, int K,
+                                                         int N32, int kslice, float unscale) {
+  __shared__ _Float16 Ah[FC_BM * FCX_LD], Al[FC_BM * FCX_LD];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, col = lane & 31;
+  const int mt = blockIdx.x, ntile = blockIdx.y, split = blockIdx.z;
+  const int K16 = (K + 15) / 16;
+  const int Npad = N32 * 32;
+  const int nb = ntile * 4 + wv;
+  const bool wave_on = nb < N32;   // wave-uniform
+  const int kbeg = split * kslice;
+  const int kend = min(K, kbeg + kslice);
+
+  f32x16 acc[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) acc[m] = f32x16{};
+
+  for (int k0 = kbeg; k0 < kend; k0 += FC_BK) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = tid + i * 256;          // 0..1023 float4 slots: row = e / 8, k4 = e % 8
+      const int row = e >> 3, k4 = (e & 7) * 4;
+      const int gm = mt * FC_BM + row, gk = k0 + k4;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (gm < M) {
+        if (gk + 3 < kend) {
+          v = *reinterpret_cast<const f32x4*>(A + (size_t)gm * lda + gk);
+        } else {
+#pragma unroll
+          for (int s = 0; s < 4; ++s) v[s] = (gk + s < kend) ? A[(size_t)gm * lda + gk + s] : 0.f;
+        }
+      }
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const _Float16 hh = (_Float16)v[s];
+        Ah[row * FCX_LD + k4 + s] = hh;
+        Al[row * FCX_LD + k4 + s] = (_Float16)(v[s] - (float)hh);
+      }
+    }
+    __syncthreads();
+    if (wave_on) {
+#pragma unroll
+      for (int g = 0; g < FC_BK / 16; ++g) {
+        const int kb = (k0 >> 4) + g;
+        if (kb >= K16) break;
+        const f16x8* wp = Wpk + (((size_t)kb * N32 + nb) * 2) * 64 + lane;
+        const f16x8 wh = wp[0], wl = wp[64];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const int o = (m * 32 + col) * FCX_LD + 16 * g + 8 * h;
+          const f16x8 ah = *reinterpret_cast<const f16x8*>(Ah + o);
+          const f16x8 al = *reinterpret_cast<const f16x8*>(Al + o);
+          acc[m] = mfma16(wl, ah, acc[m]);
+          acc[m] = mfma16(wh, al, acc[m]);
+          acc[m] = mfma16(wh, ah, acc[m]);
+        }
+      }
+    }
+  }
+  if (!wave_on) return;
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int gm = mt * FC_BM + m * 32 + col;
+    if (gm >= M) continue;
+    float* dst = part + ((size_t)split * M + gm) * Npad + 32 * nb + 4 * h;
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      *reinterpret_cast<f32x4*>(dst + 8 * g) =
+          f32x4{acc[m][4 * g], acc[m][4 * g + 1], acc[m][4 * g + 2], acc[m][4 * g + 3]} * unscale;
+  }
+}
+
+size_t fc_x3_bytes(int K, int N) { return (size_t)(K + 15) / 16 * ((N + 31) / 32) * 2 * 64 * sizeof(f16x8); }
+
+hipError_t launch_pack_fc_x3(const float* W, void* out, int K, int N, float* unscale, hipStream_t st) {
+  // power-of-two weight scale from max|W|
+  float mx = 0.f;
+  hipError_t e = device_absmax(W, (size_t)K * N, &mx);
+  if (e != hipSuccess) return e;
+  int ex = 0;
+  if (mx > 0.f) std::frexp(mx, &ex);
+  const float wscale = std::ldexp(1.0f, 14 - ex);
+  *unscale = 1.0f / wscale;
+  const int N32 = (N + 31) / 32;
+  const size_t total = (size_t)(K + 15) / 16 * N32 * 64;
+  hipLaunchKernelGGL(pack_fc_x3_kernel, dim3((total + 255) / 256), dim3(256), 0, st, W, static_cast<f16x8*>(out),
+                     K, N, N32, total, wscale);
+  return hipGetLastError();
+}
+
+hipError_t launch_fc_gemm_x3(const float* A, int lda, const void* Wpk, float unscale, float* part, int M, int K,
+                             int N, int S, int kslice, hipStream_t st) {
+  const int N32 = (N + 31) / 32;
+  dim3 grid((M + FC_BM - 1) / FC_BM, (N32 + 3) / 4, S);
+  hipLaunchKernelGGL(fc_gemm_x3_kernel, grid, dim3(256), 0, st, A, lda, static_cast<const f16x8*>(Wpk), part, M, K,
+                     N32, kslice, unscale);
+  return hipGetLastError();
 }
 
 hipError_t launch_pack_fc(const float* W, f32x4* out, int K, int N, hipStream_t st) {

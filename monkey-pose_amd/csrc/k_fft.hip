@@ -646,6 +646,21 @@ __global__ __launch_bounds__(256) void spec_epi_kernel(ConvArgs p, const float* 
 
 // ------------------------------------------------------------------------------------ launchers
 size_t fft_spec_bytes(int B) { return (size_t)B * 16 * NF * 4 * sizeof(cpx); }
+hipError_t device_absmax(const float* x, size_t n, float* out) {
+  unsigned* mx = nullptr;
+  hipError_t e = hipMalloc(&mx, sizeof(unsigned));
+  if (e == hipSuccess) e = hipMemset(mx, 0, sizeof(unsigned));
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(absmax_kernel, dim3(1024), dim3(256), 0, 0, x, n, mx);
+    e = hipGetLastError();
+  }
+  unsigned bits = 0;
+  if (e == hipSuccess) e = hipMemcpy(&bits, mx, sizeof(unsigned), hipMemcpyDeviceToHost);
+  if (mx) (void)hipFree(mx);
+  std::memcpy(out, &bits, sizeof bits);
+  return e;
+}
+
 size_t fft_weight_bytes() { return (size_t)NF * 2 * 16 * 64 * sizeof(f16x8); }
 
 hipError_t build_spec_weights(const float* w, int ks, void* Gx, float* unscale) {

@@ -66,6 +66,20 @@ std::vector<float> vec64(mp_ctx* c, const std::string& n) {
   return c->need("contextual_circuit/" + n, {1, 1, 1, 64}).host;
 }
 
+// backbone activations (BN outputs) are not tanh-bounded like the hGRU maps: split them at 2^4
+constexpr float BB_ASCALE = 16.0f;
+
+// HWIO [ks][ks][64][64] -> f16x3 fragments with a power-of-two scale putting max|w| at 2^13..2^14
+void pack_x3(const RawWeight& w, DevBuf& out, int ks, float ascale, float* unscale, const char* what) {
+  float mx = 0.f;
+  hip_check(device_absmax(w.dev->f(), w.numel(), &mx), what);
+  int e = 0;
+  if (mx > 0.f) std::frexp(mx, &e);
+  const float wscale = std::ldexp(1.0f, 14 - e);
+  *unscale = 1.0f / (wscale * ascale);
+  hip_check(launch_pack_conv64x3(w.dev->f(), out.p, ks, wscale, nullptr), what);
+}
+
 void finalize_circuit(mp_ctx* c, const std::vector<float>* outs, const std::vector<float>* outt) {
   auto it = c->raw.find("contextual_circuit/p_r");
   if (it == c->raw.end()) fail(MP_ERR_STATE, "weight not set: contextual_circuit/p_r");
@@ -76,17 +90,7 @@ void finalize_circuit(mp_ctx* c, const std::vector<float>* outs, const std::vect
   c->ssf = (int)ps[0];
   c->p_pk.alloc((size_t)8 * c->ssf * c->ssf * 2 * 64 * 16);
   if (c->dtype == MP_DTYPE_F32_SPLIT) {
-    // power-of-two weight scale putting max|p_r| at 2^13..2^14 (f16 max is 65504)
-    std::vector<float> hw(it->second.numel());
-    hip_check(hipMemcpy(hw.data(), it->second.dev->p, hw.size() * sizeof(float), hipMemcpyDeviceToHost),
-              "hipMemcpy p_r");
-    float mx = 0.f;
-    for (float v : hw) mx = std::max(mx, std::fabs(v));
-    int e = 0;
-    if (mx > 0.f) std::frexp(mx, &e);   // mx = f * 2^e, f in [0.5, 1)
-    const float wscale = std::ldexp(1.0f, 14 - e);
-    c->p_unscale = 1.0f / (wscale * 1024.0f);   // activations are scaled by 2^10 in the kernel
-    hip_check(launch_pack_conv64x3(it->second.dev->f(), c->p_pk.p, c->ssf, wscale, nullptr), "pack p_r (f16x3)");
+    pack_x3(it->second, c->p_pk, c->ssf, 1024.0f, &c->p_unscale, "pack p_r (f16x3)");
   } else if (c->dtype == MP_DTYPE_F32_FFT) {
     c->spec_g.alloc(fft_weight_bytes());
     hip_check(build_spec_weights(it->second.dev->f(), c->ssf, c->spec_g.p, &c->p_unscale), "p_r spectrum");
@@ -128,12 +132,19 @@ void finalize_pose(mp_ctx* c) {
   copy_dev(c->conv1_w, c->need("conv_1/conv_1_filters", {3, 3, 1, k}));
   copy_dev(c->conv1_b, c->need("conv_1/conv_1_biases", {k}));
   bn_fold(c, "batch_normalization", k, c->bn0_s, c->bn0_t);
-  c->conv2_pk.alloc((size_t)8 * 9 * 2 * 64 * 16);
-  c->conv3_pk.alloc((size_t)8 * 9 * 2 * 64 * 16);
-  hip_check(launch_pack_conv64(c->need("conv_2/conv_2_filters", {3, 3, k, k}).dev->f(), c->conv2_pk.v4(), 3, nullptr),
-            "pack conv_2");
-  hip_check(launch_pack_conv64(c->need("conv_3/conv_3_filters", {3, 3, k, k}).dev->f(), c->conv3_pk.v4(), 3, nullptr),
-            "pack conv_3");
+  if (c->dtype == MP_DTYPE_F32) {
+    c->conv2_pk.alloc((size_t)8 * 9 * 2 * 64 * 16);
+    c->conv3_pk.alloc((size_t)8 * 9 * 2 * 64 * 16);
+    hip_check(launch_pack_conv64(c->need("conv_2/conv_2_filters", {3, 3, k, k}).dev->f(), c->conv2_pk.v4(), 3, nullptr),
+              "pack conv_2");
+    hip_check(launch_pack_conv64(c->need("conv_3/conv_3_filters", {3, 3, k, k}).dev->f(), c->conv3_pk.v4(), 3, nullptr),
+              "pack conv_3");
+  } else {   // fp32-accurate f16x3 backbone convs (k_conv64x3.hip, BB epilogue)
+    c->conv2_pk.alloc((size_t)8 * 9 * 2 * 64 * 16);
+    c->conv3_pk.alloc((size_t)8 * 9 * 2 * 64 * 16);
+    pack_x3(c->need("conv_2/conv_2_filters", {3, 3, k, k}), c->conv2_pk, 3, BB_ASCALE, &c->conv2_us, "pack conv_2");
+    pack_x3(c->need("conv_3/conv_3_filters", {3, 3, k, k}), c->conv3_pk, 3, BB_ASCALE, &c->conv3_us, "pack conv_3");
+  }
   copy_dev(c->conv2_b, c->need("conv_2/conv_2_biases", {k}));
   copy_dev(c->conv3_b, c->need("conv_3/conv_3_biases", {k}));
   bn_fold(c, "batch_normalization_1", k, c->bn1_s, c->bn1_t);
@@ -150,8 +161,14 @@ void finalize_pose(mp_ctx* c) {
   c->fc1_in = (int)f1->second.shape[0];
   c->fc1_out = (int)f1->second.shape[1];
   const int K8 = (c->fc1_in + 7) / 8, N32 = (c->fc1_out + 31) / 32;
-  c->fc1_pk.alloc((size_t)K8 * N32 * 64 * 16);
-  hip_check(launch_pack_fc(f1->second.dev->f(), c->fc1_pk.v4(), c->fc1_in, c->fc1_out, nullptr), "pack fc_1");
+  if (c->dtype == MP_DTYPE_F32) {
+    c->fc1_pk.alloc((size_t)K8 * N32 * 64 * 16);
+    hip_check(launch_pack_fc(f1->second.dev->f(), c->fc1_pk.v4(), c->fc1_in, c->fc1_out, nullptr), "pack fc_1");
+  } else {   // fp32-accurate f16x3 (same slabs, same batch invariance)
+    c->fc1_pk.alloc(fc_x3_bytes(c->fc1_in, c->fc1_out));
+    hip_check(launch_pack_fc_x3(f1->second.dev->f(), c->fc1_pk.p, c->fc1_in, c->fc1_out, &c->fc1_unscale, nullptr),
+              "pack fc_1 (f16x3)");
+  }
   copy_dev(c->fc1_b, c->need("fc_1/fc_1_biases", {c->fc1_out}));
   bn_fold(c, "batch_normalization_4", c->fc1_out, c->bn4_s, c->bn4_t);
   auto fo = c->raw.find("fc_out/fc_out_weights");
@@ -420,22 +437,31 @@ int mp_hgru_pose_fwd(mp_ctx* ctx, const float* depth, int64_t n, int64_t h, int6
       a.bias = ctx->conv2_b.f();
       a.bn_s = ctx->bn1_s.f();
       a.bn_t = ctx->bn1_t.f();
-      hip_check(launch_conv64(3, EPI_BB, a, N, st), "conv_2");
+      const bool x3 = ctx->dtype != MP_DTYPE_F32 && H % TH3 == 0;
+      if (x3) a.ascale = BB_ASCALE;
+      hip_check(x3 ? launch_conv64x3(3, EPI_BB, a, ctx->conv2_pk.p, ctx->conv2_us, N, st)
+                   : launch_conv64(3, EPI_BB, a, N, st),
+                "conv_2");
       a.src = ctx->bufB.f();
       a.wpk = ctx->conv3_pk.v4();
       a.dst = ctx->X.f();
       a.bias = ctx->conv3_b.f();
       a.bn_s = ctx->bn2_s.f();
       a.bn_t = ctx->bn2_t.f();
-      hip_check(launch_conv64(3, EPI_BB, a, N, st), "conv_3");
+      hip_check(x3 ? launch_conv64x3(3, EPI_BB, a, ctx->conv3_pk.p, ctx->conv3_us, N, st)
+                   : launch_conv64(3, EPI_BB, a, N, st),
+                "conv_3");
     }
     run_circuit(ctx, n, H, W, ctx->timesteps, o0, ctx->fcin.f(), st);
     {
       ProfScope ps(ctx, st, "fc1");
       int ks;
       const int S = fc_choose_splits(N, ctx->fc1_in, ctx->fc1_out, &ks);
-      hip_check(launch_fc_gemm(ctx->fcin.f(), ctx->fc1_in, ctx->fc1_pk.v4(), ctx->part.f(), N, ctx->fc1_in,
-                               ctx->fc1_out, S, ks, st),
+      hip_check(ctx->dtype == MP_DTYPE_F32
+                    ? launch_fc_gemm(ctx->fcin.f(), ctx->fc1_in, ctx->fc1_pk.v4(), ctx->part.f(), N, ctx->fc1_in,
+                                     ctx->fc1_out, S, ks, st)
+                    : launch_fc_gemm_x3(ctx->fcin.f(), ctx->fc1_in, ctx->fc1_pk.p, ctx->fc1_unscale, ctx->part.f(),
+                                        N, ctx->fc1_in, ctx->fc1_out, S, ks, st),
                 "fc_1 gemm");
       hip_check(launch_fc_reduce(ctx->part.f(), S, N, ctx->fc1_out, ctx->fc1_b.f(), 1, ctx->bn4_s.f(),
                                  ctx->bn4_t.f(), ctx->h1.f(), ctx->fc1_out, st),

@@ -26,6 +26,7 @@ struct ConvArgs {
   float rho;              // B: rho[t]
   int mode;               // B: 0 = next-step gate, 1 = final step
   int H, W, tiles_x, tiles_y;
+  float ascale;           // f16x3 kernel: activation split scale (0 = the hGRU default 2^10)
 };
 
 // k_conv64.hip
@@ -44,6 +45,7 @@ hipError_t launch_conv64x3(int ks, int epi, ConvArgs a, const void* wpk, float u
 hipError_t launch_pack_conv64x3(const float* w, void* out, int ks, float wscale, hipStream_t st);
 // k_fft.hip (FFT path of the association-field conv, MP_DTYPE_F32_FFT; maps up to 64x64)
 constexpr int FFT_MAX_HW = 64;
+hipError_t device_absmax(const float* x, size_t n, float* out);   // max |x| (synchronous)
 size_t fft_spec_bytes(int B);      // one spectrum buffer (S or Y) for B images
 size_t fft_weight_bytes();         // expanded split spectral weights
 // HWIO [ks][ks][64][64] -> packed split spectral weights (synchronous, finalize time)
@@ -80,6 +82,11 @@ hipError_t launch_pack_fc(const float* W, f32x4* out, int K, int N, hipStream_t 
 int fc_choose_splits(int M, int K, int N, int* kslice);
 hipError_t launch_fc_gemm(const float* A, int lda, const f32x4* Wpk, float* part, int M, int K, int N, int S,
                           int kslice, hipStream_t st);
+// f16x3 (fp32-accurate) fc GEMM, same slabs / splits as launch_fc_gemm
+size_t fc_x3_bytes(int K, int N);
+hipError_t launch_pack_fc_x3(const float* W, void* out, int K, int N, float* unscale, hipStream_t st);
+hipError_t launch_fc_gemm_x3(const float* A, int lda, const void* Wpk, float unscale, float* part, int M, int K,
+                             int N, int S, int kslice, hipStream_t st);
 hipError_t launch_fc_reduce(const float* part, int S, int M, int N, const float* bias, int relu,
                             const float* aff_s, const float* aff_t, float* out, int ldo, hipStream_t st);
 

@@ -117,12 +117,14 @@ struct mp_ctx {
   std::vector<float> rho;
   DevBuf conv1_w, conv1_b, bn0_s, bn0_t;
   DevBuf conv2_pk, conv2_b, bn1_s, bn1_t;
+  float conv2_us = 1.f, conv3_us = 1.f;   // backbone packed f16x3 (dtype != F32): 1 / (wscale * BB_ASCALE)
   DevBuf conv3_pk, conv3_b, bn2_s, bn2_t;
   DevBuf p_pk, ir_pk, or_pk, vecs;
   DevBuf spec_g;            // MP_DTYPE_F32_FFT: compact split spectral weights of p_r (k_fft.hip)
   DevBuf or_x3, ir_x3;      // MP_DTYPE_F32_FFT: o_r / i_r packed for the f16x3 gate GEMMs
   float or_us = 1.f, ir_us = 1.f;
   DevBuf fc1_pk, fc1_b, bn4_s, bn4_t, fco_pk, fco_b;
+  float fc1_unscale = 1.f;   // fc_1 packed f16x3 (dtype F32_SPLIT / F32_FFT): 1 / weight scale
 
   // ---- workspace ----
   int64_t cap_batch = 0;

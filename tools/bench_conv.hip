@@ -38,6 +38,7 @@ struct Variant {
 template <int EPI, int NW, int SCHED>
 hipError_t run_v(const ConvArgs& a0, const void* w, float us, int B, hipStream_t st) {
   ConvArgs a = a0;
+  a.ascale = ACT_SCALE;
   a.tiles_x = a.W / TW;
   a.tiles_y = a.H / TH3;
   return launch_x3_t<15, EPI, NW, SCHED>(a, w, us, B, st);
