@@ -236,7 +236,15 @@ __device__ __forceinline__ void inv_row_from_T(const cpx* T, int y, int p, cpx (
   fft72<1>(v);
 }
 
-// forward 2-D FFT of one C8 activation map -> S
+// Rows of the block's 4-channel tile are "parked" in LDS (T's space) between the row transforms
+// and global memory: R[(2y + p) * RLD + x] = channels (2p, 2p+1) of pixel (y, x).  Global reads and
+// writes of the activation maps then run pixel-major (lane = pixel, one 16-byte float4 of 4
+// channels), instead of one strided 8-byte access per row thread.
+constexpr int RLD = 73;
+
+// forward 2-D FFT of one C8 activation map -> S.  The rows are read straight into registers (64
+// independent 8-byte loads in flight per thread): staging the tile through LDS pixel-major measured
+// slower (0.24 vs 0.18 ms at B = 256) -- the load pass and its barrier serialise ahead of the FFT.
 __global__ __launch_bounds__(192, 2) void fft_fwd_kernel(const float* __restrict__ src, void* __restrict__ S,
                                                       int H, int W) {
   __shared__ cpx T[FFT_LDS];
@@ -271,27 +279,31 @@ __global__ __launch_bounds__(192, 2) void fft_inv_kernel(const cpx* __restrict__
   const int tid = threadIdx.x;
   inv_cols_to_T(Y, b, cq, tid, T);
   __syncthreads();
-  if (tid < 128) {
-    const int y = tid >> 1, p = tid & 1;
-    if (y < H) {
-      cpx v[72];
-      inv_row_from_T(T, y, p, v);
-      float* row = P + c8_index(b, q, y, 0, e0 + 2 * p, H, W);
+  const int y = tid >> 1, p = tid & 1;
+  const bool live = tid < 128 && y < H;
+  {
+    cpx v[72];
+    if (live) inv_row_from_T(T, y, p, v);
+    __syncthreads();   // every inverse row has read T
+    if (live) {
 #pragma unroll
-      for (int x = 0; x < 32; ++x) *reinterpret_cast<float2*>(row + 8 * x) = make_float2(v[x].x, v[x].y);
-      if (W > 32) {   // W is 32 or 64 (uniform branch; per-x predicates double the live registers)
-#pragma unroll
-        for (int x = 32; x < 64; ++x) *reinterpret_cast<float2*>(row + 8 * x) = make_float2(v[x].x, v[x].y);
-      }
+      for (int x = 0; x < 64; ++x) T[tid * RLD + x] = v[x];
     }
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int i = tid; i < H * W; i += 192) {
+    const int yy = i / W, x = i - yy * W;
+    const cpx a = T[(2 * yy) * RLD + x], c = T[(2 * yy + 1) * RLD + x];
+    *reinterpret_cast<f32x4*>(P + c8_index(b, q, yy, x, e0, H, W)) = f32x4{a.x, a.y, c.x, c.y};
   }
 }
 
 // The A half-step's tail and the B half-step's head in one pass (hgru_module.py:657, 797-799):
 //   P1 = IFFT(Y)  ->  I = tanh(X - (beta*O + nu) * (P1 + lateral_bias))  ->  S = FFT(I)
-// The inverse row phase leaves each thread with one output row of two channels -- exactly the
-// packed row the forward row phase transforms -- so P1 never leaves registers and I is written
-// once (the B epilogue reads it).  p: the A-epilogue arguments (X, O, vecs; dst = I).
+// P1 never leaves the block: the inverse rows are parked in LDS, the epilogue runs pixel-major
+// over them (X, O in, I out: one float4 per lane), and the parked I rows are the forward row
+// transform's input.  p: the A-epilogue arguments (X, O, vecs; dst = I).
 __global__ __launch_bounds__(192, 2) void fft_inv_a_fwd_kernel(const cpx* __restrict__ Y, ConvArgs p,
                                                             void* __restrict__ S) {
   __shared__ cpx T[FFT_LDS];
@@ -303,40 +315,50 @@ __global__ __launch_bounds__(192, 2) void fft_inv_a_fwd_kernel(const cpx* __rest
   __syncthreads();
   const int y = tid >> 1, pp = tid & 1;
   const bool live = tid < 128 && y < H;
-  cpx v[72];
-  if (live) inv_row_from_T(T, y, pp, v);
-  __syncthreads();   // every inverse row has read T
-  // park the row in LDS (own slot, pitch 73) so the epilogue does not hold v[] beside its loads
-  cpx* R = T + tid * 73;
-  if (live) {
+  {
+    cpx v[72];
+    if (live) inv_row_from_T(T, y, pp, v);
+    __syncthreads();   // every inverse row has read T
+    if (live) {
 #pragma unroll
-    for (int x = 0; x < 64; ++x) R[x] = v[x];
-    const int ch = 8 * q + e0 + 2 * pp;
-    const float2 lat = *reinterpret_cast<const float2*>(p.vecs + V_LAT * 64 + ch);
-    const float2 be = *reinterpret_cast<const float2*>(p.vecs + V_BETA * 64 + ch);
-    const float2 nu = *reinterpret_cast<const float2*>(p.vecs + V_NU * 64 + ch);
-    const size_t r0 = c8_index(b, q, y, 0, e0 + 2 * pp, H, W);
-#pragma unroll 8
-    for (int x = 0; x < W; ++x) {   // W is 32 or 64: 8 iterations' loads in flight at a time
-      const float2 xv = *reinterpret_cast<const float2*>(p.X + r0 + 8 * x);
-      const float2 ov = *reinterpret_cast<const float2*>(p.O + r0 + 8 * x);
-      const cpx pv = R[x];
-      const float i0 = tanhf(xv.x - (be.x * ov.x + nu.x) * (pv.x + lat.x));
-      const float i1 = tanhf(xv.y - (be.y * ov.y + nu.y) * (pv.y + lat.y));
-      *reinterpret_cast<float2*>(p.dst + r0 + 8 * x) = make_float2(i0, i1);
-      R[x] = {i0, i1};
+      for (int x = 0; x < 64; ++x) T[tid * RLD + x] = v[x];
     }
-#pragma unroll
-    for (int x = 0; x < 72; ++x) v[x] = x < 64 ? R[x] : cpx{0.f, 0.f};
-    if (W <= 32) {   // uniform; columns >= W of the slot hold stale values
-#pragma unroll
-      for (int x = 32; x < 64; ++x) v[x] = {0.f, 0.f};
-    }
-  } else {
-#pragma unroll
-    for (int x = 0; x < 72; ++x) v[x] = {0.f, 0.f};
   }
-  __syncthreads();   // every row is back in registers: T's space is free
+  __syncthreads();
+  {
+    const int ch = 8 * q + e0;
+    const f32x4 lat = *reinterpret_cast<const f32x4*>(p.vecs + V_LAT * 64 + ch);
+    const f32x4 be = *reinterpret_cast<const f32x4*>(p.vecs + V_BETA * 64 + ch);
+    const f32x4 nu = *reinterpret_cast<const f32x4*>(p.vecs + V_NU * 64 + ch);
+#pragma unroll 4
+    for (int i = tid; i < 64 * 64; i += 192) {   // zero padding to 64 x 64 included
+      const int yy = i >> 6, x = i & 63;
+      cpx& ra = T[(2 * yy) * RLD + x];
+      cpx& rc = T[(2 * yy + 1) * RLD + x];
+      if (yy < H && x < W) {
+        const size_t idx = c8_index(b, q, yy, x, e0, H, W);
+        const f32x4 xv = *reinterpret_cast<const f32x4*>(p.X + idx);
+        const f32x4 ov = *reinterpret_cast<const f32x4*>(p.O + idx);
+        const f32x4 pv = {ra.x, ra.y, rc.x, rc.y};
+        f32x4 iv;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) iv[j] = tanhf(xv[j] - (be[j] * ov[j] + nu[j]) * (pv[j] + lat[j]));
+        *reinterpret_cast<f32x4*>(p.dst + idx) = iv;
+        ra = {iv[0], iv[1]};
+        rc = {iv[2], iv[3]};
+      } else {
+        ra = {0.f, 0.f};
+        rc = {0.f, 0.f};
+      }
+    }
+  }
+  __syncthreads();
+  cpx v[72];
+  if (tid < 128) {
+#pragma unroll
+    for (int x = 0; x < 72; ++x) v[x] = x < 64 ? T[tid * RLD + x] : cpx{0.f, 0.f};
+  }
+  __syncthreads();   // parked rows read: T's space is free
   if (tid < 128) fwd_rows_to_T(v, y, pp, T);
   __syncthreads();
   fwd_cols_to_S(T, S, b, cq, tid);

@@ -71,11 +71,24 @@ int main(int argc, char** argv) {
   hipEvent_t e0, e1;
   CK(hipEventCreate(&e0));
   CK(hipEventCreate(&e1));
-  std::vector<float> tf, tg, ti;
+  float* X = dalloc_rand((size_t)B * 64 * H * W, g, -1.f, 1.f);
+  float* O = dalloc_rand((size_t)B * 64 * H * W, g, -1.f, 1.f);
+  float* I;
+  CK(hipMalloc(&I, (size_t)B * 64 * H * W * sizeof(float)));
+  float* vecs = dalloc_rand(V_COUNT * 64, g, 0.5f, 1.f);
+  ConvArgs a{};
+  a.H = H;
+  a.W = W;
+  a.X = X;
+  a.O = O;
+  a.dst = I;
+  a.vecs = vecs;
+  std::vector<float> tf, tg, ti, ta;
   for (int r = 0; r < rounds; ++r) {
     tf.push_back(time_ms([&] { return launch_fft_fwd(act, S, B, H, W, 0); }, e0, e1, 10));
     tg.push_back(time_ms([&] { return launch_spec_gemm(S, Gx, Y, B, unscale, 0); }, e0, e1, 10));
     ti.push_back(time_ms([&] { return launch_fft_inv(Y, P, B, H, W, 0); }, e0, e1, 10));
+    ta.push_back(time_ms([&] { return launch_fft_inv_a_fwd(Y, a, S, B, 0); }, e0, e1, 10));
   }
   auto med = [](std::vector<float> x) {
     std::sort(x.begin(), x.end());
@@ -86,6 +99,8 @@ int main(int argc, char** argv) {
   printf("  {\"name\": \"fft_fwd\", \"median_ms\": %.4f, \"GBps\": %.1f},\n", med(tf), (spec + actb) / med(tf) / 1e6);
   printf("  {\"name\": \"spec_gemm\", \"median_ms\": %.4f, \"GBps\": %.1f},\n", med(tg),
          (2 * spec + (double)fft_weight_bytes()) / med(tg) / 1e6);
-  printf("  {\"name\": \"fft_inv\", \"median_ms\": %.4f, \"GBps\": %.1f}\n]}\n", med(ti), (spec + actb) / med(ti) / 1e6);
+  printf("  {\"name\": \"fft_inv\", \"median_ms\": %.4f, \"GBps\": %.1f},\n", med(ti), (spec + actb) / med(ti) / 1e6);
+  printf("  {\"name\": \"inv_a_fwd\", \"median_ms\": %.4f, \"GBps\": %.1f}\n]}\n", med(ta),
+         (2 * spec + 3 * actb) / med(ta) / 1e6);
   return 0;
 }
