@@ -330,25 +330,37 @@ __global__ __launch_bounds__(192, 2) void fft_inv_a_fwd_kernel(const cpx* __rest
     const f32x4 lat = *reinterpret_cast<const f32x4*>(p.vecs + V_LAT * 64 + ch);
     const f32x4 be = *reinterpret_cast<const f32x4*>(p.vecs + V_BETA * 64 + ch);
     const f32x4 nu = *reinterpret_cast<const f32x4*>(p.vecs + V_NU * 64 + ch);
-#pragma unroll 4
-    for (int i = tid; i < 64 * 64; i += 192) {   // zero padding to 64 x 64 included
-      const int yy = i >> 6, x = i & 63;
-      cpx& ra = T[(2 * yy) * RLD + x];
-      cpx& rc = T[(2 * yy + 1) * RLD + x];
-      if (yy < H && x < W) {
-        const size_t idx = c8_index(b, q, yy, x, e0, H, W);
-        const f32x4 xv = *reinterpret_cast<const f32x4*>(p.X + idx);
-        const f32x4 ov = *reinterpret_cast<const f32x4*>(p.O + idx);
-        const f32x4 pv = {ra.x, ra.y, rc.x, rc.y};
-        f32x4 iv;
+    // 64 x 64 pixels (zero padding included) in chunks of 8 per thread: the X / O loads of a
+    // chunk are unconditional (clamped addresses) so all 16 are in flight together
+    for (int i0 = 0; i0 < 64 * 64; i0 += 8 * 192) {
+      f32x4 xv[8], ov[8];
 #pragma unroll
-        for (int j = 0; j < 4; ++j) iv[j] = tanhf(xv[j] - (be[j] * ov[j] + nu[j]) * (pv[j] + lat[j]));
-        *reinterpret_cast<f32x4*>(p.dst + idx) = iv;
-        ra = {iv[0], iv[1]};
-        rc = {iv[2], iv[3]};
-      } else {
-        ra = {0.f, 0.f};
-        rc = {0.f, 0.f};
+      for (int u = 0; u < 8; ++u) {
+        const int i = min(i0 + u * 192 + tid, 64 * 64 - 1);
+        const int yy = min(i >> 6, H - 1), x = min(i & 63, W - 1);
+        const size_t idx = c8_index(b, q, yy, x, e0, H, W);
+        xv[u] = *reinterpret_cast<const f32x4*>(p.X + idx);
+        ov[u] = *reinterpret_cast<const f32x4*>(p.O + idx);
+      }
+#pragma unroll
+      for (int u = 0; u < 8; ++u) {
+        const int i = i0 + u * 192 + tid;
+        if (i >= 64 * 64) break;
+        const int yy = i >> 6, x = i & 63;
+        cpx& ra = T[(2 * yy) * RLD + x];
+        cpx& rc = T[(2 * yy + 1) * RLD + x];
+        if (yy < H && x < W) {
+          const f32x4 pv = {ra.x, ra.y, rc.x, rc.y};
+          f32x4 iv;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) iv[j] = tanhf(xv[u][j] - (be[j] * ov[u][j] + nu[j]) * (pv[j] + lat[j]));
+          *reinterpret_cast<f32x4*>(p.dst + c8_index(b, q, yy, x, e0, H, W)) = iv;
+          ra = {iv[0], iv[1]};
+          rc = {iv[2], iv[3]};
+        } else {
+          ra = {0.f, 0.f};
+          rc = {0.f, 0.f};
+        }
       }
     }
   }
@@ -383,6 +395,8 @@ constexpr int SG_NI = 32;              // images per block
 constexpr int NQUAD = NF / 4;          // 666 frequency quads
 constexpr int SG_SLD = 33;             // S tile pitch (16-B units) per (cq, part, f) row
 constexpr int SG_YLD = 16 * 4 * 2 + 1; // Y tile pitch (16-B units) per image
+template <int PROBE = 0>   // timing probes (tools/bench_fft.hip): 1 = no MFMA, 2 = no S / weight loads,
+                           // 3 = no weight loads, 4 = no S loads
 __global__ __launch_bounds__(256, 2) void spec_gemm_kernel(const uint4* __restrict__ S, const uint4* __restrict__ Gc,
                                                            uint4* __restrict__ Y, int B, int ngrp, float unscale) {
   __shared__ uint4 tile[16 * 2 * 4 * SG_SLD];   // 67,584 B
@@ -393,17 +407,34 @@ __global__ __launch_bounds__(256, 2) void spec_gemm_kernel(const uint4* __restri
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, j = lane & 31;
   const int img0 = grp * SG_NI;
   // ---- S tile: 32 images x 16 cq lines of 128 B (4 f x [hi 16 B | lo 16 B]) ----
+  // unconditional loads from clamped addresses: a per-lane "b < B ? load : 0" branch made the
+  // compiler wait for each of the 16 loads before issuing the next
+  uint4 pre[16];
+#pragma unroll
+  for (int it = 0; it < 16; ++it) {
+    const int idx = it * 256 + tid, line = idx >> 3, piece = idx & 7;
+    const int bl = line >> 4, cq = line & 15;
+    const int b = min(img0 + bl, B - 1);
+    pre[it] = S[(PROBE == 2 || PROBE == 4) ? (tid & 63) : (((size_t)b * 16 + cq) * NF + 4 * quad) * 2 + piece];
+  }
+  // ---- weights of frequency f = 4 quad + wv: one f16x8 per (t, h, part, co block), all 32 issued
+  // before the S tile is waited for, so their L2 latency overlaps the tile's HBM latency ----
+  const int f = 4 * quad + wv;
+  const uint4* gw = Gc + ((PROBE == 2 || PROBE == 3) ? 0 : (size_t)f * 2 * 16 * 64);
+  uint4 wr[8][2][2];
+#pragma unroll
+  for (int t = 0; t < 8; ++t)
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      wr[t][cb][0] = gw[(0 * 16 + 2 * t + h) * 64 + 32 * cb + j];
+      wr[t][cb][1] = gw[(1 * 16 + 2 * t + h) * 64 + 32 * cb + j];
+    }
 #pragma unroll
   for (int it = 0; it < 16; ++it) {
     const int idx = it * 256 + tid, line = idx >> 3, piece = idx & 7;
     const int bl = line >> 4, cq = line & 15, f = piece >> 1, part = piece & 1;
-    const int b = img0 + bl;
-    const uint4 v = b < B ? S[(((size_t)b * 16 + cq) * NF + 4 * quad) * 2 + piece] : uint4{0, 0, 0, 0};
-    tile[((cq * 2 + part) * 4 + f) * SG_SLD + bl] = v;
+    tile[((cq * 2 + part) * 4 + f) * SG_SLD + bl] = img0 + bl < B ? pre[it] : uint4{0, 0, 0, 0};
   }
-  // ---- weights of frequency f = 4 quad + wv: one f16x8 per (t, h, part, co block) ----
-  const int f = 4 * quad + wv;
-  const uint4* gw = Gc + (size_t)f * 2 * 16 * 64;
   __syncthreads();
   f32x16 acc[4] = {};
   const uint4 m = {0x80000000u, 0x80000000u, 0x80000000u, 0x80000000u};
@@ -414,17 +445,21 @@ __global__ __launch_bounds__(256, 2) void spec_gemm_kernel(const uint4* __restri
     const f16x8 sl = __builtin_bit_cast(f16x8, tile[((cq * 2 + 1) * 4 + wv) * SG_SLD + j]);
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb) {
-      const uint4 gh = gw[(0 * 16 + cq) * 64 + 32 * cb + j], gl = gw[(1 * 16 + cq) * 64 + 32 * cb + j];
+      const uint4 gh = wr[t][cb][0], gl = wr[t][cb][1];
       // ro = 0 rows: (gr, -gi) pairs; ro = 1 rows: (gi, gr) pairs
       const f16x8 ah0 = __builtin_bit_cast(f16x8, gh ^ m), al0 = __builtin_bit_cast(f16x8, gl ^ m);
       const f16x8 ah1 = __builtin_bit_cast(f16x8, (gh >> 16) | (gh << 16));
       const f16x8 al1 = __builtin_bit_cast(f16x8, (gl >> 16) | (gl << 16));
-      acc[cb] = mfma16(al0, sh, acc[cb]);
-      acc[cb] = mfma16(ah0, sl, acc[cb]);
-      acc[cb] = mfma16(ah0, sh, acc[cb]);
-      acc[2 + cb] = mfma16(al1, sh, acc[2 + cb]);
-      acc[2 + cb] = mfma16(ah1, sl, acc[2 + cb]);
-      acc[2 + cb] = mfma16(ah1, sh, acc[2 + cb]);
+      if constexpr (PROBE == 1) {   // keep the operand loads alive, skip the matrix cores
+        acc[cb][0] += (float)(sh[0] + sl[0] + ah0[0] + al0[0] + ah1[1] + al1[1]);
+      } else {
+        acc[cb] = mfma16(al0, sh, acc[cb]);
+        acc[cb] = mfma16(ah0, sl, acc[cb]);
+        acc[cb] = mfma16(ah0, sh, acc[cb]);
+        acc[2 + cb] = mfma16(al1, sh, acc[2 + cb]);
+        acc[2 + cb] = mfma16(ah1, sl, acc[2 + cb]);
+        acc[2 + cb] = mfma16(ah1, sh, acc[2 + cb]);
+      }
     }
   }
   __syncthreads();   // every wave has read the S tile
@@ -730,7 +765,7 @@ hipError_t launch_fft_inv_a_fwd(const void* Y, const ConvArgs& a, void* S, int B
 hipError_t launch_spec_gemm(const void* S, const void* Gx, void* Y, int B, float unscale, hipStream_t st) {
   const int ngrp = (B + SG_NI - 1) / SG_NI;
   const int nq8 = (NQUAD + 7) / 8;
-  hipLaunchKernelGGL(spec_gemm_kernel, dim3(nq8 * 8 * ngrp), dim3(256), 0, st, static_cast<const uint4*>(S),
+  hipLaunchKernelGGL(spec_gemm_kernel<0>, dim3(nq8 * 8 * ngrp), dim3(256), 0, st, static_cast<const uint4*>(S),
                      static_cast<const uint4*>(Gx), static_cast<uint4*>(Y), B, ngrp, unscale);
   return hipGetLastError();
 }

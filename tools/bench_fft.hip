@@ -83,12 +83,26 @@ int main(int argc, char** argv) {
   a.O = O;
   a.dst = I;
   a.vecs = vecs;
-  std::vector<float> tf, tg, ti, ta;
+  std::vector<float> tf, tg, ti, ta, tp1, tp2, tp3, tp4;
+  const int ngrp = (B + SG_NI - 1) / SG_NI, nq8 = (NQUAD + 7) / 8;
+  auto probe = [&](int v) {
+#define PRB(K)                                                                                          \
+  if (v == K)                                                                                         \
+    hipLaunchKernelGGL(spec_gemm_kernel<K>, dim3(nq8 * 8 * ngrp), dim3(256), 0, 0, (const uint4*)S, \
+                       (const uint4*)Gx, (uint4*)Y, B, ngrp, unscale);
+    PRB(1) PRB(2) PRB(3) PRB(4)
+#undef PRB
+    return hipGetLastError();
+  };
   for (int r = 0; r < rounds; ++r) {
     tf.push_back(time_ms([&] { return launch_fft_fwd(act, S, B, H, W, 0); }, e0, e1, 10));
     tg.push_back(time_ms([&] { return launch_spec_gemm(S, Gx, Y, B, unscale, 0); }, e0, e1, 10));
     ti.push_back(time_ms([&] { return launch_fft_inv(Y, P, B, H, W, 0); }, e0, e1, 10));
     ta.push_back(time_ms([&] { return launch_fft_inv_a_fwd(Y, a, S, B, 0); }, e0, e1, 10));
+    tp1.push_back(time_ms([&] { return probe(1); }, e0, e1, 10));
+    tp2.push_back(time_ms([&] { return probe(2); }, e0, e1, 10));
+    tp3.push_back(time_ms([&] { return probe(3); }, e0, e1, 10));
+    tp4.push_back(time_ms([&] { return probe(4); }, e0, e1, 10));
   }
   auto med = [](std::vector<float> x) {
     std::sort(x.begin(), x.end());
@@ -100,7 +114,11 @@ int main(int argc, char** argv) {
   printf("  {\"name\": \"spec_gemm\", \"median_ms\": %.4f, \"GBps\": %.1f},\n", med(tg),
          (2 * spec + (double)fft_weight_bytes()) / med(tg) / 1e6);
   printf("  {\"name\": \"fft_inv\", \"median_ms\": %.4f, \"GBps\": %.1f},\n", med(ti), (spec + actb) / med(ti) / 1e6);
-  printf("  {\"name\": \"inv_a_fwd\", \"median_ms\": %.4f, \"GBps\": %.1f}\n]}\n", med(ta),
+  printf("  {\"name\": \"inv_a_fwd\", \"median_ms\": %.4f, \"GBps\": %.1f},\n", med(ta),
          (2 * spec + 3 * actb) / med(ta) / 1e6);
+  printf("  {\"name\": \"PROBE gemm no-MFMA\", \"median_ms\": %.4f},\n", med(tp1));
+  printf("  {\"name\": \"PROBE gemm no-S/W-loads\", \"median_ms\": %.4f},\n", med(tp2));
+  printf("  {\"name\": \"PROBE gemm no-W-loads\", \"median_ms\": %.4f},\n", med(tp3));
+  printf("  {\"name\": \"PROBE gemm no-S-loads\", \"median_ms\": %.4f}\n]}\n", med(tp4));
   return 0;
 }
