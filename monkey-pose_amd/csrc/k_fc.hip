@@ -152,6 +152,9 @@ __global__ void pack_fc_x3_kernel(const float* __restrict__ W, f16x8* out, int K
 
 constexpr int FCX_LD = FC_BK + 8;   // f16 pitch of the hi / lo activation planes (+16 B: conflict-free)
 
+// K steps are software-pipelined one step ahead: the activation float4s and the weight fragments
+// of step k+1 are loaded into registers while step k's MFMAs run; loads are unconditional (row
+// index clamped, K a multiple of FC_BK), so all eight loads of a step are in flight together.
 __global__ __launch_bounds__(256) void fc_gemm_x3_kernel(const float* __restrict__ A, int lda,
                                                          const f16x8* __restrict__ Wpk,
                                                          float* __restrict__ part, int M, int K,
@@ -163,44 +166,66 @@ __global__ __launch_bounds__(256) void fc_gemm_x3_kernel(const float* __restrict
   const int Npad = N32 * 32;
   const int nb = ntile * 4 + wv;
   const bool wave_on = nb < N32;   // wave-uniform
+  const int nbc = min(nb, N32 - 1);
   const int kbeg = split * kslice;
   const int kend = min(K, kbeg + kslice);
+
+  auto load_act = [&](int k0, f32x4 (&v)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = tid + i * 256, row = e >> 3, k4 = (e & 7) * 4;
+      const int gm = mt * FC_BM + row;   // K % FC_BK == 0 (launcher): every step is interior
+      v[i] = *reinterpret_cast<const f32x4*>(A + (size_t)min(gm, M - 1) * lda + k0 + k4);
+      if (gm >= M) v[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto load_w = [&](int k0, f16x8 (&w)[FC_BK / 16][2]) {
+#pragma unroll
+    for (int g = 0; g < FC_BK / 16; ++g) {
+      const int kb = min((k0 >> 4) + g, K16 - 1);
+      const f16x8* wp = Wpk + (((size_t)kb * N32 + nbc) * 2) * 64 + lane;
+      w[g][0] = wp[0];
+      w[g][1] = wp[64];
+    }
+  };
 
   f32x16 acc[4];
 #pragma unroll
   for (int m = 0; m < 4; ++m) acc[m] = f32x16{};
-
+  f32x4 av[4];
+  f16x8 wn[FC_BK / 16][2];
+  if (kbeg < kend) {
+    load_act(kbeg, av);
+    load_w(kbeg, wn);
+  }
   for (int k0 = kbeg; k0 < kend; k0 += FC_BK) {
-    __syncthreads();
+    lds_barrier();   // the previous step's LDS reads are done
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
-      const int e = tid + i * 256;          // 0..1023 float4 slots: row = e / 8, k4 = e % 8
-      const int row = e >> 3, k4 = (e & 7) * 4;
-      const int gm = mt * FC_BM + row, gk = k0 + k4;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
-      if (gm < M) {
-        if (gk + 3 < kend) {
-          v = *reinterpret_cast<const f32x4*>(A + (size_t)gm * lda + gk);
-        } else {
-#pragma unroll
-          for (int s = 0; s < 4; ++s) v[s] = (gk + s < kend) ? A[(size_t)gm * lda + gk + s] : 0.f;
-        }
-      }
+      const int e = tid + i * 256, row = e >> 3, k4 = (e & 7) * 4;
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        const _Float16 hh = (_Float16)v[s];
+        const _Float16 hh = (_Float16)av[i][s];
         Ah[row * FCX_LD + k4 + s] = hh;
-        Al[row * FCX_LD + k4 + s] = (_Float16)(v[s] - (float)hh);
+        Al[row * FCX_LD + k4 + s] = (_Float16)(av[i][s] - (float)hh);
       }
     }
-    __syncthreads();
+    f16x8 wc[FC_BK / 16][2];
+#pragma unroll
+    for (int g = 0; g < FC_BK / 16; ++g) {
+      wc[g][0] = wn[g][0];
+      wc[g][1] = wn[g][1];
+    }
+    if (k0 + FC_BK < kend) {   // prefetch the next step
+      load_act(k0 + FC_BK, av);
+      load_w(k0 + FC_BK, wn);
+    }
+    lds_barrier();
     if (wave_on) {
 #pragma unroll
       for (int g = 0; g < FC_BK / 16; ++g) {
-        const int kb = (k0 >> 4) + g;
-        if (kb >= K16) break;
-        const f16x8* wp = Wpk + (((size_t)kb * N32 + nb) * 2) * 64 + lane;
-        const f16x8 wh = wp[0], wl = wp[64];
+        if ((k0 >> 4) + g >= K16) break;
+        const f16x8 wh = wc[g][0], wl = wc[g][1];
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
           const int o = (m * 32 + col) * FCX_LD + 16 * g + 8 * h;
@@ -246,6 +271,7 @@ hipError_t launch_pack_fc_x3(const float* W, void* out, int K, int N, float* uns
 
 hipError_t launch_fc_gemm_x3(const float* A, int lda, const void* Wpk, float unscale, float* part, int M, int K,
                              int N, int S, int kslice, hipStream_t st) {
+  if (K % FC_BK || kslice % FC_BK || lda % 4) return hipErrorInvalidValue;
   const int N32 = (N + 31) / 32;
   dim3 grid((M + FC_BM - 1) / FC_BM, (N32 + 3) / 4, S);
   hipLaunchKernelGGL(fc_gemm_x3_kernel, grid, dim3(256), 0, st, A, lda, static_cast<const f16x8*>(Wpk), part, M, K,

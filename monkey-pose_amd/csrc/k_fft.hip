@@ -186,7 +186,7 @@ __device__ __forceinline__ void fwd_cols_to_S(cpx* T, void* __restrict__ S, int 
   uint4* dst = reinterpret_cast<uint4*>(S) + ((size_t)b * 16 + cq) * NF * 2;
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
-    __syncthreads();   // T (half 0) / the previous half's staging is no longer read
+    lds_barrier();   // T (half 0) / the previous half's staging is no longer read
     if (col) {
 #pragma unroll
       for (int j = 0; j < 36; ++j) {
@@ -198,7 +198,7 @@ __device__ __forceinline__ void fwd_cols_to_S(cpx* T, void* __restrict__ S, int 
         stg[fx * STG_LD + j * 8 + 4 + c] = __builtin_bit_cast(uint32_t, lv);
       }
     }
-    __syncthreads();
+    lds_barrier();
     // per fx: 36 groups x 32 B = 72 uint4 at f = fx*72 + 36*half
     for (int i = tid; i < FX * 72; i += 192) {
       const int ffx = i / 72, w = i - ffx * 72;
@@ -266,7 +266,7 @@ __global__ __launch_bounds__(192, 2) void fft_fwd_kernel(const float* __restrict
     }
     fwd_rows_to_T(v, y, p, T);
   }
-  __syncthreads();
+  lds_barrier();
   fwd_cols_to_S(T, S, b, cq, tid);
 }
 
@@ -278,19 +278,19 @@ __global__ __launch_bounds__(192, 2) void fft_inv_kernel(const cpx* __restrict__
   const int q = cq >> 1, e0 = 4 * (cq & 1);
   const int tid = threadIdx.x;
   inv_cols_to_T(Y, b, cq, tid, T);
-  __syncthreads();
+  lds_barrier();
   const int y = tid >> 1, p = tid & 1;
   const bool live = tid < 128 && y < H;
   {
     cpx v[72];
     if (live) inv_row_from_T(T, y, p, v);
-    __syncthreads();   // every inverse row has read T
+    lds_barrier();   // every inverse row has read T
     if (live) {
 #pragma unroll
       for (int x = 0; x < 64; ++x) T[tid * RLD + x] = v[x];
     }
   }
-  __syncthreads();
+  lds_barrier();
 #pragma unroll 4
   for (int i = tid; i < H * W; i += 192) {
     const int yy = i / W, x = i - yy * W;
@@ -312,19 +312,19 @@ __global__ __launch_bounds__(192, 2) void fft_inv_a_fwd_kernel(const cpx* __rest
   const int q = cq >> 1, e0 = 4 * (cq & 1);
   const int tid = threadIdx.x;
   inv_cols_to_T(Y, b, cq, tid, T);
-  __syncthreads();
+  lds_barrier();
   const int y = tid >> 1, pp = tid & 1;
   const bool live = tid < 128 && y < H;
   {
     cpx v[72];
     if (live) inv_row_from_T(T, y, pp, v);
-    __syncthreads();   // every inverse row has read T
+    lds_barrier();   // every inverse row has read T
     if (live) {
 #pragma unroll
       for (int x = 0; x < 64; ++x) T[tid * RLD + x] = v[x];
     }
   }
-  __syncthreads();
+  lds_barrier();
   {
     const int ch = 8 * q + e0;
     const f32x4 lat = *reinterpret_cast<const f32x4*>(p.vecs + V_LAT * 64 + ch);
@@ -364,15 +364,15 @@ __global__ __launch_bounds__(192, 2) void fft_inv_a_fwd_kernel(const cpx* __rest
       }
     }
   }
-  __syncthreads();
+  lds_barrier();
   cpx v[72];
   if (tid < 128) {
 #pragma unroll
     for (int x = 0; x < 72; ++x) v[x] = x < 64 ? T[tid * RLD + x] : cpx{0.f, 0.f};
   }
-  __syncthreads();   // parked rows read: T's space is free
+  lds_barrier();   // parked rows read: T's space is free
   if (tid < 128) fwd_rows_to_T(v, y, pp, T);
-  __syncthreads();
+  lds_barrier();
   fwd_cols_to_S(T, S, b, cq, tid);
 }
 
@@ -435,7 +435,7 @@ __global__ __launch_bounds__(256, 2) void spec_gemm_kernel(const uint4* __restri
     const int bl = line >> 4, cq = line & 15, f = piece >> 1, part = piece & 1;
     tile[((cq * 2 + part) * 4 + f) * SG_SLD + bl] = img0 + bl < B ? pre[it] : uint4{0, 0, 0, 0};
   }
-  __syncthreads();
+  lds_barrier();
   f32x16 acc[4] = {};
   const uint4 m = {0x80000000u, 0x80000000u, 0x80000000u, 0x80000000u};
 #pragma unroll
@@ -462,7 +462,7 @@ __global__ __launch_bounds__(256, 2) void spec_gemm_kernel(const uint4* __restri
       }
     }
   }
-  __syncthreads();   // every wave has read the S tile
+  lds_barrier();   // every wave has read the S tile
   // ---- Y tile: lane (h, j), co block cb, row group g: channels 32cb + 8g + 4h + e, e < 4 ----
   f32x4* ytile = reinterpret_cast<f32x4*>(tile);
 #pragma unroll
@@ -477,7 +477,7 @@ __global__ __launch_bounds__(256, 2) void spec_gemm_kernel(const uint4* __restri
       ytile[j * SG_YLD + (cqo * 4 + wv) * 2] = lo;
       ytile[j * SG_YLD + (cqo * 4 + wv) * 2 + 1] = hi;
     }
-  __syncthreads();
+  lds_barrier();
 #pragma unroll
   for (int it = 0; it < 16; ++it) {
     const int idx = it * 256 + tid, line = idx >> 3, piece = idx & 7;
@@ -496,7 +496,7 @@ __global__ void spec_weights_kernel(const float* __restrict__ w, cpx* __restrict
     tc[m] = c;
     ts[m] = s;
   }
-  __syncthreads();
+  lds_barrier();
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= NF * 4096) return;
   const int co = idx & 63, ci = (idx >> 6) & 63, f = idx >> 12;

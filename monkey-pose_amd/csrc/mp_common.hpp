@@ -29,6 +29,14 @@ __device__ __forceinline__ f32x16 mfma32(float a, float b, f32x16 c) {
 
 __device__ __forceinline__ float sigmoidf_(float x) { return 1.0f / (1.0f + expf(-x)); }
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS operations, then s_barrier.
+// __syncthreads() also carries a release fence, which drains every outstanding global load and
+// store (s_waitcnt vmcnt(0)) -- including prefetches meant to stay in flight across the barrier.
+// Use only where no global-memory ordering between the block's threads is needed.
+__device__ __forceinline__ void lds_barrier() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 // per-channel parameter vectors of the hGRU epilogues, each 64 floats, in this order
 enum VecId {
   V_LAT = 0,   // lateral_bias        (hgru_module.py:498-503, added at 657)
