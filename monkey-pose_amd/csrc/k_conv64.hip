@@ -133,6 +133,9 @@ __global__ __launch_bounds__(256) void gate_init_kernel(const float* __restrict_
 // hgru_pose.py:50-60.  One thread = one pooled pixel x 8 channels (a C8 chunk).  C_in = 1 makes
 // this HBM-bound on the C8 store; the 4x4 input patch comes from L1/L2.
 // ---------------------------------------------------------------------------------------------
+// One thread per pooled output pixel, all 64 channels: the 4x4 input patch is loaded once
+// (unconditional clamped loads, zero-masked), and the filter / bias / BN vectors are
+// thread-uniform, so they come through scalar loads and enter the FMAs as SGPR operands.
 __global__ __launch_bounds__(256) void conv1_pool_bn_kernel(const float* __restrict__ in,
                                                             const float* __restrict__ w,   // [9][64]
                                                             const float* __restrict__ bias,
@@ -140,42 +143,46 @@ __global__ __launch_bounds__(256) void conv1_pool_bn_kernel(const float* __restr
                                                             const float* __restrict__ bn_t,
                                                             float* out, int B, int Hin, int Win) {
   const int Ho = Hin / 2, Wo = Win / 2;
-  const size_t total = (size_t)B * NQ * Ho * Wo;
+  const size_t total = (size_t)B * Ho * Wo;
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= total) return;
   const int x = i % Wo;
   const int y = (i / Wo) % Ho;
-  const int q = (i / ((size_t)Wo * Ho)) % NQ;
-  const int b = i / ((size_t)Wo * Ho * NQ);
+  const int b = i / ((size_t)Wo * Ho);
   float pt[4][4];
 #pragma unroll
   for (int r = 0; r < 4; ++r)
 #pragma unroll
     for (int c = 0; c < 4; ++c) {
       const int yy = 2 * y - 1 + r, xx = 2 * x - 1 + c;
-      pt[r][c] = (yy >= 0 && yy < Hin && xx >= 0 && xx < Win) ? in[((size_t)b * Hin + yy) * Win + xx] : 0.f;
+      const bool ok = yy >= 0 && yy < Hin && xx >= 0 && xx < Win;
+      const float v = in[((size_t)b * Hin + min(max(yy, 0), Hin - 1)) * Win + min(max(xx, 0), Win - 1)];
+      pt[r][c] = ok ? v : 0.f;
     }
-  float o[8];
 #pragma unroll
-  for (int e = 0; e < 8; ++e) {
-    const int ch = 8 * q + e;
-    float best = 0.f;   // relu output >= 0, so 0 is the identity of the max
+  for (int q = 0; q < NQ; ++q) {
+    float o[8];
 #pragma unroll
-    for (int dy = 0; dy < 2; ++dy)
+    for (int e = 0; e < 8; ++e) {
+      const int ch = 8 * q + e;
+      float best = 0.f;   // relu output >= 0, so 0 is the identity of the max
 #pragma unroll
-      for (int dx = 0; dx < 2; ++dx) {
-        float s = 0.f;
+      for (int dy = 0; dy < 2; ++dy)
 #pragma unroll
-        for (int ky = 0; ky < 3; ++ky)
+        for (int dx = 0; dx < 2; ++dx) {
+          float sacc = 0.f;
 #pragma unroll
-          for (int kx = 0; kx < 3; ++kx) s = fmaf(pt[dy + ky][dx + kx], w[(ky * 3 + kx) * 64 + ch], s);
-        best = fmaxf(best, fmaxf(s + bias[ch], 0.f));
-      }
-    o[e] = best * bn_s[ch] + bn_t[ch];
+          for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+            for (int kx = 0; kx < 3; ++kx) sacc = fmaf(pt[dy + ky][dx + kx], w[(ky * 3 + kx) * 64 + ch], sacc);
+          best = fmaxf(best, fmaxf(sacc + bias[ch], 0.f));
+        }
+      o[e] = best * bn_s[ch] + bn_t[ch];
+    }
+    float* dst = out + c8_index(b, q, y, x, 0, Ho, Wo);
+    *reinterpret_cast<f32x4*>(dst) = f32x4{o[0], o[1], o[2], o[3]};
+    *reinterpret_cast<f32x4*>(dst + 4) = f32x4{o[4], o[5], o[6], o[7]};
   }
-  float* dst = out + c8_index(b, q, y, x, 0, Ho, Wo);
-  *reinterpret_cast<f32x4*>(dst) = f32x4{o[0], o[1], o[2], o[3]};
-  *reinterpret_cast<f32x4*>(dst + 4) = f32x4{o[4], o[5], o[6], o[7]};
 }
 
 // layout conversions (standalone ContextualCircuit API, debug taps)
@@ -276,7 +283,7 @@ hipError_t launch_gate_init(const float* O0, float* O, float* Og, const f32x4* g
 
 hipError_t launch_conv1_pool_bn(const float* in, const float* w, const float* bias, const float* s,
                                 const float* t, float* out, int B, int Hin, int Win, hipStream_t st) {
-  const size_t total = (size_t)B * NQ * (Hin / 2) * (Win / 2);
+  const size_t total = (size_t)B * (Hin / 2) * (Win / 2);
   hipLaunchKernelGGL(conv1_pool_bn_kernel, dim3((total + 255) / 256), dim3(256), 0, st, in, w, bias,
                      s, t, out, B, Hin, Win);
   return hipGetLastError();

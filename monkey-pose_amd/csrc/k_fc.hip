@@ -286,12 +286,14 @@ hipError_t launch_pack_fc(const float* W, f32x4* out, int K, int N, hipStream_t 
   return hipGetLastError();
 }
 
-// K slices of ~4096: a function of K only, so every output row is summed in the same order
-// whatever the batch size (results are bit-identical between a crop alone and inside a batch).
+// K slices: a function of K only, so every output row is summed in the same order whatever the
+// batch size (results are bit-identical between a crop alone and inside a batch).  Large K
+// (fc_1: 262,144) in slices of ~4,096; small K in slices of 128 so a short GEMM still spreads
+// over enough blocks (fc_out, K = 1,024: 8 slices instead of 1).
 int fc_choose_splits(int M, int K, int N, int* kslice) {
   (void)M;
   (void)N;
-  int S = K / 4096;
+  int S = K >= 32768 ? K / 4096 : std::min(64, (K + 127) / 128);
   if (S < 1) S = 1;
   int ks = (K + S - 1) / S;
   ks = (ks + FC_BK - 1) / FC_BK * FC_BK;

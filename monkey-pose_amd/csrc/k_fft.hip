@@ -659,6 +659,48 @@ __global__ __launch_bounds__(256) void spec_epi_b_kernel(ConvArgs p, const float
   }
 }
 
+// first circuit_input gate (hgru_module.py:696-711) for the FFT path: O0 (NHWC) -> O, and
+// Og = O0 * sigmoid(O0 . i_r + i_b) (C8), the gate on f16x3 MFMA; one wave per 32 pixels
+__global__ __launch_bounds__(256) void gate_init_x3_kernel(const float* __restrict__ O0, float* O, float* Og,
+                                                           const f16x8* __restrict__ ir_x3, float ir_us,
+                                                           const float* __restrict__ vecs, int npix, int H,
+                                                           int W) {
+  const int lane = threadIdx.x & 63, h = lane >> 5;
+  const int blk = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (blk * 32 >= npix) return;
+  const int pix = blk * 32 + (lane & 31);
+  const bool ok = pix < npix;
+  const int pp = ok ? pix : npix - 1;
+  const int x = pp % W, y = (pp / W) % H, b = pp / (W * H);
+  f32x16 V[2], Y[2];
+#pragma unroll
+  for (int n = 0; n < 2; ++n)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const f32x4 v = *reinterpret_cast<const f32x4*>(O0 + (size_t)pp * C + 32 * n + 8 * g + 4 * h);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) V[n][4 * g + j] = v[j];
+    }
+  gate_x3(ir_x3, V, Y, lane, ir_us);
+  if (!ok) return;
+#pragma unroll
+  for (int n = 0; n < 2; ++n)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int c = 32 * n + 8 * g + 4 * h;
+      const f32x4 ib = *reinterpret_cast<const f32x4*>(vecs + V_IB * 64 + c);
+      f32x4 o, og;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        o[j] = V[n][4 * g + j];
+        og[j] = o[j] * fsigmoid(Y[n][4 * g + j] + ib[j]);
+      }
+      const size_t idx = c8_index(b, 4 * n + g, y, x, 4 * h, H, W);
+      *reinterpret_cast<f32x4*>(O + idx) = o;
+      *reinterpret_cast<f32x4*>(Og + idx) = og;
+    }
+}
+
 // 1x1 gate weights [cin][cout] -> [n2][s][hi|lo][lane] f16x8 in gate_x3's K order; thread =
 // (n2, s, lane)
 __global__ void pack_gate_x3_kernel(const float* __restrict__ g, f16x8* __restrict__ out, float wscale) {
@@ -788,6 +830,14 @@ hipError_t pack_gate_x3(const float* g, void* out, float* unscale) {
   const float wscale = std::ldexp(1.0f, 14 - ex);   // max|g| at 2^13..2^14
   *unscale = 1.0f / (wscale * GATE_VSCALE);
   hipLaunchKernelGGL(pack_gate_x3_kernel, dim3(2), dim3(256), 0, 0, g, static_cast<f16x8*>(out), wscale);
+  return hipGetLastError();
+}
+
+hipError_t launch_gate_init_x3(const float* O0, float* O, float* Og, const void* ir_x3, float ir_us, const float* vecs,
+                               int B, int H, int W, hipStream_t st) {
+  const int npix = B * H * W, nw = (npix + 31) / 32;
+  hipLaunchKernelGGL(gate_init_x3_kernel, dim3((nw + 3) / 4), dim3(256), 0, st, O0, O, Og,
+                     static_cast<const f16x8*>(ir_x3), ir_us, vecs, npix, H, W);
   return hipGetLastError();
 }
 

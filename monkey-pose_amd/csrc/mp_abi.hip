@@ -268,7 +268,9 @@ void check_map(mp_ctx* c, int64_t H, int64_t W, const char* what) {
 
 void run_circuit(mp_ctx* c, int64_t n, int H, int W, int T, const float* o0_nhwc, float* final_dst2,
                  hipStream_t st) {
-  hip_check(launch_gate_init(o0_nhwc, c->O.f(), c->Og.f(), c->ir_pk.v4(), c->vecs.f(), (int)n, H, W, st),
+  hip_check(c->dtype == MP_DTYPE_F32_FFT
+                ? launch_gate_init_x3(o0_nhwc, c->O.f(), c->Og.f(), c->ir_x3.p, c->ir_us, c->vecs.f(), (int)n, H, W, st)
+                : launch_gate_init(o0_nhwc, c->O.f(), c->Og.f(), c->ir_pk.v4(), c->vecs.f(), (int)n, H, W, st),
             "gate_init");
   for (int t = 0; t < T; ++t) {
     ConvArgs a{};

@@ -59,6 +59,8 @@ hipError_t launch_spec_epi(int epi, const ConvArgs& a, const float* P, int B, hi
 // B epilogue with f16x3 gate GEMMs (FFT path); gate weights packed by pack_gate_x3 (synchronous)
 size_t gate_x3_bytes();
 hipError_t pack_gate_x3(const float* g, void* out, float* unscale);
+hipError_t launch_gate_init_x3(const float* O0, float* O, float* Og, const void* ir_x3, float ir_us, const float* vecs,
+                               int B, int H, int W, hipStream_t st);
 hipError_t launch_spec_epi_b(const ConvArgs& a, const float* P, const void* or_x3, float or_us, const void* ir_x3,
                              float ir_us, int B, hipStream_t st);
 // k_igemm.hip (dense / hierarchical regressors)
