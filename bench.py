@@ -44,6 +44,8 @@ def parse():
     p.add_argument("--cpu-sample", type=int, default=16, help="crops timed on the CPU oracle")
     p.add_argument("--no-parity", action="store_true")
     p.add_argument("--no-extras", action="store_true")
+    p.add_argument("--backend", default="nccl", choices=["nccl", "gloo"],
+                   help="torch.distributed backend for N > 1 (nccl = RCCL over xGMI)")
     return p.parse_args()
 
 
@@ -196,8 +198,14 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # one rank per GPU; local % device_count only matters for --backend gloo rehearsals of the
+        # multi-rank path with several ranks on one GPU (RCCL refuses two ranks per device)
+        local = local % torch.cuda.device_count()
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(args.backend)
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -264,11 +272,11 @@ def main():
         "scaling": "weak",
         "vs_baseline": None,
         "dtype": {"f32": "f32", "f32_split": "f32 (f16x3 split MFMA, fp32 accumulate)",
-                  "f32_fft": "f32 (fp32 FFT convolution, fp32 MFMA spectral GEMM)"}[args.dtype],
+                  "f32_fft": "f32 (fp32 FFT convolution, fp32-accurate f16x3 spectral GEMM)"}[args.dtype],
         "data": "synthetic crops + synthetic weights (splitmix64 stand-ins; reference publishes none)",
         "config": {"workload": f"hgru_pose.model.build fwd, T={T}, {crop}x{crop} crops, "
                                f"batch {B} per GPU", "global_batch": world * B, "crop": crop,
-                   "timesteps": T, "parallelism": f"dp{world} (batch shards, RCCL weight broadcast)"},
+                   "timesteps": T, "parallelism": f"dp{world} (batch shards, one {'RCCL' if args.backend == 'nccl' else 'gloo'} weight broadcast)"},
         "roofline": (fft_roofline(kern) if args.dtype == "f32_fft" else
                      roofline(args.dtype, achieved_tf, conv_launch_ms, na + nb, conv15_flop)),
         "breakdown_ms_per_step": {"conv15": round((ms_a + ms_b) / args.steps, 3),

@@ -30,6 +30,19 @@ DTYPES = {'fp32': MP_DTYPE_F32, 'f32': MP_DTYPE_F32, 'fp32_split': MP_DTYPE_F32_
           'f32_split': MP_DTYPE_F32_SPLIT, 'fp32_fft': MP_DTYPE_F32_FFT, 'f32_fft': MP_DTYPE_F32_FFT}
 
 
+def resolve_dtype(name: str, h: int, w: int) -> str:
+    """'auto' -> the fastest fp32-class eCRF path supporting an h x w hGRU map: the FFT path for
+    maps up to 64 x 64 with width 32 or 64 (the reference's 128^2 / 64^2 crops), else the f16x3
+    direct path for multiples of 32, else exact fp32.  Explicit names pass through."""
+    if name != 'auto':
+        return name
+    if 1 <= h <= 64 and w in (32, 64):
+        return 'fp32_fft'
+    if h % 32 == 0 and w % 32 == 0:
+        return 'fp32_split'
+    return 'fp32'
+
+
 def dtype_code(name: str) -> int:
     if name not in DTYPES:
         raise ValueError(f"compute dtype must be one of {sorted(DTYPES)}, got {name!r}")

@@ -105,10 +105,11 @@ class ContextualCircuit(object):
         return out
 
     def build(self, weights: Optional[Dict[str, np.ndarray]] = None, h2_init=None,
-              compute_dtype: str = 'fp32'):
+              compute_dtype: str = 'auto'):
         """Run the circuit; returns ``(O, weights, activities)`` like the reference with
-        ``return_weights=True`` (hgru_module.py:939-954).  ``compute_dtype``: 'fp32' or
-        'fp32_split' (see include/monkeypose.h)."""
+        ``return_weights=True`` (hgru_module.py:939-954).  ``compute_dtype``: 'auto' (the FFT
+        path when the map allows), 'fp32_fft', 'fp32_split' or 'fp32' (see include/monkeypose.h
+        and _lib.resolve_dtype)."""
         import torch
         X = self.X
         if not isinstance(X, torch.Tensor) or not X.is_cuda:
@@ -117,7 +118,7 @@ class ContextualCircuit(object):
         ctx = _lib.Context(_lib.MP_MODEL_HGRU_CIRCUIT, X.device.index or 0)
         for name, val in wts.items():
             ctx.set_weight(name, val)
-        ctx.finalize(_lib.dtype_code(compute_dtype))
+        ctx.finalize(_lib.dtype_code(_lib.resolve_dtype(compute_dtype, X.shape[1], X.shape[2])))
         X = X.detach().float().contiguous()
         if h2_init is None:
             h2_init = torch.from_numpy(W.synth_hidden(tuple(X.shape))).to(X.device)

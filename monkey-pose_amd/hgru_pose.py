@@ -56,8 +56,9 @@ class model:
         }
         self.weights: Optional[Dict[str, np.ndarray]] = None   # TF variable name -> array
         self.weight_seed = 1234
-        # precision of the hGRU eCRF convs: 'fp32' (exact fp32 MFMA) or 'fp32_split' (f16x3)
-        self.compute_dtype = 'fp32'
+        # eCRF conv path (all fp32-class): 'auto' (default: FFT when the map allows, see
+        # _lib.resolve_dtype), 'fp32_fft', 'fp32_split' (direct f16x3) or 'fp32' (exact fp32 MFMA)
+        self.compute_dtype = 'auto'
         self._ctx: Optional[_lib.Context] = None
         self._ctx_key = None
         self.out_put = None
@@ -99,13 +100,13 @@ class model:
         return out
 
     def _context(self, output_shape: int, device: int, crop=(128, 128)) -> _lib.Context:
-        key = (output_shape, device, tuple(crop), id(self.weights), id(self.data_dict),
-               self.compute_dtype)
+        dtype = _lib.resolve_dtype(self.compute_dtype, crop[0] // 2, crop[1] // 2)
+        key = (output_shape, device, tuple(crop), id(self.weights), id(self.data_dict), dtype)
         if self._ctx is None or self._ctx_key != key:
             ctx = _lib.Context(_lib.MP_MODEL_HGRU_POSE, device)
             for name, val in self._resolve_weights(output_shape, crop).items():
                 ctx.set_weight(name, val)
-            ctx.finalize(_lib.dtype_code(self.compute_dtype))
+            ctx.finalize(_lib.dtype_code(dtype))
             self._ctx, self._ctx_key = ctx, key
         return self._ctx
 

@@ -81,3 +81,13 @@ def test_reference_defaults_preserved():
     m = mp.hgru_pose.model()
     assert (m.SRF, m.SSN, m.SSF, m.timesteps, m._BATCH_NORM_EPSILON) == (1, 15, 15, 8, 1e-5)
     assert m.aux == {k: v for k, v in HGRU_POSE_AUX.items()}
+
+
+def test_auto_dtype_resolution():
+    mp = pkg()
+    r = mp._lib.resolve_dtype
+    assert r('auto', 64, 64) == 'fp32_fft' and r('auto', 32, 32) == 'fp32_fft'
+    assert r('auto', 16, 32) == 'fp32_fft'
+    assert r('auto', 96, 96) == 'fp32_split' and r('auto', 50, 50) == 'fp32'
+    assert r('fp32', 64, 64) == 'fp32'
+    assert mp.hgru_pose.model().compute_dtype == 'auto'
