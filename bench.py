@@ -146,6 +146,21 @@ def extras(mp, dev, args):
         ctx.close()
     except Exception as e:  # noqa: BLE001
         out["hier_b256"] = {"error": repr(e)}
+    try:   # config 2: hGRU pose fwd, T=8, batch 64, fp32-class (same context kind, B = 64)
+        ctx = mp._lib.Context(mp._lib.MP_MODEL_HGRU_POSE, dev.index)
+        T = args.timesteps
+        for v in W.hgru_pose_vars(output_shape=69, timesteps=T, crop=128):
+            ctx.set_weight(v.name, W.synth_value(v, 1234, T))
+        ctx.finalize(mp._lib.dtype_code(args.dtype))
+        d64 = depth[:64].contiguous()
+        o64 = torch.from_numpy(W.synth_hidden((64, 64, 64, 64), seed=7)).to(dev)
+        out64 = torch.empty((64, 69), device=dev)
+        t = time_gpu(lambda: ctx.pose_fwd(d64, o64, out64, stream), 10, 2)
+        out["hgru_b64"] = {"crops_per_s": round(64 / t, 2), "ms_per_batch": round(t * 1e3, 3),
+                           "dtype": args.dtype}
+        ctx.close()
+    except Exception as e:  # noqa: BLE001
+        out["hgru_b64"] = {"error": repr(e)}
     try:   # config 1 plumbing model, measured on the GPU at batch 256
         ctx = mp._lib.Context(mp._lib.MP_MODEL_DENSE, dev.index)
         for v in W.dense_vars():
