@@ -173,21 +173,74 @@ def extras(mp, dev, args):
         ctx.close()
     except Exception as e:  # noqa: BLE001
         out["dense_b256"] = {"error": repr(e)}
+    try:   # attention CoM regressor on full frames + the device chain to the pose
+        out.update(frame_chain(mp, dev, args))
+    except Exception as e:  # noqa: BLE001
+        out["attn_b256"] = {"error": repr(e)}
     return out
+
+
+ATTN_GFLOP = 3.5421   # per frame: 5 convs at 128/64/32/16/8 px (one 5x5) + afc_1 (bench docstring)
+
+
+def frame_chain(mp, dev, args):
+    """attn_model_struct on B full 424x512 frames, the device crop of prepare_data_test, and the
+    whole test_model batch body (attention -> device crop -> hGRU pose), frames/s."""
+    import torch
+    W = mp.weights
+    T = mp.train_cnn_networks_hgru
+    B = args.batch
+    frames = torch.from_numpy(W.synth_frames(B, seed=12)).to(dev)
+    attn = T.attn_model_struct()
+    attn.load_weights(W.attn_synth_weights(seed=21))
+    com = attn.build(frames, 3)
+    stream = mp._lib.current_stream(dev)
+    t = time_gpu(lambda: attn.forward(frames, com), 5, 1)
+    res = {"attn_b256": {"frames_per_s": round(B / t, 2), "ms_per_batch": round(t * 1e3, 3),
+                         "gflop_per_frame": ATTN_GFLOP, "tflops": round(ATTN_GFLOP * 1e9 * B / t / 1e12, 2),
+                         "input": "424x512 normalised frames, bilinear resize to 128x128 inside"}}
+    md = mp.monkeydetector.MonkeyDetector(365.456, 365.456, 256, 212, [800, 800, 1200], 200, 10000)
+    md.crop_batch_device(frames, com)          # raises if any synthetic crop failed
+    tc = time_gpu(lambda: md.crop_batch_device(frames, com, check=False), 20, 2)
+    res["device_crop_b256"] = {"frames_per_s": round(B / tc, 1), "ms_per_batch": round(tc * 1e3, 4),
+                               "hbm_gbps_written": round(B * 128 * 128 * 4 / tc / 1e9, 1)}
+    pose = mp.hgru_pose.model()
+    pose.compute_dtype = args.dtype
+    o0 = torch.from_numpy(W.synth_hidden((B, 64, 64, 64), seed=7)).to(dev)
+    pipe = T.FramePosePipeline(attn, pose, md, check_crops=False)
+    pipe.run(frames, h2_init=o0)
+    tp = time_gpu(lambda: pipe.run(frames, h2_init=o0), 3, 1)
+    res["frame_chain_b256"] = {"frames_per_s": round(B / tp, 2), "ms_per_batch": round(tp * 1e3, 3),
+                               "path": "attention -> device crop -> hgru_pose (" + args.dtype + "), on device"}
+    # batch-1 latency of the same chain: H2D of one frame, chain, D2H, absolute joints on the host
+    f1 = W.synth_frames(8, seed=13)
+    o1 = o0[:1].contiguous()
+    lat = []
+    for i in range(40):
+        t0 = time.perf_counter()
+        x = torch.from_numpy(f1[i % 8:i % 8 + 1]).to(dev)
+        out, coms, _ = pipe.run(x, h2_init=o1)
+        rel = out.cpu().numpy().reshape(23, 3) * 600.0
+        md.getAbsoluteCoordinates(rel, coms.cpu().numpy()[0])
+        lat.append(time.perf_counter() - t0)
+    lat = np.array(lat[5:]) * 1e3
+    res["e2e_batch1_gpu_chain"] = {"p50_ms": round(float(np.percentile(lat, 50)), 3),
+                                   "p99_ms": round(float(np.percentile(lat, 99)), 3),
+                                   "path": "H2D frame -> attention -> device crop -> hgru_pose B=1 -> D2H"}
+    del stream
+    return res
 
 
 def e2e_latency(mp, ctx, dev, T, frames=40):
     """Config 5: one 424x512 float32 depth frame per call -> native host CoM crop -> H2D -> hGRU pose
     forward at batch 1 -> D2H -> absolute joints; p50 / p99 wall latency."""
     import torch
-    sys.path.insert(0, ROOT)
-    from oracle.crop_ref import synth_frame   # synthetic frames only (the measured path is native)
     md = mp.monkeydetector.MonkeyDetector(365.456, 365.456, 256, 212, [800, 800, 1200], 200, 10000)
     W = mp.weights
     o0 = torch.from_numpy(W.synth_hidden((1, 64, 64, 64), seed=3)).to(dev)
     out = torch.empty((1, 69), device=dev)
     stream = mp._lib.current_stream(dev)
-    fr = [synth_frame(i) for i in range(8)]
+    fr = list(W.synth_frames(8, seed=14)[..., 0] * np.float32(10000.0))   # mm, as the crop sees it
     lat = []
     for i in range(frames):
         t0 = time.perf_counter()

@@ -52,7 +52,8 @@ enum {
   MP_MODEL_HGRU_POSE = 1,    /* hgru_pose.model                (hgru_pose.py:6-216)        */
   MP_MODEL_HGRU_CIRCUIT = 2, /* hgru_module.ContextualCircuit  (hgru_module.py:54-959)     */
   MP_MODEL_DENSE = 3,        /* dense_model_struct  (train_dense_networks.py:211-509)      */
-  MP_MODEL_HIER = 4          /* hier_model_struct   (train_hier_networks.py:327-631)       */
+  MP_MODEL_HIER = 4,         /* hier_model_struct   (train_hier_networks.py:327-631)       */
+  MP_MODEL_ATTN = 5          /* attn_model_struct   (train_cnn_networks_hgru.py:422-525)   */
 };
 
 enum { MP_MEM_HOST = 0, MP_MEM_DEVICE = 1 };
@@ -115,6 +116,19 @@ int mp_dense_fwd(mp_ctx* ctx, const float* depth, int64_t n, int64_t h, int64_t 
 int mp_hier_fwd(mp_ctx* ctx, const float* depth, int64_t n, int64_t h, int64_t w, float* const* outs,
                 void* stream);
 
+/* attn_model_struct.build(depth, output_shape) -> .out_put  (train_cnn_networks_hgru.py:436-525),
+ * the attention (centre-of-mass) regressor, inference (BN from moving statistics, no dropout):
+ *   frames [n, h, w, 1] normalised full depth frames (image / image_max_depth,
+ *          train_cnn_networks_hgru.py:116; 424 x 512 in the reference), resized to 128 x 128
+ *   out    [n, output_shape] (u, v, d) / (image_orig_size[0], image_orig_size[1], image_max_depth) */
+int mp_attn_fwd(mp_ctx* ctx, const float* frames, int64_t n, int64_t h, int64_t w, float* out, void* stream);
+
+/* tf.image.resize_images(x, [ho, wo]) with the TF1 defaults (BILINEAR, align_corners=False,
+ * legacy source coordinates in = out * in_size / out_size), bit-identical to TF's float32 kernel:
+ *   x [n, h, w, c] -> out [n, ho, wo, c], device pointers */
+int mp_resize_bilinear(const float* x, int64_t n, int64_t h, int64_t w, int64_t c, int64_t ho, int64_t wo,
+                       float* out, void* stream);
+
 /* ---- host-side 3D CoM crop (no GPU; the pre-step of every regressor) -------------------------
  * MonkeyDetector(fx, fy, ux, uy, cube, d1, d2) (monkeydetector.py:31-63, tf_monkeydetector.py),
  * constructed in the reference as (365.456, 365.456, 256, 212, [800,800,1200], 200, 10000)
@@ -150,6 +164,21 @@ int mp_crop3d(const mp_camera* cam, const void* depth, int depth_dtype, int64_t 
 int mp_crop3d_batch(const mp_camera* cam, const void* frames, int depth_dtype, int64_t n, int64_t h, int64_t w,
                     const double* coms, int64_t dsize, float* patches, double* Ms, double* coms_out,
                     int nthreads);
+
+/* prepare_data_test on the device (train_cnn_networks_hgru.py:61-74) with tr_res = the attention
+ * output, for a batch of n frames in one launch (all pointers device memory, asynchronous):
+ *   frames    [n][h][w] float32 as fed to the attention net; the crop sees frames * frame_scale
+ *             (image_np * image_max_depth, line 67: frame_scale = 10000)
+ *   com_norm  [n][3] float32 attention output; com = com_norm * com_scale in float64
+ *             (com_scale = {image_orig_size[0], image_orig_size[1], image_max_depth}, line 69)
+ *   patches   [n][dsize][dsize][1] = cropArea3D(frame, com) / cam.max_depth
+ *   Ms [n][9], coms_out [n][3] float64; status [n] int32: 0 ok, else the frame's crop failed
+ *             (1 CoM depth zero / not finite, 2 empty crop, 3 degenerate bounds, 4 empty resize;
+ *             that patch is all ones) -- the host mp_crop3d raises MP_ERR_ARG in those cases.
+ * Integers (bounds, sizes, offsets, nearest-neighbour indices) are bit-exact with mp_crop3d. */
+int mp_crop3d_dev(const mp_camera* cam, const float* frames, int64_t n, int64_t h, int64_t w, float frame_scale,
+                  const float* com_norm, const double* com_scale, int64_t dsize, float* patches, double* Ms,
+                  double* coms_out, int32_t* status, void* stream);
 
 /* read a model property: "output_shape", "timesteps", "ssf", "finalized", "workspace_bytes",
  * "weight_bytes" */

@@ -7,6 +7,8 @@ The directory name carries a hyphen, so import it with ``importlib.import_module
 * ``hgru_module`` -- drop-in ``ContextualCircuit(X, ...).build()`` (reference ``hgru_module.py``)
 * ``train_dense_networks.dense_model_struct`` / ``train_hier_networks.hier_model_struct`` --
   drop-ins for the dense and hierarchical regressor heads
+* ``train_cnn_networks_hgru`` -- ``attn_model_struct`` (the attention CoM regressor),
+  ``prepare_data_test`` (device batch crop) and ``FramePosePipeline`` (frame -> CoM -> crop -> pose)
 * ``weights``     -- TF variable-name tables and deterministic synthetic initialisers
 * ``_lib``        -- ctypes binding of ``libmonkeypose.so`` (C ABI: ``include/monkeypose.h``)
 """
@@ -16,7 +18,8 @@ from . import hgru_pose  # noqa: F401
 from . import hgru_module  # noqa: F401
 from . import train_dense_networks  # noqa: F401
 from . import train_hier_networks  # noqa: F401
+from . import train_cnn_networks_hgru  # noqa: F401
 from . import monkeydetector  # noqa: F401
 from . import parallel  # noqa: F401
 
-__all__ = ["hgru_pose", "hgru_module", "train_dense_networks", "train_hier_networks", "weights", "_lib"]
+__all__ = ["hgru_pose", "hgru_module", "train_dense_networks", "train_hier_networks", "train_cnn_networks_hgru", "weights", "_lib"]

@@ -21,6 +21,7 @@ MP_MODEL_HGRU_POSE = 1
 MP_MODEL_HGRU_CIRCUIT = 2
 MP_MODEL_DENSE = 3
 MP_MODEL_HIER = 4
+MP_MODEL_ATTN = 5
 MP_MEM_HOST = 0
 MP_MEM_DEVICE = 1
 MP_DTYPE_F32 = 0
@@ -69,6 +70,11 @@ _SIGS = {
                                     ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
     "mp_hier_fwd": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
                                    ctypes.c_int64, ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p]),
+    "mp_attn_fwd": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                                   ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
+    "mp_resize_bilinear": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                                          ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
+                                          ctypes.c_void_p]),
     "mp_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64)]),
     "mp_profile_enable": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "mp_profile_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p,
@@ -186,6 +192,10 @@ class Context:
         arr = (ctypes.c_void_p * 6)(*[_ptr(o) for o in outs])
         check(self.lib.mp_hier_fwd(self.h, _ptr(depth), n, h, w, arr, ctypes.c_void_p(stream)))
 
+    def attn_fwd(self, frames, out, stream: int) -> None:
+        n, h, w, c = frames.shape
+        check(self.lib.mp_attn_fwd(self.h, _ptr(frames), n, h, w, _ptr(out), ctypes.c_void_p(stream)))
+
     def profile(self, enable: bool) -> None:
         check(self.lib.mp_profile_enable(self.h, 1 if enable else 0))
 
@@ -193,6 +203,21 @@ class Context:
         ms, cnt = ctypes.c_double(), ctypes.c_int64()
         check(self.lib.mp_profile_read(self.h, name.encode(), ctypes.byref(ms), ctypes.byref(cnt)))
         return float(ms.value), int(cnt.value)
+
+
+def resize_bilinear(x, size, stream: Optional[int] = None):
+    """``tf.image.resize_images(x, size)`` (TF1 BILINEAR, align_corners=False) of a CUDA tensor
+    [n, h, w, c] fp32 -> new tensor [n, size[0], size[1], c] (mp_resize_bilinear)."""
+    import torch
+    if not isinstance(x, torch.Tensor) or not x.is_cuda or x.dim() != 4:
+        raise TypeError("x must be a 4-D CUDA (ROCm) tensor [n, h, w, c]")
+    x = x.detach().float().contiguous()
+    n, h, w, c = x.shape
+    out = torch.empty((n, int(size[0]), int(size[1]), c), dtype=torch.float32, device=x.device)
+    st = current_stream(x.device) if stream is None else stream
+    check(load().mp_resize_bilinear(_ptr(x), n, h, w, c, int(size[0]), int(size[1]), _ptr(out),
+                                    ctypes.c_void_p(st)))
+    return out
 
 
 def current_stream(device=None) -> int:

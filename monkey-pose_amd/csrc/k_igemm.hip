@@ -121,9 +121,11 @@ __global__ __launch_bounds__(256) void igemm_conv_kernel(IgemmArgs p) {
 }
 
 // 2x2 / stride 2, TF SAME (odd sizes pad one row/column after; max ignores it, avg divides by the
-// in-image count).  One thread per output element; C innermost for coalescing.
+// in-image count), optionally followed by a per-channel affine (a folded inference BN).  One
+// thread per output element; C innermost for coalescing.
 __global__ void pool2_kernel(const float* __restrict__ x, int ldx, int cix, int N, int H, int W, int C,
-                             float* out, int ldo, int coff, int mode) {
+                             float* out, int ldo, int coff, int mode, const float* __restrict__ aff_s,
+                             const float* __restrict__ aff_t) {
   const int Ho = (H + 1) / 2, Wo = (W + 1) / 2;
   const size_t total = (size_t)N * Ho * Wo * C;
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
@@ -146,7 +148,9 @@ __global__ void pool2_kernel(const float* __restrict__ x, int ldx, int cix, int 
         ++cnt;
       }
     }
-  out[pix * ldo + coff + c] = mode == 0 ? best : sum / (float)cnt;
+  float v = mode == 0 ? best : sum / (float)cnt;
+  if (aff_s) v = v * aff_s[c] + aff_t[c];   // inference BN after the pool (attention net)
+  out[pix * ldo + coff + c] = v;
 }
 
 hipError_t launch_igemm_conv(const IgemmArgs& a, hipStream_t st) {
@@ -164,10 +168,10 @@ hipError_t launch_igemm_conv(const IgemmArgs& a, hipStream_t st) {
 }
 
 hipError_t launch_pool2(const float* x, int ldx, int cix, int N, int H, int W, int C, float* out, int ldo,
-                        int coff, int mode, hipStream_t st) {
+                        int coff, int mode, hipStream_t st, const float* aff_s, const float* aff_t) {
   const size_t total = (size_t)N * ((H + 1) / 2) * ((W + 1) / 2) * C;
   hipLaunchKernelGGL(pool2_kernel, dim3((total + 255) / 256), dim3(256), 0, st, x, ldx, cix, N, H, W, C, out,
-                     ldo, coff, mode);
+                     ldo, coff, mode, aff_s, aff_t);
   return hipGetLastError();
 }
 

@@ -31,15 +31,15 @@ thread_local std::string g_err;
 }
 
 
-namespace {
+namespace mpr {
 
 void upload(DevBuf& d, const std::vector<float>& h) {
   d.alloc(h.size() * sizeof(float));
   hip_check(hipMemcpy(d.p, h.data(), h.size() * sizeof(float), hipMemcpyHostToDevice), "hipMemcpy H2D");
 }
 
-void bn_fold(mp_ctx* c, const std::string& scope, int n, DevBuf& s_out, DevBuf& t_out,
-             std::vector<float>* hs = nullptr, std::vector<float>* ht = nullptr) {
+void bn_fold(mp_ctx* c, const std::string& scope, int n, DevBuf& s_out, DevBuf& t_out, std::vector<float>* hs,
+             std::vector<float>* ht) {
   const auto& g = c->need(scope + "/gamma", {n}).host;
   const auto& b = c->need(scope + "/beta", {n}).host;
   const auto& m = c->need(scope + "/moving_mean", {n}).host;
@@ -56,6 +56,10 @@ void bn_fold(mp_ctx* c, const std::string& scope, int n, DevBuf& s_out, DevBuf& 
   if (hs) *hs = s;
   if (ht) *ht = t;
 }
+
+}  // namespace mpr
+
+namespace {
 
 void copy_dev(DevBuf& d, const RawWeight& w) {
   d.alloc(w.numel() * sizeof(float));
@@ -325,7 +329,7 @@ const char* mp_last_error(void) { return g_err.c_str(); }
 int mp_create(int device, int model_kind, mp_ctx** out) {
   return guard([&] {
     if (!out) fail(MP_ERR_ARG, "out is NULL");
-    if (model_kind < MP_MODEL_HGRU_POSE || model_kind > MP_MODEL_HIER)
+    if (model_kind < MP_MODEL_HGRU_POSE || model_kind > MP_MODEL_ATTN)
       fail(MP_ERR_ARG, "unknown model_kind " + std::to_string(model_kind));
     int ndev = 0;
     hip_check(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
@@ -401,7 +405,7 @@ int mp_reserve(mp_ctx* ctx, int64_t max_batch) {
     if (!ctx || max_batch <= 0) fail(MP_ERR_ARG, "mp_reserve: bad argument");
     if (!ctx->finalized) fail(MP_ERR_STATE, "mp_reserve before mp_finalize_weights");
     hip_check(hipSetDevice(ctx->device), "hipSetDevice");
-    if (ctx->model == MP_MODEL_DENSE || ctx->model == MP_MODEL_HIER) return;   // sized at first call
+    if (ctx->model >= MP_MODEL_DENSE) return;   // regressors: sized at first call
     const int64_t hw = ctx->model == MP_MODEL_HGRU_POSE ? ctx->fc1_in / 64 : 64 * 64;
     ensure_ws(ctx, max_batch, hw, 1);
   });

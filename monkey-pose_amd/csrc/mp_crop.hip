@@ -9,6 +9,7 @@
 #include <thread>
 #include <vector>
 
+#include "crop_geom.hpp"
 #include "mp_runtime.hpp"
 
 #pragma clang fp contract(off)
@@ -74,16 +75,6 @@ void center_of_mass(const mp_camera& cam, const T* dpt, int64_t h, int64_t w, do
   com[2] = s / (double)num;
 }
 
-// Python slice a[s:e] on a length-n axis with s >= 0: [lo, hi)
-void py_slice(int64_t s, int64_t e, int64_t n, int64_t* lo, int64_t* hi) {
-  if (e < 0) e += n;
-  if (e < 0) e = 0;
-  if (e > n) e = n;
-  if (s > n) s = n;
-  *lo = s;
-  *hi = std::max(s, e);
-}
-
 struct CropInfo {
   int32_t xstart, xend, ystart, yend, szw, szh, offx, offy;
 };
@@ -101,66 +92,30 @@ void crop_one(const mp_camera& cam, const T* dpt, int64_t h, int64_t w, const do
     std::memcpy(com, com_in, sizeof(com));
   else
     center_of_mass(cam, dpt, h, w, com);
-  if (!(com[2] != 0.0) || !std::isfinite(com[0]) || !std::isfinite(com[1]) || !std::isfinite(com[2]))
-    fail(MP_ERR_ARG, "cropArea3D: CoM depth is zero or not finite (no valid pixel in range?)");
-  // comToBounds (monkeydetector.py:162-175)
-  const double zstart = com[2] - cam.cube[2] / 2.;
-  const double zend = com[2] + cam.cube[2] / 2.;
-  const int64_t xstart = (int64_t)std::floor((com[0] * com[2] / cam.fx - cam.cube[0] / 2.) / com[2] * cam.fx);
-  const int64_t xend = (int64_t)std::floor((com[0] * com[2] / cam.fx + cam.cube[0] / 2.) / com[2] * cam.fx);
-  const int64_t ystart = (int64_t)std::floor((com[1] * com[2] / cam.fy - cam.cube[1] / 2.) / com[2] * cam.fy);
-  const int64_t yend = (int64_t)std::floor((com[1] * com[2] / cam.fy + cam.cube[1] / 2.) / com[2] * cam.fy);
-  // getCrop (177-213): slice, zero pad to keep the aspect ratio, z threshold
-  int64_t r0, r1, c0, c1;
-  py_slice(std::max<int64_t>(ystart, 0), std::min<int64_t>(yend, h), h, &r0, &r1);
-  py_slice(std::max<int64_t>(xstart, 0), std::min<int64_t>(xend, w), w, &c0, &c1);
-  const int64_t pt = std::llabs(ystart) - std::max<int64_t>(ystart, 0);
-  const int64_t pb = std::llabs(yend) - std::min<int64_t>(yend, h);
-  const int64_t pl = std::llabs(xstart) - std::max<int64_t>(xstart, 0);
-  const int64_t pr = std::llabs(xend) - std::min<int64_t>(xend, w);
-  const int64_t rows = (r1 - r0) + pt + pb, cols = (c1 - c0) + pl + pr;
-  if (rows <= 0 || cols <= 0) fail(MP_ERR_ARG, "cropArea3D: empty crop");
-  auto crop_at = [&](int64_t y, int64_t x) -> float {   // padded, thresholded crop value
-    const int64_t sy = y - pt, sx = x - pl;
-    if (sy < 0 || sy >= r1 - r0 || sx < 0 || sx >= c1 - c0) return 0.f;
-    const T v = dpt[(r0 + sy) * w + (c0 + sx)];
-    if ((double)v < zstart && v != 0) return store_as(v, zstart);
-    if ((double)v > zend && v != 0) return 0.f;
+  mpgeom::CropGeom g;
+  const int st = mpgeom::crop_geometry(cam, com, h, w, dsz, &g);
+  if (st != mpgeom::CROP_OK) fail(MP_ERR_ARG, mpgeom::crop_status_msg(st));
+  auto crop_at = [&](int64_t y, int64_t x) -> float {   // padded, thresholded crop value (getCrop)
+    const int64_t sy = y - g.pt, sx = x - g.pl;
+    if (sy < 0 || sy >= g.r1 - g.r0 || sx < 0 || sx >= g.c1 - g.c0) return 0.f;
+    const T v = dpt[(g.r0 + sy) * w + (g.c0 + sx)];
+    if ((double)v < g.zstart && v != 0) return store_as(v, g.zstart);
+    if ((double)v > g.zend && v != 0) return 0.f;
     return (float)v;
   };
-  // cropArea3D (282-334)
-  const int64_t wb = xend - xstart, hb = yend - ystart;
-  if (wb <= 0 || hb <= 0) fail(MP_ERR_ARG, "cropArea3D: degenerate bounds");
-  int64_t szw, szh;
-  if (wb > hb) {
-    szw = dsz;
-    szh = hb * dsz / wb;   // Python 2 integer '/'
-  } else {
-    szw = wb * dsz / hb;
-    szh = dsz;
-  }
-  if (szw <= 0 || szh <= 0) fail(MP_ERR_ARG, "cropArea3D: resize target is empty");
-  const double s = rows > cols ? (double)szh / (double)rows : (double)szw / (double)cols;
-  // cv2.resize(INTER_NEAREST): inv = dst/src, ifx = 1/inv, sx = min(floor(x*ifx), src-1)
-  const double ifx = 1. / ((double)szw / (double)cols), ify = 1. / ((double)szh / (double)rows);
-  const int64_t offx = (int64_t)std::floor(dsz / 2. - szw / 2.);
-  const int64_t offy = (int64_t)std::floor(dsz / 2. - szh / 2.);
   for (int64_t i = 0; i < dsz * dsz; ++i) out[i] = (float)cam.max_depth;
-  for (int64_t y = 0; y < szh; ++y) {
-    const int64_t sy = std::min<int64_t>((int64_t)std::floor((double)y * ify), rows - 1);
-    for (int64_t x = 0; x < szw; ++x) {
-      const int64_t sx = std::min<int64_t>((int64_t)std::floor((double)x * ifx), cols - 1);
-      const int64_t oy = offy + y, ox = offx + x;
+  for (int64_t y = 0; y < g.szh; ++y) {
+    const int64_t sy = mpgeom::nn_row(g, y);
+    for (int64_t x = 0; x < g.szw; ++x) {
+      const int64_t sx = mpgeom::nn_col(g, x);
+      const int64_t oy = g.offy + y, ox = g.offx + x;
       if (oy >= 0 && oy < dsz && ox >= 0 && ox < dsz) out[oy * dsz + ox] = crop_at(sy, sx);
     }
   }
-  // M = off * scale * trans, evaluated as numpy does: (off @ scale) @ trans
-  M[0] = s;   M[1] = 0.0; M[2] = s * (double)(-xstart) + (double)offx;
-  M[3] = 0.0; M[4] = s;   M[5] = s * (double)(-ystart) + (double)offy;
-  M[6] = 0.0; M[7] = 0.0; M[8] = 1.0;
+  mpgeom::crop_matrix(g, M);
   std::memcpy(com_out, com, sizeof(com));
-  if (info) *info = CropInfo{(int32_t)xstart, (int32_t)xend, (int32_t)ystart, (int32_t)yend,
-                             (int32_t)szw, (int32_t)szh, (int32_t)offx, (int32_t)offy};
+  if (info) *info = CropInfo{(int32_t)g.xstart, (int32_t)g.xend, (int32_t)g.ystart, (int32_t)g.yend,
+                             (int32_t)g.szw, (int32_t)g.szh, (int32_t)g.offx, (int32_t)g.offy};
 }
 
 void check_cam(const mp_camera* cam) {
@@ -244,6 +199,22 @@ int mp_crop3d_batch(const mp_camera* cam, const void* frames, int depth_dtype, i
     }
     for (int t = 0; t < nt; ++t)
       if (codes[t] != MP_OK) fail(codes[t], errs[t]);
+  });
+}
+
+int mp_crop3d_dev(const mp_camera* cam, const float* frames, int64_t n, int64_t h, int64_t w, float frame_scale,
+                  const float* com_norm, const double* com_scale, int64_t dsize, float* patches, double* Ms,
+                  double* coms_out, int32_t* status, void* stream) {
+  return guard([&] {
+    check_cam(cam);
+    if (!frames || !com_norm || !com_scale || !patches || !Ms || !coms_out || !status)
+      fail(MP_ERR_ARG, "mp_crop3d_dev: null pointer");
+    if (n <= 0 || n > 65535 || h <= 0 || w <= 0 || h * w > ((int64_t)1 << 30) || dsize <= 0 || dsize > 4096)
+      fail(MP_ERR_SHAPE, "mp_crop3d_dev: bad shape");
+    if (!(cam->max_depth != 0.0)) fail(MP_ERR_ARG, "camera max_depth must be non-zero");
+    hip_check(launch_crop3d(*cam, frames, (int)n, (int)h, (int)w, frame_scale, com_norm, com_scale, (int)dsize,
+                            patches, Ms, coms_out, status, static_cast<hipStream_t>(stream)),
+              "crop3d");
   });
 }
 

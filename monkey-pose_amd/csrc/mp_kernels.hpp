@@ -1,6 +1,7 @@
 // Launcher declarations shared by the kernel translation units and the C-ABI layer.
 #pragma once
 #include "mp_common.hpp"
+#include "../../include/monkeypose.h"
 
 namespace mp {
 
@@ -78,7 +79,8 @@ struct IgemmArgs {
 };
 hipError_t launch_igemm_conv(const IgemmArgs& a, hipStream_t st);
 hipError_t launch_pool2(const float* x, int ldx, int cix, int N, int H, int W, int C, float* out, int ldo,
-                        int coff, int mode, hipStream_t st);
+                        int coff, int mode, hipStream_t st, const float* aff_s = nullptr,
+                        const float* aff_t = nullptr);
 // k_fc.hip
 hipError_t launch_pack_fc(const float* W, f32x4* out, int K, int N, hipStream_t st);
 int fc_choose_splits(int M, int K, int N, int* kslice);
@@ -89,6 +91,12 @@ size_t fc_x3_bytes(int K, int N);
 hipError_t launch_pack_fc_x3(const float* W, void* out, int K, int N, float* unscale, hipStream_t st);
 hipError_t launch_fc_gemm_x3(const float* A, int lda, const void* Wpk, float unscale, float* part, int M, int K,
                              int N, int S, int kslice, hipStream_t st);
+// k_frame.hip (frame -> CoM -> crop chain)
+hipError_t launch_resize_bilinear(const float* x, int N, int H, int W, int C, float* out, int Ho, int Wo,
+                                  hipStream_t st);
+hipError_t launch_crop3d(const mp_camera& cam, const float* frames, int N, int H, int W, float frame_scale,
+                         const float* com_norm, const double com_scale[3], int dsz, float* patches, double* Ms,
+                         double* coms_out, int32_t* status, hipStream_t st);
 hipError_t launch_fc_reduce(const float* part, int S, int M, int N, const float* bias, int relu,
                             const float* aff_s, const float* aff_t, float* out, int ldo, hipStream_t st);
 

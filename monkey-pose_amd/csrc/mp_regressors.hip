@@ -67,9 +67,28 @@ std::vector<std::string> hier_fcs() {
   return v;
 }
 
-std::vector<ConvSpec> convs_of(int model) { return model == MP_MODEL_DENSE ? dense_convs() : hier_convs(); }
+// attn_model_struct (train_cnn_networks_hgru.py:440-475): five conv + 2x2 max pool + BN stages
+std::vector<ConvSpec> attn_convs() {
+  return {{"aconv_1", 3, 1, 1, 64},
+          {"aconv_2", 3, 1, 64, 128},
+          {"aconv_3", 3, 1, 128, 256},
+          {"aconv_4", 3, 1, 256, 512},
+          {"aconv_5", 5, 1, 512, 1024}};
+}
+// tf.layers.batch_normalization calls in build order: after apool_1, apool_2, pool_3, pool_4,
+// apool_5 (442-476) and after relu(afc_1) (482-490); default scopes of a fresh "cnn" scope
+const char* kAttnBn[] = {"batch_normalization",   "batch_normalization_1", "batch_normalization_2",
+                         "batch_normalization_3", "batch_normalization_4", "batch_normalization_5"};
+constexpr int ATTN_SIZE = 128;   // tf.image.resize_images(input_image, [128, 128]) (439)
+
+std::vector<ConvSpec> convs_of(int model) {
+  if (model == MP_MODEL_DENSE) return dense_convs();
+  if (model == MP_MODEL_ATTN) return attn_convs();
+  return hier_convs();
+}
 std::vector<std::string> fcs_of(int model) {
   if (model == MP_MODEL_HIER) return hier_fcs();
+  if (model == MP_MODEL_ATTN) return {"afc_1", "afc_out"};
   return std::vector<std::string>(std::begin(kDenseFc), std::end(kDenseFc));
 }
 
@@ -124,14 +143,16 @@ void conv(mp_ctx* c, const std::string& name, int n, const View& in, const View&
   hip_check(launch_igemm_conv(a, st), name.c_str());
 }
 
-void pool(int n, const View& in, const View& out, int mode, hipStream_t st) {
+void pool(int n, const View& in, const View& out, int mode, hipStream_t st, const float* aff_s = nullptr,
+          const float* aff_t = nullptr) {
   if (out.H != same_out(in.H, 2) || out.W != same_out(in.W, 2) || out.C != in.C)
     fail(MP_ERR_SHAPE, "pool shape mismatch");
-  hip_check(launch_pool2(in.p, in.ld, in.coff, n, in.H, in.W, in.C, out.p, out.ld, out.coff, mode, st), "pool");
+  hip_check(launch_pool2(in.p, in.ld, in.coff, n, in.H, in.W, in.C, out.p, out.ld, out.coff, mode, st, aff_s, aff_t),
+            "pool");
 }
 
 void fcl(mp_ctx* c, const std::string& name, int n, const float* in, int K, float* out, int ldo, bool relu,
-         hipStream_t st) {
+         hipStream_t st, const float* aff_s = nullptr, const float* aff_t = nullptr) {
   auto it = c->layers.find(name);
   if (it == c->layers.end()) fail(MP_ERR_STATE, "fc layer missing: " + name);
   const auto& L = it->second;
@@ -140,7 +161,7 @@ void fcl(mp_ctx* c, const std::string& name, int n, const float* in, int K, floa
   const int S = fc_choose_splits(n, K, L.cout, &ks);
   float* part = buf(c, "fc_part", (size_t)S * n * ((L.cout + 31) / 32 * 32));
   hip_check(launch_fc_gemm(in, K, L.w.v4(), part, n, K, L.cout, S, ks, st), name.c_str());
-  hip_check(launch_fc_reduce(part, S, n, L.cout, L.b.f(), relu ? 1 : 0, nullptr, nullptr, out, ldo, st),
+  hip_check(launch_fc_reduce(part, S, n, L.cout, L.b.f(), relu ? 1 : 0, aff_s, aff_t, out, ldo, st),
             name.c_str());
 }
 
@@ -266,6 +287,38 @@ void hier_forward(mp_ctx* c, const float* depth, int n, int H, int W, float* con
   fcl(c, "final_fc_2", n, a1, 1024, outs[0], c->layers["final_fc_2"].cout, false, st);       // 529-530
 }
 
+// ---------------------------------------------------------------------------- attention forward
+// attn_model_struct.build (train_cnn_networks_hgru.py:436-525), inference: resize to 128x128,
+// five [conv + relu -> 2x2 max pool -> BN] stages, afc_1 + relu -> BN, afc_out.  The BN of each
+// stage runs in the pool kernel's epilogue, the last one in the afc_1 split-K reduction.
+void attn_forward(mp_ctx* c, const float* frames, int n, int H, int W, float* out, hipStream_t st) {
+  float* x = const_cast<float*>(frames);
+  if (H != ATTN_SIZE || W != ATTN_SIZE) {
+    x = buf(c, "resized", (size_t)n * ATTN_SIZE * ATTN_SIZE);
+    hip_check(launch_resize_bilinear(frames, n, H, W, 1, x, ATTN_SIZE, ATTN_SIZE, st), "resize");
+  }
+  int h = ATTN_SIZE, w = ATTN_SIZE, cin = 1;
+  View cur = V(x, 1, 0, 1, h, w);
+  const auto specs = attn_convs();
+  for (size_t i = 0; i < specs.size(); ++i) {                                                  // 440-476
+    const auto& s = specs[i];
+    float* cv = buf(c, "attn_conv", (size_t)n * h * w * s.cout);
+    conv(c, s.name, n, cur, V(cv, s.cout, 0, s.cout, h, w), 1, st);
+    const int h2 = same_out(h, 2), w2 = same_out(w, 2);
+    float* pl = buf(c, i % 2 ? "attn_pool_b" : "attn_pool_a", (size_t)n * h2 * w2 * s.cout);
+    const auto& L = c->layers[s.name];
+    pool(n, V(cv, s.cout, 0, s.cout, h, w), V(pl, s.cout, 0, s.cout, h2, w2), 0, st, L.bn_s.f(), L.bn_t.f());
+    cur = V(pl, s.cout, 0, s.cout, h2, w2);
+    h = h2;
+    w = w2;
+    cin = s.cout;
+  }
+  float* h1 = buf(c, "attn_fc1", (size_t)n * 1024);
+  const auto& F1 = c->layers["afc_1"];
+  fcl(c, "afc_1", n, cur.p, h * w * cin, h1, F1.cout, true, st, F1.bn_s.f(), F1.bn_t.f());     // 478-490
+  fcl(c, "afc_out", n, h1, F1.cout, out, c->layers["afc_out"].cout, false, st);                // 502-503
+}
+
 }  // namespace
 
 namespace mpr {
@@ -275,6 +328,10 @@ bool known_name_regressor(int model, const std::string& n) {
     if (n == s.name + "/" + s.name + "_filters" || n == s.name + "/" + s.name + "_biases") return true;
   for (const auto& f : fcs_of(model))
     if (n == f + "/" + f + "_weights" || n == f + "/" + f + "_biases") return true;
+  if (model == MP_MODEL_ATTN)
+    for (const char* b : kAttnBn)
+      for (const char* v : {"gamma", "beta", "moving_mean", "moving_variance"})
+        if (n == std::string(b) + "/" + v) return true;
   return false;
 }
 
@@ -308,8 +365,21 @@ void finalize_regressor(mp_ctx* c) {
     L.b.alloc(N * sizeof(float));
     hip_check(hipMemcpy(L.b.p, b.dev->p, N * sizeof(float), hipMemcpyDeviceToDevice), "bias");
   }
+  if (c->model == MP_MODEL_ATTN) {
+    const auto specs = attn_convs();
+    for (size_t i = 0; i < specs.size(); ++i) {
+      auto& L = c->layers[specs[i].name];
+      bn_fold(c, kAttnBn[i], L.cout, L.bn_s, L.bn_t);
+    }
+    auto& F1 = c->layers["afc_1"];
+    if (F1.K != 4 * 4 * 1024) fail(MP_ERR_WEIGHT, "afc_1 must be [16384, N] (4x4x1024 after apool_5)");
+    if (c->layers["afc_out"].K != F1.cout) fail(MP_ERR_WEIGHT, "afc_out input size != afc_1 output size");
+    bn_fold(c, kAttnBn[5], F1.cout, F1.bn_s, F1.bn_t);
+  }
   c->head_sizes.clear();
-  if (c->model == MP_MODEL_DENSE) {
+  if (c->model == MP_MODEL_ATTN) {
+    c->head_sizes.push_back(c->layers["afc_out"].cout);
+  } else if (c->model == MP_MODEL_DENSE) {
     c->head_sizes.push_back(c->layers["fc_4"].cout);
   } else {
     c->head_sizes.push_back(c->layers["final_fc_2"].cout);
@@ -345,6 +415,31 @@ int mp_hier_fwd(mp_ctx* ctx, const float* depth, int64_t n, int64_t h, int64_t w
     hip_check(hipSetDevice(ctx->device), "hipSetDevice");
     ProfScope ps(ctx, static_cast<hipStream_t>(stream), "hier");
     hier_forward(ctx, depth, (int)n, (int)h, (int)w, outs, static_cast<hipStream_t>(stream));
+  });
+}
+
+int mp_attn_fwd(mp_ctx* ctx, const float* frames, int64_t n, int64_t h, int64_t w, float* out, void* stream) {
+  return guard([&] {
+    if (!ctx || !frames || !out) fail(MP_ERR_ARG, "mp_attn_fwd: null pointer");
+    if (ctx->model != MP_MODEL_ATTN) fail(MP_ERR_STATE, "context is not an attention model");
+    if (!ctx->finalized) fail(MP_ERR_STATE, "weights not finalized");
+    if (n <= 0 || n > (1 << 20) || h < 1 || w < 1 || h > 8192 || w > 8192) fail(MP_ERR_SHAPE, "bad input shape");
+    hip_check(hipSetDevice(ctx->device), "hipSetDevice");
+    ProfScope ps(ctx, static_cast<hipStream_t>(stream), "attn");
+    attn_forward(ctx, frames, (int)n, (int)h, (int)w, out, static_cast<hipStream_t>(stream));
+  });
+}
+
+int mp_resize_bilinear(const float* x, int64_t n, int64_t h, int64_t w, int64_t c, int64_t ho, int64_t wo,
+                       float* out, void* stream) {
+  return guard([&] {
+    if (!x || !out) fail(MP_ERR_ARG, "mp_resize_bilinear: null pointer");
+    if (n <= 0 || h <= 0 || w <= 0 || c <= 0 || ho <= 0 || wo <= 0 || h > 65536 || w > 65536 || ho > 65536 ||
+        wo > 65536 || n * ho * wo * c > ((int64_t)1 << 40))
+      fail(MP_ERR_SHAPE, "mp_resize_bilinear: bad shape");
+    hip_check(launch_resize_bilinear(x, (int)n, (int)h, (int)w, (int)c, out, (int)ho, (int)wo,
+                                     static_cast<hipStream_t>(stream)),
+              "resize");
   });
 }
 

@@ -135,6 +135,7 @@ struct mp_ctx {
   // ---- dense / hierarchical regressors (mp_regressors.hip) ----
   struct PackedLayer {
     DevBuf w, b;          // conv: HWIO as [K][Cout] packed like an FC weight; fc: [in][out] packed
+    DevBuf bn_s, bn_t;    // attention net: the folded BN that follows this layer (after pool / relu)
     int k = 0, cin = 0, cout = 0, K = 0;
   };
   std::map<std::string, PackedLayer> layers;   // keyed by layer name ("conv_3_1", "p_fc_2", ...)
@@ -219,6 +220,12 @@ struct ProfScope {
     }
   }
 };
+
+// mp_abi.hip: host vector -> device; inference BN folded to a per-channel affine
+// gamma * (x - mean) / sqrt(var + eps) + beta = x * s + t  (eps = 1e-5, hgru_pose.py:17)
+void upload(DevBuf& d, const std::vector<float>& h);
+void bn_fold(mp_ctx* c, const std::string& scope, int n, DevBuf& s_out, DevBuf& t_out,
+             std::vector<float>* hs = nullptr, std::vector<float>* ht = nullptr);
 
 // mp_regressors.hip
 void finalize_regressor(mp_ctx* c);

@@ -32,7 +32,14 @@ _CROP_SIGS = {
                                        ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
                                        ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                        ctypes.c_int]),
+    "mp_crop3d_dev": (ctypes.c_int, [ctypes.POINTER(_Camera), ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                                     ctypes.c_int64, ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                     ctypes.c_void_p, ctypes.c_void_p]),
 }
+
+_CROP_MSG = {1: "CoM depth is zero or not finite (no valid pixel in range?)", 2: "empty crop",
+             3: "degenerate bounds", 4: "resize target is empty"}
 
 
 def _lib_crop():
@@ -128,6 +135,51 @@ class MonkeyDetector(object):
                                                None if c is None else _p(c), dsize, _p(patches), _p(Ms),
                                                _p(com_out), int(nt)))
         return patches, Ms.reshape(n, 3, 3), com_out
+
+    def crop_batch_device(self, frames, com_norm, com_scale=(424, 512, 10000.), frame_scale=10000.,
+                          dsize=128, check=True, stream=None):
+        """``prepare_data_test`` (train_cnn_networks_hgru.py:61-74) on the GPU for a batch, with
+        ``tr_res`` = the attention output still on the device (``mp_crop3d_dev``, one launch):
+
+        frames     CUDA [n, h, w] or [n, h, w, 1] fp32 as fed to the attention net (image / max depth)
+        com_norm   CUDA [n, 3] fp32 attention output; com = com_norm * com_scale (float64)
+        returns    (patches CUDA [n, dsize, dsize, 1] = crop / maxDepth, Ms CUDA [n, 3, 3] f64,
+                    coms CUDA [n, 3] f64); with ``check`` the per-frame status is read back (one
+                    sync) and a failed frame raises like the host ``cropArea3D``."""
+        import torch
+        if not (isinstance(frames, torch.Tensor) and frames.is_cuda and isinstance(com_norm, torch.Tensor)
+                and com_norm.is_cuda):
+            raise TypeError("frames and com_norm must be CUDA (ROCm) tensors")
+        if frames.dim() == 4:
+            if frames.shape[-1] != 1:
+                raise ValueError("frames must be single-channel")
+            frames = frames[..., 0]
+        if frames.dim() != 3:
+            raise ValueError(f"frames must be [n, h, w], got {tuple(frames.shape)}")
+        fr = frames.detach().float().contiguous()
+        n, h, w = fr.shape
+        cn = com_norm.detach().float().contiguous().view(n, 3)
+        dev = fr.device
+        patches = torch.empty((n, dsize, dsize, 1), dtype=torch.float32, device=dev)
+        Ms = torch.empty((n, 3, 3), dtype=torch.float64, device=dev)
+        coms = torch.empty((n, 3), dtype=torch.float64, device=dev)
+        status = torch.empty((n,), dtype=torch.int32, device=dev)
+        scale = torch.tensor([float(v) for v in com_scale], dtype=torch.float64, device=dev)
+        st = _lib.current_stream(dev) if stream is None else stream
+        cam = self._cam()
+        _lib.check(_lib_crop().mp_crop3d_dev(ctypes.byref(cam), ctypes.c_void_p(fr.data_ptr()), n, h, w,
+                                             float(frame_scale), ctypes.c_void_p(cn.data_ptr()),
+                                             ctypes.c_void_p(scale.data_ptr()), int(dsize),
+                                             ctypes.c_void_p(patches.data_ptr()), ctypes.c_void_p(Ms.data_ptr()),
+                                             ctypes.c_void_p(coms.data_ptr()), ctypes.c_void_p(status.data_ptr()),
+                                             ctypes.c_void_p(st)))
+        self.last_status = status
+        if check:
+            bad = torch.nonzero(status).flatten().tolist()
+            if bad:
+                code = int(status[bad[0]].item())
+                raise _lib.MonkeyPoseError(-1, f"frame {bad[0]}: cropArea3D: {_CROP_MSG.get(code, code)}")
+        return patches, Ms, coms
 
     # ------------------------------------------------------------------ geometry (host numpy)
     def comToBounds(self, com, size):

@@ -1,0 +1,120 @@
+"""Drop-in for the inference pieces of ``/root/reference/train_cnn_networks_hgru.py``: the attention
+(centre-of-mass) regressor and the frame -> CoM -> crop -> pose chain of its ``test_model`` loop.
+
+* ``attn_model_struct().build(images, num_dims)`` -> ``.out_put`` [N, num_dims]
+  (train_cnn_networks_hgru.py:422-525): ``mp_attn_fwd`` -- TF1 bilinear resize to 128x128, five
+  conv + max-pool + BN stages, afc_1 + relu + BN, afc_out, on the generic implicit-GEMM conv /
+  split-K FC kernels (fp32 MFMA).
+* ``prepare_data_test(images, tr_res, md, config)`` (61-74): with CUDA tensors it crops every
+  frame on the GPU in one launch (``mp_crop3d_dev``), bit-exact with the host ``cropArea3D``
+  integers, and the patches never leave the device; with numpy arrays it runs the native host
+  crop (``mp_crop3d_batch``).
+* ``FramePosePipeline``: ``test_model``'s per-batch body (284-321) -- attention, device crop,
+  hGRU pose regressor -- as one device-resident call.
+
+Training (``train_model``: TFRecord queues, Adam, l2 losses) is outside the inference path.
+``train_mode`` must be falsy: the reference's ``test_model`` builds the attention net with
+``train_mode=True`` (dropout 0.7 and batch-statistics BN at test time, 287); that is a training
+graph and raises here, as for the other facades.
+"""
+from __future__ import annotations
+
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import numpy as np
+
+from . import _lib
+from . import weights as W
+from ._regressor import RegressorBase
+
+
+@dataclass
+class InferenceConfig:
+    """The ``config.py`` fields the inference chain reads (config.py:31-51)."""
+    image_orig_size: List[int] = field(default_factory=lambda: [424, 512, 1])
+    image_target_size: List[int] = field(default_factory=lambda: [128, 128, 1])
+    image_max_depth: float = 10000.
+    num_joints: int = 23
+    num_dims: int = 3
+
+    @property
+    def num_classes(self) -> int:
+        return self.num_joints * self.num_dims
+
+
+class attn_model_struct(RegressorBase):
+    """``attn_model_struct`` (train_cnn_networks_hgru.py:422-525), inference."""
+
+    MODEL_KIND = _lib.MP_MODEL_ATTN
+
+    def __init__(self, trainable=True):
+        super().__init__(trainable)
+        self._BATCH_NORM_DECAY = 0.997
+        self._BATCH_NORM_EPSILON = 1e-5
+
+    def build(self, depth, output_shape, batch_norm=None, train_mode=None):
+        """``depth`` CUDA [N, H, W, 1] fp32 normalised frames (images / image_max_depth); any H, W
+        (resized to 128 x 128).  Sets and returns ``.out_put`` [N, output_shape]."""
+        depth = self._check_input(depth, batch_norm, train_mode)
+        self.output_shape = int(output_shape)
+        table = W.attn_vars(output_shape=self.output_shape)
+        self._ctx = self._context(self.output_shape, table, depth.device.index or 0)
+        return self.forward(depth)
+
+    def forward(self, depth, out=None):
+        import torch
+        depth = depth.detach().float().contiguous()
+        if out is None:
+            out = torch.empty((depth.shape[0], self.output_shape), dtype=torch.float32, device=depth.device)
+        self._ctx.attn_fwd(depth, out, _lib.current_stream(depth.device))
+        self.out_put = out
+        return out
+
+
+def prepare_data_test(image_np, tr_res, md, config, dsize: Optional[int] = None):
+    """``prepare_data_test`` (train_cnn_networks_hgru.py:61-74): returns (patches [N, 128, 128, 1]
+    = cropArea3D(image * max_depth, tr_res * [orig0, orig1, max_depth]) / max_depth, coms, Ms).
+
+    CUDA tensors in -> everything stays on the device (``coms`` [N, 3] and ``Ms`` [N, 3, 3] float64
+    tensors); numpy in -> the native host crop, ``coms`` / ``Ms`` as lists like the reference."""
+    import torch
+    dsize = int(dsize or config.image_target_size[0])
+    scale = (float(config.image_orig_size[0]), float(config.image_orig_size[1]), float(config.image_max_depth))
+    if isinstance(image_np, torch.Tensor) and image_np.is_cuda:
+        patches, Ms, coms = md.crop_batch_device(image_np, tr_res, com_scale=scale,
+                                                 frame_scale=float(config.image_max_depth), dsize=dsize)
+        return patches, coms, Ms
+    fr = np.asarray(image_np, np.float32)
+    if fr.ndim == 4:
+        fr = fr[..., 0]
+    frames_mm = fr * np.float32(config.image_max_depth)
+    coms_in = np.asarray(tr_res, np.float32).reshape(-1, 3) * np.array(scale)
+    patches, Ms, coms = md.crop_batch(frames_mm, coms=coms_in, dsize=dsize)
+    if float(md.maxDepth) != float(config.image_max_depth):
+        raise ValueError("md.maxDepth must equal config.image_max_depth for the host batch crop")
+    return patches, list(coms), [np.asmatrix(m) for m in Ms]
+
+
+class FramePosePipeline:
+    """``test_model``'s per-batch body (train_cnn_networks_hgru.py:284-321) on one GPU:
+    frames -> attention CoM -> device crop -> hGRU pose, no host round trip in between.
+
+    ``run(frames)`` returns (pose output [N, num_classes] normalised by cube_z / 2, coms [N, 3],
+    Ms [N, 3, 3]); the caller maps to millimetres with ``md.getAbsoluteCoordinates`` as the
+    reference does."""
+
+    def __init__(self, attn: attn_model_struct, pose_model, md, config: Optional[InferenceConfig] = None,
+                 check_crops: bool = True):
+        self.attn, self.pose, self.md = attn, pose_model, md
+        self.config = config or InferenceConfig()
+        self.check_crops = check_crops
+
+    def run(self, frames, h2_init=None):
+        cfg = self.config
+        com_norm = self.attn.build(frames, cfg.num_dims)
+        patches, Ms, coms = self.md.crop_batch_device(
+            frames, com_norm, com_scale=(cfg.image_orig_size[0], cfg.image_orig_size[1], cfg.image_max_depth),
+            frame_scale=float(cfg.image_max_depth), dsize=cfg.image_target_size[0], check=self.check_crops)
+        out = self.pose.build(patches, cfg.num_classes, h2_init=h2_init)
+        return out, coms, Ms

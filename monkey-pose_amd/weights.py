@@ -219,6 +219,41 @@ def hier_vars(output_shape: int = 108, part_shapes=(39, 39, 39, 39, 36), crop: i
     return v
 
 
+ATTN_CONV_SPECS = (("aconv_1", 3, 1, 64), ("aconv_2", 3, 64, 128), ("aconv_3", 3, 128, 256),
+                   ("aconv_4", 3, 256, 512), ("aconv_5", 5, 512, 1024))
+
+
+def attn_vars(output_shape: int = 3) -> List[Var]:
+    """All variables of ``attn_model_struct.build`` (train_cnn_networks_hgru.py:436-525) in build
+    order.  Input is resized to 128x128 (439), so afc_1's fan-in is 4*4*1024 for any frame size.
+    The six ``tf.layers.batch_normalization`` calls take the default scopes of a fresh ``cnn``
+    scope (``batch_normalization`` .. ``_5``); in the reference's combined test graph (attention
+    built first, train_cnn_networks_hgru.py:285-289) the pose model's BNs follow as ``_6`` ..."""
+    bn = ["cnn/batch_normalization"] + [f"cnn/batch_normalization_{i}" for i in range(1, 6)]
+    v: List[Var] = []
+    for (name, k, cin, cout), b in zip(ATTN_CONV_SPECS, bn):
+        v += _conv_b(name, k, cin, cout)
+        v += _bn(b, cout)
+    v += _fc("cnn/afc_1", 4 * 4 * 1024, 1024)
+    v += _bn(bn[5], 1024)
+    v += _fc("cnn/afc_out", 1024, output_shape)
+    return v
+
+
+def attn_synth_weights(seed: int = 1234, output_shape: int = 3) -> Dict[str, np.ndarray]:
+    """Synthetic attention weights whose CoM output lands inside a 424x512 frame: the glorot draw
+    for everything, then afc_out scaled by 1/64 with biases (0.5, 0.5, 0.15), i.e. a CoM near
+    (212, 256, 1500 mm) +- a few pixels (com = out * (424, 512, 10000),
+    train_cnn_networks_hgru.py:69).  Only the synthetic end-to-end chain needs this; a plain
+    ``synth_weights(attn_vars())`` draw gives arbitrary CoMs, most of which crop nothing."""
+    w = synth_weights(attn_vars(output_shape), seed)
+    w["cnn/afc_out/afc_out_weights"] = (w["cnn/afc_out/afc_out_weights"] / 64.0).astype(np.float32)
+    b = np.zeros(output_shape, np.float32)
+    b[:3] = (0.5, 0.5, 0.15)[:min(3, output_shape)]
+    w["cnn/afc_out/afc_out_biases"] = b
+    return w
+
+
 def synth_value(var: Var, seed: int, timesteps: int = 8) -> np.ndarray:
     """Deterministic stand-in for the reference's TF initialisers (see module docstring)."""
     s, nm, kind = var.shape, var.name, var.init
@@ -257,6 +292,24 @@ def synth_hidden(shape: Sequence[int], seed: int = 7, name: str = "h2_init",
     if limit is None:
         limit = math.sqrt(6.0 / (2 * k))
     return sym_uniform(seed, name, shape, limit)
+
+
+def synth_frames(n: int, seed: int = 11, h: int = 424, w: int = 512) -> np.ndarray:
+    """Synthetic normalised full depth frames [n,h,w,1] float32 (mm / 10000, the attention net's
+    input, train_cnn_networks_hgru.py:116): a far wall at 3000-4000 mm, one ellipsoid body at
+    800-1500 mm, ~3 % zero dropout; depths are whole millimetres as from a Kinect."""
+    yy, xx = np.mgrid[0:h, 0:w].astype(np.float64)
+    out = np.empty((n, h, w), np.float32)
+    for i in range(n):
+        u = uniform01(seed, f"frame{i}", 8)
+        f = 3000.0 + 1000.0 * u[0] + 200.0 * np.sin(xx / 37.0) * np.cos(yy / 23.0)
+        cy, cx = (0.3 + 0.4 * u[1]) * h, (0.3 + 0.4 * u[2]) * w
+        ry, rx = 30 + 60 * u[3], 30 + 60 * u[4]
+        r2 = ((yy - cy) / ry) ** 2 + ((xx - cx) / rx) ** 2
+        f = np.where(r2 < 1.0, 800.0 + 700.0 * u[5] + 50.0 * r2, f)
+        f[uniform01(seed, f"fdrop{i}", h * w).reshape(h, w) < 0.03] = 0.0
+        out[i] = (np.round(f).astype(np.float32) / np.float32(10000.0))
+    return out[..., None]
 
 
 def synth_crops(n: int, seed: int = 42, size: int = 128) -> np.ndarray:

@@ -201,3 +201,24 @@ def synth_frame(seed: int, h: int = 424, w: int = 512, dtype=np.float32, integer
     if integer:
         f = np.round(f)
     return f.astype(dtype)
+
+
+def prepare_data_test(frames_norm: np.ndarray, tr_res: np.ndarray, md: "MonkeyDetectorRef",
+                      orig_size=(424, 512), max_depth: float = 10000.0, dsize: int = 128):
+    """train_cnn_networks_hgru.py:61-74 with float32 frames [n, h, w(, 1)] (image / max depth) and
+    the attention output tr_res [n, 3]: per frame com = tr_res * [orig0, orig1, max_depth]
+    (float32 * float64 list -> float64), crop of image * max_depth (float32), patch = crop /
+    max_depth (float32).  Returns (patches [n, dsize, dsize] float32, Ms [n, 3, 3], coms [n, 3])."""
+    fr = np.asarray(frames_norm, np.float32)
+    if fr.ndim == 4:
+        fr = fr[..., 0]
+    tr = np.asarray(tr_res, np.float32)
+    scale = np.array([orig_size[0], orig_size[1], max_depth])
+    patches, Ms, coms = [], [], []
+    for i in range(fr.shape[0]):
+        com = tr[i] * scale
+        crop, M, c, _ = md.cropArea3D(fr[i] * np.float32(max_depth), com=com, dsize=(dsize, dsize))
+        patches.append(np.asarray(crop, np.float32) / np.float32(max_depth))
+        Ms.append(np.asarray(M, np.float64))
+        coms.append(np.asarray(c, np.float64))
+    return np.stack(patches), np.stack(Ms), np.stack(coms)

@@ -8,8 +8,15 @@ NumPy restatements of the two other pose regressors on the north-star path, call
   fc_layer 450-457)
 * ``hier_model_struct.build``   -- /root/reference/train_hier_networks.py:338-530
   (helpers 535-579, same semantics)
+* ``attn_model_struct.build``   -- /root/reference/train_cnn_networks_hgru.py:436-525 (helpers
+  541-570), the attention / centre-of-mass regressor, with ``tf.image.resize_images`` (439)
+  restated from TF1's published bilinear kernel (third-party, TF 1.x not importable here:
+  PARITY UNPINNED): BILINEAR, align_corners=False, scale = in/out (float32), source coordinate
+  in = out * scale (legacy, no half-pixel offset), lower = floor(in), upper = min(ceil(in),
+  size-1), lerp = in - floor(in); value = top + (bottom - top) * ylerp with top/bottom the
+  x-lerps, all float32 without fused multiply-add.
 
-Inference only (train_mode falsy: no dropout); ``batchnorm=None`` at every call site the
+Inference only (train_mode falsy: no dropout, BN from moving statistics); ``batchnorm=None`` at every call site the
 reference's test paths use, so the conv_layer batch-moment branch is never taken.
 """
 from __future__ import annotations
@@ -18,7 +25,7 @@ from typing import Dict
 
 import numpy as np
 
-from .hgru_ref import avg_pool_same, conv2d_same, fc, max_pool_same
+from .hgru_ref import avg_pool_same, batch_norm_inf, conv2d_same, fc, max_pool_same
 
 
 def _conv(wts, x, name, stride=1):
@@ -121,3 +128,49 @@ def hier_forward(depth: np.ndarray, wts: Dict[str, np.ndarray], dtype=np.float64
     f1 = np.maximum(_fc(wts, _cat(*hand), "final_fc_1"), 0)            # 525-528 (dropout ignored)
     out = _fc(wts, f1, "final_fc_2")                                   # 529-530
     return out, outs
+
+
+def resize_bilinear_tf1(x: np.ndarray, oh: int, ow: int) -> np.ndarray:
+    """tf.image.resize_images(x, [oh, ow]) (TF1 defaults) of a float32 [n, h, w, c] batch, in
+    float32 with the kernel's operation order (see module docstring)."""
+    x = np.asarray(x, np.float32)
+    n, h, w, c = x.shape
+    f32 = np.float32
+    hs, ws = f32(h) / f32(oh), f32(w) / f32(ow)
+
+    def weights(out, scale, size):
+        i = np.arange(out, dtype=np.float32) * scale
+        fl = np.floor(i)
+        lo = np.maximum(fl.astype(np.int64), 0)
+        hi = np.minimum(np.ceil(i).astype(np.int64), size - 1)
+        return lo, hi, (i - fl).astype(np.float32)
+
+    y0, y1, ly = weights(oh, hs, h)
+    x0, x1, lx = weights(ow, ws, w)
+    tl, tr = x[:, y0][:, :, x0], x[:, y0][:, :, x1]
+    bl, br = x[:, y1][:, :, x0], x[:, y1][:, :, x1]
+    lx4 = lx[None, None, :, None]
+    top = tl + (tr - tl) * lx4
+    bot = bl + (br - bl) * lx4
+    return (top + (bot - top) * ly[None, :, None, None]).astype(np.float32)
+
+
+ATTN_BN = ["cnn/batch_normalization"] + [f"cnn/batch_normalization_{i}" for i in range(1, 6)]
+
+
+def attn_forward(frames: np.ndarray, wts: Dict[str, np.ndarray], dtype=np.float64, keep=False):
+    """train_cnn_networks_hgru.py:436-525 (inference).  ``frames`` [n, h, w, 1] float32 normalised
+    depth (images / image_max_depth, 116).  Returns [n, output_shape] (u, v, d) / image size."""
+    r = resize_bilinear_tf1(frames, 128, 128)                         # 439 (float32, as TF)
+    x = r.astype(dtype)
+    t = {"resized": r}
+    for i, name in enumerate(("aconv_1", "aconv_2", "aconv_3", "aconv_4", "aconv_5")):  # 440-476
+        x = batch_norm_inf(max_pool_same(_conv(wts, x, name)), wts, ATTN_BN[i])
+        t[name] = x
+    h = np.maximum(_fc(wts, x, "afc_1"), 0)                           # 478-479
+    h = batch_norm_inf(h, wts, ATTN_BN[5])                            # 482-490 (per feature)
+    out = _fc(wts, h, "afc_out")                                      # 502-503
+    if keep:
+        t["relu1"] = h
+        return out, t
+    return out

@@ -64,6 +64,17 @@ def regressor_inputs(kind, n, crop, ws, cs):
     return W.synth_weights(table, seed=ws), W.synth_crops(n, seed=cs, size=crop)
 
 
+# (name, n, frame h, frame w, weight seed, frame seed): attention CoM regressor
+# (train_cnn_networks_hgru.py:436-525) on full frames + prepare_data_test (61-74) on its output
+ATTN_CASES = [
+    ("attn_f424", 2, 424, 512, 79, 11),
+]
+
+
+def attn_inputs(n, h, w, ws, fs):
+    return W.attn_synth_weights(seed=ws), W.synth_frames(n, seed=fs, h=h, w=w)
+
+
 def checksums(a):
     a = np.asarray(a, np.float64)
     return [float(a.sum()), float((a * a).sum()), float(np.abs(a).max())]
@@ -106,6 +117,16 @@ def main(which=None):
                                 **{f"{k}_out": v for k, v in parts.items()})
         meta[name] = dict(kind=kind, n=n, crop=crop, weight_seed=ws, crop_seed=cs)
         print(name, out[:, :4])
+    from oracle import crop_ref as CR
+    for (name, n, h, w, ws, fs) in ATTN_CASES:
+        if which and name not in which:
+            continue
+        wts, frames = attn_inputs(n, h, w, ws, fs)
+        out = RR.attn_forward(frames, wts)
+        patches, Ms, coms = CR.prepare_data_test(frames, out.astype(np.float32), CR.MonkeyDetectorRef())
+        np.savez_compressed(os.path.join(HERE, f"{name}.npz"), out=out, patches=patches, Ms=Ms, coms=coms)
+        meta[name] = dict(kind="attn", n=n, h=h, w=w, weight_seed=ws, frame_seed=fs)
+        print(name, out, coms)
     path = os.path.join(HERE, "golden.json")
     old = json.load(open(path)) if os.path.exists(path) else {}
     old.update(meta)
