@@ -66,8 +66,12 @@ enum { MP_MEM_HOST = 0, MP_MEM_DEVICE = 1 };
  *   MP_DTYPE_F32_FFT    fp32 FFT convolution on a 72x72 grid (exact circular = SAME linear conv
  *                       for maps up to 64x64): fp32 72-point FFTs + a per-frequency complex
  *                       channel GEMM on fp32 MFMA; ~50x fewer FLOPs than direct at 15x15 taps,
- *                       error ~1e-6 of max|output|.  Needs map height <= 64, width 32 or 64. */
-enum { MP_DTYPE_F32 = 0, MP_DTYPE_F32_SPLIT = 1, MP_DTYPE_F32_FFT = 2 };
+ *                       error ~1e-6 of max|output|.  Needs map height <= 64, width 32 or 64.
+ *   MP_DTYPE_BF16       the FFT path with bf16 spectra (input and output), bf16 spectral weights and
+ *                       bf16 1x1 gate weights: one v_mfma_f32_32x32x16_bf16 product per MAC, fp32
+ *                       accumulation, fp32 FFTs and elementwise math; backbone and fc_1 stay
+ *                       fp32-class.  Error ~1e-3..1e-2 of max|output| (SURVEY config 4). */
+enum { MP_DTYPE_F32 = 0, MP_DTYPE_F32_SPLIT = 1, MP_DTYPE_F32_FFT = 2, MP_DTYPE_BF16 = 3 };
 
 /* library version, (major << 16) | minor */
 int mp_version(void);
@@ -98,6 +102,23 @@ int mp_reserve(mp_ctx* ctx, int64_t max_batch);
  *   out    [n, output_shape] joint coordinates / (cube_z / 2), joint-major (j*3 + {x,y,z}) */
 int mp_hgru_pose_fwd(mp_ctx* ctx, const float* depth, int64_t n, int64_t h, int64_t w,
                      const float* o0, float* out, void* stream);
+
+/* the reference model's readable intermediates (hgru_pose.py:50-103: m.conv1, m.pool1, m.conv2,
+ * m.conv3, m.hgru, m.fc1, m.relu1); each a caller-owned device buffer, NULL = not wanted.
+ * NHWC fp32 like the reference tensors; [n, 1024] for fc1 / relu1. */
+typedef struct {
+  float* conv1;  /* [n, h, w, 64]      relu(conv_1)                       (50)      */
+  float* pool1;  /* [n, h/2, w/2, 64]  BN(max_pool(conv1))                (51-60)   */
+  float* conv2;  /* [n, h/2, w/2, 64]  BN(relu(conv_2))                   (61-70)   */
+  float* conv3;  /* [n, h/2, w/2, 64]  BN(relu(conv_3))                   (71-80)   */
+  float* hgru;   /* [n, h/2, w/2, 64]  BN(O_T), the fc_1 input            (81-90)   */
+  float* fc1;    /* [n, 1024]          fc_1 + bias (pre-activation)       (91)      */
+  float* relu1;  /* [n, 1024]          BN(relu(fc1))                      (92-103)  */
+} mp_pose_taps;
+
+/* mp_hgru_pose_fwd that also writes the requested intermediates (taps may be NULL) */
+int mp_hgru_pose_fwd_taps(mp_ctx* ctx, const float* depth, int64_t n, int64_t h, int64_t w,
+                          const float* o0, float* out, const mp_pose_taps* taps, void* stream);
 
 /* ContextualCircuit(X, timesteps, ...).build() -> O  (hgru_module.py:872-959), hgru_pose aux:
  *   x, o0, o_out  [n, h, w, k] NHWC; k must be 64, h % 16 == 0, w % 32 == 0;

@@ -27,14 +27,18 @@ MP_MEM_DEVICE = 1
 MP_DTYPE_F32 = 0
 MP_DTYPE_F32_SPLIT = 1
 MP_DTYPE_F32_FFT = 2
+MP_DTYPE_BF16 = 3
 DTYPES = {'fp32': MP_DTYPE_F32, 'f32': MP_DTYPE_F32, 'fp32_split': MP_DTYPE_F32_SPLIT,
-          'f32_split': MP_DTYPE_F32_SPLIT, 'fp32_fft': MP_DTYPE_F32_FFT, 'f32_fft': MP_DTYPE_F32_FFT}
+          'f32_split': MP_DTYPE_F32_SPLIT, 'fp32_fft': MP_DTYPE_F32_FFT, 'f32_fft': MP_DTYPE_F32_FFT,
+          'bf16': MP_DTYPE_BF16}
 
 
 def resolve_dtype(name: str, h: int, w: int) -> str:
     """'auto' -> the fastest fp32-class eCRF path supporting an h x w hGRU map: the FFT path for
     maps up to 64 x 64 with width 32 or 64 (the reference's 128^2 / 64^2 crops), else the f16x3
     direct path for multiples of 32, else exact fp32.  Explicit names pass through."""
+    if name == 'bf16' and not (1 <= h <= 64 and w in (32, 64)):
+        raise ValueError("compute dtype 'bf16' runs on the FFT path: hGRU map height <= 64, width 32 or 64")
     if name != 'auto':
         return name
     if 1 <= h <= 64 and w in (32, 64):
@@ -62,6 +66,9 @@ _SIGS = {
     "mp_hgru_pose_fwd": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                         ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
                                         ctypes.c_void_p, ctypes.c_void_p]),
+    "mp_hgru_pose_fwd_taps": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                             ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
+                                             ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "mp_hgru_circuit_fwd": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                            ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
                                            ctypes.c_int64, ctypes.c_int, ctypes.c_void_p,
@@ -83,6 +90,13 @@ _SIGS = {
 }
 
 _lib: Optional[ctypes.CDLL] = None
+
+# mp_pose_taps field order (include/monkeypose.h)
+TAP_NAMES = ("conv1", "pool1", "conv2", "conv3", "hgru", "fc1", "relu1")
+
+
+class PoseTaps(ctypes.Structure):
+    _fields_ = [(n, ctypes.c_void_p) for n in TAP_NAMES]
 
 
 class MonkeyPoseError(RuntimeError):
@@ -177,6 +191,13 @@ class Context:
         n, h, w, c = depth.shape
         check(self.lib.mp_hgru_pose_fwd(self.h, _ptr(depth), n, h, w, _ptr(o0), _ptr(out),
                                         ctypes.c_void_p(stream)))
+
+    def pose_fwd_taps(self, depth, o0, out, taps: dict, stream: int) -> None:
+        """mp_hgru_pose_fwd_taps; ``taps`` maps names of TAP_NAMES to CUDA output tensors."""
+        n, h, w, c = depth.shape
+        t = PoseTaps(*[ctypes.c_void_p(_ptr(taps[k]) if k in taps else None) for k in TAP_NAMES])
+        check(self.lib.mp_hgru_pose_fwd_taps(self.h, _ptr(depth), n, h, w, _ptr(o0), _ptr(out),
+                                             ctypes.byref(t), ctypes.c_void_p(stream)))
 
     def circuit_fwd(self, x, o0, out, timesteps: int, stream: int) -> None:
         n, h, w, k = x.shape

@@ -50,10 +50,27 @@ __device__ __forceinline__ f32x16 mfma16(f16x8 a, f16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
 
+// MP_DTYPE_BF16: spectra S / Y hold one bf16 (re, im) pair per channel (16 B per 4-channel group
+// and frequency instead of 32 B), the spectral and gate GEMMs are one v_mfma_f32_32x32x16_bf16
+// product with fp32 accumulation, no scaling (bf16 has the fp32 exponent range)
+typedef __bf16 bf16x8 __attribute__((ext_vector_type(8)));
+typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+
+__device__ __forceinline__ f32x16 mfmab(bf16x8 a, bf16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_bf16(a, b, c, 0, 0, 0);
+}
+__device__ __forceinline__ uint32_t pack_bf2(float a, float b) {
+  const bf16x2 v = {(__bf16)a, (__bf16)b};   // round to nearest even (v_cvt_pk_bf16_f32)
+  return __builtin_bit_cast(uint32_t, v);
+}
+
 
 struct cpx {
   float x, y;
 };
+__device__ __forceinline__ cpx unpack_bf2(uint32_t u) {   // bf16 -> fp32 is exact: the high half
+  return {__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)};
+}
 __device__ __forceinline__ cpx operator+(cpx a, cpx b) { return {a.x + b.x, a.y + b.y}; }
 __device__ __forceinline__ cpx operator-(cpx a, cpx b) { return {a.x - b.x, a.y - b.y}; }
 __device__ __forceinline__ cpx scale(cpx a, float s) { return {a.x * s, a.y * s}; }
@@ -154,6 +171,7 @@ __device__ __forceinline__ void fft72(cpx (&v)[72]) {
 //   column phase (148 threads): column (fx, c), fx = 0..36 (the real-input half spectrum)
 constexpr int FWD_LD = 65;        // pitch (complex) of the forward transpose T[fx][c][y]
 constexpr int STG_LD = 296;       // output staging pitch per fx, dwords (36 fy x 8 dwords + 8 pad)
+constexpr int STG_LD_B = 148;     // the same for bf16 spectra (36 fy x 4 dwords + 4 pad)
 constexpr int FFT_LDS = FX * 4 * FWD_LD;   // complex elements of the block's LDS (76,960 B)
 
 // forward row phase: the packed row v (a + ib, zero padded) -> half spectra of a and b in T
@@ -173,6 +191,7 @@ __device__ __forceinline__ void fwd_rows_to_T(cpx (&v)[72], int y, int p, cpx* T
 // forward column phase: T -> S[b][cq][fx*72+fy] (scaled, split to f16 hi / lo).  The block's
 // contiguous 85 KiB S run is written through LDS (T's space) in two fy halves, 1 KiB per
 // wave-instruction.  Called by ALL threads (contains barriers); T must be complete on entry.
+template <bool BF>
 __device__ __forceinline__ void fwd_cols_to_S(cpx* T, void* __restrict__ S, int b, int cq, int tid) {
   const bool col = tid < FX * 4;
   const int fx = tid >> 2, c = tid & 3;
@@ -183,6 +202,26 @@ __device__ __forceinline__ void fwd_cols_to_S(cpx* T, void* __restrict__ S, int 
     fft72<-1>(v);
   }
   uint32_t* stg = reinterpret_cast<uint32_t*>(T);
+  if constexpr (BF) {
+    uint4* dst = reinterpret_cast<uint4*>(S) + ((size_t)b * 16 + cq) * NF;
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      lds_barrier();
+      if (col) {
+#pragma unroll
+        for (int j = 0; j < 36; ++j) {
+          const cpx z = v[36 * half + j];
+          stg[fx * STG_LD_B + j * 4 + c] = pack_bf2(z.x, z.y);
+        }
+      }
+      lds_barrier();
+      for (int i = tid; i < FX * 36; i += 192) {   // per fx: 36 groups x 16 B at f = fx*72 + 36*half
+        const int ffx = i / 36, w = i - ffx * 36;
+        dst[ffx * 72 + 36 * half + w] = *reinterpret_cast<const uint4*>(stg + ffx * STG_LD_B + w * 4);
+      }
+    }
+    return;
+  }
   uint4* dst = reinterpret_cast<uint4*>(S) + ((size_t)b * 16 + cq) * NF * 2;
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
@@ -209,13 +248,21 @@ __device__ __forceinline__ void fwd_cols_to_S(cpx* T, void* __restrict__ S, int 
 
 // inverse column phase: Y[b][cq][f] -> T[y][c][fx] (rows y < 64).  Direct per-thread loads (72
 // independent 8-byte loads in flight per thread) measured faster than an LDS-staged read.
-__device__ __forceinline__ void inv_cols_to_T(const cpx* __restrict__ Y, int b, int cq, int tid, cpx* T) {
+template <bool BF>
+__device__ __forceinline__ void inv_cols_to_T(const void* __restrict__ Y, int b, int cq, int tid, cpx* T) {
   if (tid < FX * 4) {
     const int fx = tid >> 2, c = tid & 3;
-    const cpx* src = Y + (((size_t)b * 16 + cq) * NF + fx * 72) * 4 + c;
+    const size_t off = (((size_t)b * 16 + cq) * NF + fx * 72) * 4 + c;
     cpx v[72];
+    if constexpr (BF) {
+      const uint32_t* src = static_cast<const uint32_t*>(Y) + off;
 #pragma unroll
-    for (int fy = 0; fy < 72; ++fy) v[fy] = src[fy * 4];
+      for (int fy = 0; fy < 72; ++fy) v[fy] = unpack_bf2(src[fy * 4]);
+    } else {
+      const cpx* src = static_cast<const cpx*>(Y) + off;
+#pragma unroll
+      for (int fy = 0; fy < 72; ++fy) v[fy] = src[fy * 4];
+    }
     fft72<1>(v);
 #pragma unroll
     for (int y = 0; y < 64; ++y) T[(y * 4 + c) * FX + fx] = v[y];   // rows >= H: unused
@@ -245,6 +292,7 @@ constexpr int RLD = 73;
 // forward 2-D FFT of one C8 activation map -> S.  The rows are read straight into registers (64
 // independent 8-byte loads in flight per thread): staging the tile through LDS pixel-major measured
 // slower (0.24 vs 0.18 ms at B = 256) -- the load pass and its barrier serialise ahead of the FFT.
+template <bool BF>
 __global__ __launch_bounds__(192, 2) void fft_fwd_kernel(const float* __restrict__ src, void* __restrict__ S,
                                                       int H, int W) {
   __shared__ cpx T[FFT_LDS];
@@ -267,17 +315,18 @@ __global__ __launch_bounds__(192, 2) void fft_fwd_kernel(const float* __restrict
     fwd_rows_to_T(v, y, p, T);
   }
   lds_barrier();
-  fwd_cols_to_S(T, S, b, cq, tid);
+  fwd_cols_to_S<BF>(T, S, b, cq, tid);
 }
 
 // inverse 2-D FFT of Y -> the spatial conv result P (C8)
-__global__ __launch_bounds__(192, 2) void fft_inv_kernel(const cpx* __restrict__ Y, float* __restrict__ P,
+template <bool BF>
+__global__ __launch_bounds__(192, 2) void fft_inv_kernel(const void* __restrict__ Y, float* __restrict__ P,
                                                       int H, int W) {
   __shared__ cpx T[FFT_LDS];
   const int b = blockIdx.x >> 4, cq = blockIdx.x & 15;
   const int q = cq >> 1, e0 = 4 * (cq & 1);
   const int tid = threadIdx.x;
-  inv_cols_to_T(Y, b, cq, tid, T);
+  inv_cols_to_T<BF>(Y, b, cq, tid, T);
   lds_barrier();
   const int y = tid >> 1, p = tid & 1;
   const bool live = tid < 128 && y < H;
@@ -304,14 +353,15 @@ __global__ __launch_bounds__(192, 2) void fft_inv_kernel(const cpx* __restrict__
 // P1 never leaves the block: the inverse rows are parked in LDS, the epilogue runs pixel-major
 // over them (X, O in, I out: one float4 per lane), and the parked I rows are the forward row
 // transform's input.  p: the A-epilogue arguments (X, O, vecs; dst = I).
-__global__ __launch_bounds__(192, 2) void fft_inv_a_fwd_kernel(const cpx* __restrict__ Y, ConvArgs p,
+template <bool BF>
+__global__ __launch_bounds__(192, 2) void fft_inv_a_fwd_kernel(const void* __restrict__ Y, ConvArgs p,
                                                             void* __restrict__ S) {
   __shared__ cpx T[FFT_LDS];
   const int H = p.H, W = p.W;
   const int b = blockIdx.x >> 4, cq = blockIdx.x & 15;
   const int q = cq >> 1, e0 = 4 * (cq & 1);
   const int tid = threadIdx.x;
-  inv_cols_to_T(Y, b, cq, tid, T);
+  inv_cols_to_T<BF>(Y, b, cq, tid, T);
   lds_barrier();
   const int y = tid >> 1, pp = tid & 1;
   const bool live = tid < 128 && y < H;
@@ -373,7 +423,7 @@ __global__ __launch_bounds__(192, 2) void fft_inv_a_fwd_kernel(const cpx* __rest
   lds_barrier();   // parked rows read: T's space is free
   if (tid < 128) fwd_rows_to_T(v, y, pp, T);
   lds_barrier();
-  fwd_cols_to_S(T, S, b, cq, tid);
+  fwd_cols_to_S<BF>(T, S, b, cq, tid);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -486,6 +536,74 @@ __global__ __launch_bounds__(256, 2) void spec_gemm_kernel(const uint4* __restri
   }
 }
 
+// bf16 spectral GEMM (MP_DTYPE_BF16): the same blocking, fragments and XCD placement as
+// spec_gemm_kernel with 16-byte spectra entries (one bf16 (re, im) pair per channel): a block's S
+// tile is 32 images x 16 cq x 64 B, one v_mfma_f32_32x32x16_bf16 per (k-step, co block, re|im row
+// half), weights Gb[f][cq][co] (bf16x8 = 4 complex), Y written as bf16 pairs.
+constexpr int SGB_YLD = 16 * 4 + 1;    // Y tile pitch (16-B units) per image
+__global__ __launch_bounds__(256, 2) void spec_gemm_bf_kernel(const uint4* __restrict__ S, const uint4* __restrict__ Gb,
+                                                              uint4* __restrict__ Y, int B, int ngrp) {
+  __shared__ uint4 tile[16 * 4 * SG_SLD];   // 33,792 B (S tile [cq][f][b]; Y tile [b][cq][f])
+  const int q8 = blockIdx.x / (8 * ngrp), rem = blockIdx.x - q8 * 8 * ngrp;
+  const int grp = rem >> 3, quad = q8 * 8 + (rem & 7);
+  if (quad >= NQUAD) return;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, j = lane & 31;
+  const int img0 = grp * SG_NI;
+  uint4 pre[8];
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int idx = it * 256 + tid, line = idx >> 2, piece = idx & 3;
+    const int bl = line >> 4, cq = line & 15;
+    const int b = min(img0 + bl, B - 1);
+    pre[it] = S[((size_t)b * 16 + cq) * NF + 4 * quad + piece];
+  }
+  const int f = 4 * quad + wv;
+  const uint4* gw = Gb + (size_t)f * 16 * 64;
+  uint4 wr[8][2];
+#pragma unroll
+  for (int t = 0; t < 8; ++t)
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) wr[t][cb] = gw[(2 * t + h) * 64 + 32 * cb + j];
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int idx = it * 256 + tid, line = idx >> 2, piece = idx & 3;
+    const int bl = line >> 4, cq = line & 15;
+    tile[(cq * 4 + piece) * SG_SLD + bl] = img0 + bl < B ? pre[it] : uint4{0, 0, 0, 0};
+  }
+  lds_barrier();
+  f32x16 acc[4] = {};
+  const uint4 m = {0x80000000u, 0x80000000u, 0x80000000u, 0x80000000u};
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const bf16x8 sb = __builtin_bit_cast(bf16x8, tile[((2 * t + h) * 4 + wv) * SG_SLD + j]);
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      const uint4 g = wr[t][cb];
+      acc[cb] = mfmab(__builtin_bit_cast(bf16x8, g ^ m), sb, acc[cb]);                       // (gr, -gi)
+      acc[2 + cb] = mfmab(__builtin_bit_cast(bf16x8, (g >> 16) | (g << 16)), sb, acc[2 + cb]); // (gi, gr)
+    }
+  }
+  lds_barrier();   // every wave has read the S tile
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int cqo = 8 * cb + 2 * g + h;
+      const f32x16& re = acc[cb];
+      const f32x16& im = acc[2 + cb];
+      tile[j * SGB_YLD + cqo * 4 + wv] = uint4{pack_bf2(re[4 * g], im[4 * g]), pack_bf2(re[4 * g + 1], im[4 * g + 1]),
+                                             pack_bf2(re[4 * g + 2], im[4 * g + 2]),
+                                             pack_bf2(re[4 * g + 3], im[4 * g + 3])};
+    }
+  lds_barrier();
+#pragma unroll
+  for (int it = 0; it < 8; ++it) {
+    const int idx = it * 256 + tid, line = idx >> 2, piece = idx & 3;
+    const int bl = line >> 4, cqo = line & 15, b = img0 + bl;
+    if (b < B) Y[((size_t)b * 16 + cqo) * NF + 4 * quad + piece] = tile[bl * SGB_YLD + cqo * 4 + piece];
+  }
+}
+
 // spectral weights, once per weight set: G[f][ci][co] (complex, 1/N^2 folded in), one thread per
 // (f, ci, co), float64 accumulation
 __global__ void spec_weights_kernel(const float* __restrict__ w, cpx* __restrict__ G, int KS) {
@@ -540,6 +658,20 @@ __global__ void spec_pack_kernel(const cpx* __restrict__ G, f16x8* __restrict__ 
   Gc[(((size_t)f * 2 + 1) * 16 + cq) * 64 + co] = lv;
 }
 
+// bf16 compact weights Gb[f][cq][co]: one bf16x8 = re/im of G[ci = 4cq..4cq+3][co], unscaled
+__global__ void spec_pack_bf_kernel(const cpx* __restrict__ G, uint4* __restrict__ Gb) {
+  const int idx = blockIdx.x * blockDim.x + threadIdx.x;
+  if (idx >= NF * 16 * 64) return;
+  const int co = idx & 63, cq = (idx >> 6) & 15, f = idx >> 10;
+  uint32_t w[4];
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const cpx g = G[((size_t)f * 64 + 4 * cq + e) * 64 + co];
+    w[e] = pack_bf2(g.x, g.y);
+  }
+  Gb[((size_t)f * 16 + cq) * 64 + co] = uint4{w[0], w[1], w[2], w[3]};
+}
+
 // ---------------------------------------------------------------------------------------------
 // FFT-path B epilogue (hgru_module.py:729-740, 806-849, 696-711) on the spatial conv result P2:
 //   g2 = sigmoid(I . o_r + o_b); e = gamma*(P2 + lat); S = tanh(kappa*(I+e) + omega*(I*e));
@@ -583,9 +715,35 @@ __device__ __forceinline__ void gate_x3(const f16x8* __restrict__ gpk, const f32
   }
 }
 
+// bf16 variant (MP_DTYPE_BF16): one product, gpk = [n2][s][lane] bf16x8 in the same K order
+__device__ __forceinline__ void gate_bf(const uint4* __restrict__ gpk, const f32x16 (&V)[2], f32x16 (&Y)[2],
+                                       int lane) {
+  bf16x8 bv[4];
+#pragma unroll
+  for (int s = 0; s < 4; ++s)
+#pragma unroll
+    for (int e = 0; e < 8; ++e) bv[s][e] = (__bf16)V[s >> 1][8 * (s & 1) + e];
+#pragma unroll
+  for (int n2 = 0; n2 < 2; ++n2) {
+    f32x16 acc = {};
+#pragma unroll
+    for (int s = 0; s < 4; ++s) acc = mfmab(__builtin_bit_cast(bf16x8, gpk[(n2 * 4 + s) * 64 + lane]), bv[s], acc);
+    Y[n2] = acc;
+  }
+}
+
+template <bool BF>
+__device__ __forceinline__ void gate_any(const void* gpk, const f32x16 (&V)[2], f32x16 (&Y)[2], int lane, float us) {
+  if constexpr (BF)
+    gate_bf(static_cast<const uint4*>(gpk), V, Y, lane);
+  else
+    gate_x3(static_cast<const f16x8*>(gpk), V, Y, lane, us);
+}
+
+template <bool BF>
 __global__ __launch_bounds__(256) void spec_epi_b_kernel(ConvArgs p, const float* __restrict__ P,
-                                                         const f16x8* __restrict__ or_x3, float or_us,
-                                                         const f16x8* __restrict__ ir_x3, float ir_us, int nseg) {
+                                                         const void* __restrict__ or_x3, float or_us,
+                                                         const void* __restrict__ ir_x3, float ir_us, int nseg) {
   const int lane = threadIdx.x & 63, h = lane >> 5;
   const int seg = blockIdx.x * 4 + (threadIdx.x >> 6);
   if (seg >= nseg) return;
@@ -601,7 +759,7 @@ __global__ __launch_bounds__(256) void spec_epi_b_kernel(ConvArgs p, const float
 #pragma unroll
       for (int j = 0; j < 4; ++j) Iv[n][4 * g + j] = iv[j];
     }
-  gate_x3(or_x3, Iv, Y, lane, or_us);
+  gate_any<BF>(or_x3, Iv, Y, lane, or_us);
 #pragma unroll
   for (int n = 0; n < 2; ++n)
 #pragma unroll
@@ -631,7 +789,7 @@ __global__ __launch_bounds__(256) void spec_epi_b_kernel(ConvArgs p, const float
     }
   f32x16 (&Ov)[2] = Iv;
   if (p.mode == 0) {
-    gate_x3(ir_x3, Ov, Y, lane, ir_us);
+    gate_any<BF>(ir_x3, Ov, Y, lane, ir_us);
 #pragma unroll
     for (int n = 0; n < 2; ++n)
 #pragma unroll
@@ -661,8 +819,9 @@ __global__ __launch_bounds__(256) void spec_epi_b_kernel(ConvArgs p, const float
 
 // first circuit_input gate (hgru_module.py:696-711) for the FFT path: O0 (NHWC) -> O, and
 // Og = O0 * sigmoid(O0 . i_r + i_b) (C8), the gate on f16x3 MFMA; one wave per 32 pixels
+template <bool BF>
 __global__ __launch_bounds__(256) void gate_init_x3_kernel(const float* __restrict__ O0, float* O, float* Og,
-                                                           const f16x8* __restrict__ ir_x3, float ir_us,
+                                                           const void* __restrict__ ir_x3, float ir_us,
                                                            const float* __restrict__ vecs, int npix, int H,
                                                            int W) {
   const int lane = threadIdx.x & 63, h = lane >> 5;
@@ -681,7 +840,7 @@ __global__ __launch_bounds__(256) void gate_init_x3_kernel(const float* __restri
 #pragma unroll
       for (int j = 0; j < 4; ++j) V[n][4 * g + j] = v[j];
     }
-  gate_x3(ir_x3, V, Y, lane, ir_us);
+  gate_any<BF>(ir_x3, V, Y, lane, ir_us);
   if (!ok) return;
 #pragma unroll
   for (int n = 0; n < 2; ++n)
@@ -719,6 +878,20 @@ __global__ void pack_gate_x3_kernel(const float* __restrict__ g, f16x8* __restri
   }
   out[((n2 * 4 + s) * 2) * 64 + lane] = hv;
   out[((n2 * 4 + s) * 2 + 1) * 64 + lane] = lv;
+}
+
+__global__ void pack_gate_bf_kernel(const float* __restrict__ g, uint4* __restrict__ out) {
+  const int i = blockIdx.x * blockDim.x + threadIdx.x;
+  if (i >= 2 * 4 * 64) return;
+  const int lane = i & 63, s = (i >> 6) & 3, n2 = i >> 8, h = lane >> 5;
+  const int co = 32 * n2 + (lane & 31);
+  uint32_t w[4];
+#pragma unroll
+  for (int e = 0; e < 8; e += 2) {
+    const int ci0 = 32 * (s >> 1) + 8 * (2 * (s & 1) + (e >> 2)) + 4 * h + (e & 3);
+    w[e >> 1] = pack_bf2(g[ci0 * 64 + co], g[(ci0 + 1) * 64 + co]);
+  }
+  out[(n2 * 4 + s) * 64 + lane] = uint4{w[0], w[1], w[2], w[3]};
 }
 
 // the fused epilogue on the spatial result P: one wave per 32-pixel row segment, P loaded in the
@@ -762,7 +935,7 @@ hipError_t device_absmax(const float* x, size_t n, float* out) {
 
 size_t fft_weight_bytes() { return (size_t)NF * 2 * 16 * 64 * sizeof(f16x8); }
 
-hipError_t build_spec_weights(const float* w, int ks, void* Gx, float* unscale) {
+hipError_t build_spec_weights(const float* w, int ks, void* Gx, float* unscale, bool bf) {
   cpx* G = nullptr;
   unsigned* mx = nullptr;
   hipError_t e = hipMalloc(&G, (size_t)NF * 4096 * sizeof(cpx));
@@ -776,7 +949,11 @@ hipError_t build_spec_weights(const float* w, int ks, void* Gx, float* unscale) 
   }
   unsigned bits = 0;
   if (e == hipSuccess) e = hipMemcpy(&bits, mx, sizeof(unsigned), hipMemcpyDeviceToHost);
-  if (e == hipSuccess) {
+  if (e == hipSuccess && bf) {
+    *unscale = 1.0f;
+    hipLaunchKernelGGL(spec_pack_bf_kernel, dim3(NF * 16 * 64 / 256), dim3(256), 0, 0, G, static_cast<uint4*>(Gx));
+    e = hipGetLastError();
+  } else if (e == hipSuccess) {
     // power-of-two weight scale putting max|G| at 2^13..2^14 (f16 max is 65504)
     float m;
     std::memcpy(&m, &bits, sizeof m);
@@ -794,32 +971,50 @@ hipError_t build_spec_weights(const float* w, int ks, void* Gx, float* unscale) 
   return e;
 }
 
-hipError_t launch_fft_fwd(const float* act, void* S, int B, int H, int W, hipStream_t st) {
-  hipLaunchKernelGGL(fft_fwd_kernel, dim3(B * 16), dim3(192), 0, st, act, S, H, W);
+hipError_t launch_fft_fwd(const float* act, void* S, int B, int H, int W, hipStream_t st, bool bf) {
+  if (bf)
+    hipLaunchKernelGGL(fft_fwd_kernel<true>, dim3(B * 16), dim3(192), 0, st, act, S, H, W);
+  else
+    hipLaunchKernelGGL(fft_fwd_kernel<false>, dim3(B * 16), dim3(192), 0, st, act, S, H, W);
   return hipGetLastError();
 }
 
-hipError_t launch_fft_inv_a_fwd(const void* Y, const ConvArgs& a, void* S, int B, hipStream_t st) {
-  hipLaunchKernelGGL(fft_inv_a_fwd_kernel, dim3(B * 16), dim3(192), 0, st, static_cast<const cpx*>(Y), a, S);
+hipError_t launch_fft_inv_a_fwd(const void* Y, const ConvArgs& a, void* S, int B, hipStream_t st, bool bf) {
+  if (bf)
+    hipLaunchKernelGGL(fft_inv_a_fwd_kernel<true>, dim3(B * 16), dim3(192), 0, st, Y, a, S);
+  else
+    hipLaunchKernelGGL(fft_inv_a_fwd_kernel<false>, dim3(B * 16), dim3(192), 0, st, Y, a, S);
   return hipGetLastError();
 }
 
-hipError_t launch_spec_gemm(const void* S, const void* Gx, void* Y, int B, float unscale, hipStream_t st) {
+hipError_t launch_spec_gemm(const void* S, const void* Gx, void* Y, int B, float unscale, hipStream_t st, bool bf) {
   const int ngrp = (B + SG_NI - 1) / SG_NI;
   const int nq8 = (NQUAD + 7) / 8;
-  hipLaunchKernelGGL(spec_gemm_kernel<0>, dim3(nq8 * 8 * ngrp), dim3(256), 0, st, static_cast<const uint4*>(S),
-                     static_cast<const uint4*>(Gx), static_cast<uint4*>(Y), B, ngrp, unscale);
+  if (bf)
+    hipLaunchKernelGGL(spec_gemm_bf_kernel, dim3(nq8 * 8 * ngrp), dim3(256), 0, st, static_cast<const uint4*>(S),
+                       static_cast<const uint4*>(Gx), static_cast<uint4*>(Y), B, ngrp);
+  else
+    hipLaunchKernelGGL(spec_gemm_kernel<0>, dim3(nq8 * 8 * ngrp), dim3(256), 0, st, static_cast<const uint4*>(S),
+                       static_cast<const uint4*>(Gx), static_cast<uint4*>(Y), B, ngrp, unscale);
   return hipGetLastError();
 }
 
-hipError_t launch_fft_inv(const void* Y, float* P, int B, int H, int W, hipStream_t st) {
-  hipLaunchKernelGGL(fft_inv_kernel, dim3(B * 16), dim3(192), 0, st, static_cast<const cpx*>(Y), P, H, W);
+hipError_t launch_fft_inv(const void* Y, float* P, int B, int H, int W, hipStream_t st, bool bf) {
+  if (bf)
+    hipLaunchKernelGGL(fft_inv_kernel<true>, dim3(B * 16), dim3(192), 0, st, Y, P, H, W);
+  else
+    hipLaunchKernelGGL(fft_inv_kernel<false>, dim3(B * 16), dim3(192), 0, st, Y, P, H, W);
   return hipGetLastError();
 }
 
 size_t gate_x3_bytes() { return (size_t)2 * 4 * 2 * 64 * sizeof(f16x8); }
 
-hipError_t pack_gate_x3(const float* g, void* out, float* unscale) {
+hipError_t pack_gate_x3(const float* g, void* out, float* unscale, bool bf) {
+  if (bf) {
+    *unscale = 1.0f;
+    hipLaunchKernelGGL(pack_gate_bf_kernel, dim3(2), dim3(256), 0, 0, g, static_cast<uint4*>(out));
+    return hipGetLastError();
+  }
   std::vector<float> h(64 * 64);
   hipError_t e = hipMemcpy(h.data(), g, h.size() * sizeof(float), hipMemcpyDeviceToHost);
   if (e != hipSuccess) return e;
@@ -834,18 +1029,26 @@ hipError_t pack_gate_x3(const float* g, void* out, float* unscale) {
 }
 
 hipError_t launch_gate_init_x3(const float* O0, float* O, float* Og, const void* ir_x3, float ir_us, const float* vecs,
-                               int B, int H, int W, hipStream_t st) {
+                               int B, int H, int W, hipStream_t st, bool bf) {
   const int npix = B * H * W, nw = (npix + 31) / 32;
-  hipLaunchKernelGGL(gate_init_x3_kernel, dim3((nw + 3) / 4), dim3(256), 0, st, O0, O, Og,
-                     static_cast<const f16x8*>(ir_x3), ir_us, vecs, npix, H, W);
+  if (bf)
+    hipLaunchKernelGGL(gate_init_x3_kernel<true>, dim3((nw + 3) / 4), dim3(256), 0, st, O0, O, Og, ir_x3, ir_us, vecs,
+                       npix, H, W);
+  else
+    hipLaunchKernelGGL(gate_init_x3_kernel<false>, dim3((nw + 3) / 4), dim3(256), 0, st, O0, O, Og, ir_x3, ir_us,
+                       vecs, npix, H, W);
   return hipGetLastError();
 }
 
 hipError_t launch_spec_epi_b(const ConvArgs& a, const float* P, const void* or_x3, float or_us, const void* ir_x3,
-                             float ir_us, int B, hipStream_t st) {
+                             float ir_us, int B, hipStream_t st, bool bf) {
   const int nseg = B * a.H * (a.W / 32);
-  hipLaunchKernelGGL(spec_epi_b_kernel, dim3((nseg + 3) / 4), dim3(256), 0, st, a, P,
-                     static_cast<const f16x8*>(or_x3), or_us, static_cast<const f16x8*>(ir_x3), ir_us, nseg);
+  if (bf)
+    hipLaunchKernelGGL(spec_epi_b_kernel<true>, dim3((nseg + 3) / 4), dim3(256), 0, st, a, P, or_x3, or_us, ir_x3,
+                       ir_us, nseg);
+  else
+    hipLaunchKernelGGL(spec_epi_b_kernel<false>, dim3((nseg + 3) / 4), dim3(256), 0, st, a, P, or_x3, or_us, ir_x3,
+                       ir_us, nseg);
   return hipGetLastError();
 }
 

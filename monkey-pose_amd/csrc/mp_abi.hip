@@ -95,15 +95,16 @@ void finalize_circuit(mp_ctx* c, const std::vector<float>* outs, const std::vect
   c->p_pk.alloc((size_t)8 * c->ssf * c->ssf * 2 * 64 * 16);
   if (c->dtype == MP_DTYPE_F32_SPLIT) {
     pack_x3(it->second, c->p_pk, c->ssf, 1024.0f, &c->p_unscale, "pack p_r (f16x3)");
-  } else if (c->dtype == MP_DTYPE_F32_FFT) {
+  } else if (is_fft(c->dtype)) {
+    const bool bf = c->dtype == MP_DTYPE_BF16;
     c->spec_g.alloc(fft_weight_bytes());
-    hip_check(build_spec_weights(it->second.dev->f(), c->ssf, c->spec_g.p, &c->p_unscale), "p_r spectrum");
+    hip_check(build_spec_weights(it->second.dev->f(), c->ssf, c->spec_g.p, &c->p_unscale, bf), "p_r spectrum");
     c->or_x3.alloc(gate_x3_bytes());
     c->ir_x3.alloc(gate_x3_bytes());
-    hip_check(pack_gate_x3(c->need("contextual_circuit/o_r", {1, 1, 64, 64}).dev->f(), c->or_x3.p, &c->or_us),
-              "pack o_r (f16x3)");
-    hip_check(pack_gate_x3(c->need("contextual_circuit/i_r", {1, 1, 64, 64}).dev->f(), c->ir_x3.p, &c->ir_us),
-              "pack i_r (f16x3)");
+    hip_check(pack_gate_x3(c->need("contextual_circuit/o_r", {1, 1, 64, 64}).dev->f(), c->or_x3.p, &c->or_us, bf),
+              "pack o_r");
+    hip_check(pack_gate_x3(c->need("contextual_circuit/i_r", {1, 1, 64, 64}).dev->f(), c->ir_x3.p, &c->ir_us, bf),
+              "pack i_r");
   } else {
     hip_check(launch_pack_conv64(it->second.dev->f(), c->p_pk.v4(), c->ssf, nullptr), "pack p_r");
   }
@@ -135,6 +136,9 @@ void finalize_pose(mp_ctx* c) {
   const int k = 64;
   copy_dev(c->conv1_w, c->need("conv_1/conv_1_filters", {3, 3, 1, k}));
   copy_dev(c->conv1_b, c->need("conv_1/conv_1_biases", {k}));
+  // conv_1 as a generic implicit-GEMM weight, for the pre-pool conv1 tap only (mp_pose_taps)
+  c->conv1_ig.alloc((size_t)((9 + 7) / 8) * ((k + 31) / 32) * 64 * 16);
+  hip_check(launch_pack_fc(c->conv1_w.f(), c->conv1_ig.v4(), 9, k, nullptr), "pack conv_1 tap");
   bn_fold(c, "batch_normalization", k, c->bn0_s, c->bn0_t);
   if (c->dtype == MP_DTYPE_F32) {
     c->conv2_pk.alloc((size_t)8 * 9 * 2 * 64 * 16);
@@ -195,7 +199,7 @@ void ensure_ws(mp_ctx* c, int64_t n, int64_t H, int64_t W) {
   c->O.alloc(st);
   c->I.alloc(st);
   c->Og.alloc(st);
-  if (c->dtype == MP_DTYPE_F32_FFT) {
+  if (is_fft(c->dtype)) {
     c->specS.alloc(fft_spec_bytes((int)nb));
     c->specY.alloc(fft_spec_bytes((int)nb));
     c->specP.alloc(st);
@@ -231,35 +235,36 @@ void eCRF_conv(mp_ctx* c, int epi, const ConvArgs& a, int n, hipStream_t st) {
 //   fft_fwd(Og) -> S;  spec_gemm -> Y;  inv_a_fwd: I = A-epi(IFFT(Y)), S = FFT(I);
 //   spec_gemm -> Y;  fft_inv -> P2;  epi_b(P2, I, O) -> O', Og'
 void fft_step(mp_ctx* c, const ConvArgs& a, const ConvArgs& b, int n, hipStream_t st) {
+  const bool bf = c->dtype == MP_DTYPE_BF16;
   {
     ProfScope pa(c, st, "conv15_a");
     {
       ProfScope ps(c, st, "fft_fwd");
-      hip_check(launch_fft_fwd(a.src, c->specS.p, n, a.H, a.W, st), "fft_fwd");
+      hip_check(launch_fft_fwd(a.src, c->specS.p, n, a.H, a.W, st, bf), "fft_fwd");
     }
     {
       ProfScope ps(c, st, "spec_gemm");
-      hip_check(launch_spec_gemm(c->specS.p, c->spec_g.p, c->specY.p, n, c->p_unscale, st), "spec_gemm");
+      hip_check(launch_spec_gemm(c->specS.p, c->spec_g.p, c->specY.p, n, c->p_unscale, st, bf), "spec_gemm");
     }
     ProfScope ps(c, st, "inv_a_fwd");
-    hip_check(launch_fft_inv_a_fwd(c->specY.p, a, c->specS.p, n, st), "fft_inv_a_fwd");
+    hip_check(launch_fft_inv_a_fwd(c->specY.p, a, c->specS.p, n, st, bf), "fft_inv_a_fwd");
   }
   ProfScope pb(c, st, "conv15_b");
   {
     ProfScope ps(c, st, "spec_gemm");
-    hip_check(launch_spec_gemm(c->specS.p, c->spec_g.p, c->specY.p, n, c->p_unscale, st), "spec_gemm");
+    hip_check(launch_spec_gemm(c->specS.p, c->spec_g.p, c->specY.p, n, c->p_unscale, st, bf), "spec_gemm");
   }
   {
     ProfScope ps(c, st, "fft_inv");
-    hip_check(launch_fft_inv(c->specY.p, c->specP.f(), n, b.H, b.W, st), "fft_inv");
+    hip_check(launch_fft_inv(c->specY.p, c->specP.f(), n, b.H, b.W, st, bf), "fft_inv");
   }
   ProfScope ps(c, st, "epi_b");
-  hip_check(launch_spec_epi_b(b, c->specP.f(), c->or_x3.p, c->or_us, c->ir_x3.p, c->ir_us, n, st), "B epilogue");
+  hip_check(launch_spec_epi_b(b, c->specP.f(), c->or_x3.p, c->or_us, c->ir_x3.p, c->ir_us, n, st, bf), "B epilogue");
 }
 
 // map-size rule of the context's association-field conv path (MP_ERR_SHAPE otherwise)
 void check_map(mp_ctx* c, int64_t H, int64_t W, const char* what) {
-  if (c->dtype == MP_DTYPE_F32_FFT) {
+  if (is_fft(c->dtype)) {
     if (H < 1 || H > FFT_MAX_HW || (W != 32 && W != 64))
       fail(MP_ERR_SHAPE, std::string(what) + ": the FFT path needs map height in [1, 64] and width 32 or 64");
     return;
@@ -272,8 +277,9 @@ void check_map(mp_ctx* c, int64_t H, int64_t W, const char* what) {
 
 void run_circuit(mp_ctx* c, int64_t n, int H, int W, int T, const float* o0_nhwc, float* final_dst2,
                  hipStream_t st) {
-  hip_check(c->dtype == MP_DTYPE_F32_FFT
-                ? launch_gate_init_x3(o0_nhwc, c->O.f(), c->Og.f(), c->ir_x3.p, c->ir_us, c->vecs.f(), (int)n, H, W, st)
+  hip_check(is_fft(c->dtype)
+                ? launch_gate_init_x3(o0_nhwc, c->O.f(), c->Og.f(), c->ir_x3.p, c->ir_us, c->vecs.f(), (int)n, H, W, st,
+                                      c->dtype == MP_DTYPE_BF16)
                 : launch_gate_init(o0_nhwc, c->O.f(), c->Og.f(), c->ir_pk.v4(), c->vecs.f(), (int)n, H, W, st),
             "gate_init");
   for (int t = 0; t < T; ++t) {
@@ -300,7 +306,7 @@ void run_circuit(mp_ctx* c, int64_t n, int H, int W, int T, const float* o0_nhwc
     b.rho = c->rho[t];
     b.mode = (t == T - 1) ? 1 : 0;
     b.dst2 = (t == T - 1) ? final_dst2 : c->Og.f();
-    if (c->dtype == MP_DTYPE_F32_FFT) {
+    if (is_fft(c->dtype)) {
       fft_step(c, a, b, (int)n, st);
       continue;
     }
@@ -381,8 +387,9 @@ int mp_set_weight(mp_ctx* ctx, const char* name, const float* data, const int64_
 int mp_finalize_weights(mp_ctx* ctx, int compute_dtype) {
   return guard([&] {
     if (!ctx) fail(MP_ERR_ARG, "ctx is NULL");
-    if (compute_dtype != MP_DTYPE_F32 && compute_dtype != MP_DTYPE_F32_SPLIT && compute_dtype != MP_DTYPE_F32_FFT)
-      fail(MP_ERR_UNSUPPORTED, "compute_dtype must be MP_DTYPE_F32, MP_DTYPE_F32_SPLIT or MP_DTYPE_F32_FFT");
+    if (compute_dtype != MP_DTYPE_F32 && compute_dtype != MP_DTYPE_F32_SPLIT && compute_dtype != MP_DTYPE_F32_FFT &&
+        compute_dtype != MP_DTYPE_BF16)
+      fail(MP_ERR_UNSUPPORTED, "compute_dtype must be MP_DTYPE_F32, _F32_SPLIT, _F32_FFT or MP_DTYPE_BF16");
     if (compute_dtype != ctx->dtype) {   // workspace layout depends on the path
       ctx->cap_batch = 0;
       ctx->cap_hw = 0;
@@ -411,8 +418,8 @@ int mp_reserve(mp_ctx* ctx, int64_t max_batch) {
   });
 }
 
-int mp_hgru_pose_fwd(mp_ctx* ctx, const float* depth, int64_t n, int64_t h, int64_t w, const float* o0,
-                     float* out, void* stream) {
+int mp_hgru_pose_fwd_taps(mp_ctx* ctx, const float* depth, int64_t n, int64_t h, int64_t w, const float* o0,
+                          float* out, const mp_pose_taps* taps, void* stream) {
   return guard([&] {
     if (!ctx || !depth || !o0 || !out) fail(MP_ERR_ARG, "mp_hgru_pose_fwd: null pointer");
     if (ctx->model != MP_MODEL_HGRU_POSE) fail(MP_ERR_STATE, "context is not an hgru_pose model");
@@ -429,6 +436,31 @@ int mp_hgru_pose_fwd(mp_ctx* ctx, const float* depth, int64_t n, int64_t h, int6
     hipStream_t st = static_cast<hipStream_t>(stream);
     ensure_ws(ctx, n, H, W);
     const int N = (int)n;
+    mp_pose_taps tp{};
+    if (taps) tp = *taps;
+    if (tp.conv1) {   // relu(conv_1) before the pool: never materialised by the fused kernel
+      IgemmArgs g{};
+      g.x = depth;
+      g.ldx = 1;
+      g.N = N;
+      g.H = (int)h;
+      g.W = (int)w;
+      g.Cin = 1;
+      g.wpk = ctx->conv1_ig.v4();
+      g.K = 9;
+      g.bias = ctx->conv1_b.f();
+      g.out = tp.conv1;
+      g.ldo = 64;
+      g.Cout = 64;
+      g.Ho = (int)h;
+      g.Wo = (int)w;
+      g.KS = 3;
+      g.stride = 1;
+      g.pad_t = 1;
+      g.pad_l = 1;
+      g.relu = 1;
+      hip_check(launch_igemm_conv(g, st), "conv_1 tap");
+    }
     {
       ProfScope ps(ctx, st, "backbone");
       hip_check(launch_conv1_pool_bn(depth, ctx->conv1_w.f(), ctx->conv1_b.f(), ctx->bn0_s.f(), ctx->bn0_t.f(),
@@ -458,7 +490,14 @@ int mp_hgru_pose_fwd(mp_ctx* ctx, const float* depth, int64_t n, int64_t h, int6
                    : launch_conv64(3, EPI_BB, a, N, st),
                 "conv_3");
     }
+    if (tp.pool1) hip_check(launch_c8_to_nhwc(ctx->bufA.f(), tp.pool1, N, H, W, st), "pool1 tap");
+    if (tp.conv2) hip_check(launch_c8_to_nhwc(ctx->bufB.f(), tp.conv2, N, H, W, st), "conv2 tap");
+    if (tp.conv3) hip_check(launch_c8_to_nhwc(ctx->X.f(), tp.conv3, N, H, W, st), "conv3 tap");
     run_circuit(ctx, n, H, W, ctx->timesteps, o0, ctx->fcin.f(), st);
+    if (tp.hgru)
+      hip_check(hipMemcpyAsync(tp.hgru, ctx->fcin.f(), (size_t)N * ctx->fc1_in * sizeof(float),
+                               hipMemcpyDeviceToDevice, st),
+                "hgru tap");
     {
       ProfScope ps(ctx, st, "fc1");
       int ks;
@@ -469,6 +508,10 @@ int mp_hgru_pose_fwd(mp_ctx* ctx, const float* depth, int64_t n, int64_t h, int6
                     : launch_fc_gemm_x3(ctx->fcin.f(), ctx->fc1_in, ctx->fc1_pk.p, ctx->fc1_unscale, ctx->part.f(),
                                         N, ctx->fc1_in, ctx->fc1_out, S, ks, st),
                 "fc_1 gemm");
+      if (tp.fc1)   // fc_1 + bias before the relu (same partial sums)
+        hip_check(launch_fc_reduce(ctx->part.f(), S, N, ctx->fc1_out, ctx->fc1_b.f(), 0, nullptr, nullptr, tp.fc1,
+                                   ctx->fc1_out, st),
+                  "fc1 tap");
       hip_check(launch_fc_reduce(ctx->part.f(), S, N, ctx->fc1_out, ctx->fc1_b.f(), 1, ctx->bn4_s.f(),
                                  ctx->bn4_t.f(), ctx->h1.f(), ctx->fc1_out, st),
                 "fc_1 reduce");
@@ -484,7 +527,16 @@ int mp_hgru_pose_fwd(mp_ctx* ctx, const float* depth, int64_t n, int64_t h, int6
                                  ctx->nout, st),
                 "fc_out reduce");
     }
+    if (tp.relu1)
+      hip_check(hipMemcpyAsync(tp.relu1, ctx->h1.f(), (size_t)N * ctx->fc1_out * sizeof(float),
+                               hipMemcpyDeviceToDevice, st),
+                "relu1 tap");
   });
+}
+
+int mp_hgru_pose_fwd(mp_ctx* ctx, const float* depth, int64_t n, int64_t h, int64_t w, const float* o0,
+                     float* out, void* stream) {
+  return mp_hgru_pose_fwd_taps(ctx, depth, n, h, w, o0, out, nullptr, stream);
 }
 
 int mp_hgru_circuit_fwd(mp_ctx* ctx, const float* x, const float* o0, int64_t n, int64_t h, int64_t w,

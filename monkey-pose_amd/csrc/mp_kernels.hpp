@@ -50,20 +50,21 @@ hipError_t device_absmax(const float* x, size_t n, float* out);   // max |x| (sy
 size_t fft_spec_bytes(int B);      // one spectrum buffer (S or Y) for B images
 size_t fft_weight_bytes();         // expanded split spectral weights
 // HWIO [ks][ks][64][64] -> packed split spectral weights (synchronous, finalize time)
-hipError_t build_spec_weights(const float* w, int ks, void* Gx, float* unscale);
-hipError_t launch_fft_fwd(const float* act, void* S, int B, int H, int W, hipStream_t st);
-hipError_t launch_spec_gemm(const void* S, const void* Gx, void* Y, int B, float unscale, hipStream_t st);
-hipError_t launch_fft_inv(const void* Y, float* P, int B, int H, int W, hipStream_t st);
+hipError_t build_spec_weights(const float* w, int ks, void* Gx, float* unscale, bool bf = false);
+hipError_t launch_fft_fwd(const float* act, void* S, int B, int H, int W, hipStream_t st, bool bf = false);
+hipError_t launch_spec_gemm(const void* S, const void* Gx, void* Y, int B, float unscale, hipStream_t st,
+                            bool bf = false);
+hipError_t launch_fft_inv(const void* Y, float* P, int B, int H, int W, hipStream_t st, bool bf = false);
 // P1 = IFFT(Y); I = A-epilogue(P1) -> a.dst; S = FFT(I)   (the A half-step tail + B half-step head)
-hipError_t launch_fft_inv_a_fwd(const void* Y, const ConvArgs& a, void* S, int B, hipStream_t st);
+hipError_t launch_fft_inv_a_fwd(const void* Y, const ConvArgs& a, void* S, int B, hipStream_t st, bool bf = false);
 hipError_t launch_spec_epi(int epi, const ConvArgs& a, const float* P, int B, hipStream_t st);
 // B epilogue with f16x3 gate GEMMs (FFT path); gate weights packed by pack_gate_x3 (synchronous)
 size_t gate_x3_bytes();
-hipError_t pack_gate_x3(const float* g, void* out, float* unscale);
+hipError_t pack_gate_x3(const float* g, void* out, float* unscale, bool bf = false);
 hipError_t launch_gate_init_x3(const float* O0, float* O, float* Og, const void* ir_x3, float ir_us, const float* vecs,
-                               int B, int H, int W, hipStream_t st);
+                               int B, int H, int W, hipStream_t st, bool bf = false);
 hipError_t launch_spec_epi_b(const ConvArgs& a, const float* P, const void* or_x3, float or_us, const void* ir_x3,
-                             float ir_us, int B, hipStream_t st);
+                             float ir_us, int B, hipStream_t st, bool bf = false);
 // k_igemm.hip (dense / hierarchical regressors)
 struct IgemmArgs {
   const float* x;      // input view: pixel (n,y,x) channel ci at x[((n*H+y)*W+x)*ldx + cix + ci]

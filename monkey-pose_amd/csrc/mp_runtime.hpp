@@ -69,6 +69,9 @@ struct ProfEvent {
   hipEvent_t a, b;
 };
 
+// dtypes whose association-field conv runs on the FFT path (k_fft.hip)
+inline bool is_fft(int dtype) { return dtype == MP_DTYPE_F32_FFT || dtype == MP_DTYPE_BF16; }
+
 inline std::string strip_scope(const char* name) {
   std::string s(name);
   if (s.rfind("cnn/", 0) == 0) s = s.substr(4);
@@ -116,6 +119,7 @@ struct mp_ctx {
   float p_unscale = 1.f;   // F32_SPLIT / F32_FFT: 1 / (weight scale * activation or spectrum scale)
   std::vector<float> rho;
   DevBuf conv1_w, conv1_b, bn0_s, bn0_t;
+  DevBuf conv1_ig;          // conv_1 packed for the generic igemm (conv1 tap of mp_hgru_pose_fwd_taps)
   DevBuf conv2_pk, conv2_b, bn1_s, bn1_t;
   float conv2_us = 1.f, conv3_us = 1.f;   // backbone packed f16x3 (dtype != F32): 1 / (wscale * BB_ASCALE)
   DevBuf conv3_pk, conv3_b, bn2_s, bn2_t;

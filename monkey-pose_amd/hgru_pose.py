@@ -57,12 +57,15 @@ class model:
         self.weights: Optional[Dict[str, np.ndarray]] = None   # TF variable name -> array
         self.weight_seed = 1234
         # eCRF conv path (all fp32-class): 'auto' (default: FFT when the map allows, see
-        # _lib.resolve_dtype), 'fp32_fft', 'fp32_split' (direct f16x3) or 'fp32' (exact fp32 MFMA)
+        # _lib.resolve_dtype), 'fp32_fft', 'fp32_split' (direct f16x3), 'fp32' (exact fp32 MFMA) or
+        # 'bf16' (FFT path with bf16 spectral / gate GEMMs, ~1e-2 error; SURVEY config 4)
         self.compute_dtype = 'auto'
         self._ctx: Optional[_lib.Context] = None
         self._ctx_key = None
         self.out_put = None
         self.h2_init = None
+        self._taps = None          # intermediates of the last forward (see _tap)
+        self._last = None          # (depth, h2_init) of the last forward
 
     def __getitem__(self, name):
         return getattr(self, name)
@@ -111,13 +114,40 @@ class model:
         return self._ctx
 
     # ---------------------------------------------------------------- forward
-    def build(self, depth, output_shape, batch_norm=None, train_mode=None, h2_init=None):
+    # ------------------------------------------------------- reference intermediates (hgru_pose.py:50-103)
+    def _tap(self, name):
+        """The reference's graph tensors m.conv1 ... m.relu1.  In TF they are evaluated on demand;
+        here the first access re-runs the last forward once with every tap requested
+        (mp_hgru_pose_fwd_taps; the forward is deterministic, so out_put is unchanged), unless
+        build(..., keep_intermediates=True) already captured them."""
+        if self._taps is None:
+            if self._last is None:
+                raise AttributeError(f"{name}: call build() first")
+            self._run(*self._last, keep=True)
+        return self._taps[name]
+
+    conv1 = property(lambda self: self._tap("conv1"))
+    pool1 = property(lambda self: self._tap("pool1"))
+    conv2 = property(lambda self: self._tap("conv2"))
+    conv3 = property(lambda self: self._tap("conv3"))
+    hgru = property(lambda self: self._tap("hgru"))
+    fc1 = property(lambda self: self._tap("fc1"))
+    relu1 = property(lambda self: self._tap("relu1"))
+
+    def build(self, depth, output_shape, batch_norm=None, train_mode=None, h2_init=None,
+              keep_intermediates=False, dtype=None):
         """``hgru_pose.model.build`` (hgru_pose.py:47-105), inference only.
 
         depth     torch CUDA tensor [N, 128, 128, 1] fp32 (crop / 10000, train_cnn_networks_hgru.py:50)
         h2_init   optional [N, 64, 64, 64] initial hGRU output state; the reference draws it at
                   random per run (hgru_module.py:879-887), here it defaults to a seeded draw
+        dtype     None (keep ``compute_dtype``), 'fp32' (fp32-class, fastest path for the map:
+                  ``compute_dtype = 'auto'``) or 'bf16' (bf16 spectral / gate GEMMs on the FFT path)
         """
+        if dtype is not None:
+            if dtype not in ('fp32', 'bf16'):
+                raise ValueError("dtype must be 'fp32' or 'bf16'")
+            self.compute_dtype = 'auto' if dtype == 'fp32' else 'bf16'
         import torch
         if train_mode:
             raise NotImplementedError("train_mode=True (dropout / BN batch statistics / backward) is "
@@ -131,9 +161,9 @@ class model:
         self.output_shape = int(output_shape)
         self._ctx = self._context(self.output_shape, depth.device.index or 0,
                                   (int(depth.shape[1]), int(depth.shape[2])))
-        return self.forward(depth, h2_init)
+        return self.forward(depth, h2_init, keep_intermediates)
 
-    def forward(self, depth, h2_init=None):
+    def forward(self, depth, h2_init=None, keep_intermediates=False):
         import torch
         if self._ctx is None:
             raise RuntimeError("call build() first")
@@ -144,9 +174,26 @@ class model:
         h2_init = h2_init.detach().float().contiguous()
         if tuple(h2_init.shape) != (n, h // 2, w // 2, 64):
             raise ValueError(f"h2_init must be [{n}, {h // 2}, {w // 2}, 64]")
-        out = torch.empty((n, self.output_shape), dtype=torch.float32, device=depth.device)
-        self._ctx.pose_fwd(depth, h2_init, out, _lib.current_stream(depth.device))
         self.h2_init = h2_init
+        self._last = (depth, h2_init)
+        self._taps = None
+        return self._run(depth, h2_init, keep_intermediates)
+
+    def _run(self, depth, h2_init, keep=False):
+        import torch
+        n, h, w, _ = depth.shape
+        dev = depth.device
+        out = torch.empty((n, self.output_shape), dtype=torch.float32, device=dev)
+        stream = _lib.current_stream(dev)
+        if keep:
+            hh, ww = h // 2, w // 2
+            shapes = {"conv1": (n, h, w, 64), "pool1": (n, hh, ww, 64), "conv2": (n, hh, ww, 64),
+                      "conv3": (n, hh, ww, 64), "hgru": (n, hh, ww, 64), "fc1": (n, 1024), "relu1": (n, 1024)}
+            taps = {k: torch.empty(v, dtype=torch.float32, device=dev) for k, v in shapes.items()}
+            self._ctx.pose_fwd_taps(depth, h2_init, out, taps, stream)
+            self._taps = taps
+        else:
+            self._ctx.pose_fwd(depth, h2_init, out, stream)
         self.out_put = out
         return out
 

@@ -187,7 +187,7 @@ def hgru_pose_forward(depth: np.ndarray, wts: Dict[str, np.ndarray], O0: np.ndar
                    wts["cnn/conv_3/conv_3_biases"])                                  # 71
     c3 = batch_norm_inf(c3, wts, "cnn/batch_normalization_2")                         # 72-80
     if keep:
-        inter.update(pool1=p1, conv2=c2, conv3=c3)
+        inter.update(conv1=c1, pool1=p1, conv2=c2, conv3=c3)
     h = hgru_forward(c3, O0, wts, timesteps, keep_steps=keep)                         # 81
     if keep:
         h, steps = h
