@@ -138,18 +138,20 @@ def extras(mp, dev, args):
     B = args.batch
     depth = torch.from_numpy(W.synth_crops(B, seed=99, size=128)).to(dev)
     stream = mp._lib.current_stream(dev)
-    try:   # config 3: hierarchical cascade, batch 256
-        ctx = mp._lib.Context(mp._lib.MP_MODEL_HIER, dev.index)
-        for v in W.hier_vars():
-            ctx.set_weight(v.name, W.synth_value(v, 5))
-        ctx.finalize()
-        heads = [torch.empty((B, s), device=dev) for s in (108, 39, 39, 39, 39, 36)]
-        t = time_gpu(lambda: ctx.hier_fwd(depth, heads, stream), 5, 1)
-        out["hier_b256"] = {"crops_per_s": round(B / t, 2), "ms_per_batch": round(t * 1e3, 3),
-                            "gflop_per_crop": 7.97, "tflops": round(7.97e9 * B / t / 1e12, 2)}
-        ctx.close()
-    except Exception as e:  # noqa: BLE001
-        out["hier_b256"] = {"error": repr(e)}
+    for dt in ("fp32_split", "fp32"):   # config 3: hierarchical cascade, batch 256
+        key = "hier_b256" + ("" if dt == "fp32_split" else "_exact_fp32")
+        try:
+            ctx = mp._lib.Context(mp._lib.MP_MODEL_HIER, dev.index)
+            for v in W.hier_vars():
+                ctx.set_weight(v.name, W.synth_value(v, 5))
+            ctx.finalize(mp._lib.dtype_code(dt))
+            heads = [torch.empty((B, s), device=dev) for s in (108, 39, 39, 39, 39, 36)]
+            t = time_gpu(lambda: ctx.hier_fwd(depth, heads, stream), 5, 1)
+            out[key] = {"crops_per_s": round(B / t, 2), "ms_per_batch": round(t * 1e3, 3),
+                        "gflop_per_crop": 7.97, "tflops": round(7.97e9 * B / t / 1e12, 2), "dtype": dt}
+            ctx.close()
+        except Exception as e:  # noqa: BLE001
+            out[key] = {"error": repr(e)}
     try:   # config 2: hGRU pose fwd, T=8, batch 64, fp32-class (same context kind, B = 64)
         ctx = mp._lib.Context(mp._lib.MP_MODEL_HGRU_POSE, dev.index)
         T = args.timesteps
@@ -169,11 +171,12 @@ def extras(mp, dev, args):
         ctx = mp._lib.Context(mp._lib.MP_MODEL_DENSE, dev.index)
         for v in W.dense_vars():
             ctx.set_weight(v.name, W.synth_value(v, 6))
-        ctx.finalize()
+        ctx.finalize(mp._lib.MP_DTYPE_F32_SPLIT)
         o = torch.empty((B, 69), device=dev)
         t = time_gpu(lambda: ctx.dense_fwd(depth, o, stream), 5, 1)
         out["dense_b256"] = {"crops_per_s": round(B / t, 2), "ms_per_batch": round(t * 1e3, 3),
-                             "gflop_per_crop": 3.22, "tflops": round(3.22e9 * B / t / 1e12, 2)}
+                             "gflop_per_crop": 3.22, "tflops": round(3.22e9 * B / t / 1e12, 2),
+                             "dtype": "fp32_split"}
         ctx.close()
     except Exception as e:  # noqa: BLE001
         out["dense_b256"] = {"error": repr(e)}

@@ -18,6 +18,9 @@ class RegressorBase:
         self.var_dict = {}
         self.weights: Optional[Dict[str, np.ndarray]] = None
         self.weight_seed = 1234
+        # conv / fc precision: 'auto' (= 'fp32_split': fp32-accurate f16x3 MFMA, the fastest
+        # fp32-class path) or 'fp32' (exact fp32 MFMA)
+        self.compute_dtype = 'auto'
         self._ctx: Optional[_lib.Context] = None
         self._ctx_key = None
 
@@ -51,13 +54,22 @@ class RegressorBase:
             self.var_dict[(k.split("/")[1], k)] = v
         return out
 
+    def _dtype(self) -> str:
+        dt = {'auto': 'fp32_split', 'fp32_split': 'fp32_split', 'f32_split': 'fp32_split',
+              'fp32': 'fp32', 'f32': 'fp32'}.get(self.compute_dtype)
+        if dt is None:
+            raise ValueError(f"regressor compute_dtype must be 'auto', 'fp32_split' or 'fp32', "
+                             f"got {self.compute_dtype!r}")
+        return dt
+
     def _context(self, key, table, device: int) -> _lib.Context:
-        key = (key, device, id(self.weights), id(self.data_dict))
+        dt = self._dtype()
+        key = (key, device, id(self.weights), id(self.data_dict), dt)
         if self._ctx is None or self._ctx_key != key:
             ctx = _lib.Context(self.MODEL_KIND, device)
             for name, val in self._resolve(table).items():
                 ctx.set_weight(name, val)
-            ctx.finalize()
+            ctx.finalize(_lib.dtype_code(dt))
             self._ctx, self._ctx_key = ctx, key
         return self._ctx
 

@@ -120,6 +120,167 @@ __global__ __launch_bounds__(256) void igemm_conv_kernel(IgemmArgs p) {
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// fp32-accurate f16x3 implicit GEMM (regressor contexts finalized with MP_DTYPE_F32_SPLIT): the
+// same block geometry as igemm_conv_kernel (128 output pixels x NB*32 output channels, one
+// 32-pixel M-block per wave), D^T = W^T im2col^T on v_mfma_f32_32x32x16_f16 with both operands
+// split into f16 hi + lo (three products per MAC, fp32 accumulation).  Weights are packed like
+// fc_1's (launch_pack_fc_x3: [k/16][cout/32][hi|lo][lane] f16x8, power-of-two scale from max|W|);
+// activations are split when the im2col tile is staged into LDS (hi / lo planes [128][32 k]).
+// The next K step's im2col float4s and weight fragments are loaded into registers while the
+// current step's MFMAs run; the loads are unconditional (clamped addresses, then a select), so a
+// step's loads are all in flight together.
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+
+__device__ __forceinline__ f32x16 mfma16(f16x8 a, f16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+constexpr int IGX_LD = IG_BK + 8;   // f16 pitch of the hi / lo planes (+16 B: conflict-free b128 reads)
+
+template <int NB>
+__global__ __launch_bounds__(256) void igemm_x3_kernel(IgemmArgs p, const f16x8* __restrict__ wpk, float unscale) {
+  __shared__ _Float16 Ah[IG_BM * IGX_LD], Al[IG_BM * IGX_LD];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, col = lane & 31;
+  const int HWo = p.Ho * p.Wo;
+  const int M = p.N * HWo;
+  const int m0 = blockIdx.x * IG_BM;
+  const int nb0 = blockIdx.y * NB;
+  const int N32 = (p.Cout + 31) / 32;
+  const int K16 = (p.K + 15) / 16;
+  const bool vec = (p.Cin % 4 == 0) && (p.cix % 4 == 0) && (p.ldx % 4 == 0);
+
+  int sn[4], sy[4], sx[4];
+  bool sok[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int gm = m0 + (tid >> 3) + 32 * i;
+    sok[i] = gm < M;
+    const int g = sok[i] ? gm : 0;
+    sn[i] = g / HWo;
+    const int r = g - sn[i] * HWo;
+    sy[i] = (r / p.Wo) * p.stride - p.pad_t;
+    sx[i] = (r % p.Wo) * p.stride - p.pad_l;
+  }
+  const int k4 = (tid & 7) * 4;
+
+  auto load_act = [&](int k0, f32x4 (&v)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int kk = k0 + k4;
+      if (vec) {
+        const int kc = min(kk, p.K - 4);
+        const int tap = kc / p.Cin, ci = kc - tap * p.Cin;
+        const int iy = sy[i] + tap / p.KS, ix = sx[i] + tap % p.KS;
+        const bool ok = sok[i] && kk < p.K && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
+        const int cy = min(max(iy, 0), p.H - 1), cx = min(max(ix, 0), p.W - 1);
+        const f32x4 t =
+            *reinterpret_cast<const f32x4*>(p.x + (((size_t)sn[i] * p.H + cy) * p.W + cx) * p.ldx + p.cix + ci);
+        v[i] = ok ? t : f32x4{0.f, 0.f, 0.f, 0.f};
+      } else {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int k = kk + s;
+          const int kc = min(k, p.K - 1);
+          const int tap = kc / p.Cin, ci = kc - tap * p.Cin;
+          const int iy = sy[i] + tap / p.KS, ix = sx[i] + tap % p.KS;
+          const bool ok = sok[i] && k < p.K && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
+          const int cy = min(max(iy, 0), p.H - 1), cx = min(max(ix, 0), p.W - 1);
+          const float t = p.x[(((size_t)sn[i] * p.H + cy) * p.W + cx) * p.ldx + p.cix + ci];
+          v[i][s] = ok ? t : 0.f;
+        }
+      }
+    }
+  };
+  auto load_w = [&](int k0, f16x8 (&w)[2][NB][2]) {
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      const int kb = min((k0 >> 4) + g, K16 - 1);
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        const int nbc = min(nb0 + nb, N32 - 1);
+        const f16x8* wp = wpk + (((size_t)kb * N32 + nbc) * 2) * 64 + lane;
+        w[g][nb][0] = wp[0];
+        w[g][nb][1] = wp[64];
+      }
+    }
+  };
+
+  f32x16 acc[NB];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) acc[nb] = f32x16{};
+  f32x4 av[4];
+  f16x8 wn[2][NB][2];
+  load_act(0, av);
+  load_w(0, wn);
+  for (int k0 = 0; k0 < p.K; k0 += IG_BK) {
+    lds_barrier();   // the previous step's LDS reads are done
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = (tid >> 3) + 32 * i;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        const _Float16 hh = (_Float16)av[i][s];
+        Ah[row * IGX_LD + k4 + s] = hh;
+        Al[row * IGX_LD + k4 + s] = (_Float16)(av[i][s] - (float)hh);
+      }
+    }
+    f16x8 wc[2][NB][2];
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        wc[g][nb][0] = wn[g][nb][0];
+        wc[g][nb][1] = wn[g][nb][1];
+      }
+    if (k0 + IG_BK < p.K) {   // prefetch the next step
+      load_act(k0 + IG_BK, av);
+      load_w(k0 + IG_BK, wn);
+    }
+    lds_barrier();
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      if ((k0 >> 4) + g >= K16) break;   // block-uniform
+      const int o = (wv * 32 + col) * IGX_LD + 16 * g + 8 * h;
+      const f16x8 ah = *reinterpret_cast<const f16x8*>(Ah + o);
+      const f16x8 al = *reinterpret_cast<const f16x8*>(Al + o);
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        if (nb0 + nb >= N32) break;   // block-uniform
+        acc[nb] = mfma16(wc[g][nb][1], ah, acc[nb]);
+        acc[nb] = mfma16(wc[g][nb][0], al, acc[nb]);
+        acc[nb] = mfma16(wc[g][nb][0], ah, acc[nb]);
+      }
+    }
+  }
+
+  const int gm = m0 + wv * 32 + col;
+  if (gm >= M) return;
+  float* dst = p.out + (size_t)gm * p.ldo + p.coff;
+  const bool vst = (p.ldo % 4 == 0) && (p.coff % 4 == 0) && (p.Cout % 4 == 0);
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) {
+    if (nb0 + nb >= N32) break;
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int c = (nb0 + nb) * 32 + 8 * g + 4 * h;
+      f32x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float v = acc[nb][4 * g + j] * unscale + (c + j < p.Cout ? p.bias[c + j] : 0.f);
+        o[j] = p.relu ? fmaxf(v, 0.f) : v;
+      }
+      if (vst) {
+        if (c < p.Cout) *reinterpret_cast<f32x4*>(dst + c) = o;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (c + j < p.Cout) dst[c + j] = o[j];
+      }
+    }
+  }
+}
+
 // 2x2 / stride 2, TF SAME (odd sizes pad one row/column after; max ignores it, avg divides by the
 // in-image count), optionally followed by a per-channel affine (a folded inference BN).  One
 // thread per output element; C innermost for coalescing.
@@ -164,6 +325,22 @@ hipError_t launch_igemm_conv(const IgemmArgs& a, hipStream_t st) {
     hipLaunchKernelGGL(igemm_conv_kernel<2>, grid, dim3(256), 0, st, a);
   else
     hipLaunchKernelGGL(igemm_conv_kernel<1>, grid, dim3(256), 0, st, a);
+  return hipGetLastError();
+}
+
+hipError_t launch_igemm_x3(const IgemmArgs& a, const void* wpk, float unscale, hipStream_t st) {
+  if (a.K < 4) return hipErrorInvalidValue;   // the clamped vector load needs K >= 4
+  const int M = a.N * a.Ho * a.Wo;
+  const int N32 = (a.Cout + 31) / 32;
+  const int nb = N32 >= 4 ? 4 : (N32 >= 2 ? 2 : 1);
+  dim3 grid((M + IG_BM - 1) / IG_BM, (N32 + nb - 1) / nb);
+  const f16x8* w = static_cast<const f16x8*>(wpk);
+  if (nb == 4)
+    hipLaunchKernelGGL(igemm_x3_kernel<4>, grid, dim3(256), 0, st, a, w, unscale);
+  else if (nb == 2)
+    hipLaunchKernelGGL(igemm_x3_kernel<2>, grid, dim3(256), 0, st, a, w, unscale);
+  else
+    hipLaunchKernelGGL(igemm_x3_kernel<1>, grid, dim3(256), 0, st, a, w, unscale);
   return hipGetLastError();
 }
 

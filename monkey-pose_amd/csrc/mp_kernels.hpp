@@ -79,6 +79,8 @@ struct IgemmArgs {
   int relu;
 };
 hipError_t launch_igemm_conv(const IgemmArgs& a, hipStream_t st);
+// f16x3 (fp32-accurate) variant; wpk packed by launch_pack_fc_x3 as a [K][Cout] matrix
+hipError_t launch_igemm_x3(const IgemmArgs& a, const void* wpk, float unscale, hipStream_t st);
 hipError_t launch_pool2(const float* x, int ldx, int cix, int N, int H, int W, int C, float* out, int ldo,
                         int coff, int mode, hipStream_t st, const float* aff_s = nullptr,
                         const float* aff_t = nullptr);

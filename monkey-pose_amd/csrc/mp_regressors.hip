@@ -140,7 +140,7 @@ void conv(mp_ctx* c, const std::string& name, int n, const View& in, const View&
   a.pad_t = same_pad_before(in.H, L.k, stride);
   a.pad_l = same_pad_before(in.W, L.k, stride);
   a.relu = 1;
-  hip_check(launch_igemm_conv(a, st), name.c_str());
+  hip_check(L.x3 ? launch_igemm_x3(a, L.w.p, L.wus, st) : launch_igemm_conv(a, st), name.c_str());
 }
 
 void pool(int n, const View& in, const View& out, int mode, hipStream_t st, const float* aff_s = nullptr,
@@ -160,7 +160,9 @@ void fcl(mp_ctx* c, const std::string& name, int n, const float* in, int K, floa
   int ks;
   const int S = fc_choose_splits(n, K, L.cout, &ks);
   float* part = buf(c, "fc_part", (size_t)S * n * ((L.cout + 31) / 32 * 32));
-  hip_check(launch_fc_gemm(in, K, L.w.v4(), part, n, K, L.cout, S, ks, st), name.c_str());
+  hip_check(L.x3 ? launch_fc_gemm_x3(in, K, L.w.p, L.wus, part, n, K, L.cout, S, ks, st)
+                 : launch_fc_gemm(in, K, L.w.v4(), part, n, K, L.cout, S, ks, st),
+            name.c_str());
   hip_check(launch_fc_reduce(part, S, n, L.cout, L.b.f(), relu ? 1 : 0, aff_s, aff_t, out, ldo, st),
             name.c_str());
 }
@@ -335,6 +337,19 @@ bool known_name_regressor(int model, const std::string& n) {
   return false;
 }
 
+// a conv (HWIO as [K][Cout]) or fc ([K][N]) weight in the context's precision: fp32 fragments, or
+// the f16x3 split under MP_DTYPE_F32_SPLIT when the x3 kernel takes the shape (x3_ok)
+void pack_matrix(mp_ctx* c, mp_ctx::PackedLayer& L, const float* w, bool x3_ok) {
+  L.x3 = c->dtype == MP_DTYPE_F32_SPLIT && x3_ok;
+  if (L.x3) {
+    L.w.alloc(fc_x3_bytes(L.K, L.cout));
+    hip_check(launch_pack_fc_x3(w, L.w.p, L.K, L.cout, &L.wus, nullptr), "pack (f16x3)");
+  } else {
+    L.w.alloc((size_t)((L.K + 7) / 8) * ((L.cout + 31) / 32) * 64 * 16);
+    hip_check(launch_pack_fc(w, L.w.v4(), L.K, L.cout, nullptr), "pack");
+  }
+}
+
 void finalize_regressor(mp_ctx* c) {
   c->layers.clear();
   for (const auto& s : convs_of(c->model)) {
@@ -345,8 +360,7 @@ void finalize_regressor(mp_ctx* c) {
     L.cin = s.cin;
     L.cout = s.cout;
     L.K = s.k * s.k * s.cin;
-    L.w.alloc((size_t)((L.K + 7) / 8) * ((s.cout + 31) / 32) * 64 * 16);
-    hip_check(launch_pack_fc(w.dev->f(), L.w.v4(), L.K, s.cout, nullptr), "pack conv");
+    pack_matrix(c, L, w.dev->f(), L.K >= 4);
     L.b.alloc(s.cout * sizeof(float));
     hip_check(hipMemcpy(L.b.p, b.dev->p, s.cout * sizeof(float), hipMemcpyDeviceToDevice), "bias");
   }
@@ -360,8 +374,7 @@ void finalize_regressor(mp_ctx* c) {
     L.K = K;
     L.cin = K;
     L.cout = N;
-    L.w.alloc((size_t)((K + 7) / 8) * ((N + 31) / 32) * 64 * 16);
-    hip_check(launch_pack_fc(it->second.dev->f(), L.w.v4(), K, N, nullptr), "pack fc");
+    pack_matrix(c, L, it->second.dev->f(), K % 32 == 0);
     L.b.alloc(N * sizeof(float));
     hip_check(hipMemcpy(L.b.p, b.dev->p, N * sizeof(float), hipMemcpyDeviceToDevice), "bias");
   }

@@ -108,18 +108,20 @@ def test_resize_gpu_bit_exact():
         assert np.array_equal(got, RR.resize_bilinear_tf1(x, oh, ow)), (h, w, c, oh, ow)
 
 
-def _attn_model(wts):
+def _attn_model(wts, dtype="auto"):
     m = pkg().train_cnn_networks_hgru.attn_model_struct()
+    m.compute_dtype = dtype
     m.load_weights(wts)
     return m
 
 
 @pytest.mark.gpu
-def test_attn_gpu_matches_golden_and_oracle():
+@pytest.mark.parametrize("dtype", ["fp32", "fp32_split"])
+def test_attn_gpu_matches_golden_and_oracle(dtype):
     torch = pytest.importorskip("torch")
     m = golden_meta()["attn_f424"]
     wts, frames = MG.attn_inputs(m["n"], m["h"], m["w"], m["weight_seed"], m["frame_seed"])
-    model = _attn_model(wts)
+    model = _attn_model(wts, dtype)
     out = model.build(torch.from_numpy(frames).cuda(), 3, train_mode=False).cpu().numpy()
     assert rel_inf(out, golden_array("attn_f424", "out")) <= FP32_REL_TOL
     # batch invariance: one frame alone gives the same bits as inside the batch
@@ -129,11 +131,11 @@ def test_attn_gpu_matches_golden_and_oracle():
     W = pkg().weights
     wts2 = W.synth_weights(W.attn_vars(), seed=3)
     fr2 = W.synth_frames(3, seed=8)
-    out2 = _attn_model(wts2).build(torch.from_numpy(fr2).cuda(), 3).cpu().numpy()
+    out2 = _attn_model(wts2, dtype).build(torch.from_numpy(fr2).cuda(), 3).cpu().numpy()
     assert rel_inf(out2, RR.attn_forward(fr2, wts2)) <= FP32_REL_TOL
     # already 128 x 128 input: the resize is skipped (identity in TF as well)
     fr3 = W.synth_frames(2, seed=9, h=128, w=128)
-    out3 = _attn_model(wts2).build(torch.from_numpy(fr3).cuda(), 3).cpu().numpy()
+    out3 = _attn_model(wts2, dtype).build(torch.from_numpy(fr3).cuda(), 3).cpu().numpy()
     assert rel_inf(out3, RR.attn_forward(fr3, wts2)) <= FP32_REL_TOL
 
 

@@ -35,11 +35,16 @@ def test_dense_conv_table_is_consistent():
     assert sum(1 for s in specs if s[1] == 3) == 29 and sum(1 for s in specs if s[1] == 1) == 20
 
 
+REG_DTYPES = ["fp32", "fp32_split"]
+
+
 @pytest.mark.gpu
-def test_dense_gpu_matches_golden_and_oracle():
+@pytest.mark.parametrize("dtype", REG_DTYPES)
+def test_dense_gpu_matches_golden_and_oracle(dtype):
     torch = pytest.importorskip("torch")
     m, (wts, depth) = _inputs("dense_c128")
     model = pkg().train_dense_networks.dense_model_struct()
+    model.compute_dtype = dtype
     model.load_weights(wts)
     out = model.build(torch.from_numpy(depth).cuda(), 69, train_mode=False).cpu().numpy()
     assert rel_inf(out, golden_array("dense_c128", "out")) <= FP32_REL_TOL
@@ -50,10 +55,12 @@ def test_dense_gpu_matches_golden_and_oracle():
 
 
 @pytest.mark.gpu
-def test_hier_gpu_matches_golden_and_oracle():
+@pytest.mark.parametrize("dtype", REG_DTYPES)
+def test_hier_gpu_matches_golden_and_oracle(dtype):
     torch = pytest.importorskip("torch")
     m, (wts, depth) = _inputs("hier_c128")
     model = pkg().train_hier_networks.hier_model_struct()
+    model.compute_dtype = dtype
     model.load_weights(wts)
     out = model.build(torch.from_numpy(depth).cuda(), *MG.HIER_HEADS, train_mode=False).cpu().numpy()
     assert rel_inf(out, golden_array("hier_c128", "out")) <= FP32_REL_TOL
