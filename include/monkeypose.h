@@ -187,11 +187,13 @@ int mp_crop3d_batch(const mp_camera* cam, const void* frames, int depth_dtype, i
                     int nthreads);
 
 /* prepare_data_test on the device (train_cnn_networks_hgru.py:61-74) with tr_res = the attention
- * output, for a batch of n frames in one launch (all pointers device memory, asynchronous):
+ * output, for a batch of n frames in one launch (asynchronous; every pointer is device memory
+ * except cam and com_scale, which are read on the host at the call):
  *   frames    [n][h][w] float32 as fed to the attention net; the crop sees frames * frame_scale
  *             (image_np * image_max_depth, line 67: frame_scale = 10000)
  *   com_norm  [n][3] float32 attention output; com = com_norm * com_scale in float64
- *             (com_scale = {image_orig_size[0], image_orig_size[1], image_max_depth}, line 69)
+ *             (com_scale: host double[3] = {image_orig_size[0], image_orig_size[1], image_max_depth},
+ *             line 69)
  *   patches   [n][dsize][dsize][1] = cropArea3D(frame, com) / cam.max_depth
  *   Ms [n][9], coms_out [n][3] float64; status [n] int32: 0 ok, else the frame's crop failed
  *             (1 CoM depth zero / not finite, 2 empty crop, 3 degenerate bounds, 4 empty resize;
@@ -210,6 +212,13 @@ int mp_info(mp_ctx* ctx, const char* key, int64_t* value);
  * summed elapsed milliseconds and launch count (reading synchronises those events) */
 int mp_profile_enable(mp_ctx* ctx, int enable);
 int mp_profile_read(mp_ctx* ctx, const char* name, double* total_ms, int64_t* launches);
+
+/* ---- TF1 checkpoint support (host only; monkey-pose_amd/tf_checkpoint.py) ----
+ * CRC-32C (Castagnoli, reflected 0x82F63B78) of n bytes continuing from `init` (0 to start), as
+ * tensor_bundle (BundleEntryProto.crc32c) and LevelDB-format table blocks store it before masking.
+ * Replaces the checksum half of tf.train.NewCheckpointReader (train_cnn_networks_hgru.py:248-250,
+ * 312-313: saver.restore). */
+uint32_t mp_crc32c(uint32_t init, const void* data, size_t n);
 
 #ifdef __cplusplus
 }

@@ -10,6 +10,7 @@ The directory name carries a hyphen, so import it with ``importlib.import_module
 * ``train_cnn_networks_hgru`` -- ``attn_model_struct`` (the attention CoM regressor),
   ``prepare_data_test`` (device batch crop) and ``FramePosePipeline`` (frame -> CoM -> crop -> pose)
 * ``weights``     -- TF variable-name tables and deterministic synthetic initialisers
+* ``tf_checkpoint`` -- TF1 V2 checkpoint reader / writer (no TensorFlow needed)
 * ``_lib``        -- ctypes binding of ``libmonkeypose.so`` (C ABI: ``include/monkeypose.h``)
 """
 from . import weights  # noqa: F401
@@ -21,5 +22,6 @@ from . import train_hier_networks  # noqa: F401
 from . import train_cnn_networks_hgru  # noqa: F401
 from . import monkeydetector  # noqa: F401
 from . import parallel  # noqa: F401
+from . import tf_checkpoint  # noqa: F401
 
 __all__ = ["hgru_pose", "hgru_module", "train_dense_networks", "train_hier_networks", "train_cnn_networks_hgru", "weights", "_lib"]

@@ -33,6 +33,14 @@ class RegressorBase:
     def load_weights(self, weights: Dict[str, np.ndarray]) -> None:
         self.weights = {(k if k.startswith("cnn/") else "cnn/" + k): v for k, v in weights.items()}
         self._ctx_key = None
+        self._strict = False
+
+    def load_checkpoint(self, path: str, remap=None, strict: bool = True) -> None:
+        """Weights from a TF1 V2 checkpoint (see ``hgru_pose.model.load_checkpoint``)."""
+        from . import tf_checkpoint as C
+        t = C.model_variables(C.read_checkpoint(path))
+        self.load_weights(remap(t) if remap else t)
+        self._strict = strict
 
     def load_npz(self, path: str) -> None:
         with np.load(path, allow_pickle=False) as z:
@@ -43,6 +51,9 @@ class RegressorBase:
 
     def _resolve(self, table) -> Dict[str, np.ndarray]:
         given = dict(self.weights or {})
+        missing = [v.name for v in table if v.name not in given]
+        if missing and getattr(self, "_strict", False) and self.data_dict is None:
+            raise KeyError(f"checkpoint lacks {len(missing)} variable(s) the model needs: {missing[:8]}")
         out = {v.name: (np.asarray(given[v.name], np.float32) if v.name in given
                         else W.synth_value(v, self.weight_seed)) for v in table}
         if self.data_dict is not None:

@@ -78,6 +78,17 @@ class model:
         """Variables keyed by TF name (``cnn/...``); missing ones are synthesised."""
         self.weights = {(k if k.startswith("cnn/") else "cnn/" + k): v for k, v in weights.items()}
         self._ctx_key = None
+        self._strict = False
+
+    def load_checkpoint(self, path: str, remap=None, strict: bool = True) -> None:
+        """Weights from a TF1 V2 checkpoint (prefix, ``.index`` path or directory; see
+        ``tf_checkpoint``), optimizer slots dropped; ``remap`` maps the name dict first (e.g. the
+        pose half of ``tf_checkpoint.split_hgru_train_checkpoint``).  ``strict``: build() raises
+        if a variable the model needs is absent instead of synthesising it."""
+        from . import tf_checkpoint as C
+        t = C.model_variables(C.read_checkpoint(path))
+        self.load_weights(remap(t) if remap else t)
+        self._strict = strict
 
     def load_npz(self, path: str) -> None:
         with np.load(path, allow_pickle=False) as z:
@@ -87,6 +98,9 @@ class model:
         table = W.hgru_pose_vars(output_shape=output_shape, timesteps=self.timesteps, crop=crop)
         given = dict(self.weights or {})
         out: Dict[str, np.ndarray] = {}
+        missing = [v.name for v in table if v.name not in given]
+        if missing and getattr(self, "_strict", False) and self.data_dict is None:
+            raise KeyError(f"checkpoint lacks {len(missing)} variable(s) the model needs: {missing[:8]}")
         for v in table:
             if v.name in given:
                 out[v.name] = np.asarray(given[v.name], np.float32)

@@ -164,12 +164,12 @@ class MonkeyDetector(object):
         Ms = torch.empty((n, 3, 3), dtype=torch.float64, device=dev)
         coms = torch.empty((n, 3), dtype=torch.float64, device=dev)
         status = torch.empty((n,), dtype=torch.int32, device=dev)
-        scale = torch.tensor([float(v) for v in com_scale], dtype=torch.float64, device=dev)
+        scale = (ctypes.c_double * 3)(*[float(v) for v in com_scale])   # host array (read at the call)
         st = _lib.current_stream(dev) if stream is None else stream
         cam = self._cam()
         _lib.check(_lib_crop().mp_crop3d_dev(ctypes.byref(cam), ctypes.c_void_p(fr.data_ptr()), n, h, w,
                                              float(frame_scale), ctypes.c_void_p(cn.data_ptr()),
-                                             ctypes.c_void_p(scale.data_ptr()), int(dsize),
+                                             ctypes.cast(scale, ctypes.c_void_p), int(dsize),
                                              ctypes.c_void_p(patches.data_ptr()), ctypes.c_void_p(Ms.data_ptr()),
                                              ctypes.c_void_p(coms.data_ptr()), ctypes.c_void_p(status.data_ptr()),
                                              ctypes.c_void_p(st)))
