@@ -52,11 +52,7 @@ class CheckpointError(ValueError):
 def crc32c(data, init: int = 0) -> int:
     """CRC-32C of ``data`` (bytes-like or numpy array) continuing from ``init``; native."""
     from . import _lib
-    lib = _lib.load()
-    fn = lib.mp_crc32c
-    if fn.restype is not ctypes.c_uint32:
-        fn.restype = ctypes.c_uint32
-        fn.argtypes = [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]
+    fn = _lib.load().mp_crc32c
     if isinstance(data, np.ndarray):
         a = np.ascontiguousarray(data)
         return int(fn(init, a.ctypes.data_as(ctypes.c_void_p), a.nbytes))
