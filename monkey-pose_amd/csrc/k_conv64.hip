@@ -136,6 +136,7 @@ __global__ __launch_bounds__(256) void gate_init_kernel(const float* __restrict_
 // One thread per pooled output pixel, all 64 channels: the 4x4 input patch is loaded once
 // (unconditional clamped loads, zero-masked), and the filter / bias / BN vectors are
 // thread-uniform, so they come through scalar loads and enter the FMAs as SGPR operands.
+template <bool NHWC>   // output layout: C8 (hGRU backbone) or NHWC (attention net, aconv_1 + apool_1 + BN)
 __global__ __launch_bounds__(256) void conv1_pool_bn_kernel(const float* __restrict__ in,
                                                             const float* __restrict__ w,   // [9][64]
                                                             const float* __restrict__ bias,
@@ -179,7 +180,7 @@ __global__ __launch_bounds__(256) void conv1_pool_bn_kernel(const float* __restr
         }
       o[e] = best * bn_s[ch] + bn_t[ch];
     }
-    float* dst = out + c8_index(b, q, y, x, 0, Ho, Wo);
+    float* dst = NHWC ? out + (((size_t)b * Ho + y) * Wo + x) * 64 + 8 * q : out + c8_index(b, q, y, x, 0, Ho, Wo);
     *reinterpret_cast<f32x4*>(dst) = f32x4{o[0], o[1], o[2], o[3]};
     *reinterpret_cast<f32x4*>(dst + 4) = f32x4{o[4], o[5], o[6], o[7]};
   }
@@ -282,10 +283,14 @@ hipError_t launch_gate_init(const float* O0, float* O, float* Og, const f32x4* g
 }
 
 hipError_t launch_conv1_pool_bn(const float* in, const float* w, const float* bias, const float* s,
-                                const float* t, float* out, int B, int Hin, int Win, hipStream_t st) {
+                                const float* t, float* out, int B, int Hin, int Win, hipStream_t st, bool nhwc) {
   const size_t total = (size_t)B * (Hin / 2) * (Win / 2);
-  hipLaunchKernelGGL(conv1_pool_bn_kernel, dim3((total + 255) / 256), dim3(256), 0, st, in, w, bias,
-                     s, t, out, B, Hin, Win);
+  if (nhwc)
+    hipLaunchKernelGGL(conv1_pool_bn_kernel<true>, dim3((total + 255) / 256), dim3(256), 0, st, in, w, bias, s, t,
+                       out, B, Hin, Win);
+  else
+    hipLaunchKernelGGL(conv1_pool_bn_kernel<false>, dim3((total + 255) / 256), dim3(256), 0, st, in, w, bias, s, t,
+                       out, B, Hin, Win);
   return hipGetLastError();
 }
 

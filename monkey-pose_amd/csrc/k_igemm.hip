@@ -131,6 +131,7 @@ __global__ __launch_bounds__(256) void igemm_conv_kernel(IgemmArgs p) {
 // current step's MFMAs run; the loads are unconditional (clamped addresses, then a select), so a
 // step's loads are all in flight together.
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ f32x16 mfma16(f16x8 a, f16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
@@ -216,14 +217,16 @@ __global__ __launch_bounds__(256) void igemm_x3_kernel(IgemmArgs p, const f16x8*
   for (int k0 = 0; k0 < p.K; k0 += IG_BK) {
     lds_barrier();   // the previous step's LDS reads are done
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < 4; ++i) {   // one 8-byte store per plane and slot
       const int row = (tid >> 3) + 32 * i;
+      f16x4 hv, lv;
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        const _Float16 hh = (_Float16)av[i][s];
-        Ah[row * IGX_LD + k4 + s] = hh;
-        Al[row * IGX_LD + k4 + s] = (_Float16)(av[i][s] - (float)hh);
+        hv[s] = (_Float16)av[i][s];
+        lv[s] = (_Float16)(av[i][s] - (float)hv[s]);
       }
+      *reinterpret_cast<f16x4*>(Ah + row * IGX_LD + k4) = hv;
+      *reinterpret_cast<f16x4*>(Al + row * IGX_LD + k4) = lv;
     }
     f16x8 wc[2][NB][2];
 #pragma unroll

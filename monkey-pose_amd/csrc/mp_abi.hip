@@ -13,6 +13,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <map>
@@ -21,6 +22,7 @@
 #include <vector>
 
 #include "../../include/monkeypose.h"
+
 #include "mp_runtime.hpp"
 
 
@@ -275,8 +277,85 @@ void check_map(mp_ctx* c, int64_t H, int64_t W, const char* what) {
                            " and width a multiple of 32");
 }
 
+// the hGRU loop of images [b0, b0 + n) on stream st (FFT path), all state pointers offset
+void fft_circuit_range(mp_ctx* c, int b0, int n, int H, int W, int T, float* final_dst2, hipStream_t st) {
+  const size_t m = (size_t)b0 * 64 * H * W;              // floats per image of a C8 / NHWC map
+  void* S = static_cast<char*>(c->specS.p) + fft_spec_bytes(b0);
+  void* Y = static_cast<char*>(c->specY.p) + fft_spec_bytes(b0);
+  float* P = c->specP.f() + m;
+  for (int t = 0; t < T; ++t) {
+    ConvArgs a{};
+    a.H = H;
+    a.W = W;
+    a.src = c->Og.f() + m;
+    a.dst = c->I.f() + m;
+    a.X = c->X.f() + m;
+    a.O = c->O.f() + m;
+    a.vecs = c->vecs.f();
+    ConvArgs b{};
+    b.H = H;
+    b.W = W;
+    b.dst = c->O.f() + m;
+    b.O = c->O.f() + m;
+    b.I = c->I.f() + m;
+    b.vecs = c->vecs.f();
+    b.rho = c->rho[t];
+    b.mode = (t == T - 1) ? 1 : 0;
+    b.dst2 = (t == T - 1) ? final_dst2 + m : c->Og.f() + m;
+    const bool bf = c->dtype == MP_DTYPE_BF16;
+    hip_check(launch_fft_fwd(a.src, S, n, H, W, st, bf), "fft_fwd");
+    hip_check(launch_spec_gemm(S, c->spec_g.p, Y, n, c->p_unscale, st, bf), "spec_gemm");
+    hip_check(launch_fft_inv_a_fwd(Y, a, S, n, st, bf), "fft_inv_a_fwd");
+    hip_check(launch_spec_gemm(S, c->spec_g.p, Y, n, c->p_unscale, st, bf), "spec_gemm");
+    hip_check(launch_fft_inv(Y, P, n, H, W, st, bf), "fft_inv");
+    hip_check(launch_spec_epi_b(b, P, c->or_x3.p, c->or_us, c->ir_x3.p, c->ir_us, n, st, bf), "B epilogue");
+  }
+}
+
+int stream_count() {
+  static const int v = [] {
+    const char* e = std::getenv("MP_STREAMS");
+    return e ? std::max(1, std::min(4, std::atoi(e))) : 2;
+  }();
+  return v;
+}
+
 void run_circuit(mp_ctx* c, int64_t n, int H, int W, int T, const float* o0_nhwc, float* final_dst2,
                  hipStream_t st) {
+  // FFT path, not profiling: batch slices are independent, so they run on separate streams and
+  // their latency-bound kernels overlap (the per-kernel HIP-event profile keeps one stream)
+  const int ns = std::min<int>(stream_count(), (int)(n / 32));
+  if (is_fft(c->dtype) && !c->prof && ns >= 2) {
+    hip_check(launch_gate_init_x3(o0_nhwc, c->O.f(), c->Og.f(), c->ir_x3.p, c->ir_us, c->vecs.f(), (int)n, H, W,
+                                  st, c->dtype == MP_DTYPE_BF16),
+              "gate_init");
+    while ((int)c->sides.size() < ns - 1) {
+      hipStream_t s;
+      hipEvent_t e;
+      hip_check(hipStreamCreateWithFlags(&s, hipStreamNonBlocking), "hipStreamCreate");
+      hip_check(hipEventCreateWithFlags(&e, hipEventDisableTiming), "hipEventCreate");
+      c->sides.push_back(s);
+      c->ev_join.push_back(e);
+    }
+    if (!c->ev_fork) hip_check(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming), "hipEventCreate");
+    hip_check(hipEventRecord(c->ev_fork, st), "hipEventRecord");
+    // slices of whole 32-image GEMM groups
+    const int groups = (int)(n + 31) / 32;
+    int b0 = 0;
+    for (int k = 0; k < ns; ++k) {
+      const int g = groups / ns + (k < groups % ns ? 1 : 0);
+      const int cnt = std::min<int>(g * 32, (int)n - b0);
+      hipStream_t s = k == 0 ? st : c->sides[k - 1];
+      if (k > 0) hip_check(hipStreamWaitEvent(s, c->ev_fork, 0), "hipStreamWaitEvent");
+      fft_circuit_range(c, b0, cnt, H, W, T, final_dst2, s);
+      b0 += cnt;
+    }
+    for (int k = 1; k < ns; ++k) {
+      hip_check(hipEventRecord(c->ev_join[k - 1], c->sides[k - 1]), "hipEventRecord");
+      hip_check(hipStreamWaitEvent(st, c->ev_join[k - 1], 0), "hipStreamWaitEvent");
+    }
+    return;
+  }
   hip_check(is_fft(c->dtype)
                 ? launch_gate_init_x3(o0_nhwc, c->O.f(), c->Og.f(), c->ir_x3.p, c->ir_us, c->vecs.f(), (int)n, H, W, st,
                                       c->dtype == MP_DTYPE_BF16)

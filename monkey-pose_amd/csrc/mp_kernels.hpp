@@ -35,7 +35,8 @@ hipError_t launch_conv64(int ks, int epi, ConvArgs a, int B, hipStream_t st);
 hipError_t launch_gate_init(const float* O0, float* O, float* Og, const f32x4* gpk_ir, const float* vecs,
                             int B, int H, int W, hipStream_t st);
 hipError_t launch_conv1_pool_bn(const float* in, const float* w, const float* bias, const float* s,
-                                const float* t, float* out, int B, int Hin, int Win, hipStream_t st);
+                                const float* t, float* out, int B, int Hin, int Win, hipStream_t st,
+                                bool nhwc = false);
 hipError_t launch_nhwc_to_c8(const float* in, float* out, int B, int H, int W, hipStream_t st);
 hipError_t launch_c8_to_nhwc(const float* in, float* out, int B, int H, int W, hipStream_t st);
 hipError_t launch_pack_conv64(const float* w, f32x4* out, int ks, hipStream_t st);

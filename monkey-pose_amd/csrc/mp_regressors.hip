@@ -304,11 +304,24 @@ void attn_forward(mp_ctx* c, const float* frames, int n, int H, int W, float* ou
   const auto specs = attn_convs();
   for (size_t i = 0; i < specs.size(); ++i) {                                                  // 440-476
     const auto& s = specs[i];
+    const auto& L = c->layers[s.name];
+    const int h2 = same_out(h, 2), w2 = same_out(w, 2);
+    if (i == 0 && h % 2 == 0 && w % 2 == 0) {
+      // aconv_1 (1 -> 64, 3x3) + apool_1 + BN in one pass (the hGRU backbone's conv_1 kernel, NHWC
+      // out): the 4 MiB-per-frame pre-pool map is never written
+      float* pl = buf(c, "attn_pool_a", (size_t)n * h2 * w2 * 64);
+      hip_check(launch_conv1_pool_bn(x, c->raw.at("aconv_1/aconv_1_filters").dev->f(), L.b.f(), L.bn_s.f(),
+                                     L.bn_t.f(), pl, n, h, w, st, true),
+                "aconv_1 + apool_1");
+      cur = V(pl, 64, 0, 64, h2, w2);
+      h = h2;
+      w = w2;
+      cin = 64;
+      continue;
+    }
     float* cv = buf(c, "attn_conv", (size_t)n * h * w * s.cout);
     conv(c, s.name, n, cur, V(cv, s.cout, 0, s.cout, h, w), 1, st);
-    const int h2 = same_out(h, 2), w2 = same_out(w, 2);
     float* pl = buf(c, i % 2 ? "attn_pool_b" : "attn_pool_a", (size_t)n * h2 * w2 * s.cout);
-    const auto& L = c->layers[s.name];
     pool(n, V(cv, s.cout, 0, s.cout, h, w), V(pl, s.cout, 0, s.cout, h2, w2), 0, st, L.bn_s.f(), L.bn_t.f());
     cur = V(pl, s.cout, 0, s.cout, h2, w2);
     h = h2;

@@ -154,7 +154,15 @@ struct mp_ctx {
   std::vector<ProfEvent> events;
   std::vector<hipEvent_t> pool;
 
+  // ---- batch slices on extra streams (FFT circuit; MP_STREAMS=1 disables) ----
+  std::vector<hipStream_t> sides;
+  hipEvent_t ev_fork = nullptr;
+  std::vector<hipEvent_t> ev_join;
+
   ~mp_ctx() {
+    for (auto s : sides) (void)hipStreamDestroy(s);
+    if (ev_fork) (void)hipEventDestroy(ev_fork);
+    for (auto e : ev_join) (void)hipEventDestroy(e);
     for (auto& e : events) {
       (void)hipEventDestroy(e.a);
       (void)hipEventDestroy(e.b);

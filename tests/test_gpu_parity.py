@@ -183,6 +183,32 @@ def test_bf16_circuit_within_bf16_gate(case):
     assert err <= BF16_REL_TOL, err
 
 
+@pytest.mark.parametrize("dtype", ["fp32_fft", "bf16"])
+def test_stream_split_is_bit_identical(dtype):
+    """The FFT path runs the hGRU loop as batch slices on two streams unless profiling is on; both
+    schedules give the same bits (every reduction is per crop)."""
+    mp = pkg()
+    W = mp.weights
+    n = 96
+    ctx = mp._lib.Context(mp._lib.MP_MODEL_HGRU_POSE, 0)
+    for v in W.hgru_pose_vars(output_shape=69, timesteps=8, crop=128):
+        ctx.set_weight(v.name, W.synth_value(v, 1234, 8))
+    ctx.finalize(mp._lib.dtype_code(dtype))
+    depth = _cuda(W.synth_crops(n, seed=3, size=128))
+    o0 = _cuda(W.synth_hidden((n, 64, 64, 64), seed=4))
+    st = mp._lib.current_stream(torch.device("cuda:0"))
+    a = torch.empty((n, 69), device="cuda")
+    b = torch.empty((n, 69), device="cuda")
+    ctx.pose_fwd(depth, o0, a, st)
+    ctx.profile(True)
+    ctx.pose_fwd(depth, o0, b, st)
+    ctx.profile(False)
+    assert torch.equal(a, b)
+    one = torch.empty((1, 69), device="cuda")
+    ctx.pose_fwd(depth[70:71].contiguous(), o0[70:71].contiguous(), one, st)
+    assert torch.equal(one[0], a[70])
+
+
 def test_fft_precision_is_fp32_class():
     """The FFT path (fp32 72-point FFTs + fp32 spectral GEMM) stays fp32-class: its error against
     the float64 golden output is within a small multiple of the exact fp32 direct path's."""
