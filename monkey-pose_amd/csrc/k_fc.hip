@@ -35,13 +35,29 @@ __global__ void pack_fc_kernel(const float* __restrict__ W, f32x4* out, int K, i
   out[i] = v;
 }
 
+// 1-D grid -> (m tile, n tile, K split), XCD-aware: workgroups are dispatched round-robin over the
+// 8 XCDs (separate L2s), so the Mt*Nt blocks of one K split are given ids 8 apart -- one XCD, back
+// to back -- and the split's activation rows and weight slab are fetched into that L2 once instead
+// of once per tile on different XCDs.  Blocks past the last split exit at once.
+struct FcTile {
+  int mt, nt, split;
+};
+__device__ __forceinline__ FcTile fc_tile(int Mt, int Nt) {
+  const int id = blockIdx.x, local = id >> 3, per = Mt * Nt;
+  const int r = local % per;
+  return {r / Nt, r % Nt, (local / per) * 8 + (id & 7)};
+}
+inline int fc_grid(int Mt, int Nt, int S) { return 8 * ((S + 7) / 8) * Mt * Nt; }
+
 __global__ __launch_bounds__(256) void fc_gemm_kernel(const float* __restrict__ A, int lda,
                                                       const f32x4* __restrict__ Wpk,
                                                       float* __restrict__ part, int M, int K,
-                                                      int N32, int kslice) {
+                                                      int N32, int kslice, int S) {
   __shared__ float As[FC_BM * FC_LDA];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, col = lane & 31;
-  const int mt = blockIdx.x, ntile = blockIdx.y, split = blockIdx.z;
+  const FcTile tl = fc_tile((M + FC_BM - 1) / FC_BM, (N32 + 3) / 4);
+  if (tl.split >= S) return;
+  const int mt = tl.mt, ntile = tl.nt, split = tl.split;
   const int K8 = (K + 7) / 8;
   const int Npad = N32 * 32;
   const int nb = ntile * 4 + wv;
@@ -158,10 +174,12 @@ constexpr int FCX_LD = FC_BK + 8;   // f16 pitch of the hi / lo activation plane
 __global__ __launch_bounds__(256) void fc_gemm_x3_kernel(const float* __restrict__ A, int lda,
                                                          const f16x8* __restrict__ Wpk,
                                                          float* __restrict__ part, int M, int K,
-                                                         int N32, int kslice, float unscale) {
+                                                         int N32, int kslice, float unscale, int S) {
   __shared__ _Float16 Ah[FC_BM * FCX_LD], Al[FC_BM * FCX_LD];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, col = lane & 31;
-  const int mt = blockIdx.x, ntile = blockIdx.y, split = blockIdx.z;
+  const FcTile tl = fc_tile((M + FC_BM - 1) / FC_BM, (N32 + 3) / 4);
+  if (tl.split >= S) return;
+  const int mt = tl.mt, ntile = tl.nt, split = tl.split;
   const int K16 = (K + 15) / 16;
   const int Npad = N32 * 32;
   const int nb = ntile * 4 + wv;
@@ -273,9 +291,9 @@ hipError_t launch_fc_gemm_x3(const float* A, int lda, const void* Wpk, float uns
                              int N, int S, int kslice, hipStream_t st) {
   if (K % FC_BK || kslice % FC_BK || lda % 4) return hipErrorInvalidValue;
   const int N32 = (N + 31) / 32;
-  dim3 grid((M + FC_BM - 1) / FC_BM, (N32 + 3) / 4, S);
-  hipLaunchKernelGGL(fc_gemm_x3_kernel, grid, dim3(256), 0, st, A, lda, static_cast<const f16x8*>(Wpk), part, M, K,
-                     N32, kslice, unscale);
+  const int grid = fc_grid((M + FC_BM - 1) / FC_BM, (N32 + 3) / 4, S);
+  hipLaunchKernelGGL(fc_gemm_x3_kernel, dim3(grid), dim3(256), 0, st, A, lda, static_cast<const f16x8*>(Wpk), part,
+                     M, K, N32, kslice, unscale, S);
   return hipGetLastError();
 }
 
@@ -305,8 +323,8 @@ int fc_choose_splits(int M, int K, int N, int* kslice) {
 hipError_t launch_fc_gemm(const float* A, int lda, const f32x4* Wpk, float* part, int M, int K, int N,
                           int S, int kslice, hipStream_t st) {
   const int N32 = (N + 31) / 32;
-  dim3 grid((M + FC_BM - 1) / FC_BM, (N32 + 3) / 4, S);
-  hipLaunchKernelGGL(fc_gemm_kernel, grid, dim3(256), 0, st, A, lda, Wpk, part, M, K, N32, kslice);
+  const int grid = fc_grid((M + FC_BM - 1) / FC_BM, (N32 + 3) / 4, S);
+  hipLaunchKernelGGL(fc_gemm_kernel, dim3(grid), dim3(256), 0, st, A, lda, Wpk, part, M, K, N32, kslice, S);
   return hipGetLastError();
 }
 

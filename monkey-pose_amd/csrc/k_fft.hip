@@ -289,6 +289,16 @@ __device__ __forceinline__ void inv_row_from_T(const cpx* T, int y, int p, cpx (
 // channels), instead of one strided 8-byte access per row thread.
 constexpr int RLD = 73;
 
+// Block -> channel group, XCD-aware: the two 4-channel groups of one C8 chunk (cq = 2q, 2q+1) each
+// touch half of every 32-byte pixel chunk.  Workgroups are dispatched round-robin over the 8 XCDs
+// (separate L2s), so blocks i and i+8 share an XCD: giving them the two halves of a chunk lets one
+// L2 fetch (or write back) each line once instead of two XCDs each moving the whole line
+// (rocprofv3 FETCH/WRITE_SIZE showed 2x the algorithmic bytes on these maps otherwise).
+__device__ __forceinline__ int fft_block_cq(int blk) {
+  const int p = blk & 15;
+  return 2 * (p & 7) + (p >> 3);
+}
+
 // forward 2-D FFT of one C8 activation map -> S.  The rows are read straight into registers (64
 // independent 8-byte loads in flight per thread): staging the tile through LDS pixel-major measured
 // slower (0.24 vs 0.18 ms at B = 256) -- the load pass and its barrier serialise ahead of the FFT.
@@ -296,7 +306,7 @@ template <bool BF>
 __global__ __launch_bounds__(192, 2) void fft_fwd_kernel(const float* __restrict__ src, void* __restrict__ S,
                                                       int H, int W) {
   __shared__ cpx T[FFT_LDS];
-  const int b = blockIdx.x >> 4, cq = blockIdx.x & 15;
+  const int b = blockIdx.x >> 4, cq = fft_block_cq(blockIdx.x);
   const int q = cq >> 1, e0 = 4 * (cq & 1);
   const int tid = threadIdx.x;
   if (tid < 128) {
@@ -323,7 +333,7 @@ template <bool BF>
 __global__ __launch_bounds__(192, 2) void fft_inv_kernel(const void* __restrict__ Y, float* __restrict__ P,
                                                       int H, int W) {
   __shared__ cpx T[FFT_LDS];
-  const int b = blockIdx.x >> 4, cq = blockIdx.x & 15;
+  const int b = blockIdx.x >> 4, cq = fft_block_cq(blockIdx.x);
   const int q = cq >> 1, e0 = 4 * (cq & 1);
   const int tid = threadIdx.x;
   inv_cols_to_T<BF>(Y, b, cq, tid, T);
@@ -358,7 +368,7 @@ __global__ __launch_bounds__(192, 2) void fft_inv_a_fwd_kernel(const void* __res
                                                             void* __restrict__ S) {
   __shared__ cpx T[FFT_LDS];
   const int H = p.H, W = p.W;
-  const int b = blockIdx.x >> 4, cq = blockIdx.x & 15;
+  const int b = blockIdx.x >> 4, cq = fft_block_cq(blockIdx.x);
   const int q = cq >> 1, e0 = 4 * (cq & 1);
   const int tid = threadIdx.x;
   inv_cols_to_T<BF>(Y, b, cq, tid, T);
