@@ -180,6 +180,31 @@ def extras(mp, dev, args):
         ctx.close()
     except Exception as e:  # noqa: BLE001
         out["dense_b256"] = {"error": repr(e)}
+    try:   # dense-hierarchical hybrid on the layer-graph runtime (hipGraph replay)
+        import os as _os
+        DH = mp.train_dense_hier_networks
+        model = DH.dense_hier_model_struct()
+        g = model.record(128, 128, 108, 39, 39, 39, 39, 36)
+        model.load_weights(W.synth_weights(model._table(g), seed=8))
+        model.build(depth, 108, 39, 39, 39, 39, 36)
+        gf = mp._graph.flops_per_sample(g) / 1e9
+        rec = {"gflop_per_crop": round(gf, 3), "dtype": "fp32_split",
+               "kernels": model._ctx.info("graph_kernels"), "streams": model._ctx.info("graph_streams"),
+               "buffers": model._ctx.info("graph_buffers")}
+        for mode in ("1", "0"):   # hipGraph replay, then eager multi-stream launches (the default)
+            _os.environ["MP_GRAPH_EXEC"] = mode
+            t = time_gpu(lambda: model.forward(depth), 5, 1)
+            k = "hipgraph_replay" if mode == "1" else "eager_multistream"
+            rec[k] = {"crops_per_s": round(B / t, 2), "ms_per_batch": round(t * 1e3, 3),
+                      "tflops": round(gf * 1e9 * B / t / 1e12, 2)}
+        rec.update(rec["eager_multistream"])
+        d1 = depth[:1].contiguous()
+        t1 = time_gpu(lambda: model.forward(d1), 20, 3)
+        rec["b1_latency_ms"] = round(t1 * 1e3, 3)
+        out["dense_hier_b256"] = rec
+        model._ctx.close()
+    except Exception as e:  # noqa: BLE001
+        out["dense_hier_b256"] = {"error": repr(e)}
     try:   # attention CoM regressor on full frames + the device chain to the pose
         out.update(frame_chain(mp, dev, args))
     except Exception as e:  # noqa: BLE001

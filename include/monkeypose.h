@@ -53,7 +53,9 @@ enum {
   MP_MODEL_HGRU_CIRCUIT = 2, /* hgru_module.ContextualCircuit  (hgru_module.py:54-959)     */
   MP_MODEL_DENSE = 3,        /* dense_model_struct  (train_dense_networks.py:211-509)      */
   MP_MODEL_HIER = 4,         /* hier_model_struct   (train_hier_networks.py:327-631)       */
-  MP_MODEL_ATTN = 5          /* attn_model_struct   (train_cnn_networks_hgru.py:422-525)   */
+  MP_MODEL_ATTN = 5,         /* attn_model_struct   (train_cnn_networks_hgru.py:422-525)   */
+  MP_MODEL_GRAPH = 6         /* a recorded layer graph (mp_graph_set): dense_hier_model_struct
+                                (train_dense_hier_networks.py:327-2507)                       */
 };
 
 enum { MP_MEM_HOST = 0, MP_MEM_DEVICE = 1 };
@@ -204,7 +206,9 @@ int mp_crop3d_dev(const mp_camera* cam, const float* frames, int64_t n, int64_t 
                   double* coms_out, int32_t* status, void* stream);
 
 /* read a model property: "output_shape", "timesteps", "ssf", "finalized", "workspace_bytes",
- * "weight_bytes" */
+ * "weight_bytes"; graph contexts also "graph_kernels" (kernel launches per forward),
+ * "graph_streams" (streams the schedule uses), "graph_captured" (1 once a hipGraph was built, MP_GRAPH_EXEC=1),
+ * "graph_buffers" (activation buffers after concat placement) -- as planned by the last forward */
 int mp_info(mp_ctx* ctx, const char* key, int64_t* value);
 
 /* per-kernel device timing with HIP events recorded on the launch stream around every launch of
@@ -212,6 +216,48 @@ int mp_info(mp_ctx* ctx, const char* key, int64_t* value);
  * summed elapsed milliseconds and launch count (reading synchronises those events) */
 int mp_profile_enable(mp_ctx* ctx, int enable);
 int mp_profile_read(mp_ctx* ctx, const char* name, double* total_ms, int64_t* launches);
+
+/* ---- layer-graph runtime (MP_MODEL_GRAPH) ---------------------------------------------------
+ * The reference's regressors are TF1 graph builders: build() chains conv_layer / max_pool /
+ * tf.concat / fc_layer calls.  A facade records the same calls as ops (tensor ids in SSA order:
+ * id 0 = the [n, h, w, in_channels] input, every op defines `out`); the library then plans and runs
+ * the graph natively:
+ *   - tf.concat is free: a weighted union-find places every concatenated tensor as a channel
+ *     range of one wide NHWC buffer per concat group, which its producers write in place;
+ *   - relu / identity fold into their producer (conv_layer already applies relu; a relu after
+ *     fc_layer becomes the FC epilogue);
+ *   - kernels run as a dependency DAG over up to MP_GRAPH_STREAMS (env, default 8) HIP streams
+ *     (MP_GRAPH_EXEC=1: built once per (n, h, w) into a hipGraph and replayed instead).
+ * Replaces the graph-builder half of dense_hier_model_struct.build (train_dense_hier_networks.py:
+ * 338-2382; helpers conv_layer 2431-2446, max_pool 2426-2429, avg_pool 2416-2419, max_pool_4
+ * 2421-2424, fc_layer 2448-2455). */
+enum {
+  MP_OP_CONV = 1,     /* relu(conv2d(src, name/name_filters, stride, SAME) + name/name_biases) */
+  MP_OP_MAXPOOL = 2,  /* ksize x ksize / ksize max pool, SAME (ksize 2 or 4)                     */
+  MP_OP_AVGPOOL = 3,  /* 2x2 / 2 average pool, SAME (in-image count)                             */
+  MP_OP_CONCAT = 4,   /* tf.concat(src[0..n_src), axis=-1)                                       */
+  MP_OP_FC = 5,       /* reshape(src, [-1, K]) @ name/name_weights + name/name_biases             */
+  MP_OP_RELU = 6,     /* tf.nn.relu                                                              */
+  MP_OP_IDENTITY = 7  /* tf.identity                                                             */
+};
+#define MP_GRAPH_MAX_SRC 8
+typedef struct {
+  int32_t kind;                    /* MP_OP_* */
+  int32_t out;                     /* tensor id defined by this op (> every id it reads) */
+  int32_t n_src;
+  int32_t src[MP_GRAPH_MAX_SRC];
+  int32_t ksize, stride, cout;     /* conv: filter size, stride, out channels; pools: ksize */
+  const char* name;                /* conv / fc: the layer's variable scope ("dense_1_conv_1_scale_1") */
+} mp_graph_op;
+
+/* install the graph of an MP_MODEL_GRAPH context (before mp_finalize_weights, which packs every
+ * conv / fc layer it names); outputs: the tensor ids mp_graph_fwd writes, in order */
+int mp_graph_set(mp_ctx* ctx, const mp_graph_op* ops, int n_ops, int in_channels, const int32_t* outputs,
+                 int n_outputs);
+
+/* run the graph on x [n, h, w, in_channels]; outs[i] = caller-owned device buffer holding output
+ * tensor i densely ([n, cout] for an fc output, [n, H, W, C] otherwise) */
+int mp_graph_fwd(mp_ctx* ctx, const float* x, int64_t n, int64_t h, int64_t w, float* const* outs, void* stream);
 
 /* ---- TF1 checkpoint support (host only; monkey-pose_amd/tf_checkpoint.py) ----
  * CRC-32C (Castagnoli, reflected 0x82F63B78) of n bytes continuing from `init` (0 to start), as

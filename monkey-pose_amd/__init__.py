@@ -7,6 +7,8 @@ The directory name carries a hyphen, so import it with ``importlib.import_module
 * ``hgru_module`` -- drop-in ``ContextualCircuit(X, ...).build()`` (reference ``hgru_module.py``)
 * ``train_dense_networks.dense_model_struct`` / ``train_hier_networks.hier_model_struct`` --
   drop-ins for the dense and hierarchical regressor heads
+* ``train_dense_hier_networks.dense_hier_model_struct`` -- the dense-hierarchical hybrid, recorded
+  as a layer graph (``_graph``) and run by the native graph runtime (``mp_graph_*``)
 * ``train_cnn_networks_hgru`` -- ``attn_model_struct`` (the attention CoM regressor),
   ``prepare_data_test`` (device batch crop) and ``FramePosePipeline`` (frame -> CoM -> crop -> pose)
 * ``weights``     -- TF variable-name tables and deterministic synthetic initialisers
@@ -19,6 +21,7 @@ from . import hgru_pose  # noqa: F401
 from . import hgru_module  # noqa: F401
 from . import train_dense_networks  # noqa: F401
 from . import train_hier_networks  # noqa: F401
+from . import train_dense_hier_networks  # noqa: F401
 from . import train_cnn_networks_hgru  # noqa: F401
 from . import monkeydetector  # noqa: F401
 from . import parallel  # noqa: F401

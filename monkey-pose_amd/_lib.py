@@ -22,6 +22,7 @@ MP_MODEL_HGRU_CIRCUIT = 2
 MP_MODEL_DENSE = 3
 MP_MODEL_HIER = 4
 MP_MODEL_ATTN = 5
+MP_MODEL_GRAPH = 6
 MP_MEM_HOST = 0
 MP_MEM_DEVICE = 1
 MP_DTYPE_F32 = 0
@@ -82,6 +83,10 @@ _SIGS = {
     "mp_resize_bilinear": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
                                           ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
                                           ctypes.c_void_p]),
+    "mp_graph_set": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int, ctypes.c_int,
+                                    ctypes.c_void_p, ctypes.c_int]),
+    "mp_graph_fwd": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                                    ctypes.c_int64, ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p]),
     "mp_crc32c": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]),
     "mp_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64)]),
     "mp_profile_enable": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
@@ -213,6 +218,11 @@ class Context:
         n, h, w, c = depth.shape
         arr = (ctypes.c_void_p * 6)(*[_ptr(o) for o in outs])
         check(self.lib.mp_hier_fwd(self.h, _ptr(depth), n, h, w, arr, ctypes.c_void_p(stream)))
+
+    def graph_fwd(self, x, outs, stream: int) -> None:
+        n, h, w, c = x.shape
+        arr = (ctypes.c_void_p * len(outs))(*[_ptr(o) for o in outs])
+        check(self.lib.mp_graph_fwd(self.h, _ptr(x), n, h, w, arr, ctypes.c_void_p(stream)))
 
     def attn_fwd(self, frames, out, stream: int) -> None:
         n, h, w, c = frames.shape

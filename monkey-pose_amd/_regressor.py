@@ -46,6 +46,9 @@ class RegressorBase:
         with np.load(path, allow_pickle=False) as z:
             self.load_weights({k: z[k] for k in z.files})
 
+    def _on_context(self, ctx: _lib.Context) -> None:
+        """hook between mp_create and the weights (graph contexts install their graph here)"""
+
     def _table(self, **kw) -> List[W.Var]:
         raise NotImplementedError
 
@@ -78,6 +81,7 @@ class RegressorBase:
         key = (key, device, id(self.weights), id(self.data_dict), dt)
         if self._ctx is None or self._ctx_key != key:
             ctx = _lib.Context(self.MODEL_KIND, device)
+            self._on_context(ctx)
             for name, val in self._resolve(table).items():
                 ctx.set_weight(name, val)
             ctx.finalize(_lib.dtype_code(dt))

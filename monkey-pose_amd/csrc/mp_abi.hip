@@ -414,7 +414,7 @@ const char* mp_last_error(void) { return g_err.c_str(); }
 int mp_create(int device, int model_kind, mp_ctx** out) {
   return guard([&] {
     if (!out) fail(MP_ERR_ARG, "out is NULL");
-    if (model_kind < MP_MODEL_HGRU_POSE || model_kind > MP_MODEL_ATTN)
+    if (model_kind < MP_MODEL_HGRU_POSE || model_kind > MP_MODEL_GRAPH)
       fail(MP_ERR_ARG, "unknown model_kind " + std::to_string(model_kind));
     int ndev = 0;
     hip_check(hipGetDeviceCount(&ndev), "hipGetDeviceCount");
@@ -481,6 +481,8 @@ int mp_finalize_weights(mp_ctx* ctx, int compute_dtype) {
       finalize_pose(ctx);
     else if (ctx->model == MP_MODEL_HGRU_CIRCUIT)
       finalize_circuit(ctx, nullptr, nullptr);
+    else if (ctx->model == MP_MODEL_GRAPH)
+      finalize_graph(ctx);
     else
       finalize_regressor(ctx);
     hip_check(hipDeviceSynchronize(), "finalize sync");
@@ -646,6 +648,7 @@ int mp_info(mp_ctx* ctx, const char* key, int64_t* value) {
   return guard([&] {
     if (!ctx || !key || !value) fail(MP_ERR_ARG, "mp_info: null pointer");
     const std::string k(key);
+    if (graph_info(ctx, k, value)) return;
     if (k == "output_shape")
       *value = ctx->nout;
     else if (k == "timesteps")

@@ -99,6 +99,7 @@ inline bool known_name_hgru(int model, const std::string& n) {
 bool known_name_regressor(int model, const std::string& n);
 
 inline bool known_name(int model, const std::string& n) {
+  if (model == MP_MODEL_GRAPH) return true;   // checked against the graph at mp_finalize_weights
   return (model == MP_MODEL_HGRU_POSE || model == MP_MODEL_HGRU_CIRCUIT) ? known_name_hgru(model, n)
                                                                          : known_name_regressor(model, n);
 }
@@ -148,6 +149,9 @@ struct mp_ctx {
   std::map<std::string, DevBuf> ws;            // named activation buffers
   int64_t ws_batch = 0, ws_h = 0, ws_w = 0;
   std::vector<int> head_sizes;                 // outputs: dense {out}; hier {out, P, R, M, I, T}
+
+  // ---- recorded layer graph (MP_MODEL_GRAPH, mp_graph.hip) ----
+  std::shared_ptr<struct GraphState> graph;
 
   // ---- profiling ----
   bool prof = false;
@@ -243,5 +247,11 @@ void bn_fold(mp_ctx* c, const std::string& scope, int n, DevBuf& s_out, DevBuf& 
 
 // mp_regressors.hip
 void finalize_regressor(mp_ctx* c);
+// a conv ([K][Cout]) or fc ([K][N]) weight packed in the context's precision
+void pack_matrix(mp_ctx* c, mp_ctx::PackedLayer& L, const float* w, bool x3_ok);
+
+// mp_graph.hip
+void finalize_graph(mp_ctx* c);
+bool graph_info(mp_ctx* c, const std::string& key, int64_t* value);   // "graph_*" keys of mp_info
 
 }  // namespace mpr

@@ -8,6 +8,10 @@ NumPy restatements of the two other pose regressors on the north-star path, call
   fc_layer 450-457)
 * ``hier_model_struct.build``   -- /root/reference/train_hier_networks.py:338-530
   (helpers 535-579, same semantics)
+* ``dense_hier_model_struct.build`` -- /root/reference/train_dense_hier_networks.py:338-2382
+  (helpers 2416-2455): nine three-scale dense blocks over one width ladder, four transitions,
+  five finger heads and the whole-hand head; ``trace`` records every conv / fc (scope, shapes) in
+  build order so tests/test_dense_hier.py can pin the restatement against the reference's AST
 * ``attn_model_struct.build``   -- /root/reference/train_cnn_networks_hgru.py:436-525 (helpers
   541-570), the attention / centre-of-mass regressor, with ``tf.image.resize_images`` (439)
   restated from TF1's published bilinear kernel (third-party, TF 1.x not importable here:
@@ -174,3 +178,79 @@ def attn_forward(frames: np.ndarray, wts: Dict[str, np.ndarray], dtype=np.float6
         t["relu1"] = h
         return out, t
     return out
+
+
+# dense_hier_model_struct (train_dense_hier_networks.py:338-2382)
+DH_LADDER = (12, 16, 24, 32, 48, 64, 96, 128, 164, 198, 230)
+
+
+def dense_hier_forward(depth: np.ndarray, wts: Dict[str, np.ndarray], dtype=np.float64, trace=None):
+    """Returns (output, {p,r,m,i,t}_output).  Head sizes come from the fc_4 / final_fc_2 weights."""
+    L = DH_LADDER
+
+    def conv(x, name, stride=1):
+        w = wts[f"cnn/{name}/{name}_filters"]
+        if trace is not None:
+            trace.append(("conv", name, int(w.shape[0]), stride, x.shape[-1], int(w.shape[3])))
+        assert w.shape[2] == x.shape[-1], name
+        return _conv(wts, x, name, stride)
+
+    def fcr(x, name, relu=True):
+        w = wts[f"cnn/{name}/{name}_weights"]
+        if trace is not None:
+            trace.append(("fc", name, int(np.prod(x.shape[1:])), int(w.shape[1])))
+        y = _fc(wts, x, name)
+        return np.maximum(y, 0) if relu else y
+
+    def block(b, s, nl, ins, chain):
+        p = f"dense_{b}_conv"
+        if chain:                                                       # 348-352
+            x1 = conv(ins[0], f"{p}_1_scale_1")
+            x2 = conv(x1, f"{p}_1_scale_2", 2)
+            x3 = conv(x2, f"{p}_1_scale_3", 2)
+        else:                                                           # e.g. 455-459
+            x1, x2, x3 = (conv(ins[k], f"{p}_1_scale_{k + 1}") for k in range(3))
+        h1, h2, h3 = [x1], [x2], [x3]
+        h1.append(conv(x1, f"{p}_2_scale_1"))                           # 356-364
+        h2.append(_cat(conv(x1, f"{p}_2_scale_2_1", 2), conv(x2, f"{p}_2_scale_2_2")))
+        h3.append(_cat(conv(x2, f"{p}_2_scale_3_2", 2), conv(x3, f"{p}_2_scale_3_3")))
+        for l in range(3, nl + 1):                                      # 367-437
+            n = f"{p}_{l}_scale"
+            i1, i2, i3 = _cat(*h1), _cat(*h2), _cat(*h3)
+            o1 = conv(conv(i1, f"{n}_1_1x1"), f"{n}_1")
+            o21 = conv(conv(i1, f"{n}_2_1x1_1"), f"{n}_2_1", 2)
+            o22 = conv(conv(i2, f"{n}_2_1x1_2"), f"{n}_2_2")
+            o32 = conv(conv(i2, f"{n}_3_1x1_2"), f"{n}_3_2", 2)
+            o33 = conv(conv(i3, f"{n}_3_1x1_3"), f"{n}_3_3")
+            h1.append(o1)
+            h2.append(_cat(o21, o22))
+            h3.append(_cat(o32, o33))
+        return h1[-1], h2[-1], h3[-1]
+
+    def transition(k, outs):                                            # 440-449
+        return [max_pool_same(conv(x, f"tran_{k}_conv_{j + 1}")) for j, x in enumerate(outs)]
+
+    def finger(f, outs):                                                # 824-857
+        pools = [max_pool_same(x) for x in outs]
+        r1 = [fcr(pl, f"fc_1_{f}_{j + 1}") for j, pl in enumerate(pools)]
+        r3 = fcr(fcr(_cat(*r1), f"fc_2_{f}"), f"fc_3_{f}")
+        return pools, fcr(r3, f"fc_4_{f}", relu=False)
+
+    x = depth.astype(dtype)
+    pool1 = max_pool_same(conv(x, "conv_1"))                            # 341-343
+    t1 = transition(1, block(1, 0, 4, [pool1], True))
+    t2 = transition(2, block(2, 1, 4, t1, False))
+    pools, outs = {}, {}
+    pools["p"], outs["p"] = finger("p", block(3, 2, 6, t2, False))
+    pools["r"], outs["r"] = finger("r", block(4, 2, 6, t2, False))
+    t3 = transition(3, block(5, 1, 4, t1, False))
+    pools["m"], outs["m"] = finger("m", block(6, 2, 6, t3, False))
+    pools["i"], outs["i"] = finger("i", block(7, 2, 6, t3, False))
+    t4 = transition(4, block(8, 1, 4, t1, False))
+    pools["t"], outs["t"] = finger("t", block(9, 2, 6, t4, False))
+    hand = []
+    for f in FINGERS:                                                   # 2245-2373
+        r1 = [fcr(pl, f"fc_1_{f}h_{j + 1}") for j, pl in enumerate(pools[f])]
+        hand.append(fcr(_cat(*r1), f"fc_2_{f}h"))
+    out = fcr(fcr(_cat(*hand), "final_fc_1"), "final_fc_2", relu=False)    # 2376-2382
+    return out, outs
