@@ -266,6 +266,24 @@ int mp_graph_fwd(mp_ctx* ctx, const float* x, int64_t n, int64_t h, int64_t w, f
  * 312-313: saver.restore). */
 uint32_t mp_crc32c(uint32_t init, const void* data, size_t n);
 
+/* ---- TFRecord ingestion (host only; monkey-pose_amd/data_loader.py) ----------
+ * Replaces tf.TFRecordReader + tf.parse_single_example + tf.decode_raw (data_loader.py:10-26) and
+ * tf.python_io.TFRecordWriter + encode_example (Datareader.py:13-27).  A reader memory-maps the
+ * file and indexes its records once (length CRCs always checked, payload CRCs when verify != 0). */
+typedef struct mp_tfrecord mp_tfrecord;
+int mp_tfrecord_open(const char* path, int verify, mp_tfrecord** out, int64_t* n_records);
+void mp_tfrecord_close(mp_tfrecord* r);
+/* byte size of bytes feature `feature` (BytesList value[0], or a packed FloatList) of record rec */
+int mp_tfrecord_feature_size(mp_tfrecord* r, int64_t rec, const char* feature, int64_t* bytes);
+/* decode_raw gather: out[i] = the raw bytes of `feature` in record indices[i], each exactly
+ * bytes_per_record (else MP_ERR_SHAPE), decoded by up to nthreads host threads */
+int mp_tfrecord_read(mp_tfrecord* r, const int64_t* indices, int64_t count, const char* feature, void* out,
+                     int64_t bytes_per_record, int nthreads);
+/* write n_records tf.train.Example records {names[k]: bytes_feature(data[k] + i * bytes_per_record[k])}
+ * (features in the given order), creating or (append != 0) extending the file */
+int mp_tfrecord_write(const char* path, int64_t n_records, int n_features, const char* const* names,
+                      const void* const* data, const int64_t* bytes_per_record, int append);
+
 #ifdef __cplusplus
 }
 #endif

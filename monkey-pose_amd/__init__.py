@@ -13,6 +13,7 @@ The directory name carries a hyphen, so import it with ``importlib.import_module
   ``prepare_data_test`` (device batch crop) and ``FramePosePipeline`` (frame -> CoM -> crop -> pose)
 * ``weights``     -- TF variable-name tables and deterministic synthetic initialisers
 * ``tf_checkpoint`` -- TF1 V2 checkpoint reader / writer (no TensorFlow needed)
+* ``data_loader`` -- TFRecord ingestion (``inputs`` / ``read_and_decode``, ``create_tf_record``)
 * ``_lib``        -- ctypes binding of ``libmonkeypose.so`` (C ABI: ``include/monkeypose.h``)
 """
 from . import weights  # noqa: F401
@@ -26,5 +27,6 @@ from . import train_cnn_networks_hgru  # noqa: F401
 from . import monkeydetector  # noqa: F401
 from . import parallel  # noqa: F401
 from . import tf_checkpoint  # noqa: F401
+from . import data_loader  # noqa: F401
 
 __all__ = ["hgru_pose", "hgru_module", "train_dense_networks", "train_hier_networks", "train_cnn_networks_hgru", "weights", "_lib"]

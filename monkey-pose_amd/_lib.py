@@ -87,6 +87,16 @@ _SIGS = {
                                     ctypes.c_void_p, ctypes.c_int]),
     "mp_graph_fwd": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
                                     ctypes.c_int64, ctypes.POINTER(ctypes.c_void_p), ctypes.c_void_p]),
+    "mp_tfrecord_open": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p),
+                                        ctypes.POINTER(ctypes.c_int64)]),
+    "mp_tfrecord_close": (None, [ctypes.c_void_p]),
+    "mp_tfrecord_feature_size": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64, ctypes.c_char_p,
+                                                ctypes.POINTER(ctypes.c_int64)]),
+    "mp_tfrecord_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_char_p,
+                                        ctypes.c_void_p, ctypes.c_int64, ctypes.c_int]),
+    "mp_tfrecord_write": (ctypes.c_int, [ctypes.c_char_p, ctypes.c_int64, ctypes.c_int,
+                                         ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_void_p),
+                                         ctypes.POINTER(ctypes.c_int64), ctypes.c_int]),
     "mp_crc32c": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]),
     "mp_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64)]),
     "mp_profile_enable": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
