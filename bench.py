@@ -99,13 +99,36 @@ def fft_kernels(ctx, B, hw, steps, bf16=False):
     return out
 
 
-def fft_roofline(kern):
+# per-kernel HBM bytes per launch from rocprofv3 PMC passes (FETCH_SIZE x2 on gfx950 + WRITE_SIZE,
+# MI355X_MICROARCH.md), collected with the full-batch single-stream launches of this workload by
+# tools/pmc_bytes.py and committed under profiles/ (bench cannot profile itself)
+PMC_TRAFFIC = {False: "profiles/r1_fft2/pmc_traffic_fp32_b256.csv", True: None}
+PMC_KERNEL = {"fft_fwd": "fft_fwd_kernel<", "spec_gemm": "spec_gemm_kernel<", "inv_a_fwd": "fft_inv_a_fwd_kernel<",
+              "fft_inv": "fft_inv_kernel<", "epi_b": "spec_epi_b_kernel<"}
+
+
+def pmc_traffic(name, bf16, batch):
+    """(bytes per launch, source) of kernel `name` from the committed PMC summary, or (None, why)."""
+    import csv
+    path = PMC_TRAFFIC.get(bf16)
+    full = os.path.join(os.path.dirname(os.path.abspath(__file__)), path) if path else None
+    if batch != 256 or not full or not os.path.exists(full):
+        return None, "no PMC summary for this dtype / batch"
+    tag = PMC_KERNEL[name] + ("true>" if bf16 else "false>")
+    for r in csv.DictReader(open(full)):
+        if tag in r["kernel"]:
+            return round(float(r["traffic_MB"]) * 1e6), path
+    return None, "kernel not in the PMC summary"
+
+
+def fft_roofline(kern, bf16=False, batch=256):
     """Roofline of the dominant FFT-path kernel: its binding roof (HBM bytes or fp32 MFMA FLOPs,
     whichever bounds it tighter at peak) against its measured average launch time."""
     name = max(kern, key=lambda k: kern[k]["ms_per_step"])
     k = kern[name]
+    traffic, src = pmc_traffic(name, bf16, batch)
     r = {"kernel": name + " (k_fft.hip)", "avg_launch_ms": k["avg_launch_ms"], "launches": k["launches"],
-         "traffic": None}
+         "traffic": traffic, "traffic_source": src, "algo_bytes": k["algo_bytes"]}
     t_hbm = k["algo_bytes"] / (PEAK_HBM_GBPS * 1e9)
     peak = k.get("mfma_peak", PEAK_FP32_TFLOPS)
     t_mfma = k.get("algo_flop", 0.0) / (peak * 1e12)
@@ -388,7 +411,7 @@ def main():
                                f"batch {B} per GPU", "global_batch": world * B, "crop": crop,
                    "timesteps": T, "parallelism": f"dp{world} (batch shards, one {'RCCL' if args.backend == 'nccl' else 'gloo'} weight broadcast)",
                    "hgru_streams": (int(os.environ.get("MP_STREAMS", "2")) if fft else 1)},
-        "roofline": (fft_roofline(kern) if fft else
+        "roofline": (fft_roofline(kern, args.dtype == "bf16", B) if fft else
                      roofline(args.dtype, achieved_tf, conv_launch_ms, na + nb, conv15_flop)),
         "breakdown_ms_per_step": {"conv15": round((ms_a + ms_b) / prof_steps, 3),
                                   "fc1": round(ms_fc / max(1, nfc), 3),
