@@ -14,6 +14,7 @@ p = argparse.ArgumentParser()
 p.add_argument("--batch", type=int, default=256)
 p.add_argument("--steps", type=int, default=20)
 p.add_argument("--dtype", default="f32_fft")
+p.add_argument("--profile", action="store_true", help="also a single-stream HIP-event pass: ms per kernel class")
 a = p.parse_args()
 W = mp.weights
 dev = torch.device("cuda:0")
@@ -36,3 +37,15 @@ torch.cuda.synchronize()
 dt = (time.perf_counter() - t0) / a.steps
 print(f"MP_STREAMS={os.environ.get('MP_STREAMS', 'default')} dtype={a.dtype} B={B}: {dt * 1e3:.3f} ms/step, "
       f"{B / dt:.1f} crops/s, out[0,:3]={out[0, :3].tolist()}")
+if a.profile:
+    ctx.profile(True)
+    for _ in range(5):
+        ctx.pose_fwd(depth, o0, out, st)
+    torch.cuda.synchronize()
+    ctx.profile(False)
+    names = ["backbone", "fc1", "fft_fwd", "spec_gemm", "inv_a_fwd", "fft_inv", "epi_b"]
+    res = {}
+    for n in names:
+        ms, cnt = ctx.profile_read(n)
+        res[n] = round(ms / max(1, cnt), 4)
+    print("profile ms/launch:", res)
