@@ -121,7 +121,7 @@ def pmc_traffic(name, bf16, batch):
     return None, "kernel not in the PMC summary"
 
 
-def fft_roofline(kern, bf16=False, batch=256):
+def fft_roofline(kern, bf16=False, batch=256, hbm_meas=None):
     """Roofline of the dominant FFT-path kernel: its binding roof (HBM bytes or fp32 MFMA FLOPs,
     whichever bounds it tighter at peak) against its measured average launch time."""
     name = max(kern, key=lambda k: kern[k]["ms_per_step"])
@@ -138,7 +138,31 @@ def fft_roofline(kern, bf16=False, batch=256):
     else:
         r.update(bound="hbm", achieved=k["achieved_GBps"], peak=PEAK_HBM_GBPS, unit="GB/s",
                  peak_basis="HBM3E 8 TB/s", frac=k["hbm_frac"])
+        if hbm_meas:
+            r.update(measured_copy_GBps=hbm_meas, frac_of_measured=round(k["achieved_GBps"] / hbm_meas, 4))
     return r
+
+
+def hbm_copy_gbps(dev, nbytes=2 << 30):
+    """Measured streaming rate of this box's HBM: a 2 GiB device-to-device copy (read + write bytes
+    / time, HIP events), the practical ceiling next to the 8 TB/s spec peak (re-measure
+    the peaks on the box)."""
+    import torch
+    a = torch.empty(nbytes // 4, dtype=torch.float32, device=dev)
+    b = torch.empty_like(a)
+    a.fill_(1.0)
+    for _ in range(2):
+        b.copy_(a)
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(5):
+        b.copy_(a)
+    e1.record()
+    e1.synchronize()
+    gbps = 2.0 * nbytes * 5 / (e0.elapsed_time(e1) * 1e-3) / 1e9
+    del a, b
+    torch.cuda.empty_cache()
+    return round(gbps, 1)
 
 
 def time_gpu(fn, steps, warmup):
@@ -391,6 +415,7 @@ def main():
 
     fft = args.dtype in ("f32_fft", "bf16")
     kern = fft_kernels(ctx, B, px, prof_steps, args.dtype == "bf16") if fft else None
+    hbm_meas = hbm_copy_gbps(dev) if fft else None   # after the timed region
     value = world * B * args.steps / elapsed
     rec = {
         "metric": "depth-crops/sec hGRU-8T fwd @batch256 per GPU (128x128 crops)",
@@ -411,7 +436,7 @@ def main():
                                f"batch {B} per GPU", "global_batch": world * B, "crop": crop,
                    "timesteps": T, "parallelism": f"dp{world} (batch shards, one {'RCCL' if args.backend == 'nccl' else 'gloo'} weight broadcast)",
                    "hgru_streams": (int(os.environ.get("MP_STREAMS", "2")) if fft else 1)},
-        "roofline": (fft_roofline(kern, args.dtype == "bf16", B) if fft else
+        "roofline": (fft_roofline(kern, args.dtype == "bf16", B, hbm_meas) if fft else
                      roofline(args.dtype, achieved_tf, conv_launch_ms, na + nb, conv15_flop)),
         "breakdown_ms_per_step": {"conv15": round((ms_a + ms_b) / prof_steps, 3),
                                   "fc1": round(ms_fc / max(1, nfc), 3),
