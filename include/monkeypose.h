@@ -90,6 +90,16 @@ void mp_destroy(mp_ctx* ctx);
 int mp_set_weight(mp_ctx* ctx, const char* name, const float* data, const int64_t* shape, int ndim,
                   int mem_kind);
 
+/* replicate the weights set on ctxs[root] (mp_set_weight) into every other context of the list --
+ * one per device, or several on one device -- device to device, as a binomial tree of peer copies
+ * over xGMI: ceil(log2(nctx)) rounds, each round doubling the contexts that hold the weights, every
+ * copy of a round in flight together, nothing staged through the host.  Each context then runs
+ * its own mp_finalize_weights.  For one process driving several GPUs (SURVEY 8b's proposed
+ * weight broadcast); one process per GPU broadcasts the blob with torch.distributed (RCCL) instead
+ * (monkey-pose_amd/parallel.py).  Replaces loading data_dict / get_var once per device
+ * (hgru_pose.py:196-216). */
+int mp_bcast_weights(mp_ctx* const* ctxs, int nctx, int root);
+
 /* fold BN, pack every weight into its kernel's fragment order; must follow the last
  * mp_set_weight and precede any forward call */
 int mp_finalize_weights(mp_ctx* ctx, int compute_dtype);

@@ -63,6 +63,7 @@ _SIGS = {
     "mp_set_weight": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.c_void_p,
                                      ctypes.POINTER(ctypes.c_int64), ctypes.c_int, ctypes.c_int]),
     "mp_finalize_weights": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
+    "mp_bcast_weights": (ctypes.c_int, [ctypes.POINTER(ctypes.c_void_p), ctypes.c_int, ctypes.c_int]),
     "mp_reserve": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int64]),
     "mp_hgru_pose_fwd": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
                                         ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,

@@ -463,6 +463,70 @@ int mp_set_weight(mp_ctx* ctx, const char* name, const float* data, const int64_
   });
 }
 
+int mp_bcast_weights(mp_ctx* const* ctxs, int nctx, int root) {
+  return guard([&] {
+    if (!ctxs || nctx <= 0 || root < 0 || root >= nctx) fail(MP_ERR_ARG, "mp_bcast_weights: bad argument");
+    mp_ctx* src = ctxs[root];
+    std::vector<mp_ctx*> order{src};
+    for (int i = 0; i < nctx; ++i) {
+      if (!ctxs[i]) fail(MP_ERR_ARG, "mp_bcast_weights: null context");
+      if (ctxs[i]->model != src->model) fail(MP_ERR_ARG, "mp_bcast_weights: contexts of different model kinds");
+      for (int j = 0; j < i; ++j)
+        if (ctxs[j] == ctxs[i]) fail(MP_ERR_ARG, "mp_bcast_weights: a context is listed twice");
+      if (i != root) order.push_back(ctxs[i]);
+    }
+    if (src->raw.empty()) fail(MP_ERR_STATE, "mp_bcast_weights: the root context has no weights");
+    hip_check(hipSetDevice(src->device), "hipSetDevice");
+    hip_check(hipDeviceSynchronize(), "sync root");   // its mp_set_weight copies are complete
+    // destination tensors, same names / shapes (small ones keep their host copy for BN folding)
+    for (size_t k = 1; k < order.size(); ++k) {
+      mp_ctx* c = order[k];
+      hip_check(hipSetDevice(c->device), "hipSetDevice");
+      c->raw.clear();
+      for (const auto& kv : src->raw) {
+        RawWeight w;
+        w.shape = kv.second.shape;
+        w.host = kv.second.host;
+        w.dev = std::make_unique<DevBuf>();
+        w.dev->alloc(w.numel() * sizeof(float));
+        c->raw[kv.first] = std::move(w);
+      }
+      c->finalized = false;
+    }
+    // binomial tree: in round r, holders order[0 .. have) copy to order[have .. 2 have)
+    for (size_t have = 1; have < order.size(); have *= 2) {
+      std::vector<int> devs;
+      for (size_t i = 0; i < have && i + have < order.size(); ++i) {
+        mp_ctx *a = order[i], *b = order[i + have];
+        hip_check(hipSetDevice(b->device), "hipSetDevice");
+        if (a->device != b->device) {
+          int can = 0;
+          hip_check(hipDeviceCanAccessPeer(&can, b->device, a->device), "hipDeviceCanAccessPeer");
+          if (can) {
+            const hipError_t e = hipDeviceEnablePeerAccess(a->device, 0);
+            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) hip_check(e, "hipDeviceEnablePeerAccess");
+            (void)hipGetLastError();
+          }
+        }
+        hip_check(hipSetDevice(a->device), "hipSetDevice");
+        for (const auto& kv : a->raw) {
+          const auto& dst = b->raw.at(kv.first);
+          hip_check(hipMemcpyPeerAsync(dst.dev->p, b->device, kv.second.dev->p, a->device,
+                                       kv.second.numel() * sizeof(float), nullptr),
+                    "hipMemcpyPeerAsync");
+        }
+        devs.push_back(a->device);
+        devs.push_back(b->device);
+      }
+      for (int d : devs) {   // every copy of this round is complete before the next round reads them
+        hip_check(hipSetDevice(d), "hipSetDevice");
+        hip_check(hipDeviceSynchronize(), "bcast round sync");
+      }
+    }
+    hip_check(hipSetDevice(src->device), "hipSetDevice");
+  });
+}
+
 int mp_finalize_weights(mp_ctx* ctx, int compute_dtype) {
   return guard([&] {
     if (!ctx) fail(MP_ERR_ARG, "ctx is NULL");

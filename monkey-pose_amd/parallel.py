@@ -9,6 +9,7 @@ exchange.
 """
 from __future__ import annotations
 
+import ctypes
 from typing import Dict, List, Sequence, Tuple
 
 import numpy as np
@@ -86,3 +87,14 @@ def gather_outputs(out_shard, global_batch: int, rank: int, world: int, group=No
         s, e = shard_range(global_batch, r, world)
         rows.append(parts[r][:e - s])
     return torch.cat(rows, 0)
+
+
+def replicate_weights(contexts: Sequence, root: int = 0) -> None:
+    """One process driving several GPUs: copy the weights set on ``contexts[root]`` into every
+    other context (``mp_bcast_weights``: a binomial tree of device-to-device peer copies over xGMI,
+    nothing through the host).  Finalize each context afterwards."""
+    from . import _lib
+    if not contexts:
+        return
+    arr = (ctypes.c_void_p * len(contexts))(*[c.h for c in contexts])
+    _lib.check(contexts[0].lib.mp_bcast_weights(arr, len(contexts), int(root)))

@@ -66,3 +66,34 @@ def test_broadcast_and_gather_gloo_world2():
     for p in procs:
         p.join(timeout=60)
     assert res == {0: True, 1: True}
+
+
+@pytest.mark.gpu
+def test_replicate_weights_peer_tree():
+    """mp_bcast_weights: weights set on one context reach three others (here all on device 0, so
+    the tree's peer copies are device-local) and every replica computes bit-identical outputs."""
+    P = pkg()
+    L, W = P._lib, P.weights
+    n, crop, T = 2, 64, 8
+    table = W.hgru_pose_vars(output_shape=69, timesteps=T, crop=crop)
+    ctxs = [L.Context(L.MP_MODEL_HGRU_POSE, 0) for _ in range(4)]
+    for v in table:
+        ctxs[2].set_weight(v.name, W.synth_value(v, 1234, T))
+    P.parallel.replicate_weights(ctxs, root=2)
+    depth = torch.from_numpy(W.synth_crops(n, seed=42, size=crop)).cuda()
+    o0 = torch.from_numpy(W.synth_hidden((n, crop // 2, crop // 2, 64), seed=7)).cuda()
+    outs = []
+    for c in ctxs:
+        assert c.info("weight_bytes") == ctxs[2].info("weight_bytes")
+        c.finalize(L.MP_DTYPE_F32_FFT)
+        o = torch.empty((n, 69), device="cuda")
+        c.pose_fwd(depth, o0, o, L.current_stream())
+        outs.append(o)
+    torch.cuda.synchronize()
+    for o in outs[1:]:
+        assert torch.equal(o, outs[0])
+    other = L.Context(L.MP_MODEL_DENSE, 0)
+    with pytest.raises(L.MonkeyPoseError):
+        P.parallel.replicate_weights([ctxs[0], other])
+    with pytest.raises(L.MonkeyPoseError):
+        P.parallel.replicate_weights([L.Context(L.MP_MODEL_HGRU_POSE, 0), ctxs[0]])   # empty root
