@@ -218,3 +218,33 @@ def test_fft_precision_is_fp32_class():
     ea, eb = rel_inf(a, ref), rel_inf(b, ref)
     print(f"rel_inf err: fp32 {ea:.3e}  fp32_fft {eb:.3e}  (fft vs fp32 {rel_inf(b, a):.3e})")
     assert eb <= max(10 * ea, 1e-5)
+
+
+@pytest.mark.parametrize("n", [300, 1024])
+def test_full_size_properties(n):
+    """Beyond the metric's batch (ragged 300 = 9 GEMM groups + 12, and 1024): every sampled crop is
+    bit-identical to its own batch-1 run (slices, streams and GEMM groups never mix crops), the
+    whole batch is finite, and the last crop matches the float64 oracle within the fp32 gate."""
+    from oracle import hgru_ref as R
+    mp = pkg()
+    W = mp.weights
+    ctx = mp._lib.Context(mp._lib.MP_MODEL_HGRU_POSE, 0)
+    wts = {v.name: W.synth_value(v, 1234, 8) for v in W.hgru_pose_vars(output_shape=69, timesteps=8, crop=128)}
+    for k, v in wts.items():
+        ctx.set_weight(k, v)
+    ctx.finalize(mp._lib.MP_DTYPE_F32_FFT)
+    depth_np = W.synth_crops(n, seed=21, size=128)
+    o0_np = W.synth_hidden((n, 64, 64, 64), seed=22)
+    depth, o0 = _cuda(depth_np), _cuda(o0_np)
+    st = mp._lib.current_stream(torch.device("cuda:0"))
+    out = torch.empty((n, 69), device="cuda")
+    ctx.pose_fwd(depth, o0, out, st)
+    torch.cuda.synchronize()
+    assert bool(torch.isfinite(out).all())
+    one = torch.empty((1, 69), device="cuda")
+    for i in (0, n // 2, n - 1):
+        ctx.pose_fwd(depth[i:i + 1].contiguous(), o0[i:i + 1].contiguous(), one, st)
+        torch.cuda.synchronize()
+        assert torch.equal(one[0], out[i]), i
+    ref = R.hgru_pose_forward(depth_np[n - 1:], wts, o0_np[n - 1:], 8, np.float64)
+    assert rel_inf(out[n - 1:].cpu().numpy(), ref) <= FP32_REL_TOL
