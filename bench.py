@@ -185,8 +185,20 @@ def extras(mp, dev, args):
     B = args.batch
     depth = torch.from_numpy(W.synth_crops(B, seed=99, size=128)).to(dev)
     stream = mp._lib.current_stream(dev)
-    for dt in ("fp32_split", "fp32"):   # config 3: hierarchical cascade, batch 256
-        key = "hier_b256" + ("" if dt == "fp32_split" else "_exact_fp32")
+    try:   # config 3 through the façade's default engine: the recorded graph, multi-stream
+        hm = mp.train_hier_networks.hier_model_struct()
+        hm.load_weights({v.name: W.synth_value(v, 5) for v in W.hier_vars()})
+        hm.build(depth, 108, 39, 39, 39, 39, 36)
+        t = time_gpu(lambda: hm.forward(depth), 5, 1)
+        out["hier_b256"] = {"crops_per_s": round(B / t, 2), "ms_per_batch": round(t * 1e3, 3),
+                            "gflop_per_crop": 7.97, "tflops": round(7.97e9 * B / t / 1e12, 2),
+                            "dtype": "fp32_split", "engine": "layer-graph runtime (mp_graph_fwd)",
+                            "streams": hm._ctx.info("graph_streams")}
+        hm._ctx.close()
+    except Exception as e:  # noqa: BLE001
+        out["hier_b256"] = {"error": repr(e)}
+    for dt in ("fp32_split", "fp32"):   # config 3 on the one-stream C-ABI schedule (mp_hier_fwd)
+        key = "hier_b256_abi" + ("" if dt == "fp32_split" else "_exact_fp32")
         try:
             ctx = mp._lib.Context(mp._lib.MP_MODEL_HIER, dev.index)
             for v in W.hier_vars():

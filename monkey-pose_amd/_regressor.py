@@ -47,7 +47,7 @@ class RegressorBase:
             self.load_weights({k: z[k] for k in z.files})
 
     def _on_context(self, ctx: _lib.Context) -> None:
-        """hook between mp_create and the weights (graph contexts install their graph here)"""
+        """hook between mp_create and the weights of an MP_MODEL_GRAPH context (installs its graph)"""
 
     def _table(self, **kw) -> List[W.Var]:
         raise NotImplementedError
@@ -76,12 +76,14 @@ class RegressorBase:
                              f"got {self.compute_dtype!r}")
         return dt
 
-    def _context(self, key, table, device: int) -> _lib.Context:
+    def _context(self, key, table, device: int, kind: Optional[int] = None) -> _lib.Context:
         dt = self._dtype()
-        key = (key, device, id(self.weights), id(self.data_dict), dt)
+        kind = self.MODEL_KIND if kind is None else kind
+        key = (key, kind, device, id(self.weights), id(self.data_dict), dt)
         if self._ctx is None or self._ctx_key != key:
-            ctx = _lib.Context(self.MODEL_KIND, device)
-            self._on_context(ctx)
+            ctx = _lib.Context(kind, device)
+            if kind == _lib.MP_MODEL_GRAPH:
+                self._on_context(ctx)
             for name, val in self._resolve(table).items():
                 ctx.set_weight(name, val)
             ctx.finalize(_lib.dtype_code(dt))
@@ -100,3 +102,83 @@ class RegressorBase:
         if depth.dim() != 4 or depth.shape[-1] != 1:
             raise ValueError(f"depth must be [N, H, W, 1], got {tuple(depth.shape)}")
         return depth.detach().float().contiguous()
+
+
+class GraphRegressorBase(RegressorBase):
+    """A façade whose ``build`` is recorded as a layer graph and run by the native graph runtime
+    (``MP_MODEL_GRAPH``, ``_graph.py``): the reference's helpers (conv_layer / max_pool / avg_pool
+    / max_pool_4 / fc_layer, e.g. train_dense_hier_networks.py:2416-2455,
+    train_hier_networks.py:535-579) record ops on symbolic tensors that carry the reference's
+    attribute names.  Subclasses implement ``record(h, w, *head_sizes)`` and set ``_outputs``."""
+    MODEL_KIND = _lib.MP_MODEL_GRAPH
+    OUTPUT_ATTRS = ("output", "p_output", "r_output", "m_output", "i_output", "t_output")
+
+    # ---- the reference's helpers, recording instead of building TF ops ----
+    def conv_layer(self, bottom, in_channels, out_channels, name, filter_size=3, batchnorm=None,
+                   stride=(1, 1, 1, 1)):
+        if batchnorm is not None and name in batchnorm:
+            raise NotImplementedError("conv_layer batchnorm= (batch-moment BN) is a training option")
+        return self._g.conv(bottom, in_channels, out_channels, name, filter_size, stride[1])
+
+    def max_pool(self, bottom, name):
+        return self._g.pool(bottom, 2)
+
+    def max_pool_4(self, bottom, name):
+        return self._g.pool(bottom, 4)
+
+    def avg_pool(self, bottom, name):
+        return self._g.pool(bottom, 2, avg=True)
+
+    def fc_layer(self, bottom, in_size, out_size, name):
+        return self._g.fc(bottom, in_size, out_size, name)
+
+    def _set(self, attr, t):
+        t.label = attr
+        setattr(self, attr, t)
+        return t
+
+    def _concat(self, attr, xs):
+        return self._set(attr, self._g.concat(xs))
+
+    def _relu_fc(self, attr_fc, attr_relu, x, in_size, out_size, name):
+        f = self._set(attr_fc, self.fc_layer(x, in_size, out_size, name))
+        return self._set(attr_relu, self._g.relu(f))   # dropout only when train_mode (never here)
+
+    def _new_graph(self, h, w):
+        from . import _graph
+        self._g = _graph.GraphRecorder(int(h), int(w), 1)
+        return self._g
+
+    def _table(self, g) -> List[W.Var]:
+        from . import _graph
+        v: List[W.Var] = []
+        for name, shp in _graph.layer_shapes(g).items():
+            v += W._conv_b(name, shp[0], shp[2], shp[3]) if len(shp) == 4 else W._fc(f"cnn/{name}", *shp)
+        return v
+
+    def _on_context(self, ctx):
+        from . import _graph
+        _graph.install(ctx, self._g, self._outputs)
+
+    def _graph_build(self, depth, heads, batch_norm, train_mode):
+        depth = self._check_input(depth, batch_norm, train_mode)
+        n, h, w, _ = depth.shape
+        self.shapes = [int(s) for s in heads]
+        key = (tuple(self.shapes), int(h), int(w))
+        if getattr(self, "_rec_key", None) != key:
+            self.record(h, w, *self.shapes)
+            self._outputs = [getattr(self, a) for a in self.OUTPUT_ATTRS]
+            self._rec_key = key
+            self._ctx_key = None
+        self._ctx = self._context(key, self._table(self._g), depth.device.index or 0)
+        return self._graph_forward(depth)
+
+    def _graph_forward(self, depth):
+        import torch
+        depth = depth.detach().float().contiguous()
+        n = depth.shape[0]
+        outs = [torch.empty((n, s), dtype=torch.float32, device=depth.device) for s in self.shapes]
+        self._ctx.graph_fwd(depth, outs, _lib.current_stream(depth.device))
+        for a, o in zip(self.OUTPUT_ATTRS, outs):
+            setattr(self, a, o)
+        return outs[0]

@@ -23,7 +23,7 @@ from typing import List
 from . import _graph
 from . import _lib
 from . import weights as W
-from ._regressor import RegressorBase
+from ._regressor import GraphRegressorBase
 
 # channel ladder of the dense blocks: a block whose input is LADDER[s] wide grows its three scales
 # through LADDER[s+1 ..] (block 1: 348-437; the finger blocks: 591-822, ...)
@@ -34,36 +34,7 @@ WIDTH_OVERRIDE = {(6, "2_2"): 196}
 FINGERS = ("p", "r", "m", "i", "t")
 
 
-class dense_hier_model_struct(RegressorBase):
-    MODEL_KIND = _lib.MP_MODEL_GRAPH
-
-    # ---- the reference's helpers (2416-2455), recording instead of building TF ops ----
-    def conv_layer(self, bottom, in_channels, out_channels, name, filter_size=3, batchnorm=None,
-                   stride=(1, 1, 1, 1)):
-        if batchnorm is not None and name in batchnorm:
-            raise NotImplementedError("conv_layer batchnorm= (batch-moment BN) is a training option")
-        return self._g.conv(bottom, in_channels, out_channels, name, filter_size, stride[1])
-
-    def max_pool(self, bottom, name):
-        return self._g.pool(bottom, 2)
-
-    def max_pool_4(self, bottom, name):
-        return self._g.pool(bottom, 4)
-
-    def avg_pool(self, bottom, name):
-        return self._g.pool(bottom, 2, avg=True)
-
-    def fc_layer(self, bottom, in_size, out_size, name):
-        return self._g.fc(bottom, in_size, out_size, name)
-
-    def _set(self, attr, t):
-        t.label = attr
-        setattr(self, attr, t)
-        return t
-
-    def _concat(self, attr, xs):
-        return self._set(attr, self._g.concat(xs))
-
+class dense_hier_model_struct(GraphRegressorBase):
     # ---- one dense block (layers 1..n_layers, three scales) ----
     def _dense_block(self, b: int, s: int, n_layers: int, inputs, chain: bool):
         """Dense block ``b`` with input width LADDER[s].  ``chain`` (block 1, 348-352): scales 2 and
@@ -131,10 +102,6 @@ class dense_hier_model_struct(RegressorBase):
             pools.append(self._set(f"tran{k}_pool{j + 1}", self.max_pool(t, f"tran_{k}_pool_{j + 1}")))
         return pools
 
-    def _relu_fc(self, attr_fc, attr_relu, x, in_size, out_size, name):
-        f = self._set(attr_fc, self.fc_layer(x, in_size, out_size, name))
-        return self._set(attr_relu, self._g.relu(f))   # dropout only when train_mode (never here)
-
     def _finger_head(self, f: str, outs, size: int):
         """per-finger head (824-857): pools, three fc_1 -> concat -> fc_2 -> fc_3 -> fc_4."""
         pools = [self._set(f"pool_{f}{j + 1}", self.max_pool(x, f"pool_{f}_{j + 1}")) for j, x in enumerate(outs)]
@@ -156,7 +123,7 @@ class dense_hier_model_struct(RegressorBase):
 
     def record(self, h: int, w: int, output_shape, P_shape, R_shape, M_shape, I_shape, T_shape):
         """Record the graph of ``build`` (338-2382) for [N, h, w, 1] crops; returns the recorder."""
-        self._g = g = _graph.GraphRecorder(int(h), int(w), 1)
+        g = self._new_graph(h, w)
         x = g.input
         self.conv1 = self._set("conv1", self.conv_layer(x, 1, 12, "conv_1", filter_size=3))   # 341
         self.pool1 = self._set("pool1", self.max_pool(self.conv1, "pool_1"))                # 343
@@ -179,42 +146,15 @@ class dense_hier_model_struct(RegressorBase):
         fr = self._relu_fc("final_fc1", "final_relu1", hc, 1024 * 5, 1024, "final_fc_1")    # 2377-2380
         f2 = self._set("final_fc2", self.fc_layer(fr, 1024, int(output_shape), "final_fc_2"))
         self._set("output", g.identity(f2))                                                 # 2381-2382
-        self._outputs = [getattr(self, n) for n in ("output", "p_output", "r_output", "m_output",
-                                                     "i_output", "t_output")]
         return g
-
-    def _table(self, g) -> List[W.Var]:
-        v: List[W.Var] = []
-        for name, shp in _graph.layer_shapes(g).items():
-            v += W._conv_b(name, shp[0], shp[2], shp[3]) if len(shp) == 4 else W._fc(f"cnn/{name}", *shp)
-        return v
-
-    def _on_context(self, ctx):
-        _graph.install(ctx, self._g, self._outputs)
 
     def build(self, depth, output_shape, P_shape, R_shape, M_shape, I_shape, T_shape,
               batch_norm=None, train_mode=None):
-        depth = self._check_input(depth, batch_norm, train_mode)
-        n, h, w, _ = depth.shape
-        self.shapes = [int(output_shape), int(P_shape), int(R_shape), int(M_shape), int(I_shape),
-                       int(T_shape)]
-        key = (tuple(self.shapes), int(h), int(w))
-        if getattr(self, "_rec_key", None) != key:
-            self.record(h, w, *self.shapes)
-            self._rec_key = key
-            self._ctx_key = None
-        self._ctx = self._context(key, self._table(self._g), depth.device.index or 0)
-        return self.forward(depth)
+        return self._graph_build(depth, (output_shape, P_shape, R_shape, M_shape, I_shape, T_shape),
+                                 batch_norm, train_mode)
 
     def forward(self, depth):
-        import torch
-        depth = depth.detach().float().contiguous()
-        n = depth.shape[0]
-        outs = [torch.empty((n, s), dtype=torch.float32, device=depth.device) for s in self.shapes]
-        self._ctx.graph_fwd(depth, outs, _lib.current_stream(depth.device))
-        (self.output, self.p_output, self.r_output, self.m_output, self.i_output,
-         self.t_output) = outs
-        return self.output
+        return self._graph_forward(depth)
 
 
 def _flat(x) -> int:

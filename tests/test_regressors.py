@@ -55,11 +55,12 @@ def test_dense_gpu_matches_golden_and_oracle(dtype):
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("engine", ["graph", "mp_hier_fwd"])
 @pytest.mark.parametrize("dtype", REG_DTYPES)
-def test_hier_gpu_matches_golden_and_oracle(dtype):
+def test_hier_gpu_matches_golden_and_oracle(dtype, engine):
     torch = pytest.importorskip("torch")
     m, (wts, depth) = _inputs("hier_c128")
-    model = pkg().train_hier_networks.hier_model_struct()
+    model = pkg().train_hier_networks.hier_model_struct(use_graph=engine == "graph")
     model.compute_dtype = dtype
     model.load_weights(wts)
     out = model.build(torch.from_numpy(depth).cuda(), *MG.HIER_HEADS, train_mode=False).cpu().numpy()
@@ -77,3 +78,27 @@ def test_regressors_reject_training():
         pkg().train_dense_networks.dense_model_struct().build(x, 69, train_mode=True)
     with pytest.raises(NotImplementedError):
         pkg().train_hier_networks.hier_model_struct().build(x, 108, 39, 39, 39, 39, 36, batch_norm=["conv_1"])
+
+
+REF_HIER = "/root/reference/train_hier_networks.py"
+
+
+@pytest.mark.skipif(not __import__("os").path.exists(REF_HIER), reason="reference sources not present")
+def test_hier_recorded_graph_is_the_reference_graph():
+    """hier_model_struct.record() op for op against the reference's own build (AST extraction)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import extract_dense_hier as X
+    ops, _ = X.extract(MG.HIER_HEADS, path=X.REF_HIER)
+    rec = pkg().train_hier_networks.hier_model_struct().record(128, 128, *MG.HIER_HEADS).records()
+    assert len(rec) == len(ops) == 91
+    for a, b in zip(rec, ops):
+        assert a == {k: v for k, v in b.items() if k != "line"}
+
+
+def test_hier_recorded_graph_uses_the_hier_variables():
+    m = pkg().train_hier_networks.hier_model_struct()
+    g = m.record(128, 128, *MG.HIER_HEADS)
+    W = pkg().weights
+    assert {v.name: v.shape for v in m._table(g)} == {v.name: v.shape for v in W.hier_vars()}

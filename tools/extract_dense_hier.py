@@ -1,4 +1,5 @@
 """Dev tool (run in the build container only; /root/reference does not exist on the GPU box).
+Also reads hier_model_struct.build (train_hier_networks.py:338-530) with ``path=REF_HIER``.
 
 Reads dense_hier_model_struct.build (/root/reference/train_dense_hier_networks.py:338-2382) as an
 AST -- the file as a whole is Python 2 and does not parse, the build body does -- and writes the
@@ -14,12 +15,13 @@ import json
 import sys
 
 REF = "/root/reference/train_dense_hier_networks.py"
+REF_HIER = "/root/reference/train_hier_networks.py"   # hier_model_struct.build (338-530), same vocabulary
 
 
-def _src_build():
-    lines = open(REF).read().split("\n")
+def _src_build(path=REF):
+    lines = open(path).read().split("\n")
     start = next(i for i, l in enumerate(lines) if l.strip().startswith("def build(self,depth,output_shape,P_shape"))
-    end = next(i for i in range(start + 1, len(lines)) if lines[i].strip().startswith("def batchnorm"))
+    end = next(i for i in range(start + 1, len(lines)) if lines[i].strip().startswith("def "))
     body = "\n".join(l[4:] if l.startswith("    ") else l for l in lines[start:end])
     return ast.parse(body).body[0], start + 1
 
@@ -36,8 +38,8 @@ def _const(node):
     return ast.literal_eval(node)
 
 
-def extract(heads=(108, 39, 39, 39, 39, 36)):
-    fn, line0 = _src_build()
+def extract(heads=(108, 39, 39, 39, 39, 36), path=REF):
+    fn, line0 = _src_build(path)
     shapes = {"lr_input": (128, 128, 1)}
     alias = {}
     ops = []
