@@ -39,11 +39,12 @@ REG_DTYPES = ["fp32", "fp32_split"]
 
 
 @pytest.mark.gpu
+@pytest.mark.parametrize("engine", ["graph", "mp_dense_fwd"])
 @pytest.mark.parametrize("dtype", REG_DTYPES)
-def test_dense_gpu_matches_golden_and_oracle(dtype):
+def test_dense_gpu_matches_golden_and_oracle(dtype, engine):
     torch = pytest.importorskip("torch")
     m, (wts, depth) = _inputs("dense_c128")
-    model = pkg().train_dense_networks.dense_model_struct()
+    model = pkg().train_dense_networks.dense_model_struct(use_graph=engine == "graph")
     model.compute_dtype = dtype
     model.load_weights(wts)
     out = model.build(torch.from_numpy(depth).cuda(), 69, train_mode=False).cpu().numpy()
@@ -102,3 +103,27 @@ def test_hier_recorded_graph_uses_the_hier_variables():
     g = m.record(128, 128, *MG.HIER_HEADS)
     W = pkg().weights
     assert {v.name: v.shape for v in m._table(g)} == {v.name: v.shape for v in W.hier_vars()}
+
+
+REF_DENSE = "/root/reference/train_dense_networks.py"
+
+
+@pytest.mark.skipif(not __import__("os").path.exists(REF_DENSE), reason="reference sources not present")
+def test_dense_recorded_graph_is_the_reference_graph():
+    """dense_model_struct.record() op for op against the reference's own build (AST extraction)."""
+    import os
+    import sys
+    sys.path.insert(0, os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "tools"))
+    import extract_dense_hier as X
+    ops, _ = X.extract((69,), path=X.REF_DENSE)
+    rec = pkg().train_dense_networks.dense_model_struct().record(128, 128, 69).records()
+    assert len(rec) == len(ops) == 88
+    for a, b in zip(rec, ops):
+        assert a == {k: v for k, v in b.items() if k != "line"}
+
+
+def test_dense_recorded_graph_uses_the_dense_variables():
+    m = pkg().train_dense_networks.dense_model_struct()
+    g = m.record(128, 128, 69)
+    W = pkg().weights
+    assert {v.name: v.shape for v in m._table(g)} == {v.name: v.shape for v in W.dense_vars()}

@@ -1,5 +1,6 @@
 """Dev tool (run in the build container only; /root/reference does not exist on the GPU box).
-Also reads hier_model_struct.build (train_hier_networks.py:338-530) with ``path=REF_HIER``.
+Also reads hier_model_struct.build (train_hier_networks.py:338-530) with ``path=REF_HIER`` and
+dense_model_struct.build (train_dense_networks.py:223-408) with ``path=REF_DENSE``.
 
 Reads dense_hier_model_struct.build (/root/reference/train_dense_hier_networks.py:338-2382) as an
 AST -- the file as a whole is Python 2 and does not parse, the build body does -- and writes the
@@ -16,11 +17,12 @@ import sys
 
 REF = "/root/reference/train_dense_hier_networks.py"
 REF_HIER = "/root/reference/train_hier_networks.py"   # hier_model_struct.build (338-530), same vocabulary
+REF_DENSE = "/root/reference/train_dense_networks.py"  # dense_model_struct.build (223-408)
 
 
 def _src_build(path=REF):
     lines = open(path).read().split("\n")
-    start = next(i for i, l in enumerate(lines) if l.strip().startswith("def build(self,depth,output_shape,P_shape"))
+    start = next(i for i, l in enumerate(lines) if l.strip().startswith("def build(self,depth,output_shape"))
     end = next(i for i in range(start + 1, len(lines)) if lines[i].strip().startswith("def "))
     body = "\n".join(l[4:] if l.startswith("    ") else l for l in lines[start:end])
     return ast.parse(body).body[0], start + 1
