@@ -461,6 +461,7 @@ void launch_kern(mp_ctx* c, G& g, G::Kern& k, hipStream_t st) {
   switch (k.kind) {
     case MP_OP_CONV: {
       ProfScope ps(c, st, "graph_conv");
+      ProfScope pl(c, st, g.ops[k.op].name.c_str());   // per layer, read back by its scope name
       hip_check(k.L->x3 ? launch_igemm_x3(k.ia, k.L->w.p, k.L->wus, st) : launch_igemm_conv(k.ia, st),
                 g.ops[k.op].name.c_str());
       break;
@@ -475,6 +476,7 @@ void launch_kern(mp_ctx* c, G& g, G::Kern& k, hipStream_t st) {
     }
     default: {
       ProfScope ps(c, st, "graph_fc");
+      ProfScope pl(c, st, g.ops[k.op].name.c_str());
       const auto& L = *k.L;
       const int M = (int)g.pn;
       hip_check(L.x3 ? launch_fc_gemm_x3(k.fa, k.fK, L.w.p, L.wus, k.part.f(), M, k.fK, k.fN, k.fS, k.fks, st)
