@@ -91,3 +91,37 @@ def test_auto_dtype_resolution():
     assert r('auto', 96, 96) == 'fp32_split' and r('auto', 50, 50) == 'fp32'
     assert r('fp32', 64, 64) == 'fp32'
     assert mp.hgru_pose.model().compute_dtype == 'auto'
+
+
+@pytest.mark.gpu
+def test_plain_c_client_matches_python(tmp_path):
+    """tools/abi_demo.c (built by build() next to the .so) drives the ABI from C with hipMalloc'd
+    buffers and no torch; its output equals the ctypes façade's bit for bit."""
+    import subprocess
+    torch = pytest.importorskip("torch")
+    P = pkg()
+    W = P.weights
+    demo = os.path.join(os.path.dirname(P._lib.LIB_PATH), "abi_demo")
+    assert os.path.exists(demo), "abi_demo not built (run __graft_entry__.build())"
+    n, crop = 2, 64
+    table = W.hgru_pose_vars(output_shape=69, timesteps=8, crop=crop)
+    wts = {v.name: W.synth_value(v, 1234, 8) for v in table}
+    depth = W.synth_crops(n, seed=42, size=crop)
+    o0 = W.synth_hidden((n, crop // 2, crop // 2, 64), seed=7)
+    with open(tmp_path / "manifest.txt", "w") as f:
+        f.write(f"{n} {crop} {crop} 69 {P._lib.MP_DTYPE_F32_FFT}\n")
+        for v in table:
+            f.write(f"{v.name} {len(v.shape)} {' '.join(str(d) for d in v.shape)}\n")
+    with open(tmp_path / "weights.bin", "wb") as f:
+        for v in table:
+            f.write(np.ascontiguousarray(wts[v.name], np.float32).tobytes())
+    depth.astype(np.float32).tofile(tmp_path / "depth.bin")
+    o0.astype(np.float32).tofile(tmp_path / "o0.bin")
+    r = subprocess.run([demo, str(tmp_path)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    got = np.fromfile(tmp_path / "out.bin", np.float32).reshape(n, 69)
+    m = P.hgru_pose.model()
+    m.load_weights(wts)
+    m.compute_dtype = "fp32_fft"
+    ref = m.build(torch.from_numpy(depth).cuda(), 69, h2_init=torch.from_numpy(o0).cuda()).cpu().numpy()
+    assert np.array_equal(got, ref)
