@@ -70,6 +70,10 @@ struct GraphState {
     float* fout = nullptr;
     mpr::DevBuf part;
     const mp_ctx::PackedLayer* L = nullptr;
+    // fused 1-channel 3x3 conv + relu + 2x2 max pool (KIND_CONV1_POOL)
+    const float *cw = nullptr, *cb = nullptr;
+    int cH = 0, cW = 0;
+    mpr::DevBuf ones, zeros;
   };
   int64_t pn = 0, ph = 0, pw = 0;
   bool planned = false;
@@ -153,6 +157,11 @@ struct UF {
 };
 
 using G = GraphState;
+
+// internal kernel kind: conv (1 -> 64 channels, 3x3, stride 1) + relu + 2x2 max pool in one pass,
+// for a conv whose only consumer is that pool (hier conv_1 -> pool_1): the pre-pool map is never
+// written (the hGRU backbone's conv_1 kernel, NHWC out, unit affine)
+constexpr int KIND_CONV1_POOL = 100;
 
 void plan(mp_ctx* c, G& g, int64_t n, int64_t h, int64_t w) {
   g.drop_exec();
@@ -299,10 +308,53 @@ void plan(mp_ctx* c, G& g, int64_t n, int64_t h, int64_t w) {
     x = root(x);
     return x == 0 ? 0 : T[x].off;
   };
+  // conv_1 + pool fusion candidates: conv index -> pool index
+  std::vector<int> fused_pool(g.ops.size(), -1);
+  std::vector<char> fused_away(g.ops.size(), 0);
+  if (env_int("MP_GRAPH_FUSE", 1))
+    for (size_t i = 0; i < g.ops.size(); ++i) {
+      const auto& op = g.ops[i];
+      if (op.kind != MP_OP_CONV || op.ksize != 3 || op.stride != 1 || op.cout != 64) continue;
+      const int s = op.src[0];
+      if (root(s) != s || T[s].C != 1 || T[s].H % 2 || T[s].W % 2 || ld(s) != 1 || coff(s) != 0) continue;
+      if (uses[op.out] != 1) continue;
+      for (size_t j = i + 1; j < g.ops.size(); ++j) {
+        const auto& pj = g.ops[j];
+        if (pj.kind == MP_OP_MAXPOOL && pj.ksize == 2 && pj.src[0] == op.out && root(pj.out) == pj.out &&
+            ld(pj.out) == 64 && coff(pj.out) == 0) {
+          fused_pool[i] = (int)j;
+          fused_away[j] = 1;
+          // the pre-pool map is never materialised: drop its (singleton) buffer
+          g.groups[T[op.out].group]->buf.release();
+        }
+      }
+    }
   // kernels and their producers
   for (size_t i = 0; i < g.ops.size(); ++i) {
     const auto& op = g.ops[i];
     auto& o = T[op.out];
+    if (fused_away[i]) continue;   // produced by its conv's fused kernel (below)
+    if (fused_pool[i] >= 0) {
+      const auto& pj = g.ops[fused_pool[i]];
+      auto k = std::make_unique<G::Kern>();
+      k->op = (int)i;
+      k->kind = KIND_CONV1_POOL;
+      const auto& L = c->layers.at(op.name);
+      if (L.cin != 1 || L.cout != 64 || L.k != 3) fail(MP_ERR_SHAPE, "conv " + op.name + ": weights mismatch");
+      k->L = &L;
+      k->px = base(op.src[0]);
+      k->cH = T[op.src[0]].H;
+      k->cW = T[op.src[0]].W;
+      k->cw = c->raw.at(op.name + "/" + op.name + "_filters").dev->f();
+      k->cb = L.b.f();
+      k->pout = base(pj.out);
+      std::vector<float> one(64, 1.f), zero(64, 0.f);
+      upload(k->ones, one);
+      upload(k->zeros, zero);
+      T[pj.out].prod = {(int)g.kerns.size()};
+      g.kerns.push_back(std::move(k));
+      continue;
+    }
     if (op.kind == MP_OP_CONCAT) {
       for (int s : op.src) {
         const auto& p = T[root(s)].prod;
@@ -459,6 +511,14 @@ void plan(mp_ctx* c, G& g, int64_t n, int64_t h, int64_t w) {
 
 void launch_kern(mp_ctx* c, G& g, G::Kern& k, hipStream_t st) {
   switch (k.kind) {
+    case KIND_CONV1_POOL: {
+      ProfScope ps(c, st, "graph_conv");
+      ProfScope pl(c, st, g.ops[k.op].name.c_str());
+      hip_check(launch_conv1_pool_bn(k.px, k.cw, k.cb, k.ones.f(), k.zeros.f(), k.pout, (int)g.pn, k.cH, k.cW, st,
+                                     true),
+                g.ops[k.op].name.c_str());
+      break;
+    }
     case MP_OP_CONV: {
       ProfScope ps(c, st, "graph_conv");
       ProfScope pl(c, st, g.ops[k.op].name.c_str());   // per layer, read back by its scope name
