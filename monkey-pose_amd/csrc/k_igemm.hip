@@ -312,11 +312,45 @@ __global__ __launch_bounds__(256) void igemm_x3w_kernel(IgemmArgs p, const f16x8
     const int gm = m0 + (tid >> 3) + 32 * i;
     sok[i] = gm < M;
     const int g = sok[i] ? gm : 0;
-    sn[i] = g / HWo;
-    const int r = g - sn[i] * HWo;
+    int r;
+    if (p.pmajor) {
+      sn[i] = g % p.N;
+      r = g / p.N;
+    } else {
+      sn[i] = g / HWo;
+      r = g - sn[i] * HWo;
+    }
     sy[i] = (r / p.Wo) * p.stride - p.pad_t;
     sx[i] = (r % p.Wo) * p.stride - p.pad_l;
   }
+  // K steps: all of K, or (position-major tiles with Cin % IG_BK == 0) only the taps that are
+  // inside the image for at least one of the block's output positions -- ky x kx rectangles of
+  // whole IG_BK steps (a 5x5 conv on a 4x4 map keeps 9-16 of its 25 taps per position)
+  int ky_lo = 0, kx_lo = 0, nky = 1, kxsteps = (p.K + IG_BK - 1) / IG_BK;
+  const bool skip = p.pmajor && p.Cin % IG_BK == 0;
+  if (skip) {
+    const int p0 = m0 / p.N, p1 = (min(m0 + IG_BM, M) - 1) / p.N;
+    int y0 = 1 << 30, y1 = -1, x0 = 1 << 30, x1 = -1;
+    for (int q = p0; q <= p1; ++q) {
+      const int yy = q / p.Wo, xx = q % p.Wo;
+      y0 = min(y0, yy);
+      y1 = max(y1, yy);
+      x0 = min(x0, xx);
+      x1 = max(x1, xx);
+    }
+    ky_lo = max(0, p.pad_t - y1 * p.stride);
+    const int ky_hi = min(p.KS - 1, p.H - 1 + p.pad_t - y0 * p.stride);
+    kx_lo = max(0, p.pad_l - x1 * p.stride);
+    const int kx_hi = min(p.KS - 1, p.W - 1 + p.pad_l - x0 * p.stride);
+    nky = max(0, ky_hi - ky_lo + 1);
+    kxsteps = max(0, kx_hi - kx_lo + 1) * (p.Cin / IG_BK);
+  }
+  const int nsteps = nky * kxsteps;
+  auto kof = [&](int st) {   // k0 of K step st
+    if (!skip) return st * IG_BK;
+    const int r = st / kxsteps;
+    return ((ky_lo + r) * p.KS + kx_lo) * p.Cin + (st - r * kxsteps) * IG_BK;
+  };
   const int k4 = (tid & 7) * 4;
 
   auto load_act = [&](int k0, f32x4 (&v)[4]) {
@@ -366,10 +400,13 @@ __global__ __launch_bounds__(256) void igemm_x3w_kernel(IgemmArgs p, const f16x8
     for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = f32x16{};
   f32x4 av[4];
   f16x8 wnx[4];
-  load_act(0, av);
-  load_w(0, wnx);
+  if (nsteps > 0) {
+    load_act(kof(0), av);
+    load_w(kof(0), wnx);
+  }
   const bool wave_on = nb0 + 2 * wn < N32;   // wave-uniform
-  for (int k0 = 0; k0 < p.K; k0 += IG_BK) {
+  for (int st = 0; st < nsteps; ++st) {
+    const int k0 = kof(st);
     lds_barrier();   // the previous step's LDS reads are done
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -385,9 +422,9 @@ __global__ __launch_bounds__(256) void igemm_x3w_kernel(IgemmArgs p, const f16x8
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) Ws[tid + 256 * u] = wnx[u];
-    if (k0 + IG_BK < p.K) {   // prefetch the next step
-      load_act(k0 + IG_BK, av);
-      load_w(k0 + IG_BK, wnx);
+    if (st + 1 < nsteps) {   // prefetch the next step
+      load_act(kof(st + 1), av);
+      load_w(kof(st + 1), wnx);
     }
     lds_barrier();
     if (wave_on) {
@@ -421,7 +458,8 @@ __global__ __launch_bounds__(256) void igemm_x3w_kernel(IgemmArgs p, const f16x8
   for (int mb = 0; mb < 2; ++mb) {
     const int gm = m0 + (2 * wm + mb) * 32 + col;
     if (gm >= M) continue;
-    float* dst = p.out + (size_t)gm * p.ldo + p.coff;
+    const size_t pix = p.pmajor ? (size_t)(gm % p.N) * HWo + gm / p.N : (size_t)gm;   // NHWC pixel index
+    float* dst = p.out + pix * p.ldo + p.coff;
 #pragma unroll
     for (int nb = 0; nb < 2; ++nb) {
       const int cb = nb0 + 2 * wn + nb;
@@ -506,7 +544,14 @@ hipError_t launch_igemm_x3(const IgemmArgs& a, const void* wpk, float unscale, h
     return e ? std::atoi(e) : 1;
   }();
   if (wide && N32 >= 3) {   // Cout > 64: 2 x 2 wave tiles, weights staged in LDS
-    hipLaunchKernelGGL(igemm_x3w_kernel, dim3((M + IG_BM - 1) / IG_BM, (N32 + 3) / 4), dim3(256), 0, st, a, w,
+    static const int tapskip = [] {
+      const char* e = std::getenv("MP_IGEMM_TAPSKIP");
+      return e ? std::atoi(e) : 1;
+    }();
+    IgemmArgs b = a;
+    // small maps (<= 8 x 8) with padded taps: position-major tiles so padding taps can be skipped
+    b.pmajor = tapskip && a.KS > 1 && a.Ho * a.Wo <= 64 && a.Cin % IG_BK == 0 ? 1 : 0;
+    hipLaunchKernelGGL(igemm_x3w_kernel, dim3((M + IG_BM - 1) / IG_BM, (N32 + 3) / 4), dim3(256), 0, st, b, w,
                        unscale);
     return hipGetLastError();
   }

@@ -78,6 +78,8 @@ struct IgemmArgs {
   int ldo, coff, Cout;
   int Ho, Wo, KS, stride, pad_t, pad_l;
   int relu;
+  int pmajor;          // wide f16x3 kernel only: M ordered position-major (m = pos * N + n), each
+                       // block's K loop skips the taps that are padding for all of its positions
 };
 hipError_t launch_igemm_conv(const IgemmArgs& a, hipStream_t st);
 // f16x3 (fp32-accurate) variant; wpk packed by launch_pack_fc_x3 as a [K][Cout] matrix
