@@ -286,13 +286,12 @@ __global__ __launch_bounds__(256) void igemm_x3_kernel(IgemmArgs p, const f16x8*
   }
 }
 
-// Wide-N f16x3 implicit GEMM (Cout > 64): block = 128 output pixels x 128 output channels with the
-// four waves in a 2 x 2 grid, each wave 64 pixels x 64 channels (2 x 2 MFMA tiles).  The K step's
-// weight fragments (2 k16 x 4 cout blocks x hi|lo = 16 KiB) are staged in LDS once per block
-// instead of being loaded by every wave from L1 (4x fewer weight loads than igemm_x3_kernel, whose
-// waves each own 32 pixels x 128 channels), and every weight fragment read from LDS feeds two
-// pixel blocks.  Same operand split, packing, K pipeline and epilogue as igemm_x3_kernel.
-__global__ __launch_bounds__(256) void igemm_x3w_kernel(IgemmArgs p, const f16x8* __restrict__ wpk, float unscale) {
+// Position-major variant of igemm_x3w_kernel (below) for small maps with many padding taps (p.pmajor):
+// m = position * N + image, so a block's pixels share one (or a few) output positions and its K
+// loop visits only the taps inside the image for them.  Separate from igemm_x3w_kernel: the extra
+// index arithmetic costs the row-major kernel 1.5-3 % (measured same-box A/B).
+constexpr bool PM = true;
+__global__ __launch_bounds__(256) void igemm_x3w_pm_kernel(IgemmArgs p, const f16x8* __restrict__ wpk, float unscale) {
   __shared__ _Float16 Ah[IG_BM * IGX_LD], Al[IG_BM * IGX_LD];
   __shared__ f16x8 Ws[2 * 4 * 2 * 64];   // [k16 g][cout block nb][part][lane]
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, col = lane & 31;
@@ -313,7 +312,7 @@ __global__ __launch_bounds__(256) void igemm_x3w_kernel(IgemmArgs p, const f16x8
     sok[i] = gm < M;
     const int g = sok[i] ? gm : 0;
     int r;
-    if (p.pmajor) {
+    if (PM) {
       sn[i] = g % p.N;
       r = g / p.N;
     } else {
@@ -327,7 +326,7 @@ __global__ __launch_bounds__(256) void igemm_x3w_kernel(IgemmArgs p, const f16x8
   // inside the image for at least one of the block's output positions -- ky x kx rectangles of
   // whole IG_BK steps (a 5x5 conv on a 4x4 map keeps 9-16 of its 25 taps per position)
   int ky_lo = 0, kx_lo = 0, nky = 1, kxsteps = (p.K + IG_BK - 1) / IG_BK;
-  const bool skip = p.pmajor && p.Cin % IG_BK == 0;
+  const bool skip = PM;   // the launcher sets PM only with Cin % IG_BK == 0
   if (skip) {
     const int p0 = m0 / p.N, p1 = (min(m0 + IG_BM, M) - 1) / p.N;
     int y0 = 1 << 30, y1 = -1, x0 = 1 << 30, x1 = -1;
@@ -458,8 +457,169 @@ __global__ __launch_bounds__(256) void igemm_x3w_kernel(IgemmArgs p, const f16x8
   for (int mb = 0; mb < 2; ++mb) {
     const int gm = m0 + (2 * wm + mb) * 32 + col;
     if (gm >= M) continue;
-    const size_t pix = p.pmajor ? (size_t)(gm % p.N) * HWo + gm / p.N : (size_t)gm;   // NHWC pixel index
+    const size_t pix = PM ? (size_t)(gm % p.N) * HWo + gm / p.N : (size_t)gm;   // NHWC pixel index
     float* dst = p.out + pix * p.ldo + p.coff;
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      const int cb = nb0 + 2 * wn + nb;
+      if (cb >= N32) break;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int c = cb * 32 + 8 * g + 4 * h;
+        f32x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float v = acc[mb][nb][4 * g + j] * unscale + (c + j < p.Cout ? p.bias[c + j] : 0.f);
+          o[j] = p.relu ? fmaxf(v, 0.f) : v;
+        }
+        if (vst) {
+          if (c < p.Cout) *reinterpret_cast<f32x4*>(dst + c) = o;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (c + j < p.Cout) dst[c + j] = o[j];
+        }
+      }
+    }
+  }
+}
+
+// Wide-N f16x3 implicit GEMM (Cout > 64): block = 128 output pixels x 128 output channels with the
+// four waves in a 2 x 2 grid, each wave 64 pixels x 64 channels (2 x 2 MFMA tiles).  The K step's
+// weight fragments (2 k16 x 4 cout blocks x hi|lo = 16 KiB) are staged in LDS once per block
+// instead of being loaded by every wave from L1 (4x fewer weight loads than igemm_x3_kernel, whose
+// waves each own 32 pixels x 128 channels), and every weight fragment read from LDS feeds two
+// pixel blocks.  Same operand split, packing, K pipeline and epilogue as igemm_x3_kernel.
+__global__ __launch_bounds__(256) void igemm_x3w_kernel(IgemmArgs p, const f16x8* __restrict__ wpk, float unscale) {
+  __shared__ _Float16 Ah[IG_BM * IGX_LD], Al[IG_BM * IGX_LD];
+  __shared__ f16x8 Ws[2 * 4 * 2 * 64];   // [k16 g][cout block nb][part][lane]
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, col = lane & 31;
+  const int wm = wv & 1, wn = wv >> 1;   // this wave: pixels 64 wm .. +63, cout blocks 2 wn, 2 wn + 1
+  const int HWo = p.Ho * p.Wo;
+  const int M = p.N * HWo;
+  const int m0 = blockIdx.x * IG_BM;
+  const int nb0 = blockIdx.y * 4;
+  const int N32 = (p.Cout + 31) / 32;
+  const int K16 = (p.K + 15) / 16;
+  const bool vec = (p.Cin % 4 == 0) && (p.cix % 4 == 0) && (p.ldx % 4 == 0);
+
+  int sn[4], sy[4], sx[4];
+  bool sok[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    const int gm = m0 + (tid >> 3) + 32 * i;
+    sok[i] = gm < M;
+    const int g = sok[i] ? gm : 0;
+    sn[i] = g / HWo;
+    const int r = g - sn[i] * HWo;
+    sy[i] = (r / p.Wo) * p.stride - p.pad_t;
+    sx[i] = (r % p.Wo) * p.stride - p.pad_l;
+  }
+  const int k4 = (tid & 7) * 4;
+
+  auto load_act = [&](int k0, f32x4 (&v)[4]) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int kk = k0 + k4;
+      if (vec) {
+        const int kc = min(kk, p.K - 4);
+        const int tap = kc / p.Cin, ci = kc - tap * p.Cin;
+        const int iy = sy[i] + tap / p.KS, ix = sx[i] + tap % p.KS;
+        const bool ok = sok[i] && kk < p.K && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
+        const int cy = min(max(iy, 0), p.H - 1), cx = min(max(ix, 0), p.W - 1);
+        const f32x4 t =
+            *reinterpret_cast<const f32x4*>(p.x + (((size_t)sn[i] * p.H + cy) * p.W + cx) * p.ldx + p.cix + ci);
+        v[i] = ok ? t : f32x4{0.f, 0.f, 0.f, 0.f};
+      } else {
+#pragma unroll
+        for (int s = 0; s < 4; ++s) {
+          const int k = kk + s;
+          const int kc = min(k, p.K - 1);
+          const int tap = kc / p.Cin, ci = kc - tap * p.Cin;
+          const int iy = sy[i] + tap / p.KS, ix = sx[i] + tap % p.KS;
+          const bool ok = sok[i] && k < p.K && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
+          const int cy = min(max(iy, 0), p.H - 1), cx = min(max(ix, 0), p.W - 1);
+          const float t = p.x[(((size_t)sn[i] * p.H + cy) * p.W + cx) * p.ldx + p.cix + ci];
+          v[i][s] = ok ? t : 0.f;
+        }
+      }
+    }
+  };
+  // this thread's 4 of the step's 1,024 weight fragments (16 KiB; slot e = tid + 256 u of
+  // [g][nb][part][lane]); cout blocks past N32 and k16 past K16 are clamped (their products are
+  // never stored / multiply zero activations)
+  auto load_w = [&](int k0, f16x8 (&w)[4]) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = tid + 256 * u, l = e & 63, part = (e >> 6) & 1, nb = (e >> 7) & 3, g = e >> 9;
+      const int kb = min((k0 >> 4) + g, K16 - 1), nbc = min(nb0 + nb, N32 - 1);
+      w[u] = wpk[(((size_t)kb * N32 + nbc) * 2 + part) * 64 + l];
+    }
+  };
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = f32x16{};
+  f32x4 av[4];
+  f16x8 wnx[4];
+  load_act(0, av);
+  load_w(0, wnx);
+  const bool wave_on = nb0 + 2 * wn < N32;   // wave-uniform
+  for (int k0 = 0; k0 < p.K; k0 += IG_BK) {
+    lds_barrier();   // the previous step's LDS reads are done
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = (tid >> 3) + 32 * i;
+      f16x4 hv, lv;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        hv[s] = (_Float16)av[i][s];
+        lv[s] = (_Float16)(av[i][s] - (float)hv[s]);
+      }
+      *reinterpret_cast<f16x4*>(Ah + row * IGX_LD + k4) = hv;
+      *reinterpret_cast<f16x4*>(Al + row * IGX_LD + k4) = lv;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) Ws[tid + 256 * u] = wnx[u];
+    if (k0 + IG_BK < p.K) {   // prefetch the next step
+      load_act(k0 + IG_BK, av);
+      load_w(k0 + IG_BK, wnx);
+    }
+    lds_barrier();
+    if (wave_on) {
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        if ((k0 >> 4) + g >= K16) break;   // block-uniform
+        f16x8 ah[2], al[2];
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb) {
+          const int o = ((2 * wm + mb) * 32 + col) * IGX_LD + 16 * g + 8 * h;
+          ah[mb] = *reinterpret_cast<const f16x8*>(Ah + o);
+          al[mb] = *reinterpret_cast<const f16x8*>(Al + o);
+        }
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) {
+          const f16x8 wh = Ws[((g * 4 + 2 * wn + nb) * 2 + 0) * 64 + lane];
+          const f16x8 wl = Ws[((g * 4 + 2 * wn + nb) * 2 + 1) * 64 + lane];
+#pragma unroll
+          for (int mb = 0; mb < 2; ++mb) {
+            acc[mb][nb] = mfma16(wl, ah[mb], acc[mb][nb]);
+            acc[mb][nb] = mfma16(wh, al[mb], acc[mb][nb]);
+            acc[mb][nb] = mfma16(wh, ah[mb], acc[mb][nb]);
+          }
+        }
+      }
+    }
+  }
+  if (!wave_on) return;
+  const bool vst = (p.ldo % 4 == 0) && (p.coff % 4 == 0) && (p.Cout % 4 == 0);
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb) {
+    const int gm = m0 + (2 * wm + mb) * 32 + col;
+    if (gm >= M) continue;
+    float* dst = p.out + (size_t)gm * p.ldo + p.coff;
 #pragma unroll
     for (int nb = 0; nb < 2; ++nb) {
       const int cb = nb0 + 2 * wn + nb;
@@ -549,10 +709,27 @@ hipError_t launch_igemm_x3(const IgemmArgs& a, const void* wpk, float unscale, h
       return e ? std::atoi(e) : 1;
     }();
     IgemmArgs b = a;
-    // small maps (<= 8 x 8) with padded taps: position-major tiles so padding taps can be skipped
-    b.pmajor = tapskip && a.KS > 1 && a.Ho * a.Wo <= 64 && a.Cin % IG_BK == 0 ? 1 : 0;
-    hipLaunchKernelGGL(igemm_x3w_kernel, dim3((M + IG_BM - 1) / IG_BM, (N32 + 3) / 4), dim3(256), 0, st, b, w,
-                       unscale);
+    // small maps (<= 8 x 8) where at least 40 % of the im2col taps are padding: position-major
+    // tiles so the padding taps can be skipped (measured: a 5x5 conv on 4x4 maps, 51 % padding,
+    // 1.4x faster; on 8x8 maps, 28 % padding, slower -- a position-major tile gathers 128 images'
+    // pixels and loses the neighbouring-pixel input reuse of a row-major tile)
+    b.pmajor = 0;
+    if (tapskip && a.KS > 1 && a.Ho * a.Wo <= 64 && a.Cin % IG_BK == 0) {
+      long valid = 0;
+      for (int y = 0; y < a.Ho; ++y)
+        for (int x = 0; x < a.Wo; ++x)
+          for (int ky = 0; ky < a.KS; ++ky)
+            for (int kx = 0; kx < a.KS; ++kx) {
+              const int iy = y * a.stride - a.pad_t + ky, ix = x * a.stride - a.pad_l + kx;
+              valid += iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+            }
+      b.pmajor = valid * 10 <= 6L * a.Ho * a.Wo * a.KS * a.KS ? 1 : 0;
+    }
+    const dim3 grid((M + IG_BM - 1) / IG_BM, (N32 + 3) / 4);
+    if (b.pmajor)
+      hipLaunchKernelGGL(igemm_x3w_pm_kernel, grid, dim3(256), 0, st, b, w, unscale);
+    else
+      hipLaunchKernelGGL(igemm_x3w_kernel, grid, dim3(256), 0, st, b, w, unscale);
     return hipGetLastError();
   }
   if (nb == 4)
