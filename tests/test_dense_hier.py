@@ -204,3 +204,47 @@ def test_graph_runtime_small_graph():
         assert rel_inf(o.cpu().numpy(), want) < 1e-5
         assert rel_inf(oc.cpu().numpy(), np.concatenate([ra, rb], -1)) < 1e-5
         assert ctx.info("graph_buffers") == 4    # groups: {a, b, c}, p, {f1, f2, cat}, out
+
+
+@pytest.mark.gpu
+def test_graph_runtime_rejects_unsupported_graphs():
+    """Planning errors surface as MonkeyPoseError before any launch: a tensor needed at two different
+    channel offsets (concat placement conflict), a relu on an fc output that has another consumer,
+    and an unknown layer scope at finalize."""
+    torch = pytest.importorskip("torch")
+    mp = pkg()
+    G, L = mp._graph, mp._lib
+    rng = np.random.default_rng(1)
+
+    def ctx_for(g, outs, wts):
+        ctx = L.Context(L.MP_MODEL_GRAPH, 0)
+        G.install(ctx, g, outs)
+        for k, v in wts.items():
+            ctx.set_weight(k, v.astype(np.float32))
+        ctx.finalize(L.MP_DTYPE_F32_SPLIT)
+        return ctx
+
+    conv_w = {"a/a_filters": rng.standard_normal((3, 3, 1, 8)), "a/a_biases": np.zeros(8),
+              "b/b_filters": rng.standard_normal((3, 3, 1, 8)), "b/b_biases": np.zeros(8)}
+    x = torch.zeros((1, 8, 8, 1), device="cuda")
+    # a sits at offset 0 of cat(a, b) and at offset 8 of cat(b, a)
+    g = G.GraphRecorder(8, 8, 1)
+    a = g.conv(g.input, 1, 8, "a")
+    b = g.conv(g.input, 1, 8, "b")
+    c1, c2 = g.concat([a, b]), g.concat([b, a])
+    ctx = ctx_for(g, [c1, c2], conv_w)
+    with pytest.raises(L.MonkeyPoseError, match="placement conflict"):
+        ctx.graph_fwd(x, [torch.empty((1, 8, 8, 16), device="cuda")] * 2, L.current_stream())
+    # relu of an fc output that is also a graph output
+    g = G.GraphRecorder(8, 8, 1)
+    f = g.fc(g.conv(g.input, 1, 8, "a"), 512, 4, "f")
+    r = g.relu(f)
+    wts = dict(conv_w, **{"f/f_weights": rng.standard_normal((512, 4)), "f/f_biases": np.zeros(4)})
+    ctx = ctx_for(g, [r, f], wts)
+    with pytest.raises(L.MonkeyPoseError, match="relu"):
+        ctx.graph_fwd(x, [torch.empty((1, 4), device="cuda")] * 2, L.current_stream())
+    # a layer whose weights were never set
+    g = G.GraphRecorder(8, 8, 1)
+    z = g.conv(g.input, 1, 8, "zz")
+    with pytest.raises(L.MonkeyPoseError, match="weight not set"):
+        ctx_for(g, [z], {})
