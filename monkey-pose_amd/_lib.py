@@ -14,7 +14,7 @@ from typing import Optional
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libmonkeypose.so")
+LIB_PATH = os.environ.get("MP_LIB_PATH") or os.path.join(_HERE, "libmonkeypose.so")
 
 MP_OK = 0
 MP_MODEL_HGRU_POSE = 1

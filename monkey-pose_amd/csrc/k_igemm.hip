@@ -14,6 +14,9 @@
 #include "mp_kernels.hpp"
 
 #include <cstdlib>
+#ifndef HX_EXP
+#define HX_EXP 0
+#endif
 
 namespace mp {
 
@@ -645,6 +648,187 @@ __global__ __launch_bounds__(256) void igemm_x3w_kernel(IgemmArgs p, const f16x8
   }
 }
 
+// Halo-tiled f16x3 convolution (stride 1, odd KS, SAME, Cin % 32 == 0, Cout > 64): the im2col
+// kernels above gather, split and stage every input element once per tap (9x for 3x3); here a
+// block's 128 output pixels are whole rows (NI images x R rows x W cols, 128 % W == 0) and the
+// input rows they need, with their halo, are staged once per 32-channel chunk as split f16
+// (pixel pitch 144 B: [hi 32][lo 32][pad], conflict-free b128 reads for a row of 32 pixels), so
+// each element is converted ~1.4-2x instead of KS^2 times.  All KS^2 taps of a chunk then read
+// their fragments from the same LDS image at a per-tap offset.  Double-buffered: chunk c+1's loads
+// are in flight during chunk c's MFMAs and are written to the other buffer after them (one barrier
+// per chunk).  Weight fragments come straight from L2 / L1 (packed [k/16][n/32][hi|lo][lane], each
+// wave-load one contiguous KiB), one tap ahead.  Waves: 2 x 2 grid of 64 pixels x 64 couts.
+constexpr int HX_PITCH = 72;   // f16 per staged pixel
+constexpr int HX_ITEMS = 9;    // f32x4 halo items per thread per chunk (<= 2304 = 288 pixels)
+
+struct HaloGeom {
+  int R, NI, HH, WW, PH;   // rows per tile, images per tile, halo rows / cols per image, halo pixels
+};
+
+template <int KS>
+__global__ __launch_bounds__(256, 2) void igemm_x3h_kernel(IgemmArgs p, HaloGeom hg, const f16x8* __restrict__ wpk,
+                                                          float unscale) {
+  extern __shared__ _Float16 hs[];   // [2][PH][HX_PITCH]
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, col = lane & 31;
+  const int wm = wv & 1, wn = wv >> 1;
+  const int HW = p.H * p.W;
+  const int M = p.N * HW;
+  const int m0 = blockIdx.x * IG_BM;
+  const int nb0 = blockIdx.y * 4;
+  const int N32 = (p.Cout + 31) / 32;
+  const int pad = KS / 2;
+  const int n0 = m0 / HW, y0 = (m0 - n0 * HW) / p.W;   // first image / row of the tile
+  const int nchunk = p.Cin / 32;
+  const int bufsz = hg.PH * HX_PITCH;
+
+  // halo staging: item e = (halo pixel e / 8, channel quad e % 8)
+  auto load_halo = [&](int c, f32x4 (&v)[HX_ITEMS]) {
+#pragma unroll
+    for (int u = 0; u < HX_ITEMS; ++u) {
+      const int e = tid + 256 * u;
+      const int hp = e >> 3, q = e & 7;
+      const int i = hp / (hg.HH * hg.WW), r = hp - i * hg.HH * hg.WW;
+      const int hy = r / hg.WW, hx = r - hy * hg.WW;
+      const int n = n0 + i, y = y0 + hy - pad, x = hx - pad;
+      const bool ok = hp < hg.PH && n < p.N && y >= 0 && y < p.H && x >= 0 && x < p.W;
+      const int cn = min(n, p.N - 1), cy = min(max(y, 0), p.H - 1), cx = min(max(x, 0), p.W - 1);
+      const f32x4 t = *reinterpret_cast<const f32x4*>(p.x + (((size_t)cn * p.H + cy) * p.W + cx) * p.ldx + p.cix +
+                                                      c * 32 + 4 * q);
+      v[u] = ok ? t : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto store_halo = [&](int buf, const f32x4 (&v)[HX_ITEMS]) {
+#pragma unroll
+    for (int u = 0; u < HX_ITEMS; ++u) {
+      const int e = tid + 256 * u;
+      const int hp = e >> 3, q = e & 7;
+      if (hp >= hg.PH) continue;
+      f16x4 hv, lv;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        hv[s] = (_Float16)v[u][s];
+        lv[s] = (_Float16)(v[u][s] - (float)hv[s]);
+      }
+      _Float16* d = hs + buf * bufsz + hp * HX_PITCH + 4 * q;
+      *reinterpret_cast<f16x4*>(d) = hv;
+      *reinterpret_cast<f16x4*>(d + 32) = lv;
+    }
+  };
+  // this wave's weight fragments of (chunk c, tap t): [g][nb][hi|lo]
+  auto load_w = [&](int c, int t, f16x8 (&w)[2][2][2]) {
+#pragma unroll
+    for (int g = 0; g < 2; ++g)
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) {
+        const int kb = (t * p.Cin + c * 32) / 16 + g, nbc = min(nb0 + 2 * wn + nb, N32 - 1);
+        const f16x8* src = wpk + ((size_t)kb * N32 + nbc) * 2 * 64 + lane;
+        w[g][nb][0] = src[0];
+        w[g][nb][1] = src[64];
+      }
+  };
+
+  // halo offset (in f16) of this lane's output pixel in each of its two 32-pixel blocks
+  int pbase[2];
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb) {
+    const int pp = (2 * wm + mb) * 32 + col;
+    const int i = pp / (hg.R * p.W), r = (pp / p.W) % hg.R, x = pp % p.W;
+    pbase[mb] = ((i * hg.HH + r) * hg.WW + x) * HX_PITCH + 8 * h;
+  }
+
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = f32x16{};
+  const bool wave_on = nb0 + 2 * wn < N32;   // wave-uniform
+
+  f32x4 hv[HX_ITEMS];
+  load_halo(0, hv);
+  store_halo(0, hv);
+  f16x8 wc[2][2][2], wnx[2][2][2];
+  load_w(0, 0, wnx);
+  lds_barrier();
+  for (int c = 0; c < nchunk; ++c) {
+    if (c + 1 < nchunk) load_halo(c + 1, hv);
+    const _Float16* hb = hs + (c & 1) * bufsz;
+#pragma unroll
+    for (int t = 0; t < KS * KS; ++t) {
+#pragma unroll
+      for (int g = 0; g < 2; ++g)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) {
+          wc[g][nb][0] = wnx[g][nb][0];
+          wc[g][nb][1] = wnx[g][nb][1];
+        }
+#if HX_EXP != 1
+      if (t + 1 < KS * KS)
+        load_w(c, t + 1, wnx);
+      else if (c + 1 < nchunk)
+        load_w(c + 1, 0, wnx);
+#endif
+      const int toff = ((t / KS) * hg.WW + t % KS) * HX_PITCH;
+      if (wave_on) {
+#pragma unroll
+        for (int g = 0; g < 2; ++g) {
+          f16x8 ah[2], al[2];
+#pragma unroll
+          for (int mb = 0; mb < 2; ++mb) {
+            ah[mb] = *reinterpret_cast<const f16x8*>(hb + pbase[mb] + toff + 16 * g);
+            al[mb] = *reinterpret_cast<const f16x8*>(hb + pbase[mb] + toff + 32 + 16 * g);
+          }
+#pragma unroll
+          for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+            for (int mb = 0; mb < 2; ++mb) {
+#if HX_EXP == 2
+              acc[mb][nb][0] += (float)wc[g][nb][1][0] * (float)ah[mb][1] + (float)wc[g][nb][0][2] * (float)al[mb][3];
+#else
+              acc[mb][nb] = mfma16(wc[g][nb][1], ah[mb], acc[mb][nb]);
+              acc[mb][nb] = mfma16(wc[g][nb][0], al[mb], acc[mb][nb]);
+              acc[mb][nb] = mfma16(wc[g][nb][0], ah[mb], acc[mb][nb]);
+#endif
+            }
+        }
+      }
+    }
+    if (c + 1 < nchunk) {
+      store_halo((c + 1) & 1, hv);   // that buffer was last read in chunk c - 1, before the last barrier
+      lds_barrier();
+    }
+  }
+  if (!wave_on) return;
+  const bool vst = (p.ldo % 4 == 0) && (p.coff % 4 == 0) && (p.Cout % 4 == 0);
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb) {
+    const int gm = m0 + (2 * wm + mb) * 32 + col;
+    if (gm >= M) continue;
+    float* dst = p.out + (size_t)gm * p.ldo + p.coff;
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      const int cb = nb0 + 2 * wn + nb;
+      if (cb >= N32) break;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int c = cb * 32 + 8 * g + 4 * h;
+        f32x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float v = acc[mb][nb][4 * g + j] * unscale + (c + j < p.Cout ? p.bias[c + j] : 0.f);
+          o[j] = p.relu ? fmaxf(v, 0.f) : v;
+        }
+        if (vst) {
+          if (c < p.Cout) *reinterpret_cast<f32x4*>(dst + c) = o;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (c + j < p.Cout) dst[c + j] = o[j];
+        }
+      }
+    }
+  }
+}
+
 // 2x2 / stride 2, TF SAME (odd sizes pad one row/column after; max ignores it, avg divides by the
 // in-image count), optionally followed by a per-channel affine (a folded inference BN).  One
 // thread per output element; C innermost for coalescing.
@@ -708,6 +892,48 @@ hipError_t launch_igemm_x3(const IgemmArgs& a, const void* wpk, float unscale, h
       const char* e = std::getenv("MP_IGEMM_TAPSKIP");
       return e ? std::atoi(e) : 1;
     }();
+    static const int halo = [] {
+      const char* e = std::getenv("MP_IGEMM_HALO");
+      return e ? std::atoi(e) : 1;
+    }();
+    // halo tiles: stride 1, SAME, odd KS in {3, 5}, Cin % 32 == 0, tiles of whole rows of one
+    // image (or whole images), halo within HX_ITEMS per thread and two buffers within 80 KiB
+    if (halo && a.stride == 1 && (a.KS == 3 || a.KS == 5) && a.pad_t == a.KS / 2 && a.pad_l == a.KS / 2 &&
+        a.Ho == a.H && a.Wo == a.W && a.Cin % 32 == 0 && a.ldx % 4 == 0 && a.cix % 4 == 0 && a.W <= IG_BM &&
+        IG_BM % a.W == 0) {
+      HaloGeom hg;
+      const int HW = a.H * a.W;
+      bool ok = true;
+      if (HW >= IG_BM) {
+        hg.NI = 1;
+        hg.R = IG_BM / a.W;
+        ok = a.H % hg.R == 0;
+      } else {
+        hg.NI = IG_BM / HW;
+        hg.R = a.H;
+        ok = IG_BM % HW == 0;
+      }
+      hg.HH = hg.R + a.KS - 1;
+      hg.WW = a.W + a.KS - 1;
+      hg.PH = hg.NI * hg.HH * hg.WW;
+      const size_t lds = 2 * (size_t)hg.PH * HX_PITCH * sizeof(_Float16);
+      if (ok && hg.PH * 8 <= 256 * HX_ITEMS && lds <= 80 * 1024) {
+        static const bool attr = [] {
+          (void)hipFuncSetAttribute(reinterpret_cast<const void*>(igemm_x3h_kernel<3>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+          (void)hipFuncSetAttribute(reinterpret_cast<const void*>(igemm_x3h_kernel<5>),
+                                    hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+          return true;
+        }();
+        (void)attr;
+        const dim3 grid((M + IG_BM - 1) / IG_BM, (N32 + 3) / 4);
+        if (a.KS == 3)
+          hipLaunchKernelGGL(igemm_x3h_kernel<3>, grid, dim3(256), lds, st, a, hg, w, unscale);
+        else
+          hipLaunchKernelGGL(igemm_x3h_kernel<5>, grid, dim3(256), lds, st, a, hg, w, unscale);
+        return hipGetLastError();
+      }
+    }
     IgemmArgs b = a;
     // small maps (<= 8 x 8) where at least 40 % of the im2col taps are padding: position-major
     // tiles so the padding taps can be skipped (measured: a 5x5 conv on 4x4 maps, 51 % padding,

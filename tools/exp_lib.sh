@@ -1,0 +1,10 @@
+#!/bin/bash
+# build an A/B variant of libmonkeypose.so: one source recompiled with extra flags, linked with the
+# in-tree objects.  usage: tools/exp_lib.sh <source.hip> <out.so> <flags...>   (load it with MP_LIB_PATH)
+set -e
+cd "$(dirname "$0")/../monkey-pose_amd/csrc"
+src=$1; out=$2; shift 2
+obj=/tmp/exp_$(basename "$out" .so).o
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result "$@" -c "$src" -o "$obj"
+objs=$(ls build/*.o | grep -v "build/${src%.hip}.o")
+/opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$out" $objs "$obj" -Wl,-rpath,/opt/rocm/lib
