@@ -32,6 +32,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <cstring>
 #include <vector>
 
@@ -70,6 +71,35 @@ struct cpx {
 };
 __device__ __forceinline__ cpx unpack_bf2(uint32_t u) {   // bf16 -> fp32 is exact: the high half
   return {__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)};
+}
+// hGRU state maps of the FFT path (O, I, Og and the B half-step's P2): fp32 C8, or -- BM, the
+// MP_DTYPE_BF16 default -- bf16 C8 at the same element index (half the bytes; round to nearest
+// even on store, exact on load).  The drive X (conv_3 output) and the final NHWC output stay fp32.
+template <bool BM>
+__device__ __forceinline__ f32x4 map_ld4(const float* base, size_t idx) {
+  if constexpr (BM) {
+    const uint2 u = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(base) + idx);
+    const cpx a = unpack_bf2(u.x), b = unpack_bf2(u.y);
+    return f32x4{a.x, a.y, b.x, b.y};
+  } else {
+    return *reinterpret_cast<const f32x4*>(base + idx);
+  }
+}
+template <bool BM>
+__device__ __forceinline__ void map_st4(float* base, size_t idx, f32x4 v) {
+  if constexpr (BM)
+    *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(base) + idx) = uint2{pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])};
+  else
+    *reinterpret_cast<f32x4*>(base + idx) = v;
+}
+template <bool BM>
+__device__ __forceinline__ cpx map_ld2(const float* base, size_t idx) {
+  if constexpr (BM) {
+    return unpack_bf2(*reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint16_t*>(base) + idx));
+  } else {
+    const float2 t = *reinterpret_cast<const float2*>(base + idx);
+    return {t.x, t.y};
+  }
 }
 __device__ __forceinline__ cpx operator+(cpx a, cpx b) { return {a.x + b.x, a.y + b.y}; }
 __device__ __forceinline__ cpx operator-(cpx a, cpx b) { return {a.x - b.x, a.y - b.y}; }
@@ -302,7 +332,7 @@ __device__ __forceinline__ int fft_block_cq(int blk) {
 // forward 2-D FFT of one C8 activation map -> S.  The rows are read straight into registers (64
 // independent 8-byte loads in flight per thread): staging the tile through LDS pixel-major measured
 // slower (0.24 vs 0.18 ms at B = 256) -- the load pass and its barrier serialise ahead of the FFT.
-template <bool BF>
+template <bool BF, bool BM>
 __global__ __launch_bounds__(192, 2) void fft_fwd_kernel(const float* __restrict__ src, void* __restrict__ S,
                                                       int H, int W) {
   __shared__ cpx T[FFT_LDS];
@@ -312,16 +342,35 @@ __global__ __launch_bounds__(192, 2) void fft_fwd_kernel(const float* __restrict
   if (tid < 128) {
     const int y = tid >> 1, p = tid & 1;
     cpx v[72];
-    const float* row = src + c8_index(b, q, y < H ? y : 0, 0, e0 + 2 * p, H, W);
+    // lane p of the row's lane pair loads all 4 channels of pixel 2k + p (one 16-byte fp32 / 8-byte
+    // bf16 load; the pair reads one contiguous run), then the pair swaps the channel pair the other
+    // lane transforms (DPP quad_perm [1,0,3,2]): half the load instructions of per-pair loads
+    const size_t row = c8_index(b, q, y < H ? y : 0, 0, e0, H, W);
 #pragma unroll
-    for (int x = 0; x < 72; ++x) {
-      if (x < 64 && y < H && x < W) {
-        const float2 t = *reinterpret_cast<const float2*>(row + 8 * x);
-        v[x] = {t.x, t.y};
+    for (int k = 0; k < 32; ++k) {
+      const int x = 2 * k + p;
+      const bool in = y < H && x < W;
+      cpx lo, hi;   // channels (e0, e0+1) and (e0+2, e0+3) of pixel x
+      if constexpr (BM) {
+        // unconditional (clamped) loads keep all 32 in flight; out-of-map pixels are zeroed after
+        uint2 u = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(src) + row + 8 * min(x, W - 1));
+        if (!in) u = uint2{0u, 0u};
+        lo = unpack_bf2(u.x);
+        hi = unpack_bf2(u.y);
       } else {
-        v[x] = {0.f, 0.f};
+        f32x4 u = *reinterpret_cast<const f32x4*>(src + row + 8 * min(x, W - 1));
+        if (!in) u = f32x4{0.f, 0.f, 0.f, 0.f};
+        lo = {u[0], u[1]};
+        hi = {u[2], u[3]};
       }
+      const cpx mine = p ? hi : lo, send = p ? lo : hi;
+      const cpx recv = {__int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(send.x), 0xB1, 0xF, 0xF, false)),
+                        __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(send.y), 0xB1, 0xF, 0xF, false))};
+      v[2 * k] = p ? recv : mine;
+      v[2 * k + 1] = p ? mine : recv;
     }
+#pragma unroll
+    for (int x = 64; x < 72; ++x) v[x] = {0.f, 0.f};
     fwd_rows_to_T(v, y, p, T);
   }
   lds_barrier();
@@ -329,7 +378,7 @@ __global__ __launch_bounds__(192, 2) void fft_fwd_kernel(const float* __restrict
 }
 
 // inverse 2-D FFT of Y -> the spatial conv result P (C8)
-template <bool BF>
+template <bool BF, bool BM>
 __global__ __launch_bounds__(192, 2) void fft_inv_kernel(const void* __restrict__ Y, float* __restrict__ P,
                                                       int H, int W) {
   __shared__ cpx T[FFT_LDS];
@@ -354,7 +403,7 @@ __global__ __launch_bounds__(192, 2) void fft_inv_kernel(const void* __restrict_
   for (int i = tid; i < H * W; i += 192) {
     const int yy = i / W, x = i - yy * W;
     const cpx a = T[(2 * yy) * RLD + x], c = T[(2 * yy + 1) * RLD + x];
-    *reinterpret_cast<f32x4*>(P + c8_index(b, q, yy, x, e0, H, W)) = f32x4{a.x, a.y, c.x, c.y};
+    map_st4<BM>(P, c8_index(b, q, yy, x, e0, H, W), f32x4{a.x, a.y, c.x, c.y});
   }
 }
 
@@ -363,7 +412,7 @@ __global__ __launch_bounds__(192, 2) void fft_inv_kernel(const void* __restrict_
 // P1 never leaves the block: the inverse rows are parked in LDS, the epilogue runs pixel-major
 // over them (X, O in, I out: one float4 per lane), and the parked I rows are the forward row
 // transform's input.  p: the A-epilogue arguments (X, O, vecs; dst = I).
-template <bool BF>
+template <bool BF, bool BM>
 __global__ __launch_bounds__(192, 2) void fft_inv_a_fwd_kernel(const void* __restrict__ Y, ConvArgs p,
                                                             void* __restrict__ S) {
   __shared__ cpx T[FFT_LDS];
@@ -400,7 +449,7 @@ __global__ __launch_bounds__(192, 2) void fft_inv_a_fwd_kernel(const void* __res
         const int yy = min(i >> 6, H - 1), x = min(i & 63, W - 1);
         const size_t idx = c8_index(b, q, yy, x, e0, H, W);
         xv[u] = *reinterpret_cast<const f32x4*>(p.X + idx);
-        ov[u] = *reinterpret_cast<const f32x4*>(p.O + idx);
+        ov[u] = map_ld4<BM>(p.O, idx);
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
@@ -414,7 +463,7 @@ __global__ __launch_bounds__(192, 2) void fft_inv_a_fwd_kernel(const void* __res
           f32x4 iv;
 #pragma unroll
           for (int j = 0; j < 4; ++j) iv[j] = tanhf(xv[u][j] - (be[j] * ov[u][j] + nu[j]) * (pv[j] + lat[j]));
-          *reinterpret_cast<f32x4*>(p.dst + c8_index(b, q, yy, x, e0, H, W)) = iv;
+          map_st4<BM>(p.dst, c8_index(b, q, yy, x, e0, H, W), iv);
           ra = {iv[0], iv[1]};
           rc = {iv[2], iv[3]};
         } else {
@@ -750,7 +799,7 @@ __device__ __forceinline__ void gate_any(const void* gpk, const f32x16 (&V)[2], 
     gate_x3(static_cast<const f16x8*>(gpk), V, Y, lane, us);
 }
 
-template <bool BF>
+template <bool BF, bool BM>
 __global__ __launch_bounds__(256) void spec_epi_b_kernel(ConvArgs p, const float* __restrict__ P,
                                                          const void* __restrict__ or_x3, float or_us,
                                                          const void* __restrict__ ir_x3, float ir_us, int nseg) {
@@ -761,11 +810,19 @@ __global__ __launch_bounds__(256) void spec_epi_b_kernel(ConvArgs p, const float
   const int x = (seg % xs) * 32 + (lane & 31);
   const int y = (seg / xs) % H, b = seg / xs / H;
   f32x16 Iv[2], Y[2];
+  // bf16 maps: P2 and O are issued with I, in flight during the o_r gate GEMM (0.195 -> 0.181 ms
+  // at B = 256); with fp32 maps the 64 extra live VGPRs cost more than they hide (0.268 -> 0.295)
+  f32x4 pvs[2][4], ovs[2][4];
 #pragma unroll
   for (int n = 0; n < 2; ++n)
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      const f32x4 iv = *reinterpret_cast<const f32x4*>(p.I + c8_index(b, 4 * n + g, y, x, 4 * h, H, W));
+      const size_t idx = c8_index(b, 4 * n + g, y, x, 4 * h, H, W);
+      const f32x4 iv = map_ld4<BM>(p.I, idx);
+      if constexpr (BM) {
+        pvs[n][g] = map_ld4<BM>(P, idx);
+        ovs[n][g] = map_ld4<BM>(p.O, idx);
+      }
 #pragma unroll
       for (int j = 0; j < 4; ++j) Iv[n][4 * g + j] = iv[j];
     }
@@ -776,8 +833,8 @@ __global__ __launch_bounds__(256) void spec_epi_b_kernel(ConvArgs p, const float
     for (int g = 0; g < 4; ++g) {
       const int c = 32 * n + 8 * g + 4 * h;
       const size_t idx = c8_index(b, 4 * n + g, y, x, 4 * h, H, W);
-      const f32x4 pv = *reinterpret_cast<const f32x4*>(P + idx);
-      const f32x4 ov = *reinterpret_cast<const f32x4*>(p.O + idx);
+      const f32x4 pv = BM ? pvs[n][g] : map_ld4<BM>(P, idx);
+      const f32x4 ov = BM ? ovs[n][g] : map_ld4<BM>(p.O, idx);
       const f32x4 lat = *reinterpret_cast<const f32x4*>(p.vecs + V_LAT * 64 + c);
       const f32x4 ga = *reinterpret_cast<const f32x4*>(p.vecs + V_GAMMA * 64 + c);
       const f32x4 ka = *reinterpret_cast<const f32x4*>(p.vecs + V_KAPPA * 64 + c);
@@ -795,7 +852,7 @@ __global__ __launch_bounds__(256) void spec_epi_b_kernel(ConvArgs p, const float
         o[j] = on;
         Iv[n][r] = on;
       }
-      *reinterpret_cast<f32x4*>(p.dst + idx) = o;
+      map_st4<BM>(p.dst, idx, o);
     }
   f32x16 (&Ov)[2] = Iv;
   if (p.mode == 0) {
@@ -809,7 +866,7 @@ __global__ __launch_bounds__(256) void spec_epi_b_kernel(ConvArgs p, const float
         f32x4 o;
 #pragma unroll
         for (int j = 0; j < 4; ++j) o[j] = Ov[n][4 * g + j] * fsigmoid(Y[n][4 * g + j] + ib[j]);
-        *reinterpret_cast<f32x4*>(p.dst2 + c8_index(b, 4 * n + g, y, x, 4 * h, H, W)) = o;
+        map_st4<BM>(p.dst2, c8_index(b, 4 * n + g, y, x, 4 * h, H, W), o);
       }
   } else {
 #pragma unroll
@@ -829,7 +886,7 @@ __global__ __launch_bounds__(256) void spec_epi_b_kernel(ConvArgs p, const float
 
 // first circuit_input gate (hgru_module.py:696-711) for the FFT path: O0 (NHWC) -> O, and
 // Og = O0 * sigmoid(O0 . i_r + i_b) (C8), the gate on f16x3 MFMA; one wave per 32 pixels
-template <bool BF>
+template <bool BF, bool BM>
 __global__ __launch_bounds__(256) void gate_init_x3_kernel(const float* __restrict__ O0, float* O, float* Og,
                                                            const void* __restrict__ ir_x3, float ir_us,
                                                            const float* __restrict__ vecs, int npix, int H,
@@ -865,8 +922,8 @@ __global__ __launch_bounds__(256) void gate_init_x3_kernel(const float* __restri
         og[j] = o[j] * fsigmoid(Y[n][4 * g + j] + ib[j]);
       }
       const size_t idx = c8_index(b, 4 * n + g, y, x, 4 * h, H, W);
-      *reinterpret_cast<f32x4*>(O + idx) = o;
-      *reinterpret_cast<f32x4*>(Og + idx) = og;
+      map_st4<BM>(O, idx, o);
+      map_st4<BM>(Og, idx, og);
     }
 }
 
@@ -927,6 +984,13 @@ __global__ __launch_bounds__(256) void spec_epi_kernel(ConvArgs p, const float* 
 }
 
 // ------------------------------------------------------------------------------------ launchers
+bool fft_bf16_maps() {
+  static const bool v = [] {
+    const char* e = std::getenv("MP_BF16_MAPS");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  return v;
+}
 size_t fft_spec_bytes(int B) { return (size_t)B * 16 * NF * 4 * sizeof(cpx); }
 hipError_t device_absmax(const float* x, size_t n, float* out) {
   unsigned* mx = nullptr;
@@ -982,18 +1046,22 @@ hipError_t build_spec_weights(const float* w, int ks, void* Gx, float* unscale, 
 }
 
 hipError_t launch_fft_fwd(const float* act, void* S, int B, int H, int W, hipStream_t st, bool bf) {
-  if (bf)
-    hipLaunchKernelGGL(fft_fwd_kernel<true>, dim3(B * 16), dim3(192), 0, st, act, S, H, W);
+  if (bf && fft_bf16_maps())
+    hipLaunchKernelGGL((fft_fwd_kernel<true, true>), dim3(B * 16), dim3(192), 0, st, act, S, H, W);
+  else if (bf)
+    hipLaunchKernelGGL((fft_fwd_kernel<true, false>), dim3(B * 16), dim3(192), 0, st, act, S, H, W);
   else
-    hipLaunchKernelGGL(fft_fwd_kernel<false>, dim3(B * 16), dim3(192), 0, st, act, S, H, W);
+    hipLaunchKernelGGL((fft_fwd_kernel<false, false>), dim3(B * 16), dim3(192), 0, st, act, S, H, W);
   return hipGetLastError();
 }
 
 hipError_t launch_fft_inv_a_fwd(const void* Y, const ConvArgs& a, void* S, int B, hipStream_t st, bool bf) {
-  if (bf)
-    hipLaunchKernelGGL(fft_inv_a_fwd_kernel<true>, dim3(B * 16), dim3(192), 0, st, Y, a, S);
+  if (bf && fft_bf16_maps())
+    hipLaunchKernelGGL((fft_inv_a_fwd_kernel<true, true>), dim3(B * 16), dim3(192), 0, st, Y, a, S);
+  else if (bf)
+    hipLaunchKernelGGL((fft_inv_a_fwd_kernel<true, false>), dim3(B * 16), dim3(192), 0, st, Y, a, S);
   else
-    hipLaunchKernelGGL(fft_inv_a_fwd_kernel<false>, dim3(B * 16), dim3(192), 0, st, Y, a, S);
+    hipLaunchKernelGGL((fft_inv_a_fwd_kernel<false, false>), dim3(B * 16), dim3(192), 0, st, Y, a, S);
   return hipGetLastError();
 }
 
@@ -1010,10 +1078,12 @@ hipError_t launch_spec_gemm(const void* S, const void* Gx, void* Y, int B, float
 }
 
 hipError_t launch_fft_inv(const void* Y, float* P, int B, int H, int W, hipStream_t st, bool bf) {
-  if (bf)
-    hipLaunchKernelGGL(fft_inv_kernel<true>, dim3(B * 16), dim3(192), 0, st, Y, P, H, W);
+  if (bf && fft_bf16_maps())
+    hipLaunchKernelGGL((fft_inv_kernel<true, true>), dim3(B * 16), dim3(192), 0, st, Y, P, H, W);
+  else if (bf)
+    hipLaunchKernelGGL((fft_inv_kernel<true, false>), dim3(B * 16), dim3(192), 0, st, Y, P, H, W);
   else
-    hipLaunchKernelGGL(fft_inv_kernel<false>, dim3(B * 16), dim3(192), 0, st, Y, P, H, W);
+    hipLaunchKernelGGL((fft_inv_kernel<false, false>), dim3(B * 16), dim3(192), 0, st, Y, P, H, W);
   return hipGetLastError();
 }
 
@@ -1041,11 +1111,14 @@ hipError_t pack_gate_x3(const float* g, void* out, float* unscale, bool bf) {
 hipError_t launch_gate_init_x3(const float* O0, float* O, float* Og, const void* ir_x3, float ir_us, const float* vecs,
                                int B, int H, int W, hipStream_t st, bool bf) {
   const int npix = B * H * W, nw = (npix + 31) / 32;
-  if (bf)
-    hipLaunchKernelGGL(gate_init_x3_kernel<true>, dim3((nw + 3) / 4), dim3(256), 0, st, O0, O, Og, ir_x3, ir_us, vecs,
+  if (bf && fft_bf16_maps())
+    hipLaunchKernelGGL((gate_init_x3_kernel<true, true>), dim3((nw + 3) / 4), dim3(256), 0, st, O0, O, Og, ir_x3, ir_us, vecs,
+                       npix, H, W);
+  else if (bf)
+    hipLaunchKernelGGL((gate_init_x3_kernel<true, false>), dim3((nw + 3) / 4), dim3(256), 0, st, O0, O, Og, ir_x3, ir_us, vecs,
                        npix, H, W);
   else
-    hipLaunchKernelGGL(gate_init_x3_kernel<false>, dim3((nw + 3) / 4), dim3(256), 0, st, O0, O, Og, ir_x3, ir_us,
+    hipLaunchKernelGGL((gate_init_x3_kernel<false, false>), dim3((nw + 3) / 4), dim3(256), 0, st, O0, O, Og, ir_x3, ir_us,
                        vecs, npix, H, W);
   return hipGetLastError();
 }
@@ -1053,11 +1126,14 @@ hipError_t launch_gate_init_x3(const float* O0, float* O, float* Og, const void*
 hipError_t launch_spec_epi_b(const ConvArgs& a, const float* P, const void* or_x3, float or_us, const void* ir_x3,
                              float ir_us, int B, hipStream_t st, bool bf) {
   const int nseg = B * a.H * (a.W / 32);
-  if (bf)
-    hipLaunchKernelGGL(spec_epi_b_kernel<true>, dim3((nseg + 3) / 4), dim3(256), 0, st, a, P, or_x3, or_us, ir_x3,
+  if (bf && fft_bf16_maps())
+    hipLaunchKernelGGL((spec_epi_b_kernel<true, true>), dim3((nseg + 3) / 4), dim3(256), 0, st, a, P, or_x3, or_us, ir_x3,
+                       ir_us, nseg);
+  else if (bf)
+    hipLaunchKernelGGL((spec_epi_b_kernel<true, false>), dim3((nseg + 3) / 4), dim3(256), 0, st, a, P, or_x3, or_us, ir_x3,
                        ir_us, nseg);
   else
-    hipLaunchKernelGGL(spec_epi_b_kernel<false>, dim3((nseg + 3) / 4), dim3(256), 0, st, a, P, or_x3, or_us, ir_x3,
+    hipLaunchKernelGGL((spec_epi_b_kernel<false, false>), dim3((nseg + 3) / 4), dim3(256), 0, st, a, P, or_x3, or_us, ir_x3,
                        ir_us, nseg);
   return hipGetLastError();
 }

@@ -279,29 +279,33 @@ void check_map(mp_ctx* c, int64_t H, int64_t W, const char* what) {
 
 // the hGRU loop of images [b0, b0 + n) on stream st (FFT path), all state pointers offset
 void fft_circuit_range(mp_ctx* c, int b0, int n, int H, int W, int T, float* final_dst2, hipStream_t st) {
-  const size_t m = (size_t)b0 * 64 * H * W;              // floats per image of a C8 / NHWC map
+  const size_t m = (size_t)b0 * 64 * H * W;              // elements per image of a C8 / NHWC map
   void* S = static_cast<char*>(c->specS.p) + fft_spec_bytes(b0);
   void* Y = static_cast<char*>(c->specY.p) + fft_spec_bytes(b0);
-  float* P = c->specP.f() + m;
+  // state maps O, I, Og, P2 (bf16 under MP_DTYPE_BF16, k_fft.hip map_ld4): the same element
+  // offset, in units of their element type; X and the NHWC output stay fp32
+  const bool bm = c->dtype == MP_DTYPE_BF16 && fft_bf16_maps();
+  auto map = [&](DevBuf& buf) { return bm ? reinterpret_cast<float*>(reinterpret_cast<uint16_t*>(buf.p) + m) : buf.f() + m; };
+  float* P = map(c->specP);
   for (int t = 0; t < T; ++t) {
     ConvArgs a{};
     a.H = H;
     a.W = W;
-    a.src = c->Og.f() + m;
-    a.dst = c->I.f() + m;
+    a.src = map(c->Og);
+    a.dst = map(c->I);
     a.X = c->X.f() + m;
-    a.O = c->O.f() + m;
+    a.O = map(c->O);
     a.vecs = c->vecs.f();
     ConvArgs b{};
     b.H = H;
     b.W = W;
-    b.dst = c->O.f() + m;
-    b.O = c->O.f() + m;
-    b.I = c->I.f() + m;
+    b.dst = map(c->O);
+    b.O = map(c->O);
+    b.I = map(c->I);
     b.vecs = c->vecs.f();
     b.rho = c->rho[t];
     b.mode = (t == T - 1) ? 1 : 0;
-    b.dst2 = (t == T - 1) ? final_dst2 + m : c->Og.f() + m;
+    b.dst2 = (t == T - 1) ? final_dst2 + m : map(c->Og);
     const bool bf = c->dtype == MP_DTYPE_BF16;
     hip_check(launch_fft_fwd(a.src, S, n, H, W, st, bf), "fft_fwd");
     hip_check(launch_spec_gemm(S, c->spec_g.p, Y, n, c->p_unscale, st, bf), "spec_gemm");

@@ -48,6 +48,9 @@ hipError_t launch_pack_conv64x3(const float* w, void* out, int ks, float wscale,
 // k_fft.hip (FFT path of the association-field conv, MP_DTYPE_F32_FFT; maps up to 64x64)
 constexpr int FFT_MAX_HW = 64;
 hipError_t device_absmax(const float* x, size_t n, float* out);   // max |x| (synchronous)
+// MP_DTYPE_BF16 keeps the hGRU state maps O, I, Og, P2 in bf16 (MP_BF16_MAPS=0: fp32, for A/B);
+// their element offsets are unchanged, so a map pointer offset by m elements is (bf16*)base + m
+bool fft_bf16_maps();
 size_t fft_spec_bytes(int B);      // one spectrum buffer (S or Y) for B images
 size_t fft_weight_bytes();         // expanded split spectral weights
 // HWIO [ks][ks][64][64] -> packed split spectral weights (synchronous, finalize time)
