@@ -171,6 +171,10 @@ constexpr int FCX_LD = FC_BK + 8;   // f16 pitch of the hi / lo activation plane
 // K steps are software-pipelined one step ahead: the activation float4s and the weight fragments
 // of step k+1 are loaded into registers while step k's MFMAs run; loads are unconditional (row
 // index clamped, K a multiple of FC_BK), so all eight loads of a step are in flight together.
+// NP = 3: the fp32-accurate f16x3 product; NP = 1 (dtype bf16's fc_1): hi x hi only -- one MFMA per
+// MAC and only the hi weight planes are read (half the weight bytes), f16 operands (11-bit
+// mantissa, finer than bf16), fp32 accumulation
+template <int NP>
 __global__ __launch_bounds__(256) void fc_gemm_x3_kernel(const float* __restrict__ A, int lda,
                                                          const f16x8* __restrict__ Wpk,
                                                          float* __restrict__ part, int M, int K,
@@ -203,7 +207,7 @@ __global__ __launch_bounds__(256) void fc_gemm_x3_kernel(const float* __restrict
       const int kb = min((k0 >> 4) + g, K16 - 1);
       const f16x8* wp = Wpk + (((size_t)kb * N32 + nbc) * 2) * 64 + lane;
       w[g][0] = wp[0];
-      w[g][1] = wp[64];
+      if constexpr (NP == 3) w[g][1] = wp[64];
     }
   };
 
@@ -225,14 +229,14 @@ __global__ __launch_bounds__(256) void fc_gemm_x3_kernel(const float* __restrict
       for (int s = 0; s < 4; ++s) {
         const _Float16 hh = (_Float16)av[i][s];
         Ah[row * FCX_LD + k4 + s] = hh;
-        Al[row * FCX_LD + k4 + s] = (_Float16)(av[i][s] - (float)hh);
+        if constexpr (NP == 3) Al[row * FCX_LD + k4 + s] = (_Float16)(av[i][s] - (float)hh);
       }
     }
     f16x8 wc[FC_BK / 16][2];
 #pragma unroll
     for (int g = 0; g < FC_BK / 16; ++g) {
       wc[g][0] = wn[g][0];
-      wc[g][1] = wn[g][1];
+      if constexpr (NP == 3) wc[g][1] = wn[g][1];
     }
     if (k0 + FC_BK < kend) {   // prefetch the next step
       load_act(k0 + FC_BK, av);
@@ -243,14 +247,17 @@ __global__ __launch_bounds__(256) void fc_gemm_x3_kernel(const float* __restrict
 #pragma unroll
       for (int g = 0; g < FC_BK / 16; ++g) {
         if ((k0 >> 4) + g >= K16) break;
-        const f16x8 wh = wc[g][0], wl = wc[g][1];
+        const f16x8 wh = wc[g][0];
+        [[maybe_unused]] const f16x8 wl = wc[g][1];
 #pragma unroll
         for (int m = 0; m < 4; ++m) {
           const int o = (m * 32 + col) * FCX_LD + 16 * g + 8 * h;
           const f16x8 ah = *reinterpret_cast<const f16x8*>(Ah + o);
-          const f16x8 al = *reinterpret_cast<const f16x8*>(Al + o);
-          acc[m] = mfma16(wl, ah, acc[m]);
-          acc[m] = mfma16(wh, al, acc[m]);
+          if constexpr (NP == 3) {
+            const f16x8 al = *reinterpret_cast<const f16x8*>(Al + o);
+            acc[m] = mfma16(wl, ah, acc[m]);
+            acc[m] = mfma16(wh, al, acc[m]);
+          }
           acc[m] = mfma16(wh, ah, acc[m]);
         }
       }
@@ -288,12 +295,16 @@ hipError_t launch_pack_fc_x3(const float* W, void* out, int K, int N, float* uns
 }
 
 hipError_t launch_fc_gemm_x3(const float* A, int lda, const void* Wpk, float unscale, float* part, int M, int K,
-                             int N, int S, int kslice, hipStream_t st) {
+                             int N, int S, int kslice, hipStream_t st, int nprod) {
   if (K % FC_BK || kslice % FC_BK || lda % 4) return hipErrorInvalidValue;
   const int N32 = (N + 31) / 32;
   const int grid = fc_grid((M + FC_BM - 1) / FC_BM, (N32 + 3) / 4, S);
-  hipLaunchKernelGGL(fc_gemm_x3_kernel, dim3(grid), dim3(256), 0, st, A, lda, static_cast<const f16x8*>(Wpk), part,
-                     M, K, N32, kslice, unscale, S);
+  if (nprod == 1)
+    hipLaunchKernelGGL(fc_gemm_x3_kernel<1>, dim3(grid), dim3(256), 0, st, A, lda, static_cast<const f16x8*>(Wpk),
+                       part, M, K, N32, kslice, unscale, S);
+  else
+    hipLaunchKernelGGL(fc_gemm_x3_kernel<3>, dim3(grid), dim3(256), 0, st, A, lda, static_cast<const f16x8*>(Wpk),
+                       part, M, K, N32, kslice, unscale, S);
   return hipGetLastError();
 }
 

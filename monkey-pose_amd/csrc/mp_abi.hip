@@ -657,7 +657,8 @@ int mp_hgru_pose_fwd_taps(mp_ctx* ctx, const float* depth, int64_t n, int64_t h,
                     ? launch_fc_gemm(ctx->fcin.f(), ctx->fc1_in, ctx->fc1_pk.v4(), ctx->part.f(), N, ctx->fc1_in,
                                      ctx->fc1_out, S, ks, st)
                     : launch_fc_gemm_x3(ctx->fcin.f(), ctx->fc1_in, ctx->fc1_pk.p, ctx->fc1_unscale, ctx->part.f(),
-                                        N, ctx->fc1_in, ctx->fc1_out, S, ks, st),
+                                        N, ctx->fc1_in, ctx->fc1_out, S, ks, st,
+                                        ctx->dtype == MP_DTYPE_BF16 ? 1 : 3),   // bf16: one f16 product
                 "fc_1 gemm");
       if (tp.fc1)   // fc_1 + bias before the relu (same partial sums)
         hip_check(launch_fc_reduce(ctx->part.f(), S, N, ctx->fc1_out, ctx->fc1_b.f(), 0, nullptr, nullptr, tp.fc1,

@@ -95,11 +95,12 @@ hipError_t launch_pack_fc(const float* W, f32x4* out, int K, int N, hipStream_t 
 int fc_choose_splits(int M, int K, int N, int* kslice);
 hipError_t launch_fc_gemm(const float* A, int lda, const f32x4* Wpk, float* part, int M, int K, int N, int S,
                           int kslice, hipStream_t st);
-// f16x3 (fp32-accurate) fc GEMM, same slabs / splits as launch_fc_gemm
+// f16x3 (fp32-accurate) fc GEMM, same slabs / splits as launch_fc_gemm; nprod = 1: the hi x hi
+// product only (single f16 MFMA, hi weight planes only -- MP_DTYPE_BF16's fc_1)
 size_t fc_x3_bytes(int K, int N);
 hipError_t launch_pack_fc_x3(const float* W, void* out, int K, int N, float* unscale, hipStream_t st);
 hipError_t launch_fc_gemm_x3(const float* A, int lda, const void* Wpk, float unscale, float* part, int M, int K,
-                             int N, int S, int kslice, hipStream_t st);
+                             int N, int S, int kslice, hipStream_t st, int nprod = 3);
 // k_frame.hip (frame -> CoM -> crop chain)
 hipError_t launch_resize_bilinear(const float* x, int N, int H, int W, int C, float* out, int Ho, int Wo,
                                   hipStream_t st);
