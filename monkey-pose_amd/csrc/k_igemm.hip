@@ -13,6 +13,7 @@
 // the im2col tile [128][32 k] is gathered into LDS (+4 float row pad: conflict-free b128 reads).
 #include "mp_kernels.hpp"
 
+#include <algorithm>
 #include <cstdlib>
 #ifndef HX_EXP
 #define HX_EXP 0
@@ -347,10 +348,18 @@ __global__ __launch_bounds__(256) void igemm_x3w_pm_kernel(IgemmArgs p, const f1
     nky = max(0, ky_hi - ky_lo + 1);
     kxsteps = max(0, kx_hi - kx_lo + 1) * (p.Cin / IG_BK);
   }
+  // split-K (p.part, gridDim.z ranges): this block sums input channels [z cps, (z+1) cps) chunks of
+  // every visited tap -- the grouping depends on the layer only, never on the batch
+  const int nz = p.part ? (int)gridDim.z : 1, cps = p.Cin / IG_BK / nz, zc = (int)blockIdx.z * cps;
+  if (nz > 1) kxsteps = kxsteps / (p.Cin / IG_BK) * cps;
   const int nsteps = nky * kxsteps;
   auto kof = [&](int st) {   // k0 of K step st
     if (!skip) return st * IG_BK;
     const int r = st / kxsteps;
+    if (nz > 1) {
+      const int rem = st - r * kxsteps, kxo = rem / cps;
+      return ((ky_lo + r) * p.KS + kx_lo + kxo) * p.Cin + (zc + rem - kxo * cps) * IG_BK;
+    }
     return ((ky_lo + r) * p.KS + kx_lo) * p.Cin + (st - r * kxsteps) * IG_BK;
   };
   const int k4 = (tid & 7) * 4;
@@ -455,6 +464,24 @@ __global__ __launch_bounds__(256) void igemm_x3w_pm_kernel(IgemmArgs p, const f1
     }
   }
   if (!wave_on) return;
+  if (nz > 1) {   // raw partial sums [z][gm][N32 * 32]; the reduce applies the epilogue
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb) {
+      const int gm = m0 + (2 * wm + mb) * 32 + col;
+      if (gm >= M) continue;
+      float* dst = p.part + ((size_t)blockIdx.z * M + gm) * (N32 * 32);
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) {
+        const int cb = nb0 + 2 * wn + nb;
+        if (cb >= N32) break;
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<f32x4*>(dst + cb * 32 + 8 * g + 4 * h) =
+              f32x4{acc[mb][nb][4 * g], acc[mb][nb][4 * g + 1], acc[mb][nb][4 * g + 2], acc[mb][nb][4 * g + 3]};
+      }
+    }
+    return;
+  }
   const bool vst = (p.ldo % 4 == 0) && (p.coff % 4 == 0) && (p.Cout % 4 == 0);
 #pragma unroll
   for (int mb = 0; mb < 2; ++mb) {
@@ -484,6 +511,26 @@ __global__ __launch_bounds__(256) void igemm_x3w_pm_kernel(IgemmArgs p, const f1
         }
       }
     }
+  }
+}
+
+// the split-K reduce of igemm_x3w_pm_kernel: out = relu?((sum_z part[z]) * unscale + bias), z in
+// order; one thread per 4 output channels of one (position-major) row
+__global__ __launch_bounds__(256) void igemm_pm_reduce_kernel(IgemmArgs p, int S, float unscale) {
+  const int HWo = p.Ho * p.Wo, M = p.N * HWo, N32 = (p.Cout + 31) / 32, nq = N32 * 8;
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (size_t)M * nq) return;
+  const int gm = (int)(i / nq), c = (int)(i - (size_t)gm * nq) * 4;
+  if (c >= p.Cout) return;
+  const float* src = p.part + (size_t)gm * (N32 * 32) + c;
+  f32x4 s = *reinterpret_cast<const f32x4*>(src);
+  for (int z = 1; z < S; ++z) s += *reinterpret_cast<const f32x4*>(src + (size_t)z * M * (N32 * 32));
+  float* dst = p.out + ((size_t)(gm % p.N) * HWo + gm / p.N) * p.ldo + p.coff + c;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (c + j >= p.Cout) break;
+    const float v = s[j] * unscale + p.bias[c + j];
+    dst[j] = p.relu ? fmaxf(v, 0.f) : v;
   }
 }
 
@@ -876,6 +923,80 @@ hipError_t launch_igemm_conv(const IgemmArgs& a, hipStream_t st) {
   return hipGetLastError();
 }
 
+namespace {
+int env_flag(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return e ? std::atoi(e) : dflt;
+}
+
+// halo tiles: stride 1, SAME, odd KS in {3, 5}, Cin % 32 == 0, tiles of whole rows of one image (or
+// whole images), halo within HX_ITEMS per thread and two buffers within 80 KiB
+bool halo_geom(const IgemmArgs& a, HaloGeom& hg, size_t& lds) {
+  static const int halo = env_flag("MP_IGEMM_HALO", 1);
+  if (!(halo && a.stride == 1 && (a.KS == 3 || a.KS == 5) && a.pad_t == a.KS / 2 && a.pad_l == a.KS / 2 &&
+        a.Ho == a.H && a.Wo == a.W && a.Cin % 32 == 0 && a.ldx % 4 == 0 && a.cix % 4 == 0 && a.W <= IG_BM &&
+        IG_BM % a.W == 0))
+    return false;
+  const int HW = a.H * a.W;
+  bool ok = true;
+  if (HW >= IG_BM) {
+    hg.NI = 1;
+    hg.R = IG_BM / a.W;
+    ok = a.H % hg.R == 0;
+  } else {
+    hg.NI = IG_BM / HW;
+    hg.R = a.H;
+    ok = IG_BM % HW == 0;
+  }
+  hg.HH = hg.R + a.KS - 1;
+  hg.WW = a.W + a.KS - 1;
+  hg.PH = hg.NI * hg.HH * hg.WW;
+  lds = 2 * (size_t)hg.PH * HX_PITCH * sizeof(_Float16);
+  return ok && hg.PH * 8 <= 256 * HX_ITEMS && lds <= 80 * 1024;
+}
+
+// small maps (<= 8 x 8) where at least 40 % of the im2col taps are padding: position-major tiles so
+// the padding taps can be skipped (measured: a 5x5 conv on 4x4 maps, 51 % padding, 1.4x faster; on
+// 8x8 maps, 28 % padding, slower -- a position-major tile gathers 128 images' pixels and loses the
+// neighbouring-pixel input reuse of a row-major tile)
+bool pm_path(const IgemmArgs& a) {
+  static const int tapskip = env_flag("MP_IGEMM_TAPSKIP", 1);
+  if (!(tapskip && a.KS > 1 && a.Ho * a.Wo <= 64 && a.Cin % IG_BK == 0)) return false;
+  long valid = 0;
+  for (int y = 0; y < a.Ho; ++y)
+    for (int x = 0; x < a.Wo; ++x)
+      for (int ky = 0; ky < a.KS; ++ky)
+        for (int kx = 0; kx < a.KS; ++kx) {
+          const int iy = y * a.stride - a.pad_t + ky, ix = x * a.stride - a.pad_l + kx;
+          valid += iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
+        }
+  return valid * 10 <= 6L * a.Ho * a.Wo * a.KS * a.KS;
+}
+
+bool wide_path(const IgemmArgs& a) {
+  static const int wide = env_flag("MP_IGEMM_WIDE", 1);
+  return wide && (a.Cout + 31) / 32 >= 3;   // Cout > 64: 2 x 2 wave tiles, weights staged in LDS
+}
+}  // namespace
+
+int igemm_pm_splits(const IgemmArgs& a) {
+  // off by default: one stream, hier con_6 0.75 -> 0.47 ms, but the graph runtime already runs the
+  // five limbs' con_6 side by side on its streams and there the split lost (34.4k -> 32.6k crops/s)
+  static const int maxs = std::max(1, env_flag("MP_IGEMM_PM_SPLITS", 1));
+  if (a.K < 4 || !wide_path(a)) return 1;
+  HaloGeom hg;
+  size_t lds;
+  if (halo_geom(a, hg, lds) || !pm_path(a)) return 1;
+  int S = maxs;
+  while (S > 1 && a.Cin % (S * IG_BK)) S /= 2;
+  return S;
+}
+
+size_t igemm_pm_part_floats(const IgemmArgs& a) {
+  const int S = igemm_pm_splits(a);
+  return S > 1 ? (size_t)S * a.N * a.Ho * a.Wo * ((a.Cout + 31) / 32 * 32) : 0;
+}
+
 hipError_t launch_igemm_x3(const IgemmArgs& a, const void* wpk, float unscale, hipStream_t st) {
   if (a.K < 4) return hipErrorInvalidValue;   // the clamped vector load needs K >= 4
   const int M = a.N * a.Ho * a.Wo;
@@ -883,79 +1004,44 @@ hipError_t launch_igemm_x3(const IgemmArgs& a, const void* wpk, float unscale, h
   const int nb = N32 >= 4 ? 4 : (N32 >= 2 ? 2 : 1);
   dim3 grid((M + IG_BM - 1) / IG_BM, (N32 + nb - 1) / nb);
   const f16x8* w = static_cast<const f16x8*>(wpk);
-  static const int wide = [] {
-    const char* e = std::getenv("MP_IGEMM_WIDE");
-    return e ? std::atoi(e) : 1;
-  }();
-  if (wide && N32 >= 3) {   // Cout > 64: 2 x 2 wave tiles, weights staged in LDS
-    static const int tapskip = [] {
-      const char* e = std::getenv("MP_IGEMM_TAPSKIP");
-      return e ? std::atoi(e) : 1;
-    }();
-    static const int halo = [] {
-      const char* e = std::getenv("MP_IGEMM_HALO");
-      return e ? std::atoi(e) : 1;
-    }();
-    // halo tiles: stride 1, SAME, odd KS in {3, 5}, Cin % 32 == 0, tiles of whole rows of one
-    // image (or whole images), halo within HX_ITEMS per thread and two buffers within 80 KiB
-    if (halo && a.stride == 1 && (a.KS == 3 || a.KS == 5) && a.pad_t == a.KS / 2 && a.pad_l == a.KS / 2 &&
-        a.Ho == a.H && a.Wo == a.W && a.Cin % 32 == 0 && a.ldx % 4 == 0 && a.cix % 4 == 0 && a.W <= IG_BM &&
-        IG_BM % a.W == 0) {
-      HaloGeom hg;
-      const int HW = a.H * a.W;
-      bool ok = true;
-      if (HW >= IG_BM) {
-        hg.NI = 1;
-        hg.R = IG_BM / a.W;
-        ok = a.H % hg.R == 0;
-      } else {
-        hg.NI = IG_BM / HW;
-        hg.R = a.H;
-        ok = IG_BM % HW == 0;
-      }
-      hg.HH = hg.R + a.KS - 1;
-      hg.WW = a.W + a.KS - 1;
-      hg.PH = hg.NI * hg.HH * hg.WW;
-      const size_t lds = 2 * (size_t)hg.PH * HX_PITCH * sizeof(_Float16);
-      if (ok && hg.PH * 8 <= 256 * HX_ITEMS && lds <= 80 * 1024) {
-        static const bool attr = [] {
-          (void)hipFuncSetAttribute(reinterpret_cast<const void*>(igemm_x3h_kernel<3>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
-          (void)hipFuncSetAttribute(reinterpret_cast<const void*>(igemm_x3h_kernel<5>),
-                                    hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
-          return true;
-        }();
-        (void)attr;
-        const dim3 grid((M + IG_BM - 1) / IG_BM, (N32 + 3) / 4);
-        if (a.KS == 3)
-          hipLaunchKernelGGL(igemm_x3h_kernel<3>, grid, dim3(256), lds, st, a, hg, w, unscale);
-        else
-          hipLaunchKernelGGL(igemm_x3h_kernel<5>, grid, dim3(256), lds, st, a, hg, w, unscale);
-        return hipGetLastError();
-      }
+  if (wide_path(a)) {
+    HaloGeom hg;
+    size_t lds = 0;
+    if (halo_geom(a, hg, lds)) {
+      static const bool attr = [] {
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(igemm_x3h_kernel<3>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(igemm_x3h_kernel<5>),
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+        return true;
+      }();
+      (void)attr;
+      const dim3 hgrid((M + IG_BM - 1) / IG_BM, (N32 + 3) / 4);
+      if (a.KS == 3)
+        hipLaunchKernelGGL(igemm_x3h_kernel<3>, hgrid, dim3(256), lds, st, a, hg, w, unscale);
+      else
+        hipLaunchKernelGGL(igemm_x3h_kernel<5>, hgrid, dim3(256), lds, st, a, hg, w, unscale);
+      return hipGetLastError();
     }
     IgemmArgs b = a;
-    // small maps (<= 8 x 8) where at least 40 % of the im2col taps are padding: position-major
-    // tiles so the padding taps can be skipped (measured: a 5x5 conv on 4x4 maps, 51 % padding,
-    // 1.4x faster; on 8x8 maps, 28 % padding, slower -- a position-major tile gathers 128 images'
-    // pixels and loses the neighbouring-pixel input reuse of a row-major tile)
-    b.pmajor = 0;
-    if (tapskip && a.KS > 1 && a.Ho * a.Wo <= 64 && a.Cin % IG_BK == 0) {
-      long valid = 0;
-      for (int y = 0; y < a.Ho; ++y)
-        for (int x = 0; x < a.Wo; ++x)
-          for (int ky = 0; ky < a.KS; ++ky)
-            for (int kx = 0; kx < a.KS; ++kx) {
-              const int iy = y * a.stride - a.pad_t + ky, ix = x * a.stride - a.pad_l + kx;
-              valid += iy >= 0 && iy < a.H && ix >= 0 && ix < a.W;
-            }
-      b.pmajor = valid * 10 <= 6L * a.Ho * a.Wo * a.KS * a.KS ? 1 : 0;
+    b.pmajor = pm_path(a) ? 1 : 0;
+    const int S = b.pmajor && a.part ? igemm_pm_splits(a) : 1;
+    if (S > 1) {
+      // split-K over input-channel ranges (z = range): raw partial sums to a.part, then a fixed-order
+      // reduce with the epilogue -- 4x the blocks for the under-filled small-map convs (hier con_6:
+      // 256 blocks of 128 x 128 on 256 CUs otherwise)
+      const dim3 sgrid((M + IG_BM - 1) / IG_BM, (N32 + 3) / 4, S);
+      hipLaunchKernelGGL(igemm_x3w_pm_kernel, sgrid, dim3(256), 0, st, b, w, unscale);
+      const size_t total = (size_t)M * (N32 * 8);
+      hipLaunchKernelGGL(igemm_pm_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, b, S, unscale);
+      return hipGetLastError();
     }
-    const dim3 grid((M + IG_BM - 1) / IG_BM, (N32 + 3) / 4);
+    b.part = nullptr;
+    const dim3 wgrid((M + IG_BM - 1) / IG_BM, (N32 + 3) / 4);
     if (b.pmajor)
-      hipLaunchKernelGGL(igemm_x3w_pm_kernel, grid, dim3(256), 0, st, b, w, unscale);
+      hipLaunchKernelGGL(igemm_x3w_pm_kernel, wgrid, dim3(256), 0, st, b, w, unscale);
     else
-      hipLaunchKernelGGL(igemm_x3w_kernel, grid, dim3(256), 0, st, b, w, unscale);
+      hipLaunchKernelGGL(igemm_x3w_kernel, wgrid, dim3(256), 0, st, b, w, unscale);
     return hipGetLastError();
   }
   if (nb == 4)

@@ -399,6 +399,13 @@ void plan(mp_ctx* c, G& g, int64_t n, int64_t h, int64_t w) {
       a.pad_l = same_pad_before(S.W, L.k, op.stride);
       a.relu = 1;
       k->L = &L;
+      if (L.x3) {   // split-K workspace of the position-major small-map path (k_igemm.hip)
+        const size_t pf = igemm_pm_part_floats(a);
+        if (pf) {
+          k->part.alloc(pf * sizeof(float));
+          a.part = k->part.f();
+        }
+      }
     } else if (op.kind == MP_OP_MAXPOOL || op.kind == MP_OP_AVGPOOL) {
       if (op.ksize != 2) fail(MP_ERR_UNSUPPORTED, "pool window " + std::to_string(op.ksize) + " (only 2x2/2)");
       k->px = base(s);

@@ -83,7 +83,13 @@ struct IgemmArgs {
   int relu;
   int pmajor;          // wide f16x3 kernel only: M ordered position-major (m = pos * N + n), each
                        // block's K loop skips the taps that are padding for all of its positions
+  float* part = nullptr;   // position-major split-K workspace (igemm_pm_splits(a) x M x Cout32
+                           // floats, caller-owned); null: no split
 };
+// input-channel splits of the position-major tap-skipping path for this conv (1 = none); a property
+// of the layer alone (never of the batch), so every crop's sums group the same way at any batch
+int igemm_pm_splits(const IgemmArgs& a);
+size_t igemm_pm_part_floats(const IgemmArgs& a);
 hipError_t launch_igemm_conv(const IgemmArgs& a, hipStream_t st);
 // f16x3 (fp32-accurate) variant; wpk packed by launch_pack_fc_x3 as a [K][Cout] matrix
 hipError_t launch_igemm_x3(const IgemmArgs& a, const void* wpk, float unscale, hipStream_t st);
