@@ -75,13 +75,12 @@ def fft_kernels(ctx, B, hw, steps, bf16=False):
     NF, act = 72 * 37, B * 64 * hw * 4                 # frequencies; one fp32 C8 activation map
     ent = 16 if bf16 else 32                           # bytes per (4-channel group, frequency)
     spec = B * 16 * NF * ent                           # one spectrum buffer [b][cq][f][ent]
-    # the state maps O, I, Og, P2 are bf16 under dtype bf16 (k_fft.hip map_ld4; MP_BF16_MAPS=0: fp32);
-    # the drive X stays fp32
+    # the maps X, O, I, Og, P2 are bf16 under dtype bf16 (k_fft.hip map_ld4; MP_BF16_MAPS=0: fp32)
     sm = act // 2 if bf16 and os.environ.get("MP_BF16_MAPS", "1") != "0" else act
     algo = {   # name: (bytes, flops) per launch
         "fft_fwd": (sm + spec, 0.0),                   # Og in; S out
         "spec_gemm": (2 * spec + NF * ent * 1024, 8.0 * B * NF * 64 * 64),   # S in, Y out, weights
-        "inv_a_fwd": (2 * spec + act + 2 * sm, 0.0),   # Y, X, O in; I, S out
+        "inv_a_fwd": (2 * spec + 3 * sm, 0.0),         # Y, X, O in; I, S out
         "fft_inv": (spec + sm, 0.0),                   # Y in; P out
         "epi_b": (5 * sm, 0.0),                        # P, I, O in; O', Og' out
     }
@@ -457,7 +456,7 @@ def main():
         "vs_baseline": None,
         "dtype": {"f32": "f32", "f32_split": "f32 (f16x3 split MFMA, fp32 accumulate)",
                   "f32_fft": "f32 (fp32 FFT convolution, fp32-accurate f16x3 spectral GEMM)",
-                  "bf16": "bf16 (bf16 spectra and hGRU state maps, bf16 spectral / gate GEMMs, fp32 accumulate, fp32 FFTs and elementwise math)"}[args.dtype],
+                  "bf16": "bf16 (bf16 spectra and hGRU maps, bf16 spectral / gate GEMMs, fp32 accumulate, fp32 FFTs and elementwise math)"}[args.dtype],
         "data": "synthetic crops + synthetic weights (splitmix64 stand-ins; reference publishes none)",
         "config": {"workload": f"hgru_pose.model.build fwd, T={T}, {crop}x{crop} crops, "
                                f"batch {B} per GPU", "global_batch": world * B, "crop": crop,

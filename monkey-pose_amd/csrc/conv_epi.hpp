@@ -46,7 +46,11 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& p, const f32x16& a
           const float v = fmaxf(acc[n][4 * g + j] + bb[j], 0.f);   // relu(conv + b)
           o[j] = v * ss[j] + tt[j];                                    // folded BN
         }
-        *reinterpret_cast<f32x4*>(p.dst + c8_index(b, 4 * n + g, y, x, 4 * h, H, W)) = o;
+        const size_t idx = c8_index(b, 4 * n + g, y, x, 4 * h, H, W);
+        if (p.dst_bf16)
+          *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(p.dst) + idx) = bf16x4_pack(o);
+        else
+          *reinterpret_cast<f32x4*>(p.dst + idx) = o;
       }
   } else if constexpr (EPI == EPI_HGRU_A) {
     // I = tanh(X - (beta*O + nu) * (P1 + lateral_bias))      hgru_module.py:657, 797-799

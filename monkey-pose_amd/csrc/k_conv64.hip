@@ -187,7 +187,7 @@ __global__ __launch_bounds__(256) void conv1_pool_bn_kernel(const float* __restr
 }
 
 // layout conversions (standalone ContextualCircuit API, debug taps)
-__global__ void nhwc_to_c8_kernel(const float* __restrict__ in, float* out, int B, int H, int W) {
+__global__ void nhwc_to_c8_kernel(const float* __restrict__ in, float* out, int B, int H, int W, bool bf) {
   const size_t total = (size_t)B * H * W * NQ;
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= total) return;
@@ -195,22 +195,36 @@ __global__ void nhwc_to_c8_kernel(const float* __restrict__ in, float* out, int 
   const size_t pix = i / NQ;
   const int x = pix % W, y = (pix / W) % H, b = pix / ((size_t)W * H);
   const f32x4* s = reinterpret_cast<const f32x4*>(in + pix * C + 8 * q);
-  f32x4* d = reinterpret_cast<f32x4*>(out + c8_index(b, q, y, x, 0, H, W));
-  d[0] = s[0];
-  d[1] = s[1];
+  const size_t o = c8_index(b, q, y, x, 0, H, W);
+  if (bf) {
+    uint2* d = reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out) + o);
+    d[0] = bf16x4_pack(s[0]);
+    d[1] = bf16x4_pack(s[1]);
+  } else {
+    f32x4* d = reinterpret_cast<f32x4*>(out + o);
+    d[0] = s[0];
+    d[1] = s[1];
+  }
 }
 
-__global__ void c8_to_nhwc_kernel(const float* __restrict__ in, float* out, int B, int H, int W) {
+__global__ void c8_to_nhwc_kernel(const float* __restrict__ in, float* out, int B, int H, int W, bool bf) {
   const size_t total = (size_t)B * H * W * NQ;
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= total) return;
   const int q = i % NQ;
   const size_t pix = i / NQ;
   const int x = pix % W, y = (pix / W) % H, b = pix / ((size_t)W * H);
-  const f32x4* s = reinterpret_cast<const f32x4*>(in + c8_index(b, q, y, x, 0, H, W));
+  const size_t o = c8_index(b, q, y, x, 0, H, W);
   f32x4* d = reinterpret_cast<f32x4*>(out + pix * C + 8 * q);
-  d[0] = s[0];
-  d[1] = s[1];
+  if (bf) {
+    const uint2* s = reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(in) + o);
+    d[0] = bf16x4_unpack(s[0]);
+    d[1] = bf16x4_unpack(s[1]);
+  } else {
+    const f32x4* s = reinterpret_cast<const f32x4*>(in + o);
+    d[0] = s[0];
+    d[1] = s[1];
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -294,15 +308,15 @@ hipError_t launch_conv1_pool_bn(const float* in, const float* w, const float* bi
   return hipGetLastError();
 }
 
-hipError_t launch_nhwc_to_c8(const float* in, float* out, int B, int H, int W, hipStream_t st) {
+hipError_t launch_nhwc_to_c8(const float* in, float* out, int B, int H, int W, hipStream_t st, bool bf) {
   const size_t total = (size_t)B * H * W * NQ;
-  hipLaunchKernelGGL(nhwc_to_c8_kernel, dim3((total + 255) / 256), dim3(256), 0, st, in, out, B, H, W);
+  hipLaunchKernelGGL(nhwc_to_c8_kernel, dim3((total + 255) / 256), dim3(256), 0, st, in, out, B, H, W, bf);
   return hipGetLastError();
 }
 
-hipError_t launch_c8_to_nhwc(const float* in, float* out, int B, int H, int W, hipStream_t st) {
+hipError_t launch_c8_to_nhwc(const float* in, float* out, int B, int H, int W, hipStream_t st, bool bf) {
   const size_t total = (size_t)B * H * W * NQ;
-  hipLaunchKernelGGL(c8_to_nhwc_kernel, dim3((total + 255) / 256), dim3(256), 0, st, in, out, B, H, W);
+  hipLaunchKernelGGL(c8_to_nhwc_kernel, dim3((total + 255) / 256), dim3(256), 0, st, in, out, B, H, W, bf);
   return hipGetLastError();
 }
 

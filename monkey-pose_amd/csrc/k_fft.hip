@@ -72,9 +72,9 @@ struct cpx {
 __device__ __forceinline__ cpx unpack_bf2(uint32_t u) {   // bf16 -> fp32 is exact: the high half
   return {__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)};
 }
-// hGRU state maps of the FFT path (O, I, Og and the B half-step's P2): fp32 C8, or -- BM, the
-// MP_DTYPE_BF16 default -- bf16 C8 at the same element index (half the bytes; round to nearest
-// even on store, exact on load).  The drive X (conv_3 output) and the final NHWC output stay fp32.
+// hGRU maps of the FFT path (the drive X, the states O, I, Og and the B half-step's P2): fp32 C8,
+// or -- BM, the MP_DTYPE_BF16 default -- bf16 C8 at the same element index (half the bytes; round
+// to nearest even on store, exact on load).  The final NHWC output for fc_1 stays fp32.
 template <bool BM>
 __device__ __forceinline__ f32x4 map_ld4(const float* base, size_t idx) {
   if constexpr (BM) {
@@ -448,7 +448,7 @@ __global__ __launch_bounds__(192, 2) void fft_inv_a_fwd_kernel(const void* __res
         const int i = min(i0 + u * 192 + tid, 64 * 64 - 1);
         const int yy = min(i >> 6, H - 1), x = min(i & 63, W - 1);
         const size_t idx = c8_index(b, q, yy, x, e0, H, W);
-        xv[u] = *reinterpret_cast<const f32x4*>(p.X + idx);
+        xv[u] = map_ld4<BM>(p.X, idx);
         ov[u] = map_ld4<BM>(p.O, idx);
       }
 #pragma unroll

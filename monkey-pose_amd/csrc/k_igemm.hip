@@ -15,9 +15,6 @@
 
 #include <algorithm>
 #include <cstdlib>
-#ifndef HX_EXP
-#define HX_EXP 0
-#endif
 
 namespace mp {
 
@@ -808,12 +805,10 @@ __global__ __launch_bounds__(256, 2) void igemm_x3h_kernel(IgemmArgs p, HaloGeom
           wc[g][nb][0] = wnx[g][nb][0];
           wc[g][nb][1] = wnx[g][nb][1];
         }
-#if HX_EXP != 1
       if (t + 1 < KS * KS)
         load_w(c, t + 1, wnx);
       else if (c + 1 < nchunk)
         load_w(c + 1, 0, wnx);
-#endif
       const int toff = ((t / KS) * hg.WW + t % KS) * HX_PITCH;
       if (wave_on) {
 #pragma unroll
@@ -828,13 +823,9 @@ __global__ __launch_bounds__(256, 2) void igemm_x3h_kernel(IgemmArgs p, HaloGeom
           for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
             for (int mb = 0; mb < 2; ++mb) {
-#if HX_EXP == 2
-              acc[mb][nb][0] += (float)wc[g][nb][1][0] * (float)ah[mb][1] + (float)wc[g][nb][0][2] * (float)al[mb][3];
-#else
               acc[mb][nb] = mfma16(wc[g][nb][1], ah[mb], acc[mb][nb]);
               acc[mb][nb] = mfma16(wc[g][nb][0], al[mb], acc[mb][nb]);
               acc[mb][nb] = mfma16(wc[g][nb][0], ah[mb], acc[mb][nb]);
-#endif
             }
         }
       }

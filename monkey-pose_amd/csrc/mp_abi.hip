@@ -224,6 +224,9 @@ void ensure_ws(mp_ctx* c, int64_t n, int64_t H, int64_t W) {
 }
 
 
+// MP_DTYPE_BF16 keeps the FFT loop's maps (X, O, I, Og, P2) in bf16 (k_fft.hip map_ld4)
+bool bf16_maps(const mp_ctx* c) { return c->dtype == MP_DTYPE_BF16 && fft_bf16_maps(); }
+
 // one association-field conv p_r * a.src with its fused hGRU epilogue, in the context's precision
 void eCRF_conv(mp_ctx* c, int epi, const ConvArgs& a, int n, hipStream_t st) {
   if (c->dtype == MP_DTYPE_F32_SPLIT)
@@ -282,9 +285,9 @@ void fft_circuit_range(mp_ctx* c, int b0, int n, int H, int W, int T, float* fin
   const size_t m = (size_t)b0 * 64 * H * W;              // elements per image of a C8 / NHWC map
   void* S = static_cast<char*>(c->specS.p) + fft_spec_bytes(b0);
   void* Y = static_cast<char*>(c->specY.p) + fft_spec_bytes(b0);
-  // state maps O, I, Og, P2 (bf16 under MP_DTYPE_BF16, k_fft.hip map_ld4): the same element
-  // offset, in units of their element type; X and the NHWC output stay fp32
-  const bool bm = c->dtype == MP_DTYPE_BF16 && fft_bf16_maps();
+  // maps X, O, I, Og, P2 (bf16 under MP_DTYPE_BF16, k_fft.hip map_ld4): the same element offset,
+  // in units of their element type; the NHWC output stays fp32
+  const bool bm = bf16_maps(c);
   auto map = [&](DevBuf& buf) { return bm ? reinterpret_cast<float*>(reinterpret_cast<uint16_t*>(buf.p) + m) : buf.f() + m; };
   float* P = map(c->specP);
   for (int t = 0; t < T; ++t) {
@@ -293,7 +296,7 @@ void fft_circuit_range(mp_ctx* c, int b0, int n, int H, int W, int T, float* fin
     a.W = W;
     a.src = map(c->Og);
     a.dst = map(c->I);
-    a.X = c->X.f() + m;
+    a.X = map(c->X);
     a.O = map(c->O);
     a.vecs = c->vecs.f();
     ConvArgs b{};
@@ -634,6 +637,7 @@ int mp_hgru_pose_fwd_taps(mp_ctx* ctx, const float* depth, int64_t n, int64_t h,
       a.src = ctx->bufB.f();
       a.wpk = ctx->conv3_pk.v4();
       a.dst = ctx->X.f();
+      a.dst_bf16 = bf16_maps(ctx) ? 1 : 0;
       a.bias = ctx->conv3_b.f();
       a.bn_s = ctx->bn2_s.f();
       a.bn_t = ctx->bn2_t.f();
@@ -643,7 +647,7 @@ int mp_hgru_pose_fwd_taps(mp_ctx* ctx, const float* depth, int64_t n, int64_t h,
     }
     if (tp.pool1) hip_check(launch_c8_to_nhwc(ctx->bufA.f(), tp.pool1, N, H, W, st), "pool1 tap");
     if (tp.conv2) hip_check(launch_c8_to_nhwc(ctx->bufB.f(), tp.conv2, N, H, W, st), "conv2 tap");
-    if (tp.conv3) hip_check(launch_c8_to_nhwc(ctx->X.f(), tp.conv3, N, H, W, st), "conv3 tap");
+    if (tp.conv3) hip_check(launch_c8_to_nhwc(ctx->X.f(), tp.conv3, N, H, W, st, bf16_maps(ctx)), "conv3 tap");
     run_circuit(ctx, n, H, W, ctx->timesteps, o0, ctx->fcin.f(), st);
     if (tp.hgru)
       hip_check(hipMemcpyAsync(tp.hgru, ctx->fcin.f(), (size_t)N * ctx->fc1_in * sizeof(float),
@@ -704,7 +708,7 @@ int mp_hgru_circuit_fwd(mp_ctx* ctx, const float* x, const float* o0, int64_t n,
     hip_check(hipSetDevice(ctx->device), "hipSetDevice");
     hipStream_t st = static_cast<hipStream_t>(stream);
     ensure_ws(ctx, n, h, w);
-    hip_check(launch_nhwc_to_c8(x, ctx->X.f(), (int)n, (int)h, (int)w, st), "nhwc_to_c8");
+    hip_check(launch_nhwc_to_c8(x, ctx->X.f(), (int)n, (int)h, (int)w, st, bf16_maps(ctx)), "nhwc_to_c8");
     if (ctx->model == MP_MODEL_HGRU_POSE) {
       // the pose context's output affine is BN_3: use identity by running with a temporary copy
       fail(MP_ERR_UNSUPPORTED, "use an MP_MODEL_HGRU_CIRCUIT context for the standalone circuit");

@@ -20,6 +20,17 @@ __device__ __forceinline__ size_t c8_index(int b, int q, int y, int x, int e, in
   return ((((size_t)b * NQ + q) * H + y) * W + x) * 8 + e;
 }
 
+// bf16 C8 maps (MP_DTYPE_BF16's hGRU maps): 4 channels = 8 bytes, round to nearest even on store
+__device__ __forceinline__ uint2 bf16x4_pack(f32x4 v) {
+  typedef __bf16 bf2_t __attribute__((ext_vector_type(2)));
+  const bf2_t a = {(__bf16)v[0], (__bf16)v[1]}, b = {(__bf16)v[2], (__bf16)v[3]};
+  return uint2{__builtin_bit_cast(uint32_t, a), __builtin_bit_cast(uint32_t, b)};
+}
+__device__ __forceinline__ f32x4 bf16x4_unpack(uint2 u) {
+  return f32x4{__uint_as_float(u.x << 16), __uint_as_float(u.x & 0xffff0000u), __uint_as_float(u.y << 16),
+               __uint_as_float(u.y & 0xffff0000u)};
+}
+
 // v_mfma_f32_32x32x2_f32: exact fp32 (fma chain), 64 cycles issue per SIMD.
 // A lane l: A[i=l&31][k=l>>5];  B lane l: B[k=l>>5][j=l&31];
 // D lane l: D[i=(r&3)+8(r>>2)+4(l>>5)][j=l&31], r = 0..15.

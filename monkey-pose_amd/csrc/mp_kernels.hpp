@@ -28,6 +28,7 @@ struct ConvArgs {
   int mode;               // B: 0 = next-step gate, 1 = final step
   int H, W, tiles_x, tiles_y;
   float ascale;           // f16x3 kernel: activation split scale (0 = the hGRU default 2^10)
+  int dst_bf16;           // BB: dst is a bf16 C8 map (MP_DTYPE_BF16's hGRU drive X)
 };
 
 // k_conv64.hip
@@ -37,8 +38,9 @@ hipError_t launch_gate_init(const float* O0, float* O, float* Og, const f32x4* g
 hipError_t launch_conv1_pool_bn(const float* in, const float* w, const float* bias, const float* s,
                                 const float* t, float* out, int B, int Hin, int Win, hipStream_t st,
                                 bool nhwc = false);
-hipError_t launch_nhwc_to_c8(const float* in, float* out, int B, int H, int W, hipStream_t st);
-hipError_t launch_c8_to_nhwc(const float* in, float* out, int B, int H, int W, hipStream_t st);
+// bf: the C8 side is a bf16 map
+hipError_t launch_nhwc_to_c8(const float* in, float* out, int B, int H, int W, hipStream_t st, bool bf = false);
+hipError_t launch_c8_to_nhwc(const float* in, float* out, int B, int H, int W, hipStream_t st, bool bf = false);
 hipError_t launch_pack_conv64(const float* w, f32x4* out, int ks, hipStream_t st);
 hipError_t launch_pack_gate(const float* g, f32x4* out, hipStream_t st);
 // k_conv64x3.hip (fp32-accurate split-f16 MFMA path)
