@@ -33,7 +33,9 @@ __device__ __forceinline__ f32x16 mfma16(f16x8 a, f16x8 b, f32x16 c) {
 // each).  SCHED selects the tap-loop schedule: 0 = fragments loaded at the top of each tap and
 // left to the compiler; 1 = one-tap-ahead prefetch with the halo reads of M-block m pinned right
 // after its MFMAs (sched_group_barrier).
-template <int KS, int EPI, int NW, int SCHED>
+// NP = 3: the fp32-accurate split (hi*lo, lo*hi, hi*hi); NP = 1: hi*hi only (MP_DTYPE_BF16's
+// backbone: one f16 product per MAC, 11-bit operands, fp32 accumulation)
+template <int KS, int EPI, int NW, int SCHED, int NP = 3>
 __global__ __launch_bounds__(NW * 64, 1) void conv64x3_kernel(ConvArgs p, const f16x8* __restrict__ wpk,
                                                               float unscale) {
   constexpr int R = KS / 2;
@@ -80,7 +82,7 @@ __global__ __launch_bounds__(NW * 64, 1) void conv64x3_kernel(ConvArgs p, const 
         }
       }
       halo[(hy * 4 + hh) * HX + hx] = vh;
-      halo[(hy * 4 + 2 + hh) * HX + hx] = vl;
+      if constexpr (NP == 3) halo[(hy * 4 + 2 + hh) * HX + hx] = vl;
     }
     __syncthreads();
 
@@ -96,11 +98,13 @@ __global__ __launch_bounds__(NW * 64, 1) void conv64x3_kernel(ConvArgs p, const 
 #pragma unroll
           for (int m = 0; m < MB; ++m) {
             const f16x8 ch = hrow[m * 4 * HX + kx];
-            const f16x8 cl = hrow[m * 4 * HX + 2 * HX + kx];
-            acc[0][m] = mfma16(w0, cl, acc[0][m]);
-            acc[1][m] = mfma16(w2, cl, acc[1][m]);
-            acc[0][m] = mfma16(w1, ch, acc[0][m]);
-            acc[1][m] = mfma16(w3, ch, acc[1][m]);
+            if constexpr (NP == 3) {
+              const f16x8 cl = hrow[m * 4 * HX + 2 * HX + kx];
+              acc[0][m] = mfma16(w0, cl, acc[0][m]);
+              acc[1][m] = mfma16(w2, cl, acc[1][m]);
+              acc[0][m] = mfma16(w1, ch, acc[0][m]);
+              acc[1][m] = mfma16(w3, ch, acc[1][m]);
+            }
             acc[0][m] = mfma16(w0, ch, acc[0][m]);
             acc[1][m] = mfma16(w2, ch, acc[1][m]);
           }
@@ -116,7 +120,7 @@ __global__ __launch_bounds__(NW * 64, 1) void conv64x3_kernel(ConvArgs p, const 
 #pragma unroll
       for (int m = 0; m < MB; ++m) {
         bh[m] = hb[m * 4 * HX];
-        bl[m] = hb[m * 4 * HX + 2 * HX];
+        bl[m] = NP == 3 ? hb[m * 4 * HX + 2 * HX] : f16x8{};
       }
       int nky = 0, nkx = 0;
       for (int tap = 0; tap < KK; ++tap) {
@@ -135,17 +139,19 @@ __global__ __launch_bounds__(NW * 64, 1) void conv64x3_kernel(ConvArgs p, const 
 #pragma unroll
         for (int m = 0; m < MB; ++m) {
           const f16x8 ch = bh[m], cl = bl[m];
-          acc[0][m] = mfma16(cw[0], cl, acc[0][m]);
-          acc[1][m] = mfma16(cw[2], cl, acc[1][m]);
-          acc[0][m] = mfma16(cw[1], ch, acc[0][m]);
-          acc[1][m] = mfma16(cw[3], ch, acc[1][m]);
+          if constexpr (NP == 3) {
+            acc[0][m] = mfma16(cw[0], cl, acc[0][m]);
+            acc[1][m] = mfma16(cw[2], cl, acc[1][m]);
+            acc[0][m] = mfma16(cw[1], ch, acc[0][m]);
+            acc[1][m] = mfma16(cw[3], ch, acc[1][m]);
+          }
           acc[0][m] = mfma16(cw[0], ch, acc[0][m]);
           acc[1][m] = mfma16(cw[2], ch, acc[1][m]);
           bh[m] = hn[m * 4 * HX];
-          bl[m] = hn[m * 4 * HX + 2 * HX];
+          if constexpr (NP == 3) bl[m] = hn[m * 4 * HX + 2 * HX];
           if (m == 0) __builtin_amdgcn_sched_group_barrier(0x020, 4, 0);   // the 4 weight loads
-          __builtin_amdgcn_sched_group_barrier(0x008, 6, 0);               // 6 MFMA
-          __builtin_amdgcn_sched_group_barrier(0x100, 2, 0);               // 2 ds_read
+          __builtin_amdgcn_sched_group_barrier(0x008, 2 * NP, 0);          // 6 (2) MFMA
+          __builtin_amdgcn_sched_group_barrier(0x100, NP == 3 ? 2 : 1, 0); // 2 (1) ds_read
         }
       }
     }
@@ -183,10 +189,10 @@ __global__ void pack_conv64x3_kernel(const float* __restrict__ w, f16x8* out, in
   dst[64] = lv;
 }
 
-template <int KS, int EPI, int NW, int SCHED>
+template <int KS, int EPI, int NW, int SCHED, int NP = 3>
 static hipError_t launch_x3_t(const ConvArgs& a, const void* wpk, float unscale, int B, hipStream_t st) {
   const int nblk = B * a.tiles_x * a.tiles_y;
-  hipLaunchKernelGGL((conv64x3_kernel<KS, EPI, NW, SCHED>), dim3(nblk), dim3(NW * 64), 0, st, a,
+  hipLaunchKernelGGL((conv64x3_kernel<KS, EPI, NW, SCHED, NP>), dim3(nblk), dim3(NW * 64), 0, st, a,
                      static_cast<const f16x8*>(wpk), unscale);
   return hipGetLastError();
 }
@@ -194,10 +200,15 @@ static hipError_t launch_x3_t(const ConvArgs& a, const void* wpk, float unscale,
 // the production variant per kernel size (chosen with tools/bench_conv.hip)
 constexpr int X3_NW = 8, X3_SCHED = 1;
 
-hipError_t launch_conv64x3(int ks, int epi, ConvArgs a, const void* wpk, float unscale, int B, hipStream_t st) {
+hipError_t launch_conv64x3(int ks, int epi, ConvArgs a, const void* wpk, float unscale, int B, hipStream_t st,
+                           int nprod) {
   a.tiles_x = a.W / TW;
   a.tiles_y = a.H / TH3;
   if (a.ascale == 0.f) a.ascale = ACT_SCALE;
+  if (nprod == 1) {
+    if (ks == 3 && epi == EPI_BB) return launch_x3_t<3, EPI_BB, X3_NW, X3_SCHED, 1>(a, wpk, unscale, B, st);
+    return hipErrorInvalidValue;
+  }
 #define MP_CASE(K, E) \
   if (ks == K && epi == E) return launch_x3_t<K, E, X3_NW, X3_SCHED>(a, wpk, unscale, B, st);
   MP_CASE(15, EPI_HGRU_A)

@@ -631,7 +631,8 @@ int mp_hgru_pose_fwd_taps(mp_ctx* ctx, const float* depth, int64_t n, int64_t h,
       a.bn_t = ctx->bn1_t.f();
       const bool x3 = ctx->dtype != MP_DTYPE_F32 && H % TH3 == 0;
       if (x3) a.ascale = BB_ASCALE;
-      hip_check(x3 ? launch_conv64x3(3, EPI_BB, a, ctx->conv2_pk.p, ctx->conv2_us, N, st)
+      const int np = ctx->dtype == MP_DTYPE_BF16 ? 1 : 3;   // bf16: one f16 product per MAC
+      hip_check(x3 ? launch_conv64x3(3, EPI_BB, a, ctx->conv2_pk.p, ctx->conv2_us, N, st, np)
                    : launch_conv64(3, EPI_BB, a, N, st),
                 "conv_2");
       a.src = ctx->bufB.f();
@@ -641,7 +642,7 @@ int mp_hgru_pose_fwd_taps(mp_ctx* ctx, const float* depth, int64_t n, int64_t h,
       a.bias = ctx->conv3_b.f();
       a.bn_s = ctx->bn2_s.f();
       a.bn_t = ctx->bn2_t.f();
-      hip_check(x3 ? launch_conv64x3(3, EPI_BB, a, ctx->conv3_pk.p, ctx->conv3_us, N, st)
+      hip_check(x3 ? launch_conv64x3(3, EPI_BB, a, ctx->conv3_pk.p, ctx->conv3_us, N, st, np)
                    : launch_conv64(3, EPI_BB, a, N, st),
                 "conv_3");
     }

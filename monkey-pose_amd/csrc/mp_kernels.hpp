@@ -45,7 +45,9 @@ hipError_t launch_pack_conv64(const float* w, f32x4* out, int ks, hipStream_t st
 hipError_t launch_pack_gate(const float* g, f32x4* out, hipStream_t st);
 // k_conv64x3.hip (fp32-accurate split-f16 MFMA path)
 constexpr int TH3 = 32;
-hipError_t launch_conv64x3(int ks, int epi, ConvArgs a, const void* wpk, float unscale, int B, hipStream_t st);
+// nprod = 1: one f16 product per MAC (EPI_BB only; MP_DTYPE_BF16's backbone)
+hipError_t launch_conv64x3(int ks, int epi, ConvArgs a, const void* wpk, float unscale, int B, hipStream_t st,
+                           int nprod = 3);
 hipError_t launch_pack_conv64x3(const float* w, void* out, int ks, float wscale, hipStream_t st);
 // k_fft.hip (FFT path of the association-field conv, MP_DTYPE_F32_FFT; maps up to 64x64)
 constexpr int FFT_MAX_HW = 64;
