@@ -598,13 +598,18 @@ __global__ __launch_bounds__(256, 2) void spec_gemm_kernel(const uint4* __restri
 // bf16 spectral GEMM (MP_DTYPE_BF16): the same blocking, fragments and XCD placement as
 // spec_gemm_kernel with 16-byte spectra entries (one bf16 (re, im) pair per channel): a block's S
 // tile is 32 images x 16 cq x 64 B, one v_mfma_f32_32x32x16_bf16 per (k-step, co block, re|im row
-// half), weights Gb[f][cq][co] (bf16x8 = 4 complex), Y written as bf16 pairs.
+// half), weights Gb[f][cq][co] (bf16x8 = 4 complex), Y written as bf16 pairs.  A quad's 64-B piece
+// is half a 128-B line, so the two quads of a line (2k, 2k+1) run on one XCD, one after the other
+// in dispatch order: with quad q on XCD q % 8 (the fp32 kernel's placement) every S / Y line was
+// moved by two L2s (PMC: 1.76x the algorithmic reads).
+constexpr int NQ16 = (NQUAD + 15) / 16;
 constexpr int SGB_YLD = 16 * 4 + 1;    // Y tile pitch (16-B units) per image
 __global__ __launch_bounds__(256, 2) void spec_gemm_bf_kernel(const uint4* __restrict__ S, const uint4* __restrict__ Gb,
                                                               uint4* __restrict__ Y, int B, int ngrp) {
   __shared__ uint4 tile[16 * 4 * SG_SLD];   // 33,792 B (S tile [cq][f][b]; Y tile [b][cq][f])
-  const int q8 = blockIdx.x / (8 * ngrp), rem = blockIdx.x - q8 * 8 * ngrp;
-  const int grp = rem >> 3, quad = q8 * 8 + (rem & 7);
+  // block -> (quad, image group): XCD x = rem % 8 takes the quad pair (2x, 2x+1) of each 16
+  const int q16 = blockIdx.x / (16 * ngrp), rem = blockIdx.x - q16 * 16 * ngrp;
+  const int sq = rem >> 3, grp = sq >> 1, quad = q16 * 16 + 2 * (rem & 7) + (sq & 1);
   if (quad >= NQUAD) return;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, j = lane & 31;
   const int img0 = grp * SG_NI;
@@ -1069,7 +1074,7 @@ hipError_t launch_spec_gemm(const void* S, const void* Gx, void* Y, int B, float
   const int ngrp = (B + SG_NI - 1) / SG_NI;
   const int nq8 = (NQUAD + 7) / 8;
   if (bf)
-    hipLaunchKernelGGL(spec_gemm_bf_kernel, dim3(nq8 * 8 * ngrp), dim3(256), 0, st, static_cast<const uint4*>(S),
+    hipLaunchKernelGGL(spec_gemm_bf_kernel, dim3(NQ16 * 16 * ngrp), dim3(256), 0, st, static_cast<const uint4*>(S),
                        static_cast<const uint4*>(Gx), static_cast<uint4*>(Y), B, ngrp);
   else
     hipLaunchKernelGGL(spec_gemm_kernel<0>, dim3(nq8 * 8 * ngrp), dim3(256), 0, st, static_cast<const uint4*>(S),
