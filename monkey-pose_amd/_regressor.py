@@ -70,9 +70,9 @@ class RegressorBase:
 
     def _dtype(self) -> str:
         dt = {'auto': 'fp32_split', 'fp32_split': 'fp32_split', 'f32_split': 'fp32_split',
-              'fp32': 'fp32', 'f32': 'fp32'}.get(self.compute_dtype)
+              'fp32': 'fp32', 'f32': 'fp32', 'bf16': 'bf16'}.get(self.compute_dtype)
         if dt is None:
-            raise ValueError(f"regressor compute_dtype must be 'auto', 'fp32_split' or 'fp32', "
+            raise ValueError(f"regressor compute_dtype must be 'auto', 'fp32_split', 'fp32' or 'bf16', "
                              f"got {self.compute_dtype!r}")
         return dt
 

@@ -142,7 +142,9 @@ __device__ __forceinline__ f32x16 mfma16(f16x8 a, f16x8 b, f32x16 c) {
 
 constexpr int IGX_LD = IG_BK + 8;   // f16 pitch of the hi / lo planes (+16 B: conflict-free b128 reads)
 
-template <int NB>
+// NP (every f16 split kernel below): 3 = the fp32-accurate hi*lo + lo*hi + hi*hi products; 1 = hi*hi
+// only (MP_DTYPE_BF16 regressors: one f16 MFMA per MAC, the lo planes neither staged nor loaded)
+template <int NB, int NP>
 __global__ __launch_bounds__(256) void igemm_x3_kernel(IgemmArgs p, const f16x8* __restrict__ wpk, float unscale) {
   __shared__ _Float16 Ah[IG_BM * IGX_LD], Al[IG_BM * IGX_LD];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, col = lane & 31;
@@ -205,7 +207,7 @@ __global__ __launch_bounds__(256) void igemm_x3_kernel(IgemmArgs p, const f16x8*
         const int nbc = min(nb0 + nb, N32 - 1);
         const f16x8* wp = wpk + (((size_t)kb * N32 + nbc) * 2) * 64 + lane;
         w[g][nb][0] = wp[0];
-        w[g][nb][1] = wp[64];
+        if constexpr (NP == 3) w[g][nb][1] = wp[64];
       }
     }
   };
@@ -229,7 +231,7 @@ __global__ __launch_bounds__(256) void igemm_x3_kernel(IgemmArgs p, const f16x8*
         lv[s] = (_Float16)(av[i][s] - (float)hv[s]);
       }
       *reinterpret_cast<f16x4*>(Ah + row * IGX_LD + k4) = hv;
-      *reinterpret_cast<f16x4*>(Al + row * IGX_LD + k4) = lv;
+      if constexpr (NP == 3) *reinterpret_cast<f16x4*>(Al + row * IGX_LD + k4) = lv;
     }
     f16x8 wc[2][NB][2];
 #pragma unroll
@@ -253,8 +255,10 @@ __global__ __launch_bounds__(256) void igemm_x3_kernel(IgemmArgs p, const f16x8*
 #pragma unroll
       for (int nb = 0; nb < NB; ++nb) {
         if (nb0 + nb >= N32) break;   // block-uniform
-        acc[nb] = mfma16(wc[g][nb][1], ah, acc[nb]);
-        acc[nb] = mfma16(wc[g][nb][0], al, acc[nb]);
+        if constexpr (NP == 3) {
+          acc[nb] = mfma16(wc[g][nb][1], ah, acc[nb]);
+          acc[nb] = mfma16(wc[g][nb][0], al, acc[nb]);
+        }
         acc[nb] = mfma16(wc[g][nb][0], ah, acc[nb]);
       }
     }
@@ -292,6 +296,7 @@ __global__ __launch_bounds__(256) void igemm_x3_kernel(IgemmArgs p, const f16x8*
 // loop visits only the taps inside the image for them.  Separate from igemm_x3w_kernel: the extra
 // index arithmetic costs the row-major kernel 1.5-3 % (measured same-box A/B).
 constexpr bool PM = true;
+template <int NP>
 __global__ __launch_bounds__(256) void igemm_x3w_pm_kernel(IgemmArgs p, const f16x8* __restrict__ wpk, float unscale) {
   __shared__ _Float16 Ah[IG_BM * IGX_LD], Al[IG_BM * IGX_LD];
   __shared__ f16x8 Ws[2 * 4 * 2 * 64];   // [k16 g][cout block nb][part][lane]
@@ -397,7 +402,7 @@ __global__ __launch_bounds__(256) void igemm_x3w_pm_kernel(IgemmArgs p, const f1
     for (int u = 0; u < 4; ++u) {
       const int e = tid + 256 * u, l = e & 63, part = (e >> 6) & 1, nb = (e >> 7) & 3, g = e >> 9;
       const int kb = min((k0 >> 4) + g, K16 - 1), nbc = min(nb0 + nb, N32 - 1);
-      w[u] = wpk[(((size_t)kb * N32 + nbc) * 2 + part) * 64 + l];
+      if (NP == 3 || part == 0) w[u] = wpk[(((size_t)kb * N32 + nbc) * 2 + part) * 64 + l];
     }
   };
 
@@ -426,7 +431,7 @@ __global__ __launch_bounds__(256) void igemm_x3w_pm_kernel(IgemmArgs p, const f1
         lv[s] = (_Float16)(av[i][s] - (float)hv[s]);
       }
       *reinterpret_cast<f16x4*>(Ah + row * IGX_LD + k4) = hv;
-      *reinterpret_cast<f16x4*>(Al + row * IGX_LD + k4) = lv;
+      if constexpr (NP == 3) *reinterpret_cast<f16x4*>(Al + row * IGX_LD + k4) = lv;
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) Ws[tid + 256 * u] = wnx[u];
@@ -452,8 +457,10 @@ __global__ __launch_bounds__(256) void igemm_x3w_pm_kernel(IgemmArgs p, const f1
           const f16x8 wl = Ws[((g * 4 + 2 * wn + nb) * 2 + 1) * 64 + lane];
 #pragma unroll
           for (int mb = 0; mb < 2; ++mb) {
-            acc[mb][nb] = mfma16(wl, ah[mb], acc[mb][nb]);
-            acc[mb][nb] = mfma16(wh, al[mb], acc[mb][nb]);
+            if constexpr (NP == 3) {
+              acc[mb][nb] = mfma16(wl, ah[mb], acc[mb][nb]);
+              acc[mb][nb] = mfma16(wh, al[mb], acc[mb][nb]);
+            }
             acc[mb][nb] = mfma16(wh, ah[mb], acc[mb][nb]);
           }
         }
@@ -537,6 +544,7 @@ __global__ __launch_bounds__(256) void igemm_pm_reduce_kernel(IgemmArgs p, int S
 // instead of being loaded by every wave from L1 (4x fewer weight loads than igemm_x3_kernel, whose
 // waves each own 32 pixels x 128 channels), and every weight fragment read from LDS feeds two
 // pixel blocks.  Same operand split, packing, K pipeline and epilogue as igemm_x3_kernel.
+template <int NP>
 __global__ __launch_bounds__(256) void igemm_x3w_kernel(IgemmArgs p, const f16x8* __restrict__ wpk, float unscale) {
   __shared__ _Float16 Ah[IG_BM * IGX_LD], Al[IG_BM * IGX_LD];
   __shared__ f16x8 Ws[2 * 4 * 2 * 64];   // [k16 g][cout block nb][part][lane]
@@ -600,7 +608,7 @@ __global__ __launch_bounds__(256) void igemm_x3w_kernel(IgemmArgs p, const f16x8
     for (int u = 0; u < 4; ++u) {
       const int e = tid + 256 * u, l = e & 63, part = (e >> 6) & 1, nb = (e >> 7) & 3, g = e >> 9;
       const int kb = min((k0 >> 4) + g, K16 - 1), nbc = min(nb0 + nb, N32 - 1);
-      w[u] = wpk[(((size_t)kb * N32 + nbc) * 2 + part) * 64 + l];
+      if (NP == 3 || part == 0) w[u] = wpk[(((size_t)kb * N32 + nbc) * 2 + part) * 64 + l];
     }
   };
 
@@ -626,7 +634,7 @@ __global__ __launch_bounds__(256) void igemm_x3w_kernel(IgemmArgs p, const f16x8
         lv[s] = (_Float16)(av[i][s] - (float)hv[s]);
       }
       *reinterpret_cast<f16x4*>(Ah + row * IGX_LD + k4) = hv;
-      *reinterpret_cast<f16x4*>(Al + row * IGX_LD + k4) = lv;
+      if constexpr (NP == 3) *reinterpret_cast<f16x4*>(Al + row * IGX_LD + k4) = lv;
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) Ws[tid + 256 * u] = wnx[u];
@@ -652,8 +660,10 @@ __global__ __launch_bounds__(256) void igemm_x3w_kernel(IgemmArgs p, const f16x8
           const f16x8 wl = Ws[((g * 4 + 2 * wn + nb) * 2 + 1) * 64 + lane];
 #pragma unroll
           for (int mb = 0; mb < 2; ++mb) {
-            acc[mb][nb] = mfma16(wl, ah[mb], acc[mb][nb]);
-            acc[mb][nb] = mfma16(wh, al[mb], acc[mb][nb]);
+            if constexpr (NP == 3) {
+              acc[mb][nb] = mfma16(wl, ah[mb], acc[mb][nb]);
+              acc[mb][nb] = mfma16(wh, al[mb], acc[mb][nb]);
+            }
             acc[mb][nb] = mfma16(wh, ah[mb], acc[mb][nb]);
           }
         }
@@ -709,7 +719,7 @@ struct HaloGeom {
   int R, NI, HH, WW, PH;   // rows per tile, images per tile, halo rows / cols per image, halo pixels
 };
 
-template <int KS>
+template <int KS, int NP>
 __global__ __launch_bounds__(256, 2) void igemm_x3h_kernel(IgemmArgs p, HaloGeom hg, const f16x8* __restrict__ wpk,
                                                           float unscale) {
   extern __shared__ _Float16 hs[];   // [2][PH][HX_PITCH]
@@ -755,7 +765,7 @@ __global__ __launch_bounds__(256, 2) void igemm_x3h_kernel(IgemmArgs p, HaloGeom
       }
       _Float16* d = hs + buf * bufsz + hp * HX_PITCH + 4 * q;
       *reinterpret_cast<f16x4*>(d) = hv;
-      *reinterpret_cast<f16x4*>(d + 32) = lv;
+      if constexpr (NP == 3) *reinterpret_cast<f16x4*>(d + 32) = lv;
     }
   };
   // this wave's weight fragments of (chunk c, tap t): [g][nb][hi|lo]
@@ -767,7 +777,7 @@ __global__ __launch_bounds__(256, 2) void igemm_x3h_kernel(IgemmArgs p, HaloGeom
         const int kb = (t * p.Cin + c * 32) / 16 + g, nbc = min(nb0 + 2 * wn + nb, N32 - 1);
         const f16x8* src = wpk + ((size_t)kb * N32 + nbc) * 2 * 64 + lane;
         w[g][nb][0] = src[0];
-        w[g][nb][1] = src[64];
+        if constexpr (NP == 3) w[g][nb][1] = src[64];
       }
   };
 
@@ -823,8 +833,10 @@ __global__ __launch_bounds__(256, 2) void igemm_x3h_kernel(IgemmArgs p, HaloGeom
           for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
             for (int mb = 0; mb < 2; ++mb) {
-              acc[mb][nb] = mfma16(wc[g][nb][1], ah[mb], acc[mb][nb]);
-              acc[mb][nb] = mfma16(wc[g][nb][0], al[mb], acc[mb][nb]);
+              if constexpr (NP == 3) {
+                acc[mb][nb] = mfma16(wc[g][nb][1], ah[mb], acc[mb][nb]);
+                acc[mb][nb] = mfma16(wc[g][nb][0], al[mb], acc[mb][nb]);
+              }
               acc[mb][nb] = mfma16(wc[g][nb][0], ah[mb], acc[mb][nb]);
             }
         }
@@ -995,23 +1007,29 @@ hipError_t launch_igemm_x3(const IgemmArgs& a, const void* wpk, float unscale, h
   const int nb = N32 >= 4 ? 4 : (N32 >= 2 ? 2 : 1);
   dim3 grid((M + IG_BM - 1) / IG_BM, (N32 + nb - 1) / nb);
   const f16x8* w = static_cast<const f16x8*>(wpk);
+  const bool one = a.nprod == 1;   // MP_DTYPE_BF16: one f16 product per MAC
   if (wide_path(a)) {
     HaloGeom hg;
     size_t lds = 0;
     if (halo_geom(a, hg, lds)) {
       static const bool attr = [] {
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(igemm_x3h_kernel<3>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
-        (void)hipFuncSetAttribute(reinterpret_cast<const void*>(igemm_x3h_kernel<5>),
-                                  hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
+        for (const void* f : {reinterpret_cast<const void*>(igemm_x3h_kernel<3, 3>),
+                              reinterpret_cast<const void*>(igemm_x3h_kernel<5, 3>),
+                              reinterpret_cast<const void*>(igemm_x3h_kernel<3, 1>),
+                              reinterpret_cast<const void*>(igemm_x3h_kernel<5, 1>)})
+          (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
         return true;
       }();
       (void)attr;
       const dim3 hgrid((M + IG_BM - 1) / IG_BM, (N32 + 3) / 4);
-      if (a.KS == 3)
-        hipLaunchKernelGGL(igemm_x3h_kernel<3>, hgrid, dim3(256), lds, st, a, hg, w, unscale);
+      if (a.KS == 3 && one)
+        hipLaunchKernelGGL((igemm_x3h_kernel<3, 1>), hgrid, dim3(256), lds, st, a, hg, w, unscale);
+      else if (a.KS == 3)
+        hipLaunchKernelGGL((igemm_x3h_kernel<3, 3>), hgrid, dim3(256), lds, st, a, hg, w, unscale);
+      else if (one)
+        hipLaunchKernelGGL((igemm_x3h_kernel<5, 1>), hgrid, dim3(256), lds, st, a, hg, w, unscale);
       else
-        hipLaunchKernelGGL(igemm_x3h_kernel<5>, hgrid, dim3(256), lds, st, a, hg, w, unscale);
+        hipLaunchKernelGGL((igemm_x3h_kernel<5, 3>), hgrid, dim3(256), lds, st, a, hg, w, unscale);
       return hipGetLastError();
     }
     IgemmArgs b = a;
@@ -1022,25 +1040,38 @@ hipError_t launch_igemm_x3(const IgemmArgs& a, const void* wpk, float unscale, h
       // reduce with the epilogue -- 4x the blocks for the under-filled small-map convs (hier con_6:
       // 256 blocks of 128 x 128 on 256 CUs otherwise)
       const dim3 sgrid((M + IG_BM - 1) / IG_BM, (N32 + 3) / 4, S);
-      hipLaunchKernelGGL(igemm_x3w_pm_kernel, sgrid, dim3(256), 0, st, b, w, unscale);
+      if (one)
+        hipLaunchKernelGGL(igemm_x3w_pm_kernel<1>, sgrid, dim3(256), 0, st, b, w, unscale);
+      else
+        hipLaunchKernelGGL(igemm_x3w_pm_kernel<3>, sgrid, dim3(256), 0, st, b, w, unscale);
       const size_t total = (size_t)M * (N32 * 8);
       hipLaunchKernelGGL(igemm_pm_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, b, S, unscale);
       return hipGetLastError();
     }
     b.part = nullptr;
     const dim3 wgrid((M + IG_BM - 1) / IG_BM, (N32 + 3) / 4);
-    if (b.pmajor)
-      hipLaunchKernelGGL(igemm_x3w_pm_kernel, wgrid, dim3(256), 0, st, b, w, unscale);
+    if (b.pmajor && one)
+      hipLaunchKernelGGL(igemm_x3w_pm_kernel<1>, wgrid, dim3(256), 0, st, b, w, unscale);
+    else if (b.pmajor)
+      hipLaunchKernelGGL(igemm_x3w_pm_kernel<3>, wgrid, dim3(256), 0, st, b, w, unscale);
+    else if (one)
+      hipLaunchKernelGGL(igemm_x3w_kernel<1>, wgrid, dim3(256), 0, st, b, w, unscale);
     else
-      hipLaunchKernelGGL(igemm_x3w_kernel, wgrid, dim3(256), 0, st, b, w, unscale);
+      hipLaunchKernelGGL(igemm_x3w_kernel<3>, wgrid, dim3(256), 0, st, b, w, unscale);
     return hipGetLastError();
   }
-  if (nb == 4)
-    hipLaunchKernelGGL(igemm_x3_kernel<4>, grid, dim3(256), 0, st, a, w, unscale);
+  if (nb == 4 && one)
+    hipLaunchKernelGGL((igemm_x3_kernel<4, 1>), grid, dim3(256), 0, st, a, w, unscale);
+  else if (nb == 4)
+    hipLaunchKernelGGL((igemm_x3_kernel<4, 3>), grid, dim3(256), 0, st, a, w, unscale);
+  else if (nb == 2 && one)
+    hipLaunchKernelGGL((igemm_x3_kernel<2, 1>), grid, dim3(256), 0, st, a, w, unscale);
   else if (nb == 2)
-    hipLaunchKernelGGL(igemm_x3_kernel<2>, grid, dim3(256), 0, st, a, w, unscale);
+    hipLaunchKernelGGL((igemm_x3_kernel<2, 3>), grid, dim3(256), 0, st, a, w, unscale);
+  else if (one)
+    hipLaunchKernelGGL((igemm_x3_kernel<1, 1>), grid, dim3(256), 0, st, a, w, unscale);
   else
-    hipLaunchKernelGGL(igemm_x3_kernel<1>, grid, dim3(256), 0, st, a, w, unscale);
+    hipLaunchKernelGGL((igemm_x3_kernel<1, 3>), grid, dim3(256), 0, st, a, w, unscale);
   return hipGetLastError();
 }
 

@@ -540,8 +540,9 @@ int mp_finalize_weights(mp_ctx* ctx, int compute_dtype) {
     if (compute_dtype != MP_DTYPE_F32 && compute_dtype != MP_DTYPE_F32_SPLIT && compute_dtype != MP_DTYPE_F32_FFT &&
         compute_dtype != MP_DTYPE_BF16)
       fail(MP_ERR_UNSUPPORTED, "compute_dtype must be MP_DTYPE_F32, _F32_SPLIT, _F32_FFT or MP_DTYPE_BF16");
-    if (ctx->model >= MP_MODEL_DENSE && compute_dtype != MP_DTYPE_F32 && compute_dtype != MP_DTYPE_F32_SPLIT)
-      fail(MP_ERR_UNSUPPORTED, "regressor contexts run MP_DTYPE_F32 or MP_DTYPE_F32_SPLIT");
+    if (ctx->model >= MP_MODEL_DENSE && compute_dtype != MP_DTYPE_F32 && compute_dtype != MP_DTYPE_F32_SPLIT &&
+        compute_dtype != MP_DTYPE_BF16)
+      fail(MP_ERR_UNSUPPORTED, "regressor contexts run MP_DTYPE_F32, MP_DTYPE_F32_SPLIT or MP_DTYPE_BF16");
     if (compute_dtype != ctx->dtype) {   // workspace layout depends on the path
       ctx->cap_batch = 0;
       ctx->cap_hw = 0;

@@ -398,6 +398,7 @@ void plan(mp_ctx* c, G& g, int64_t n, int64_t h, int64_t w) {
       a.pad_t = same_pad_before(S.H, L.k, op.stride);
       a.pad_l = same_pad_before(S.W, L.k, op.stride);
       a.relu = 1;
+      a.nprod = L.nprod;
       k->L = &L;
       if (L.x3) {   // split-K workspace of the position-major small-map path (k_igemm.hip)
         const size_t pf = igemm_pm_part_floats(a);
@@ -546,7 +547,8 @@ void launch_kern(mp_ctx* c, G& g, G::Kern& k, hipStream_t st) {
       ProfScope pl(c, st, g.ops[k.op].name.c_str());
       const auto& L = *k.L;
       const int M = (int)g.pn;
-      hip_check(L.x3 ? launch_fc_gemm_x3(k.fa, k.fK, L.w.p, L.wus, k.part.f(), M, k.fK, k.fN, k.fS, k.fks, st)
+      hip_check(L.x3 ? launch_fc_gemm_x3(k.fa, k.fK, L.w.p, L.wus, k.part.f(), M, k.fK, k.fN, k.fS, k.fks, st,
+                                         L.nprod)
                      : launch_fc_gemm(k.fa, k.fK, L.w.v4(), k.part.f(), M, k.fK, k.fN, k.fS, k.fks, st),
                 g.ops[k.op].name.c_str());
       hip_check(launch_fc_reduce(k.part.f(), k.fS, M, k.fN, L.b.f(), k.relu ? 1 : 0, nullptr, nullptr, k.fout,

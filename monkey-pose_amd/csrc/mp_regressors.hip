@@ -140,6 +140,7 @@ void conv(mp_ctx* c, const std::string& name, int n, const View& in, const View&
   a.pad_t = same_pad_before(in.H, L.k, stride);
   a.pad_l = same_pad_before(in.W, L.k, stride);
   a.relu = 1;
+  a.nprod = L.nprod;
   hip_check(L.x3 ? launch_igemm_x3(a, L.w.p, L.wus, st) : launch_igemm_conv(a, st), name.c_str());
 }
 
@@ -160,7 +161,7 @@ void fcl(mp_ctx* c, const std::string& name, int n, const float* in, int K, floa
   int ks;
   const int S = fc_choose_splits(n, K, L.cout, &ks);
   float* part = buf(c, "fc_part", (size_t)S * n * ((L.cout + 31) / 32 * 32));
-  hip_check(L.x3 ? launch_fc_gemm_x3(in, K, L.w.p, L.wus, part, n, K, L.cout, S, ks, st)
+  hip_check(L.x3 ? launch_fc_gemm_x3(in, K, L.w.p, L.wus, part, n, K, L.cout, S, ks, st, L.nprod)
                  : launch_fc_gemm(in, K, L.w.v4(), part, n, K, L.cout, S, ks, st),
             name.c_str());
   hip_check(launch_fc_reduce(part, S, n, L.cout, L.b.f(), relu ? 1 : 0, aff_s, aff_t, out, ldo, st),
@@ -353,7 +354,9 @@ bool known_name_regressor(int model, const std::string& n) {
 // a conv (HWIO as [K][Cout]) or fc ([K][N]) weight in the context's precision: fp32 fragments, or
 // the f16x3 split under MP_DTYPE_F32_SPLIT when the x3 kernel takes the shape (x3_ok)
 void pack_matrix(mp_ctx* c, mp_ctx::PackedLayer& L, const float* w, bool x3_ok) {
-  L.x3 = c->dtype == MP_DTYPE_F32_SPLIT && x3_ok;
+  // MP_DTYPE_BF16 keeps the split packing and runs its hi x hi product only (L.nprod = 1)
+  L.x3 = (c->dtype == MP_DTYPE_F32_SPLIT || c->dtype == MP_DTYPE_BF16) && x3_ok;
+  L.nprod = c->dtype == MP_DTYPE_BF16 ? 1 : 3;
   if (L.x3) {
     L.w.alloc(fc_x3_bytes(L.K, L.cout));
     hip_check(launch_pack_fc_x3(w, L.w.p, L.K, L.cout, &L.wus, nullptr), "pack (f16x3)");

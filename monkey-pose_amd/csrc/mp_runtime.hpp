@@ -142,8 +142,9 @@ struct mp_ctx {
     DevBuf w, b;          // conv: HWIO as [K][Cout] packed like an FC weight; fc: [in][out] packed
     DevBuf bn_s, bn_t;    // attention net: the folded BN that follows this layer (after pool / relu)
     int k = 0, cin = 0, cout = 0, K = 0;
-    bool x3 = false;      // MP_DTYPE_F32_SPLIT: w holds the f16x3 packing (launch_pack_fc_x3)
+    bool x3 = false;      // MP_DTYPE_F32_SPLIT / _BF16: w holds the f16x3 packing (launch_pack_fc_x3)
     float wus = 1.f;      // its 1 / weight scale
+    int nprod = 3;        // products per MAC: 3 (fp32-accurate split) or 1 (MP_DTYPE_BF16: hi x hi)
   };
   std::map<std::string, PackedLayer> layers;   // keyed by layer name ("conv_3_1", "p_fc_2", ...)
   std::map<std::string, DevBuf> ws;            // named activation buffers

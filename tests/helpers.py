@@ -24,6 +24,7 @@ HGRU_POSE_AUX = {
 
 # fp32 parity gate of SURVEY.md 8d / BASELINE.md: ||out - ref||_inf / ||ref||_inf <= 1e-4
 FP32_REL_TOL = 1e-4
+BF16_REL_TOL = 5e-2   # stated gate of every bf16 path (bf16 cannot meet 1e-4)
 
 
 def golden_meta():

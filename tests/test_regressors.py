@@ -3,7 +3,7 @@ regressors: CPU oracle pinned to the golden vectors, GPU path (C ABI) against or
 import numpy as np
 import pytest
 
-from helpers import FP32_REL_TOL, MG, golden_array, golden_meta, pkg, rel_inf
+from helpers import BF16_REL_TOL, FP32_REL_TOL, MG, golden_array, golden_meta, pkg, rel_inf
 from oracle import regressors_ref as RR
 
 
@@ -127,3 +127,26 @@ def test_dense_recorded_graph_uses_the_dense_variables():
     g = m.record(128, 128, 69)
     W = pkg().weights
     assert {v.name: v.shape for v in m._table(g)} == {v.name: v.shape for v in W.dense_vars()}
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("engine", ["graph", "abi"])
+@pytest.mark.parametrize("kind", ["dense", "hier"])
+def test_regressors_bf16_within_bf16_gate(kind, engine):
+    """compute_dtype='bf16': the split kernels' hi x hi product only (one f16 MFMA per MAC), fp32
+    accumulation; stated gate 5e-2 like the hGRU bf16 path, batch invariance kept."""
+    torch = pytest.importorskip("torch")
+    case = f"{kind}_c128"
+    m, (wts, depth) = _inputs(case)
+    P = pkg()
+    model = (P.train_dense_networks.dense_model_struct(use_graph=engine == "graph") if kind == "dense"
+             else P.train_hier_networks.hier_model_struct(use_graph=engine == "graph"))
+    model.compute_dtype = "bf16"
+    model.load_weights(wts)
+    args = (69,) if kind == "dense" else MG.HIER_HEADS
+    out = model.build(torch.from_numpy(depth).cuda(), *args, train_mode=False).cpu().numpy()
+    err = rel_inf(out, golden_array(case, "out"))
+    print(f"bf16 {kind} {engine}: rel_inf {err:.3e}")
+    assert err <= BF16_REL_TOL
+    one = model.forward(torch.from_numpy(depth[1:2]).cuda()).cpu().numpy()
+    assert np.array_equal(one[0], out[1])

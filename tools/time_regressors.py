@@ -1,0 +1,37 @@
+"""Times the dense / hier / dense-hier regressors (layer-graph runtime, default streams) at batch B
+for each compute dtype.  usage: python tools/time_regressors.py [B] [dtype ...]
+(dtypes: fp32_split, bf16, fp32; synthetic weights and crops)."""
+import importlib
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import torch  # noqa: E402
+
+mp = importlib.import_module("monkey-pose_amd")
+W = mp.weights
+B = int(sys.argv[1]) if len(sys.argv) > 1 else 256
+dtypes = sys.argv[2:] or ["fp32_split", "bf16"]
+x = torch.from_numpy(W.synth_crops(B, seed=42, size=128)).cuda()
+models = {
+    "dense": (mp.train_dense_networks.dense_model_struct, (69,), 3.22),
+    "hier": (mp.train_hier_networks.hier_model_struct, (108, 39, 39, 39, 39, 36), 7.97),
+    "dense_hier": (mp.train_dense_hier_networks.dense_hier_model_struct, (108, 39, 39, 39, 39, 36), 5.081),
+}
+for name, (cls, args, gf) in models.items():
+    for dt in dtypes:
+        m = cls()
+        m.compute_dtype = dt
+        m.build(x, *args, train_mode=False)
+        for _ in range(3):
+            m.forward(x)
+        torch.cuda.synchronize()
+        n = 10
+        t0 = time.perf_counter()
+        for _ in range(n):
+            m.forward(x)
+        torch.cuda.synchronize()
+        t = (time.perf_counter() - t0) / n
+        print(f"{name:10s} {dt:10s} B={B}: {t * 1e3:7.3f} ms  {B / t:9.1f} crops/s  "
+              f"{gf * B / t / 1e3:6.1f} fp32-equiv TFLOP/s", flush=True)
