@@ -140,6 +140,26 @@ __device__ __forceinline__ f32x16 mfma16(f16x8 a, f16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
 }
 
+// XCD-aware tile order for the wide / halo / position-major kernels.  Workgroups are dispatched in
+// linear order round-robin over the 8 XCDs, each with its own L2; with the plain (blockIdx.x = M
+// tile, blockIdx.y = N tile) order every XCD touched every weight panel and every input row, and
+// the PMC counters showed the HBM reads at 2-8x the input (halo) and 80x the weights (hier con_6).
+// Here XCD x takes the contiguous virtual range [x T/8, (x+1) T/8) of the T tiles: N-fastest
+// (n_major = false: a block's neighbours share its input rows) or M-fastest (n_major = true: they
+// share its weight panel).  Identity when T % 8 != 0 or p.xcd == 0.
+__device__ __forceinline__ void xcd_tile(const IgemmArgs& p, bool n_major, int& mt, int& nt) {
+  const int nM = (int)gridDim.x, nN = (int)gridDim.y, T = nM * nN;
+  const int L = (int)blockIdx.x + nM * (int)blockIdx.y;
+  const int v = (p.xcd && T % 8 == 0) ? (L % 8) * (T / 8) + L / 8 : L;
+  if (n_major) {
+    nt = v / nM;
+    mt = v - nt * nM;
+  } else {
+    mt = v / nN;
+    nt = v - mt * nN;
+  }
+}
+
 constexpr int IGX_LD = IG_BK + 8;   // f16 pitch of the hi / lo planes (+16 B: conflict-free b128 reads)
 
 // NP (every f16 split kernel below): 3 = the fp32-accurate hi*lo + lo*hi + hi*hi products; 1 = hi*hi
@@ -304,8 +324,10 @@ __global__ __launch_bounds__(256) void igemm_x3w_pm_kernel(IgemmArgs p, const f1
   const int wm = wv & 1, wn = wv >> 1;   // this wave: pixels 64 wm .. +63, cout blocks 2 wn, 2 wn + 1
   const int HWo = p.Ho * p.Wo;
   const int M = p.N * HWo;
-  const int m0 = blockIdx.x * IG_BM;
-  const int nb0 = blockIdx.y * 4;
+  int mt_, nt_;
+  xcd_tile(p, true, mt_, nt_);   // blocks of one weight panel share an L2
+  const int m0 = mt_ * IG_BM;
+  const int nb0 = nt_ * 4;
   const int N32 = (p.Cout + 31) / 32;
   const int K16 = (p.K + 15) / 16;
   const bool vec = (p.Cin % 4 == 0) && (p.cix % 4 == 0) && (p.ldx % 4 == 0);
@@ -552,8 +574,10 @@ __global__ __launch_bounds__(256) void igemm_x3w_kernel(IgemmArgs p, const f16x8
   const int wm = wv & 1, wn = wv >> 1;   // this wave: pixels 64 wm .. +63, cout blocks 2 wn, 2 wn + 1
   const int HWo = p.Ho * p.Wo;
   const int M = p.N * HWo;
-  const int m0 = blockIdx.x * IG_BM;
-  const int nb0 = blockIdx.y * 4;
+  int mt_, nt_;
+  xcd_tile(p, false, mt_, nt_);   // neighbouring tiles share input rows
+  const int m0 = mt_ * IG_BM;
+  const int nb0 = nt_ * 4;
   const int N32 = (p.Cout + 31) / 32;
   const int K16 = (p.K + 15) / 16;
   const bool vec = (p.Cin % 4 == 0) && (p.cix % 4 == 0) && (p.ldx % 4 == 0);
@@ -727,8 +751,10 @@ __global__ __launch_bounds__(256, 2) void igemm_x3h_kernel(IgemmArgs p, HaloGeom
   const int wm = wv & 1, wn = wv >> 1;
   const int HW = p.H * p.W;
   const int M = p.N * HW;
-  const int m0 = blockIdx.x * IG_BM;
-  const int nb0 = blockIdx.y * 4;
+  int mt_, nt_;
+  xcd_tile(p, false, mt_, nt_);   // neighbouring row tiles share halo rows
+  const int m0 = mt_ * IG_BM;
+  const int nb0 = nt_ * 4;
   const int N32 = (p.Cout + 31) / 32;
   const int pad = KS / 2;
   const int n0 = m0 / HW, y0 = (m0 - n0 * HW) / p.W;   // first image / row of the tile
@@ -1008,6 +1034,7 @@ hipError_t launch_igemm_x3(const IgemmArgs& a, const void* wpk, float unscale, h
   dim3 grid((M + IG_BM - 1) / IG_BM, (N32 + nb - 1) / nb);
   const f16x8* w = static_cast<const f16x8*>(wpk);
   const bool one = a.nprod == 1;   // MP_DTYPE_BF16: one f16 product per MAC
+  static const int xcd = env_flag("MP_IGEMM_XCD", 1);
   if (wide_path(a)) {
     HaloGeom hg;
     size_t lds = 0;
@@ -1022,17 +1049,20 @@ hipError_t launch_igemm_x3(const IgemmArgs& a, const void* wpk, float unscale, h
       }();
       (void)attr;
       const dim3 hgrid((M + IG_BM - 1) / IG_BM, (N32 + 3) / 4);
+      IgemmArgs h = a;
+      h.xcd = xcd;
       if (a.KS == 3 && one)
-        hipLaunchKernelGGL((igemm_x3h_kernel<3, 1>), hgrid, dim3(256), lds, st, a, hg, w, unscale);
+        hipLaunchKernelGGL((igemm_x3h_kernel<3, 1>), hgrid, dim3(256), lds, st, h, hg, w, unscale);
       else if (a.KS == 3)
-        hipLaunchKernelGGL((igemm_x3h_kernel<3, 3>), hgrid, dim3(256), lds, st, a, hg, w, unscale);
+        hipLaunchKernelGGL((igemm_x3h_kernel<3, 3>), hgrid, dim3(256), lds, st, h, hg, w, unscale);
       else if (one)
-        hipLaunchKernelGGL((igemm_x3h_kernel<5, 1>), hgrid, dim3(256), lds, st, a, hg, w, unscale);
+        hipLaunchKernelGGL((igemm_x3h_kernel<5, 1>), hgrid, dim3(256), lds, st, h, hg, w, unscale);
       else
-        hipLaunchKernelGGL((igemm_x3h_kernel<5, 3>), hgrid, dim3(256), lds, st, a, hg, w, unscale);
+        hipLaunchKernelGGL((igemm_x3h_kernel<5, 3>), hgrid, dim3(256), lds, st, h, hg, w, unscale);
       return hipGetLastError();
     }
     IgemmArgs b = a;
+    b.xcd = xcd;
     b.pmajor = pm_path(a) ? 1 : 0;
     const int S = b.pmajor && a.part ? igemm_pm_splits(a) : 1;
     if (S > 1) {

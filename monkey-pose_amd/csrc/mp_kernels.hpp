@@ -90,6 +90,7 @@ struct IgemmArgs {
   float* part = nullptr;   // position-major split-K workspace (igemm_pm_splits(a) x M x Cout32
                            // floats, caller-owned); null: no split
   int nprod = 3;           // f16 split kernels: 3 = fp32-accurate f16x3, 1 = hi x hi only (bf16 dtype)
+  int xcd = 0;             // set by the launcher: XCD-aware tile order (k_igemm.hip xcd_tile)
 };
 // input-channel splits of the position-major tap-skipping path for this conv (1 = none); a property
 // of the layer alone (never of the batch), so every crop's sums group the same way at any batch
