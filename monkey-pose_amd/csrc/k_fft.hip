@@ -101,6 +101,11 @@ __device__ __forceinline__ cpx map_ld2(const float* base, size_t idx) {
     return {t.x, t.y};
   }
 }
+// sigmoid / tanh on v_exp_f32 + v_rcp_f32 (absolute error ~1e-7).  The A epilogue keeps ocml's
+// tanhf: ftanh there measured no faster (inv_a_fwd is not VALU-bound) and raised the FFT path's
+// error 6.1e-7 -> 8.1e-7
+__device__ __forceinline__ float fsigmoid(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
+__device__ __forceinline__ float ftanh(float x) { return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __expf(2.f * x)); }
 __device__ __forceinline__ cpx operator+(cpx a, cpx b) { return {a.x + b.x, a.y + b.y}; }
 __device__ __forceinline__ cpx operator-(cpx a, cpx b) { return {a.x - b.x, a.y - b.y}; }
 __device__ __forceinline__ cpx scale(cpx a, float s) { return {a.x * s, a.y * s}; }
@@ -749,8 +754,6 @@ __global__ void spec_pack_bf_kernel(const cpx* __restrict__ G, uint4* __restrict
 // v_rcp_f32 (abs error ~1e-7).
 constexpr float GATE_VSCALE = 256.0f;   // activations entering a gate: |v| < 255 stays in f16 range
 
-__device__ __forceinline__ float fsigmoid(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
-__device__ __forceinline__ float ftanh(float x) { return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __expf(2.f * x)); }
 
 // Y[n2] = sum_cin G[cin][32 n2 + row] V[cin][pixel], f16x3; gpk = [n2][s][hi|lo][lane] f16x8
 __device__ __forceinline__ void gate_x3(const f16x8* __restrict__ gpk, const f32x16 (&V)[2], f32x16 (&Y)[2],
