@@ -175,7 +175,7 @@ constexpr int FCX_LD = FC_BK + 8;   // f16 pitch of the hi / lo activation plane
 // MAC and only the hi weight planes are read (half the weight bytes), f16 operands (11-bit
 // mantissa, finer than bf16), fp32 accumulation
 template <int NP>
-__global__ __launch_bounds__(256) void fc_gemm_x3_kernel(const float* __restrict__ A, int lda,
+__global__ __launch_bounds__(256, 3) void fc_gemm_x3_kernel(const float* __restrict__ A, int lda,
                                                          const f16x8* __restrict__ Wpk,
                                                          float* __restrict__ part, int M, int K,
                                                          int N32, int kslice, float unscale, int S) {

@@ -165,7 +165,7 @@ constexpr int IGX_LD = IG_BK + 8;   // f16 pitch of the hi / lo planes (+16 B: c
 // NP (every f16 split kernel below): 3 = the fp32-accurate hi*lo + lo*hi + hi*hi products; 1 = hi*hi
 // only (MP_DTYPE_BF16 regressors: one f16 MFMA per MAC, the lo planes neither staged nor loaded)
 template <int NB, int NP>
-__global__ __launch_bounds__(256) void igemm_x3_kernel(IgemmArgs p, const f16x8* __restrict__ wpk, float unscale) {
+__global__ __launch_bounds__(256, NB == 4 ? 2 : 3) void igemm_x3_kernel(IgemmArgs p, const f16x8* __restrict__ wpk, float unscale) {
   __shared__ _Float16 Ah[IG_BM * IGX_LD], Al[IG_BM * IGX_LD];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, col = lane & 31;
   const int HWo = p.Ho * p.Wo;
@@ -317,7 +317,7 @@ __global__ __launch_bounds__(256) void igemm_x3_kernel(IgemmArgs p, const f16x8*
 // index arithmetic costs the row-major kernel 1.5-3 % (measured same-box A/B).
 constexpr bool PM = true;
 template <int NP>
-__global__ __launch_bounds__(256) void igemm_x3w_pm_kernel(IgemmArgs p, const f16x8* __restrict__ wpk, float unscale) {
+__global__ __launch_bounds__(256, 3) void igemm_x3w_pm_kernel(IgemmArgs p, const f16x8* __restrict__ wpk, float unscale) {
   __shared__ _Float16 Ah[IG_BM * IGX_LD], Al[IG_BM * IGX_LD];
   __shared__ f16x8 Ws[2 * 4 * 2 * 64];   // [k16 g][cout block nb][part][lane]
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, col = lane & 31;
@@ -567,7 +567,7 @@ __global__ __launch_bounds__(256) void igemm_pm_reduce_kernel(IgemmArgs p, int S
 // waves each own 32 pixels x 128 channels), and every weight fragment read from LDS feeds two
 // pixel blocks.  Same operand split, packing, K pipeline and epilogue as igemm_x3_kernel.
 template <int NP>
-__global__ __launch_bounds__(256) void igemm_x3w_kernel(IgemmArgs p, const f16x8* __restrict__ wpk, float unscale) {
+__global__ __launch_bounds__(256, 3) void igemm_x3w_kernel(IgemmArgs p, const f16x8* __restrict__ wpk, float unscale) {
   __shared__ _Float16 Ah[IG_BM * IGX_LD], Al[IG_BM * IGX_LD];
   __shared__ f16x8 Ws[2 * 4 * 2 * 64];   // [k16 g][cout block nb][part][lane]
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, col = lane & 31;
