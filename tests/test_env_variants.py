@@ -1,0 +1,60 @@
+"""The A/B switches read once at library load (MP_BF16_MAPS, MP_IGEMM_PM_SPLITS, MP_IGEMM_XCD,
+MP_IGEMM_HALO) keep their paths correct: each case runs in one child process with the switch set
+(the parent's library already made its choice), against the committed golden vectors."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+_CHILD = r"""
+import json, sys
+sys.path.insert(0, {tests!r})
+import torch
+from helpers import MG, golden_array, golden_meta, pkg, rel_inf
+kind, dtype = {kind!r}, {dtype!r}
+meta = golden_meta()
+P = pkg()
+if kind == "pose":
+    m = meta["pose_c64_t8"]
+    wts, depth, O0 = MG.pose_inputs(m["n"], m["crop"], m["timesteps"], m["weight_seed"], m["crop_seed"], m["o0_seed"])
+    model = P.hgru_pose.model()
+    model.compute_dtype = dtype
+    model.load_weights(wts)
+    out = model.build(torch.from_numpy(depth).cuda(), m["output_shape"], train_mode=False,
+                      h2_init=torch.from_numpy(O0).cuda()).cpu().numpy()
+    ref = golden_array("pose_c64_t8", "out")
+else:
+    m = meta["hier_c128"]
+    wts, depth = MG.regressor_inputs(m["kind"], m["n"], m["crop"], m["weight_seed"], m["crop_seed"])
+    model = P.train_hier_networks.hier_model_struct()
+    model.compute_dtype = dtype
+    model.load_weights(wts)
+    out = model.build(torch.from_numpy(depth).cuda(), *MG.HIER_HEADS, train_mode=False).cpu().numpy()
+    ref = golden_array("hier_c128", "out")
+print(json.dumps({{"err": float(rel_inf(out, ref))}}))
+"""
+
+CASES = [
+    # (env, model, dtype, gate)
+    ({"MP_BF16_MAPS": "0"}, "pose", "bf16", 5e-2),
+    ({"MP_IGEMM_PM_SPLITS": "4"}, "hier", "fp32_split", 1e-4),
+    ({"MP_IGEMM_PM_SPLITS": "4"}, "hier", "bf16", 5e-2),
+    ({"MP_IGEMM_XCD": "0", "MP_IGEMM_HALO": "0"}, "hier", "fp32_split", 1e-4),
+]
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("env,kind,dtype,gate", CASES,
+                         ids=[f"{'+'.join(f'{k}={v}' for k, v in e.items())}-{k}-{d}" for e, k, d, _ in CASES])
+def test_switch_keeps_parity(env, kind, dtype, gate):
+    code = _CHILD.format(tests=os.path.join(ROOT, "tests"), kind=kind, dtype=dtype)
+    r = subprocess.run([sys.executable, "-c", code], env={**os.environ, **env}, capture_output=True, text=True,
+                       timeout=110)
+    assert r.returncode == 0, r.stderr[-2000:]
+    err = json.loads(r.stdout.strip().splitlines()[-1])["err"]
+    print(f"{env} {kind} {dtype}: rel_inf {err:.3e}")
+    assert err <= gate, err
