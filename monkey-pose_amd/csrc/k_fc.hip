@@ -174,14 +174,17 @@ constexpr int FCX_LD = FC_BK + 8;   // f16 pitch of the hi / lo activation plane
 // NP = 3: the fp32-accurate f16x3 product; NP = 1 (dtype bf16's fc_1): hi x hi only -- one MFMA per
 // MAC and only the hi weight planes are read (half the weight bytes), f16 operands (11-bit
 // mantissa, finer than bf16), fp32 accumulation
-template <int NP>
+// MB: 32-row m-blocks per block (4 = 128 rows; small batches take 1 or 2 so the MFMAs of empty rows
+// and their staging are not paid: fc_1 at batch 1 / 64)
+template <int NP, int MB>
 __global__ __launch_bounds__(256, 3) void fc_gemm_x3_kernel(const float* __restrict__ A, int lda,
                                                          const f16x8* __restrict__ Wpk,
                                                          float* __restrict__ part, int M, int K,
                                                          int N32, int kslice, float unscale, int S) {
-  __shared__ _Float16 Ah[FC_BM * FCX_LD], Al[FC_BM * FCX_LD];
+  constexpr int BM = 32 * MB;
+  __shared__ _Float16 Ah[BM * FCX_LD], Al[BM * FCX_LD];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, col = lane & 31;
-  const FcTile tl = fc_tile((M + FC_BM - 1) / FC_BM, (N32 + 3) / 4);
+  const FcTile tl = fc_tile((M + BM - 1) / BM, (N32 + 3) / 4);
   if (tl.split >= S) return;
   const int mt = tl.mt, ntile = tl.nt, split = tl.split;
   const int K16 = (K + 15) / 16;
@@ -192,11 +195,11 @@ __global__ __launch_bounds__(256, 3) void fc_gemm_x3_kernel(const float* __restr
   const int kbeg = split * kslice;
   const int kend = min(K, kbeg + kslice);
 
-  auto load_act = [&](int k0, f32x4 (&v)[4]) {
+  auto load_act = [&](int k0, f32x4 (&v)[MB]) {
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < MB; ++i) {
       const int e = tid + i * 256, row = e >> 3, k4 = (e & 7) * 4;
-      const int gm = mt * FC_BM + row;   // K % FC_BK == 0 (launcher): every step is interior
+      const int gm = mt * BM + row;   // K % FC_BK == 0 (launcher): every step is interior
       v[i] = *reinterpret_cast<const f32x4*>(A + (size_t)min(gm, M - 1) * lda + k0 + k4);
       if (gm >= M) v[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
@@ -211,10 +214,10 @@ __global__ __launch_bounds__(256, 3) void fc_gemm_x3_kernel(const float* __restr
     }
   };
 
-  f32x16 acc[4];
+  f32x16 acc[MB];
 #pragma unroll
-  for (int m = 0; m < 4; ++m) acc[m] = f32x16{};
-  f32x4 av[4];
+  for (int m = 0; m < MB; ++m) acc[m] = f32x16{};
+  f32x4 av[MB];
   f16x8 wn[FC_BK / 16][2];
   if (kbeg < kend) {
     load_act(kbeg, av);
@@ -223,7 +226,7 @@ __global__ __launch_bounds__(256, 3) void fc_gemm_x3_kernel(const float* __restr
   for (int k0 = kbeg; k0 < kend; k0 += FC_BK) {
     lds_barrier();   // the previous step's LDS reads are done
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
+    for (int i = 0; i < MB; ++i) {
       const int e = tid + i * 256, row = e >> 3, k4 = (e & 7) * 4;
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
@@ -250,7 +253,7 @@ __global__ __launch_bounds__(256, 3) void fc_gemm_x3_kernel(const float* __restr
         const f16x8 wh = wc[g][0];
         [[maybe_unused]] const f16x8 wl = wc[g][1];
 #pragma unroll
-        for (int m = 0; m < 4; ++m) {
+        for (int m = 0; m < MB; ++m) {
           const int o = (m * 32 + col) * FCX_LD + 16 * g + 8 * h;
           const f16x8 ah = *reinterpret_cast<const f16x8*>(Ah + o);
           if constexpr (NP == 3) {
@@ -265,8 +268,8 @@ __global__ __launch_bounds__(256, 3) void fc_gemm_x3_kernel(const float* __restr
   }
   if (!wave_on) return;
 #pragma unroll
-  for (int m = 0; m < 4; ++m) {
-    const int gm = mt * FC_BM + m * 32 + col;
+  for (int m = 0; m < MB; ++m) {
+    const int gm = mt * BM + m * 32 + col;
     if (gm >= M) continue;
     float* dst = part + ((size_t)split * M + gm) * Npad + 32 * nb + 4 * h;
 #pragma unroll
@@ -298,13 +301,22 @@ hipError_t launch_fc_gemm_x3(const float* A, int lda, const void* Wpk, float uns
                              int N, int S, int kslice, hipStream_t st, int nprod) {
   if (K % FC_BK || kslice % FC_BK || lda % 4) return hipErrorInvalidValue;
   const int N32 = (N + 31) / 32;
-  const int grid = fc_grid((M + FC_BM - 1) / FC_BM, (N32 + 3) / 4, S);
-  if (nprod == 1)
-    hipLaunchKernelGGL(fc_gemm_x3_kernel<1>, dim3(grid), dim3(256), 0, st, A, lda, static_cast<const f16x8*>(Wpk),
-                       part, M, K, N32, kslice, unscale, S);
-  else
-    hipLaunchKernelGGL(fc_gemm_x3_kernel<3>, dim3(grid), dim3(256), 0, st, A, lda, static_cast<const f16x8*>(Wpk),
-                       part, M, K, N32, kslice, unscale, S);
+  const int mb = M <= 32 ? 1 : (M <= 64 ? 2 : 4);   // 32-row m-blocks per block
+  const int grid = fc_grid((M + 32 * mb - 1) / (32 * mb), (N32 + 3) / 4, S);
+  const f16x8* w = static_cast<const f16x8*>(Wpk);
+#define MP_FC_X3(NPV, MBV)                                                                                   \
+  hipLaunchKernelGGL((fc_gemm_x3_kernel<NPV, MBV>), dim3(grid), dim3(256), 0, st, A, lda, w, part, M, K, N32, \
+                     kslice, unscale, S)
+  if (nprod == 1) {
+    if (mb == 1) MP_FC_X3(1, 1);
+    else if (mb == 2) MP_FC_X3(1, 2);
+    else MP_FC_X3(1, 4);
+  } else {
+    if (mb == 1) MP_FC_X3(3, 1);
+    else if (mb == 2) MP_FC_X3(3, 2);
+    else MP_FC_X3(3, 4);
+  }
+#undef MP_FC_X3
   return hipGetLastError();
 }
 
