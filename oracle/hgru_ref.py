@@ -155,17 +155,41 @@ def hgru_step(X, O, t, wts, scope="cnn/contextual_circuit", return_all=False):
     return On
 
 
-def hgru_forward(X, O0, wts, timesteps=8, scope="cnn/contextual_circuit", keep_steps=False):
+def hidden_init_state(X, hidden_init="random", O0=None):
+    """The initial output state O0 of ``ContextualCircuit.build`` (hgru_module.py:875-890):
+    'identity' -> X (876-878), 'zeros' -> zeros_like(X) (888-890), 'random' -> the externally
+    supplied draw ``O0`` (879-887, DEFECT 2).  The initial I is never read (795-804)."""
+    if hidden_init == "identity":
+        return X
+    if hidden_init == "zeros":
+        return X * 0
+    if hidden_init == "random":
+        if O0 is None:
+            raise ValueError("hidden_init='random' needs the drawn O0")
+        return O0
+    raise RuntimeError(hidden_init)     # hgru_module.py:891-892
+
+
+def hgru_forward(X, O0, wts, timesteps=8, scope="cnn/contextual_circuit", keep_steps=False,
+                 keep_inputs=False):
     """``ContextualCircuit.build`` (872-954) with hidden_init='random' made explicit: ``O0`` is
     the (DEFECT 2) externally supplied initial output state; the random I0 is dead because the
     gru_gates input integration ignores the previous I (795-804).  Returns O_T (DEFECT 3: the
-    reference returns the tuple (O, weights, activities); only O is consumed)."""
+    reference returns the tuple (O, weights, activities); only O is consumed).
+    ``keep_steps``: also the per-step O_t after the rho gain, as ``store_states`` writes them
+    (912-915); ``keep_inputs`` additionally the per-step I_t -> (O, O_steps, I_steps)."""
     O = O0.astype(X.dtype)
-    steps = []
+    steps, isteps = [], []
     for t in range(timesteps):
-        O = hgru_step(X, O, t, wts, scope)
-        if keep_steps:
+        if keep_inputs:
+            O, parts = hgru_step(X, O, t, wts, scope, return_all=True)
+            isteps.append(parts["I"].copy())
+        else:
+            O = hgru_step(X, O, t, wts, scope)
+        if keep_steps or keep_inputs:
             steps.append(O.copy())
+    if keep_inputs:
+        return O, steps, isteps
     return (O, steps) if keep_steps else O
 
 
