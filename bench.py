@@ -27,7 +27,7 @@ sys.path.insert(0, ROOT)
 PEAK_FP32_TFLOPS = 157.3   # MI355X dense fp32 (MFMA = vector), MI355X_MICROARCH.md chip table
 PEAK_F16_TFLOPS = 2516.6   # MI355X dense f16/bf16 MFMA (no sparsity)
 PEAK_HBM_GBPS = 8000.0     # MI355X HBM3E
-BF16_REL_TOL = 5e-2        # stated gate of the bf16 path (bf16 cannot meet 1e-4)
+BF16_REL_TOL = 5e-3        # stated gate of the bf16 path (bf16 cannot meet 1e-4; measured ~8e-4)
 
 
 def parse():

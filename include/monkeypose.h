@@ -67,7 +67,8 @@ enum { MP_MEM_HOST = 0, MP_MEM_DEVICE = 1 };
  *                       matrix-core cycles.  Needs map height and width multiples of 32.
  *   MP_DTYPE_F32_FFT    fp32 FFT convolution on a 72x72 grid (exact circular = SAME linear conv
  *                       for maps up to 64x64): fp32 72-point FFTs + a per-frequency complex
- *                       channel GEMM on fp32 MFMA; ~50x fewer FLOPs than direct at 15x15 taps,
+ *                       channel GEMM in the f16x3 split (three v_mfma_f32_32x32x16_f16 per complex
+ *                       MAC term, fp32 accumulation); ~50x fewer FLOPs than direct at 15x15 taps,
  *                       error ~1e-6 of max|output|.  Needs map height <= 64, width 32 or 64.
  *   MP_DTYPE_BF16       the FFT path with bf16 spectra (input and output), bf16 spectral weights and
  *                       bf16 1x1 gate weights: one v_mfma_f32_32x32x16_bf16 product per MAC, fp32
@@ -107,6 +108,15 @@ int mp_finalize_weights(mp_ctx* ctx, int compute_dtype);
 /* pre-allocate the activation workspace for batches up to max_batch (otherwise grown lazily) */
 int mp_reserve(mp_ctx* ctx, int64_t max_batch);
 
+/* ContextualCircuit aux 'hidden_init' (hgru_module.py:875-892): the initial output state O0.
+ * ('random' draws a fresh xavier tensor per sess.run, hgru_module.py:879-887: the caller draws it
+ * and passes it as o0.)  The initial I is never read by the hgru_pose aux (795-804). */
+enum {
+  MP_HIDDEN_GIVEN = 0,    /* o0 as passed (hidden_init='random', made explicit)            */
+  MP_HIDDEN_ZEROS = 1,    /* O0 = zeros_like(X)                      (888-890); o0 unused */
+  MP_HIDDEN_IDENTITY = 2  /* O0 = X, the circuit's drive             (876-878); o0 unused */
+};
+
 /* hgru_pose.model.build (hgru_pose.py:47-105), inference:
  *   depth  [n, h, w, 1]   normalised depth crops (h = w = 128 in the reference)
  *   o0     [n, h/2, w/2, 64] initial hGRU output state (hidden_init='random',
@@ -126,6 +136,14 @@ typedef struct {
   float* hgru;   /* [n, h/2, w/2, 64]  BN(O_T), the fc_1 input            (81-90)   */
   float* fc1;    /* [n, 1024]          fc_1 + bias (pre-activation)       (91)      */
   float* relu1;  /* [n, 1024]          BN(relu(fc1))                      (92-103)  */
+  /* store_states (hgru_module.py:889-915): every timestep's states, [n, T, h/2, w/2, 64] NHWC
+   * (the reference's stack transposed to batch-major, 909-912).  states_O[:, t] = O_t after the
+   * rho gain, states_I[:, t] = I_t.  (The reference's own stacks swap O and I on alternate steps:
+   * full() takes (store_O, store_I) where the loop passes (store_I, store_O), hgru_module.py:825,
+   * 897-908; here each stack holds what its name says.) */
+  float* states_O;
+  float* states_I;
+  int32_t hidden_init; /* MP_HIDDEN_*: the initial state; o0 may be NULL unless MP_HIDDEN_GIVEN */
 } mp_pose_taps;
 
 /* mp_hgru_pose_fwd that also writes the requested intermediates (taps may be NULL) */
@@ -137,6 +155,13 @@ int mp_hgru_pose_fwd_taps(mp_ctx* ctx, const float* depth, int64_t n, int64_t h,
  *   timesteps <= the length of the "contextual_circuit/rho" weight */
 int mp_hgru_circuit_fwd(mp_ctx* ctx, const float* x, const float* o0, int64_t n, int64_t h,
                         int64_t w, int64_t k, int timesteps, float* o_out, void* stream);
+
+/* mp_hgru_circuit_fwd with the aux 'hidden_init' (MP_HIDDEN_*; o0 may be NULL unless
+ * MP_HIDDEN_GIVEN) and 'store_states' (hgru_module.py:889-915): states_O / states_I, each
+ * [n, timesteps, h, w, k] NHWC or NULL, receive every step's O_t (after the rho gain) and I_t */
+int mp_hgru_circuit_fwd_ex(mp_ctx* ctx, const float* x, const float* o0, int64_t n, int64_t h, int64_t w,
+                           int64_t k, int timesteps, int hidden_init, float* o_out, float* states_O,
+                           float* states_I, void* stream);
 
 /* dense_model_struct.build(depth, output_shape) -> .output  (train_dense_networks.py:223-408):
  *   depth [n, h, w, 1] (h, w multiples of 32 in the reference's 128x128), out [n, output_shape] */

@@ -75,6 +75,10 @@ _SIGS = {
                                            ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
                                            ctypes.c_int64, ctypes.c_int, ctypes.c_void_p,
                                            ctypes.c_void_p]),
+    "mp_hgru_circuit_fwd_ex": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                              ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                                              ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
+                                              ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "mp_dense_fwd": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
                                     ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
     "mp_hier_fwd": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
@@ -110,10 +114,14 @@ _lib: Optional[ctypes.CDLL] = None
 
 # mp_pose_taps field order (include/monkeypose.h)
 TAP_NAMES = ("conv1", "pool1", "conv2", "conv3", "hgru", "fc1", "relu1")
+STATE_NAMES = ("states_O", "states_I")      # store_states stacks [n, T, h/2, w/2, 64]
+
+# ContextualCircuit aux 'hidden_init' (hgru_module.py:875-892) -> MP_HIDDEN_*
+MP_HIDDEN = {"random": 0, "zeros": 1, "identity": 2}
 
 
 class PoseTaps(ctypes.Structure):
-    _fields_ = [(n, ctypes.c_void_p) for n in TAP_NAMES]
+    _fields_ = [(n, ctypes.c_void_p) for n in TAP_NAMES + STATE_NAMES] + [("hidden_init", ctypes.c_int32)]
 
 
 class MonkeyPoseError(RuntimeError):
@@ -146,8 +154,8 @@ def check(status: int) -> None:
         raise MonkeyPoseError(status, load().mp_last_error().decode())
 
 
-def _ptr(t) -> int:
-    return int(t.data_ptr())
+def _ptr(t):
+    return None if t is None else int(t.data_ptr())
 
 
 class Context:
@@ -209,17 +217,21 @@ class Context:
         check(self.lib.mp_hgru_pose_fwd(self.h, _ptr(depth), n, h, w, _ptr(o0), _ptr(out),
                                         ctypes.c_void_p(stream)))
 
-    def pose_fwd_taps(self, depth, o0, out, taps: dict, stream: int) -> None:
-        """mp_hgru_pose_fwd_taps; ``taps`` maps names of TAP_NAMES to CUDA output tensors."""
+    def pose_fwd_taps(self, depth, o0, out, taps: dict, stream: int, hidden_init: int = 0) -> None:
+        """mp_hgru_pose_fwd_taps; ``taps`` maps names of TAP_NAMES / STATE_NAMES to CUDA output
+        tensors; ``o0`` may be None unless ``hidden_init`` is MP_HIDDEN['random']."""
         n, h, w, c = depth.shape
-        t = PoseTaps(*[ctypes.c_void_p(_ptr(taps[k]) if k in taps else None) for k in TAP_NAMES])
+        t = PoseTaps(*[ctypes.c_void_p(_ptr(taps[k]) if k in taps else None) for k in TAP_NAMES + STATE_NAMES],
+                     int(hidden_init))
         check(self.lib.mp_hgru_pose_fwd_taps(self.h, _ptr(depth), n, h, w, _ptr(o0), _ptr(out),
                                              ctypes.byref(t), ctypes.c_void_p(stream)))
 
-    def circuit_fwd(self, x, o0, out, timesteps: int, stream: int) -> None:
+    def circuit_fwd(self, x, o0, out, timesteps: int, stream: int, hidden_init: int = 0, states_O=None,
+                    states_I=None) -> None:
         n, h, w, k = x.shape
-        check(self.lib.mp_hgru_circuit_fwd(self.h, _ptr(x), _ptr(o0), n, h, w, k, int(timesteps),
-                                           _ptr(out), ctypes.c_void_p(stream)))
+        check(self.lib.mp_hgru_circuit_fwd_ex(self.h, _ptr(x), _ptr(o0), n, h, w, k, int(timesteps),
+                                              int(hidden_init), _ptr(out), _ptr(states_O), _ptr(states_I),
+                                              ctypes.c_void_p(stream)))
 
     def dense_fwd(self, depth, out, stream: int) -> None:
         n, h, w, c = depth.shape

@@ -30,21 +30,26 @@ class RegressorBase:
     def __contains__(self, name):
         return hasattr(self, name)
 
-    def load_weights(self, weights: Dict[str, np.ndarray]) -> None:
+    def load_weights(self, weights: Dict[str, np.ndarray], synthesize_missing: bool = False) -> None:
+        """Variables keyed by TF name (``cnn/...``).  Like ``saver.restore`` of a checkpoint
+        (train_cnn_networks_hgru.py:248-250), every variable the model needs must be present:
+        build() raises ``KeyError`` naming the missing ones, unless ``synthesize_missing=True``
+        fills them with the seeded stand-in initialisers (``weights.synth_value``).  A model with
+        no weights loaded at all runs on those stand-ins, as the reference runs on its
+        initialisers."""
         self.weights = {(k if k.startswith("cnn/") else "cnn/" + k): v for k, v in weights.items()}
         self._ctx_key = None
-        self._strict = False
+        self._strict = not synthesize_missing
 
     def load_checkpoint(self, path: str, remap=None, strict: bool = True) -> None:
         """Weights from a TF1 V2 checkpoint (see ``hgru_pose.model.load_checkpoint``)."""
         from . import tf_checkpoint as C
         t = C.model_variables(C.read_checkpoint(path))
-        self.load_weights(remap(t) if remap else t)
-        self._strict = strict
+        self.load_weights(remap(t) if remap else t, synthesize_missing=not strict)
 
-    def load_npz(self, path: str) -> None:
+    def load_npz(self, path: str, synthesize_missing: bool = False) -> None:
         with np.load(path, allow_pickle=False) as z:
-            self.load_weights({k: z[k] for k in z.files})
+            self.load_weights({k: z[k] for k in z.files}, synthesize_missing)
 
     def _on_context(self, ctx: _lib.Context) -> None:
         """hook between mp_create and the weights of an MP_MODEL_GRAPH context (installs its graph)"""
@@ -54,9 +59,13 @@ class RegressorBase:
 
     def _resolve(self, table) -> Dict[str, np.ndarray]:
         given = dict(self.weights or {})
-        missing = [v.name for v in table if v.name not in given]
-        if missing and getattr(self, "_strict", False) and self.data_dict is None:
-            raise KeyError(f"checkpoint lacks {len(missing)} variable(s) the model needs: {missing[:8]}")
+        covered = set()
+        for layer in (self.data_dict or {}):
+            covered |= {f"cnn/{layer}/{layer}{s}" for s in ("_weights", "_biases", "_filters")}
+        missing = [v.name for v in table if v.name not in given and v.name not in covered]
+        if missing and self.weights is not None and getattr(self, "_strict", True):
+            raise KeyError(f"the loaded weights lack {len(missing)} variable(s) the model needs "
+                           f"(load_weights(..., synthesize_missing=True) fills them): {missing[:8]}")
         out = {v.name: (np.asarray(given[v.name], np.float32) if v.name in given
                         else W.synth_value(v, self.weight_seed)) for v in table}
         if self.data_dict is not None:

@@ -207,7 +207,10 @@ __global__ void nhwc_to_c8_kernel(const float* __restrict__ in, float* out, int 
   }
 }
 
-__global__ void c8_to_nhwc_kernel(const float* __restrict__ in, float* out, int B, int H, int W, bool bf) {
+// dst_img: elements between consecutive images of the NHWC output (H*W*C when dense; larger when
+// writing one timestep of a [n, T, H, W, C] state stack)
+__global__ void c8_to_nhwc_kernel(const float* __restrict__ in, float* out, int B, int H, int W, bool bf,
+                                  size_t dst_img) {
   const size_t total = (size_t)B * H * W * NQ;
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= total) return;
@@ -215,7 +218,7 @@ __global__ void c8_to_nhwc_kernel(const float* __restrict__ in, float* out, int 
   const size_t pix = i / NQ;
   const int x = pix % W, y = (pix / W) % H, b = pix / ((size_t)W * H);
   const size_t o = c8_index(b, q, y, x, 0, H, W);
-  f32x4* d = reinterpret_cast<f32x4*>(out + pix * C + 8 * q);
+  f32x4* d = reinterpret_cast<f32x4*>(out + b * dst_img + ((size_t)y * W + x) * C + 8 * q);
   if (bf) {
     const uint2* s = reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(in) + o);
     d[0] = bf16x4_unpack(s[0]);
@@ -314,9 +317,12 @@ hipError_t launch_nhwc_to_c8(const float* in, float* out, int B, int H, int W, h
   return hipGetLastError();
 }
 
-hipError_t launch_c8_to_nhwc(const float* in, float* out, int B, int H, int W, hipStream_t st, bool bf) {
+hipError_t launch_c8_to_nhwc(const float* in, float* out, int B, int H, int W, hipStream_t st, bool bf,
+                             size_t dst_img) {
   const size_t total = (size_t)B * H * W * NQ;
-  hipLaunchKernelGGL(c8_to_nhwc_kernel, dim3((total + 255) / 256), dim3(256), 0, st, in, out, B, H, W, bf);
+  if (dst_img == 0) dst_img = (size_t)H * W * C;
+  hipLaunchKernelGGL(c8_to_nhwc_kernel, dim3((total + 255) / 256), dim3(256), 0, st, in, out, B, H, W, bf,
+                     dst_img);
   return hipGetLastError();
 }
 

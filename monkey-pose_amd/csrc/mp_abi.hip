@@ -280,8 +280,27 @@ void check_map(mp_ctx* c, int64_t H, int64_t W, const char* what) {
                            " and width a multiple of 32");
 }
 
+// per-step state outputs (store_states, hgru_module.py:889-915): [batch][T][H][W][64] NHWC fp32,
+// O_t after the rho gain and I_t of each step; NULL = not wanted
+struct StateOut {
+  float* O = nullptr;
+  float* I = nullptr;
+  int T = 0;
+};
+
+// copy step t's O / I maps (C8, bf16 under MP_DTYPE_BF16 maps) of images [b0, b0 + n) into the stacks
+void store_step(const StateOut* so, const float* Omap, const float* Imap, int b0, int n, int H, int W, int t,
+                bool bf, hipStream_t st) {
+  if (!so) return;
+  const size_t img = (size_t)H * W * 64, stride = img * so->T;
+  const size_t off = (size_t)b0 * stride + (size_t)t * img;
+  if (so->O) hip_check(launch_c8_to_nhwc(Omap, so->O + off, n, H, W, st, bf, stride), "store_states O");
+  if (so->I) hip_check(launch_c8_to_nhwc(Imap, so->I + off, n, H, W, st, bf, stride), "store_states I");
+}
+
 // the hGRU loop of images [b0, b0 + n) on stream st (FFT path), all state pointers offset
-void fft_circuit_range(mp_ctx* c, int b0, int n, int H, int W, int T, float* final_dst2, hipStream_t st) {
+void fft_circuit_range(mp_ctx* c, int b0, int n, int H, int W, int T, float* final_dst2, const StateOut* so,
+                       hipStream_t st) {
   const size_t m = (size_t)b0 * 64 * H * W;              // elements per image of a C8 / NHWC map
   void* S = static_cast<char*>(c->specS.p) + fft_spec_bytes(b0);
   void* Y = static_cast<char*>(c->specY.p) + fft_spec_bytes(b0);
@@ -316,6 +335,7 @@ void fft_circuit_range(mp_ctx* c, int b0, int n, int H, int W, int T, float* fin
     hip_check(launch_spec_gemm(S, c->spec_g.p, Y, n, c->p_unscale, st, bf), "spec_gemm");
     hip_check(launch_fft_inv(Y, P, n, H, W, st, bf), "fft_inv");
     hip_check(launch_spec_epi_b(b, P, c->or_x3.p, c->or_us, c->ir_x3.p, c->ir_us, n, st, bf), "B epilogue");
+    store_step(so, b.O, b.I, b0, n, H, W, t, bm, st);
   }
 }
 
@@ -328,7 +348,7 @@ int stream_count() {
 }
 
 void run_circuit(mp_ctx* c, int64_t n, int H, int W, int T, const float* o0_nhwc, float* final_dst2,
-                 hipStream_t st) {
+                 const StateOut* so, hipStream_t st) {
   // FFT path, not profiling: batch slices are independent, so they run on separate streams and
   // their latency-bound kernels overlap (the per-kernel HIP-event profile keeps one stream)
   const int ns = std::min<int>(stream_count(), (int)(n / 32));
@@ -354,7 +374,7 @@ void run_circuit(mp_ctx* c, int64_t n, int H, int W, int T, const float* o0_nhwc
       const int cnt = std::min<int>(g * 32, (int)n - b0);
       hipStream_t s = k == 0 ? st : c->sides[k - 1];
       if (k > 0) hip_check(hipStreamWaitEvent(s, c->ev_fork, 0), "hipStreamWaitEvent");
-      fft_circuit_range(c, b0, cnt, H, W, T, final_dst2, s);
+      fft_circuit_range(c, b0, cnt, H, W, T, final_dst2, so, s);
       b0 += cnt;
     }
     for (int k = 1; k < ns; ++k) {
@@ -394,17 +414,41 @@ void run_circuit(mp_ctx* c, int64_t n, int H, int W, int T, const float* o0_nhwc
     b.dst2 = (t == T - 1) ? final_dst2 : c->Og.f();
     if (is_fft(c->dtype)) {
       fft_step(c, a, b, (int)n, st);
-      continue;
-    }
-    {
-      ProfScope ps(c, st, "conv15_a");
-      eCRF_conv(c, EPI_HGRU_A, a, (int)n, st);
-    }
-    {
+    } else {
+      {
+        ProfScope ps(c, st, "conv15_a");
+        eCRF_conv(c, EPI_HGRU_A, a, (int)n, st);
+      }
       ProfScope ps(c, st, "conv15_b");
       eCRF_conv(c, EPI_HGRU_B, b, (int)n, st);
     }
+    store_step(so, c->O.f(), c->I.f(), 0, (int)n, H, W, t, bf16_maps(c), st);
   }
+}
+
+// the initial output state for hidden_init (hgru_module.py:875-892) as an NHWC fp32 pointer:
+// MP_HIDDEN_GIVEN -> the caller's o0; ZEROS -> a zeroed workspace map; IDENTITY -> X (the
+// caller's NHWC x for the circuit, the C8 drive converted into a workspace map for the pose model)
+const float* hidden_state(mp_ctx* c, int hidden_init, const float* o0, const float* x_nhwc, int64_t n, int H, int W,
+                          hipStream_t st) {
+  const size_t bytes = (size_t)n * H * W * 64 * sizeof(float);
+  switch (hidden_init) {
+    case MP_HIDDEN_GIVEN:
+      if (!o0) fail(MP_ERR_ARG, "o0 is NULL (hidden_init = MP_HIDDEN_GIVEN)");
+      return o0;
+    case MP_HIDDEN_ZEROS:
+      c->h0.alloc(bytes);
+      hip_check(hipMemsetAsync(c->h0.p, 0, bytes, st), "hidden_init zeros");
+      return c->h0.f();
+    case MP_HIDDEN_IDENTITY:
+      if (x_nhwc) return x_nhwc;
+      c->h0.alloc(bytes);
+      hip_check(launch_c8_to_nhwc(c->X.f(), c->h0.f(), (int)n, H, W, st, bf16_maps(c)), "hidden_init identity");
+      return c->h0.f();
+    default:
+      fail(MP_ERR_ARG, "hidden_init must be MP_HIDDEN_GIVEN, MP_HIDDEN_ZEROS or MP_HIDDEN_IDENTITY");
+  }
+  return nullptr;
 }
 
 }  // namespace
@@ -576,7 +620,10 @@ int mp_reserve(mp_ctx* ctx, int64_t max_batch) {
 int mp_hgru_pose_fwd_taps(mp_ctx* ctx, const float* depth, int64_t n, int64_t h, int64_t w, const float* o0,
                           float* out, const mp_pose_taps* taps, void* stream) {
   return guard([&] {
-    if (!ctx || !depth || !o0 || !out) fail(MP_ERR_ARG, "mp_hgru_pose_fwd: null pointer");
+    mp_pose_taps tp{};
+    if (taps) tp = *taps;
+    if (!ctx || !depth || !out || (!o0 && tp.hidden_init == MP_HIDDEN_GIVEN))
+      fail(MP_ERR_ARG, "mp_hgru_pose_fwd: null pointer");
     if (ctx->model != MP_MODEL_HGRU_POSE) fail(MP_ERR_STATE, "context is not an hgru_pose model");
     if (!ctx->finalized) fail(MP_ERR_STATE, "weights not finalized");
     if (n <= 0 || n > (1 << 20)) fail(MP_ERR_SHAPE, "batch must be in [1, 2^20]");
@@ -591,8 +638,6 @@ int mp_hgru_pose_fwd_taps(mp_ctx* ctx, const float* depth, int64_t n, int64_t h,
     hipStream_t st = static_cast<hipStream_t>(stream);
     ensure_ws(ctx, n, H, W);
     const int N = (int)n;
-    mp_pose_taps tp{};
-    if (taps) tp = *taps;
     if (tp.conv1) {   // relu(conv_1) before the pool: never materialised by the fused kernel
       IgemmArgs g{};
       g.x = depth;
@@ -650,7 +695,12 @@ int mp_hgru_pose_fwd_taps(mp_ctx* ctx, const float* depth, int64_t n, int64_t h,
     if (tp.pool1) hip_check(launch_c8_to_nhwc(ctx->bufA.f(), tp.pool1, N, H, W, st), "pool1 tap");
     if (tp.conv2) hip_check(launch_c8_to_nhwc(ctx->bufB.f(), tp.conv2, N, H, W, st), "conv2 tap");
     if (tp.conv3) hip_check(launch_c8_to_nhwc(ctx->X.f(), tp.conv3, N, H, W, st, bf16_maps(ctx)), "conv3 tap");
-    run_circuit(ctx, n, H, W, ctx->timesteps, o0, ctx->fcin.f(), st);
+    const float* h0 = hidden_state(ctx, tp.hidden_init, o0, nullptr, n, H, W, st);
+    StateOut so;
+    so.O = tp.states_O;
+    so.I = tp.states_I;
+    so.T = ctx->timesteps;
+    run_circuit(ctx, n, H, W, ctx->timesteps, h0, ctx->fcin.f(), (so.O || so.I) ? &so : nullptr, st);
     if (tp.hgru)
       hip_check(hipMemcpyAsync(tp.hgru, ctx->fcin.f(), (size_t)N * ctx->fc1_in * sizeof(float),
                                hipMemcpyDeviceToDevice, st),
@@ -699,8 +749,16 @@ int mp_hgru_pose_fwd(mp_ctx* ctx, const float* depth, int64_t n, int64_t h, int6
 
 int mp_hgru_circuit_fwd(mp_ctx* ctx, const float* x, const float* o0, int64_t n, int64_t h, int64_t w,
                         int64_t k, int timesteps, float* o_out, void* stream) {
+  return mp_hgru_circuit_fwd_ex(ctx, x, o0, n, h, w, k, timesteps, MP_HIDDEN_GIVEN, o_out, nullptr, nullptr,
+                                stream);
+}
+
+int mp_hgru_circuit_fwd_ex(mp_ctx* ctx, const float* x, const float* o0, int64_t n, int64_t h, int64_t w,
+                           int64_t k, int timesteps, int hidden_init, float* o_out, float* states_O,
+                           float* states_I, void* stream) {
   return guard([&] {
-    if (!ctx || !x || !o0 || !o_out) fail(MP_ERR_ARG, "mp_hgru_circuit_fwd: null pointer");
+    if (!ctx || !x || !o_out || (!o0 && hidden_init == MP_HIDDEN_GIVEN))
+      fail(MP_ERR_ARG, "mp_hgru_circuit_fwd: null pointer");
     if (!ctx->finalized) fail(MP_ERR_STATE, "weights not finalized");
     if (k != 64) fail(MP_ERR_SHAPE, "channel count k must be 64");
     if (n <= 0 || h <= 0 || w <= 0) fail(MP_ERR_SHAPE, "empty input");
@@ -715,7 +773,12 @@ int mp_hgru_circuit_fwd(mp_ctx* ctx, const float* x, const float* o0, int64_t n,
       // the pose context's output affine is BN_3: use identity by running with a temporary copy
       fail(MP_ERR_UNSUPPORTED, "use an MP_MODEL_HGRU_CIRCUIT context for the standalone circuit");
     }
-    run_circuit(ctx, n, (int)h, (int)w, timesteps, o0, o_out, st);
+    const float* h0 = hidden_state(ctx, hidden_init, o0, x, n, (int)h, (int)w, st);
+    StateOut so;
+    so.O = states_O;
+    so.I = states_I;
+    so.T = timesteps;
+    run_circuit(ctx, n, (int)h, (int)w, timesteps, h0, o_out, (states_O || states_I) ? &so : nullptr, st);
   });
 }
 

@@ -40,7 +40,8 @@ hipError_t launch_conv1_pool_bn(const float* in, const float* w, const float* bi
                                 bool nhwc = false);
 // bf: the C8 side is a bf16 map
 hipError_t launch_nhwc_to_c8(const float* in, float* out, int B, int H, int W, hipStream_t st, bool bf = false);
-hipError_t launch_c8_to_nhwc(const float* in, float* out, int B, int H, int W, hipStream_t st, bool bf = false);
+hipError_t launch_c8_to_nhwc(const float* in, float* out, int B, int H, int W, hipStream_t st, bool bf = false,
+                             size_t dst_img = 0);
 hipError_t launch_pack_conv64(const float* w, f32x4* out, int ks, hipStream_t st);
 hipError_t launch_pack_gate(const float* g, f32x4* out, hipStream_t st);
 // k_conv64x3.hip (fp32-accurate split-f16 MFMA path)

@@ -135,6 +135,7 @@ struct mp_ctx {
   int64_t cap_batch = 0;
   int64_t cap_hw = 0;
   DevBuf bufA, bufB, X, O, I, Og, fcin, part, h1;
+  DevBuf h0;                // hidden_init zeros / identity: the NHWC initial state (allocated on use)
   DevBuf specS, specY, specP;   // MP_DTYPE_F32_FFT: input / output spectra, spatial conv result
 
   // ---- dense / hierarchical regressors (mp_regressors.hip) ----

@@ -3,7 +3,8 @@
 Supports the configuration the pose model uses (``hgru_pose.py:20-39`` merged over the defaults
 of ``auxilliary_variables``, ``hgru_module.py:9-51``): association-field eCRF with a full
 SSFxSSF conv, 1x1 GRU gates on the input, multiplicative excitation, learned gamma/kappa/omega,
-adaptation (rho), xi = zeta = 1, tanh recurrence, no rectification.  Other aux combinations raise
+adaptation (rho), xi = zeta = 1, tanh recurrence, no rectification, with any ``hidden_init``
+('random', 'zeros', 'identity') and ``store_states``.  Other aux combinations raise
 ``NotImplementedError`` rather than silently computing something else.  Inference only.
 """
 from __future__ import annotations
@@ -22,10 +23,12 @@ SUPPORTED_AUX = {
     'zeta': False, 'gamma': True, 'beta': True, 'nu': True, 'batch_norm': False,
     'atrous_convolutions': False, 'output_gru_gates': False, 'association_field': True,
     'multiplicative_excitation': True, 'gru_gates': True, 'adapation': True,
-    'dense_connections': False, 'integration_type': 'alternate', 'hidden_init': 'random',
+    'dense_connections': False, 'integration_type': 'alternate',
     'lesion_beta': False, 'lesion_nu': False, 'lesion_omega': False, 'lesion_kappa': False,
-    'dropout': None, 'store_states': False,
+    'dropout': None,
 }
+# keys with more than one implemented value (build(), hgru_module.py:872-959)
+CHOICE_AUX = {'hidden_init': ('random', 'zeros', 'identity'), 'store_states': (False, True)}
 # keys that only affect training / initialisation, never the forward values
 _IGNORED = {'symmetric_weights', 'symmetric_gate_weights', 'trainable', 'pre_batchnorm',
             'post_batchnorm', 'train', 'normal_initializer', 'gate_bias_init', 'dtype',
@@ -68,7 +71,10 @@ class ContextualCircuit(object):
         bad = {k: merged[k] for k in SUPPORTED_AUX if merged.get(k) != SUPPORTED_AUX[k]}
         if bad:
             raise NotImplementedError(f"aux settings outside the implemented hGRU variant: {bad}")
-        unknown = set(merged) - set(SUPPORTED_AUX) - _IGNORED
+        bad = {k: merged[k] for k, ok in CHOICE_AUX.items() if merged.get(k) not in ok}
+        if bad:
+            raise NotImplementedError(f"aux values outside {CHOICE_AUX}: {bad}")
+        unknown = set(merged) - set(SUPPORTED_AUX) - set(CHOICE_AUX) - _IGNORED
         if unknown:
             raise NotImplementedError(f"unsupported aux keys: {sorted(unknown)}")
         for key, val in merged.items():
@@ -108,8 +114,16 @@ class ContextualCircuit(object):
               compute_dtype: str = 'auto'):
         """Run the circuit; returns ``(O, weights, activities)`` like the reference with
         ``return_weights=True`` (hgru_module.py:939-954).  ``compute_dtype``: 'auto' (the FFT
-        path when the map allows), 'fp32_fft', 'fp32_split' or 'fp32' (see include/monkeypose.h
-        and _lib.resolve_dtype)."""
+        path when the map allows), 'fp32_fft', 'fp32_split', 'fp32' or 'bf16' (see
+        include/monkeypose.h and _lib.resolve_dtype).
+
+        hidden_init (875-892): 'random' -> O0 = ``h2_init`` (default: a seeded xavier-like draw;
+        the reference redraws it every sess.run), 'zeros' -> zeros_like(X), 'identity' -> X.
+        store_states (889-915): O is the per-step stack ``[n, T, h, w, k]`` (O_t after the rho
+        gain, 909-912) and ``weights['store_O']`` / ``weights['store_I']`` hold the O_t / I_t
+        stacks.  (The reference's TensorArrays trade places every step -- ``full`` takes
+        ``(store_O, store_I)`` where the loop passes ``(store_I, store_O)``, 825 vs 897-908 -- so
+        its stacked "O" alternates O_t and I_t; here each stack holds what its name says.)"""
         import torch
         X = self.X
         if not isinstance(X, torch.Tensor) or not X.is_cuda:
@@ -120,16 +134,28 @@ class ContextualCircuit(object):
             ctx.set_weight(name, val)
         ctx.finalize(_lib.dtype_code(_lib.resolve_dtype(compute_dtype, X.shape[1], X.shape[2])))
         X = X.detach().float().contiguous()
-        if h2_init is None:
-            h2_init = torch.from_numpy(W.synth_hidden(tuple(X.shape))).to(X.device)
-        h2_init = h2_init.detach().float().contiguous()
-        if h2_init.shape != X.shape:
-            raise ValueError("h2_init must have the shape of X")
+        if self.hidden_init == 'random':
+            if h2_init is None:
+                h2_init = torch.from_numpy(W.synth_hidden(tuple(X.shape))).to(X.device)
+            h2_init = h2_init.detach().float().contiguous()
+            if h2_init.shape != X.shape:
+                raise ValueError("h2_init must have the shape of X")
+        elif h2_init is not None:
+            raise ValueError(f"h2_init is only used with hidden_init='random' (got {self.hidden_init!r})")
         O = torch.empty_like(X)
-        ctx.circuit_fwd(X, h2_init, O, self.timesteps, _lib.current_stream(X.device))
+        sO = sI = None
+        if self.store_states:
+            sO = torch.empty((X.shape[0], self.timesteps) + tuple(X.shape[1:]), dtype=torch.float32,
+                             device=X.device)
+            sI = torch.empty_like(sO)
+        ctx.circuit_fwd(X, h2_init, O, self.timesteps, _lib.current_stream(X.device),
+                        _lib.MP_HIDDEN[self.hidden_init], sO, sI)
         torch.cuda.current_stream(X.device).synchronize()
         ctx.close()
         self.h2_init = h2_init
         weights_out = {k_.split("/")[-1]: v for k_, v in wts.items()}
         weights_out['p_t'] = weights_out['p_r']
+        if self.store_states:
+            weights_out['store_O'], weights_out['store_I'] = sO, sI
+            return sO, weights_out, {}
         return O, weights_out, {}

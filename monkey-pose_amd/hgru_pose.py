@@ -66,6 +66,8 @@ class model:
         self.h2_init = None
         self._taps = None          # intermediates of the last forward (see _tap)
         self._last = None          # (depth, h2_init) of the last forward
+        self.states_O = None       # build(..., store_states=True): [N, T, 64, 64, 64] per-step states
+        self.states_I = None
 
     def __getitem__(self, name):
         return getattr(self, name)
@@ -74,11 +76,16 @@ class model:
         return hasattr(self, name)
 
     # ---------------------------------------------------------------- weights
-    def load_weights(self, weights: Dict[str, np.ndarray]) -> None:
-        """Variables keyed by TF name (``cnn/...``); missing ones are synthesised."""
+    def load_weights(self, weights: Dict[str, np.ndarray], synthesize_missing: bool = False) -> None:
+        """Variables keyed by TF name (``cnn/...``).  Like ``saver.restore`` of a checkpoint
+        (train_cnn_networks_hgru.py:248-250), every variable the model needs must be present:
+        build() raises ``KeyError`` naming the missing ones, unless ``synthesize_missing=True``
+        fills them with the seeded stand-in initialisers (``weights.synth_value``).  A model with
+        no weights loaded at all runs on those stand-ins, as the reference runs on its
+        initialisers."""
         self.weights = {(k if k.startswith("cnn/") else "cnn/" + k): v for k, v in weights.items()}
         self._ctx_key = None
-        self._strict = False
+        self._strict = not synthesize_missing
 
     def load_checkpoint(self, path: str, remap=None, strict: bool = True) -> None:
         """Weights from a TF1 V2 checkpoint (prefix, ``.index`` path or directory; see
@@ -87,20 +94,23 @@ class model:
         if a variable the model needs is absent instead of synthesising it."""
         from . import tf_checkpoint as C
         t = C.model_variables(C.read_checkpoint(path))
-        self.load_weights(remap(t) if remap else t)
-        self._strict = strict
+        self.load_weights(remap(t) if remap else t, synthesize_missing=not strict)
 
-    def load_npz(self, path: str) -> None:
+    def load_npz(self, path: str, synthesize_missing: bool = False) -> None:
         with np.load(path, allow_pickle=False) as z:
-            self.load_weights({k: z[k] for k in z.files})
+            self.load_weights({k: z[k] for k in z.files}, synthesize_missing)
 
     def _resolve_weights(self, output_shape: int, crop=(128, 128)) -> Dict[str, np.ndarray]:
         table = W.hgru_pose_vars(output_shape=output_shape, timesteps=self.timesteps, crop=crop)
         given = dict(self.weights or {})
         out: Dict[str, np.ndarray] = {}
-        missing = [v.name for v in table if v.name not in given]
-        if missing and getattr(self, "_strict", False) and self.data_dict is None:
-            raise KeyError(f"checkpoint lacks {len(missing)} variable(s) the model needs: {missing[:8]}")
+        covered = set()
+        for layer in (self.data_dict or {}):
+            covered |= {f"cnn/{layer}/{layer}{s}" for s in ("_weights", "_biases", "_filters")}
+        missing = [v.name for v in table if v.name not in given and v.name not in covered]
+        if missing and self.weights is not None and getattr(self, "_strict", True):
+            raise KeyError(f"the loaded weights lack {len(missing)} variable(s) the model needs "
+                           f"(load_weights(..., synthesize_missing=True) fills them): {missing[:8]}")
         for v in table:
             if v.name in given:
                 out[v.name] = np.asarray(given[v.name], np.float32)
@@ -149,14 +159,21 @@ class model:
     relu1 = property(lambda self: self._tap("relu1"))
 
     def build(self, depth, output_shape, batch_norm=None, train_mode=None, h2_init=None,
-              keep_intermediates=False, dtype=None):
+              keep_intermediates=False, dtype=None, store_states=False):
         """``hgru_pose.model.build`` (hgru_pose.py:47-105), inference only.
 
         depth     torch CUDA tensor [N, 128, 128, 1] fp32 (crop / 10000, train_cnn_networks_hgru.py:50)
-        h2_init   optional [N, 64, 64, 64] initial hGRU output state; the reference draws it at
-                  random per run (hgru_module.py:879-887), here it defaults to a seeded draw
+        h2_init   optional [N, 64, 64, 64] initial hGRU output state for ``aux['hidden_init'] ==
+                  'random'`` (the default): the reference draws it at random per run
+                  (hgru_module.py:879-887), here it defaults to a seeded draw.  'zeros' / 'identity'
+                  (888-890, 876-878) need none.
         dtype     None (keep ``compute_dtype``), 'fp32' (fp32-class, fastest path for the map:
                   ``compute_dtype = 'auto'``) or 'bf16' (bf16 spectral / gate GEMMs on the FFT path)
+        store_states  also keep every hGRU timestep's states (the circuit's ``store_states``,
+                  hgru_module.py:889-915) as ``self.states_O`` / ``self.states_I``, each
+                  [N, T, 64, 64, 64]: O_t after the rho gain and I_t.  (With
+                  ``aux['store_states']`` the reference itself would feed the 5-D stack into fc_1;
+                  that configuration is rejected.)
         """
         if dtype is not None:
             if dtype not in ('fp32', 'bf16'):
@@ -173,41 +190,66 @@ class model:
         if depth.dim() != 4 or depth.shape[-1] != 1:
             raise ValueError(f"depth must be [N, H, W, 1], got {tuple(depth.shape)}")
         self.output_shape = int(output_shape)
+        self._hidden_init()   # validate the aux before any work
         self._ctx = self._context(self.output_shape, depth.device.index or 0,
                                   (int(depth.shape[1]), int(depth.shape[2])))
-        return self.forward(depth, h2_init, keep_intermediates)
+        return self.forward(depth, h2_init, keep_intermediates, store_states)
 
-    def forward(self, depth, h2_init=None, keep_intermediates=False):
+    def _hidden_init(self) -> str:
+        hi = self.aux.get('hidden_init', 'random')
+        if hi not in _lib.MP_HIDDEN:
+            raise NotImplementedError(f"aux hidden_init={hi!r}: the reference raises (hgru_module.py:891-892)")
+        if self.aux.get('store_states', False):
+            raise NotImplementedError("aux store_states=True makes hgru_layer return the [N, T, ...] stack, "
+                                      "which fc_1 cannot take; use build(..., store_states=True)")
+        return hi
+
+    def forward(self, depth, h2_init=None, keep_intermediates=False, store_states=False):
         import torch
         if self._ctx is None:
             raise RuntimeError("call build() first")
         depth = depth.detach().float().contiguous()
         n, h, w, _ = depth.shape
-        if h2_init is None:
-            h2_init = torch.from_numpy(W.synth_hidden((n, h // 2, w // 2, 64))).to(depth.device)
-        h2_init = h2_init.detach().float().contiguous()
-        if tuple(h2_init.shape) != (n, h // 2, w // 2, 64):
-            raise ValueError(f"h2_init must be [{n}, {h // 2}, {w // 2}, 64]")
+        hi = self._hidden_init()
+        if hi == 'random':
+            if h2_init is None:
+                h2_init = torch.from_numpy(W.synth_hidden((n, h // 2, w // 2, 64))).to(depth.device)
+            h2_init = h2_init.detach().float().contiguous()
+            if tuple(h2_init.shape) != (n, h // 2, w // 2, 64):
+                raise ValueError(f"h2_init must be [{n}, {h // 2}, {w // 2}, 64]")
+        elif h2_init is not None:
+            raise ValueError(f"h2_init is only used with aux hidden_init='random' (got {hi!r})")
         self.h2_init = h2_init
         self._last = (depth, h2_init)
         self._taps = None
-        return self._run(depth, h2_init, keep_intermediates)
+        self.states_O = self.states_I = None
+        return self._run(depth, h2_init, keep_intermediates, store_states)
 
-    def _run(self, depth, h2_init, keep=False):
+    def _run(self, depth, h2_init, keep=False, store_states=False):
         import torch
         n, h, w, _ = depth.shape
         dev = depth.device
         out = torch.empty((n, self.output_shape), dtype=torch.float32, device=dev)
         stream = _lib.current_stream(dev)
+        hidden = _lib.MP_HIDDEN[self._hidden_init()]
+        hh, ww = h // 2, w // 2
+        taps = {}
         if keep:
-            hh, ww = h // 2, w // 2
             shapes = {"conv1": (n, h, w, 64), "pool1": (n, hh, ww, 64), "conv2": (n, hh, ww, 64),
                       "conv3": (n, hh, ww, 64), "hgru": (n, hh, ww, 64), "fc1": (n, 1024), "relu1": (n, 1024)}
             taps = {k: torch.empty(v, dtype=torch.float32, device=dev) for k, v in shapes.items()}
-            self._ctx.pose_fwd_taps(depth, h2_init, out, taps, stream)
-            self._taps = taps
+        if store_states:
+            T = self._ctx.info("timesteps")
+            for k in _lib.STATE_NAMES:
+                taps[k] = torch.empty((n, T, hh, ww, 64), dtype=torch.float32, device=dev)
+        if taps or hidden:
+            self._ctx.pose_fwd_taps(depth, h2_init, out, taps, stream, hidden)
         else:
             self._ctx.pose_fwd(depth, h2_init, out, stream)
+        if keep:
+            self._taps = {k: taps[k] for k in _lib.TAP_NAMES}
+        if store_states:
+            self.states_O, self.states_I = taps["states_O"], taps["states_I"]
         self.out_put = out
         return out
 

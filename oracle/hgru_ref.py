@@ -196,8 +196,9 @@ def hgru_forward(X, O0, wts, timesteps=8, scope="cnn/contextual_circuit", keep_s
 # ---------------------------------------------------------------------------------------------
 # hgru_pose.model.build (hgru_pose.py:47-105), inference (train_mode falsy)
 # ---------------------------------------------------------------------------------------------
-def hgru_pose_forward(depth: np.ndarray, wts: Dict[str, np.ndarray], O0: np.ndarray,
-                      timesteps: int = 8, dtype=np.float64, keep: bool = False):
+def hgru_pose_forward(depth: np.ndarray, wts: Dict[str, np.ndarray], O0: Optional[np.ndarray],
+                      timesteps: int = 8, dtype=np.float64, keep: bool = False,
+                      hidden_init: str = "random"):
     x = depth.astype(dtype)
     inter = {}
     c1 = bias_relu(conv2d_same(x, wts["cnn/conv_1/conv_1_filters"].astype(dtype)),
@@ -212,10 +213,12 @@ def hgru_pose_forward(depth: np.ndarray, wts: Dict[str, np.ndarray], O0: np.ndar
     c3 = batch_norm_inf(c3, wts, "cnn/batch_normalization_2")                         # 72-80
     if keep:
         inter.update(conv1=c1, pool1=p1, conv2=c2, conv3=c3)
-    h = hgru_forward(c3, O0, wts, timesteps, keep_steps=keep)                         # 81
+    O0 = hidden_init_state(c3, hidden_init, O0)                                       # 81
+    h = hgru_forward(c3, O0, wts, timesteps, keep_inputs=keep)
     if keep:
-        h, steps = h
+        h, steps, isteps = h
         inter["hgru_steps"] = steps
+        inter["hgru_isteps"] = isteps
     h = batch_norm_inf(h, wts, "cnn/batch_normalization_3")                           # 82-90
     f1 = fc(h, wts["cnn/fc_1/fc_1_weights"], wts["cnn/fc_1/fc_1_biases"])             # 91
     r1 = np.maximum(f1, 0)                                                            # 92

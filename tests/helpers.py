@@ -24,7 +24,12 @@ HGRU_POSE_AUX = {
 
 # fp32 parity gate of SURVEY.md 8d / BASELINE.md: ||out - ref||_inf / ||ref||_inf <= 1e-4
 FP32_REL_TOL = 1e-4
-BF16_REL_TOL = 5e-2   # stated gate of every bf16 path (bf16 cannot meet 1e-4)
+# stated gates of the bf16 paths (bf16 cannot meet 1e-4): model outputs (pose, regressors;
+# measured 6e-4 - 9e-4) and the raw per-step hGRU state maps, stored in bf16 (8-bit mantissa) and
+# fed back through 8 steps without a head to average the rounding (measured up to 1.04e-2 of
+# max|O_t|, 4.8e-3 on the circuit output)
+BF16_REL_TOL = 5e-3
+BF16_STATE_REL_TOL = 2e-2
 
 
 def golden_meta():

@@ -1,0 +1,161 @@
+"""GPU parity of every hGRU timestep (``store_states``, hgru_module.py:889-915) and of the
+``hidden_init`` choices (875-892), through the C ABI (``mp_hgru_pose_fwd_taps`` states_O /
+states_I, ``mp_hgru_circuit_fwd_ex``).
+
+Gate: per step, ``||O_t - ref||_inf / ||ref||_inf <= 1e-4`` against the float64
+oracle, whose own per-step structure is pinned to the reference's code by
+``tests/test_hgru_structure.py``; plus the committed per-step checksums of
+``tests/golden/golden.json``.  At the metric's batch (256, two batch slices on two streams) the
+sampled crops of both slices are checked against the oracle and bit for bit against their own
+batch-1 runs."""
+import numpy as np
+import pytest
+
+from helpers import BF16_STATE_REL_TOL, FP32_REL_TOL, HGRU_POSE_AUX, MG, golden_meta, pkg, rel_inf
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+
+
+def _cuda(a):
+    return torch.from_numpy(np.ascontiguousarray(a, dtype=np.float32)).cuda()
+
+
+def _checksums_close(a, want, rtol=1e-4):
+    a = np.asarray(a, np.float64)
+    s, ss, mx = float(a.sum()), float((a * a).sum()), float(np.abs(a).max())
+    ws, wss, wmx = want
+    assert abs(ss - wss) <= rtol * wss, (ss, wss)
+    assert abs(mx - wmx) <= rtol * wmx, (mx, wmx)
+    assert abs(s - ws) <= rtol * np.sqrt(wss * a.size), (s, ws)   # |sum| <= sqrt(N * sum sq)
+
+
+def _pose_ctx(dtype, crop=128, seed=1234):
+    mp = pkg()
+    W = mp.weights
+    wts = W.synth_weights(W.hgru_pose_vars(output_shape=69, timesteps=8, crop=crop), seed=seed)
+    m = mp.hgru_pose.model()
+    m.compute_dtype = dtype
+    m.load_weights(wts)
+    return m, wts
+
+
+@pytest.mark.parametrize("dtype", ["fp32_fft", "fp32", "bf16"])
+@pytest.mark.parametrize("case", [c[0] for c in MG.POSE_CASES])
+def test_pose_every_step_matches_oracle(case, dtype):
+    from oracle import hgru_ref as R
+    meta = golden_meta()[case]
+    if dtype == "fp32" and meta["crop"] == 128:
+        pytest.skip("exact-fp32 direct path: the 64x64 case covers it (slow at 128)")
+    n, crop, T = meta["n"], meta["crop"], meta["timesteps"]
+    wts, depth, O0 = MG.pose_inputs(n, crop, T, meta["weight_seed"], meta["crop_seed"], meta["o0_seed"])
+    m = pkg().hgru_pose.model()
+    m.compute_dtype = dtype
+    m.load_weights(wts)
+    out = m.build(_cuda(depth), 69, h2_init=_cuda(O0), store_states=True)
+    sO, sI = m.states_O.cpu().numpy(), m.states_I.cpu().numpy()
+    plain = m.forward(_cuda(depth), h2_init=_cuda(O0))
+    assert torch.equal(out, plain), "store_states must not change the output"
+    assert m.states_O is None
+    assert sO.shape == (n, T, crop // 2, crop // 2, 64) and sI.shape == sO.shape
+    _, inter = R.hgru_pose_forward(depth, wts, O0, T, np.float64, keep=True)
+    tol = BF16_STATE_REL_TOL if dtype == "bf16" else FP32_REL_TOL
+    errs = []
+    for t in range(T):
+        eo, ei = rel_inf(sO[:, t], inter["hgru_steps"][t]), rel_inf(sI[:, t], inter["hgru_isteps"][t])
+        errs.append((eo, ei))
+        assert eo <= tol and ei <= tol, (t, eo, ei)
+        if dtype != "bf16":
+            _checksums_close(sO[:, t], meta["step_checksums"][t])
+    print(f"{case} {dtype}: per-step max rel err O {max(e[0] for e in errs):.2e} I {max(e[1] for e in errs):.2e}")
+
+
+@pytest.mark.parametrize("dtype", ["fp32_fft", "bf16"])
+def test_pose_states_at_metric_batch(dtype):
+    """B = 256 (the metric's batch; two 128-crop slices on two streams): crops from both slices
+    match the oracle at every step and equal their own batch-1 run bit for bit."""
+    from oracle import hgru_ref as R
+    mp = pkg()
+    W = mp.weights
+    n = 256
+    m, wts = _pose_ctx(dtype)
+    depth_np = W.synth_crops(n, seed=31, size=128)
+    o0_np = W.synth_hidden((n, 64, 64, 64), seed=32)
+    out = m.build(_cuda(depth_np), 69, h2_init=_cuda(o0_np), store_states=True)
+    torch.cuda.synchronize()
+    sO, sI = m.states_O, m.states_I
+    assert bool(torch.isfinite(sO).all()) and bool(torch.isfinite(sI).all())
+    tol = BF16_STATE_REL_TOL if dtype == "bf16" else FP32_REL_TOL
+    for i in (5, 200):                           # slice 0 and slice 1
+        o1 = m.forward(_cuda(depth_np[i:i + 1]), h2_init=_cuda(o0_np[i:i + 1]), store_states=True)
+        torch.cuda.synchronize()
+        assert torch.equal(o1[0], out[i])
+        assert torch.equal(m.states_O[0], sO[i]) and torch.equal(m.states_I[0], sI[i])
+        _, inter = R.hgru_pose_forward(depth_np[i:i + 1], wts, o0_np[i:i + 1], 8, np.float64, keep=True)
+        a, b = sO[i].cpu().numpy(), sI[i].cpu().numpy()
+        for t in range(8):
+            assert rel_inf(a[t], inter["hgru_steps"][t][0]) <= tol, (i, t)
+            assert rel_inf(b[t], inter["hgru_isteps"][t][0]) <= tol, (i, t)
+
+
+@pytest.mark.parametrize("hidden_init", ["zeros", "identity"])
+@pytest.mark.parametrize("dtype", ["fp32_fft", "fp32"])
+def test_pose_hidden_init(hidden_init, dtype):
+    from oracle import hgru_ref as R
+    mp = pkg()
+    W = mp.weights
+    m, wts = _pose_ctx(dtype, crop=64)
+    m.aux["hidden_init"] = hidden_init
+    depth = W.synth_crops(2, seed=42, size=64)
+    out = m.build(_cuda(depth), 69, store_states=True).cpu().numpy()
+    ref, inter = R.hgru_pose_forward(depth, wts, None, 8, np.float64, keep=True, hidden_init=hidden_init)
+    assert rel_inf(out, ref) <= FP32_REL_TOL
+    assert rel_inf(m.states_O[:, 0].cpu().numpy(), inter["hgru_steps"][0]) <= FP32_REL_TOL
+    with pytest.raises(ValueError):
+        m.forward(_cuda(depth), h2_init=_cuda(np.zeros((2, 32, 32, 64))))
+
+
+def test_pose_rejects_unknown_hidden_init_and_aux_store_states():
+    m, _ = _pose_ctx("fp32_fft", crop=64)
+    x = torch.zeros((1, 64, 64, 1), device="cuda")
+    m.aux["hidden_init"] = "ones"
+    with pytest.raises(NotImplementedError):
+        m.build(x, 69)
+    m.aux["hidden_init"] = "random"
+    m.aux["store_states"] = True
+    with pytest.raises(NotImplementedError):
+        m.build(x, 69)
+
+
+@pytest.mark.parametrize("hidden_init", ["random", "zeros", "identity"])
+@pytest.mark.parametrize("dtype", ["fp32_fft", "fp32"])
+@pytest.mark.parametrize("case", [c[0] for c in MG.CIRCUIT_CASES])
+def test_circuit_store_states_and_hidden_init(case, dtype, hidden_init):
+    """ContextualCircuit(aux={..., hidden_init, store_states: True}).build(): O is the per-step
+    stack [n, T, h, w, k] and weights['store_O'] / ['store_I'] the O_t / I_t stacks."""
+    from oracle import hgru_ref as R
+    mp = pkg()
+    meta = golden_meta()[case]
+    n, h, w, ssf, T = meta["n"], meta["h"], meta["w"], meta["ssf"], meta["timesteps"]
+    wts, X, O0 = MG.circuit_inputs(n, h, w, ssf, T, meta["weight_seed"], meta["x_seed"], meta["o0_seed"])
+    aux = dict(HGRU_POSE_AUX, hidden_init=hidden_init, store_states=True)
+    cc = mp.hgru_module.ContextualCircuit(_cuda(X), timesteps=T, SRF=1, SSN=ssf, SSF=ssf, aux=aux)
+    O, weights, _ = cc.build(weights=wts, h2_init=_cuda(O0) if hidden_init == "random" else None,
+                             compute_dtype=dtype)
+    assert tuple(O.shape) == (n, T, h, w, 64)
+    assert O is weights["store_O"]
+    o0 = R.hidden_init_state(X.astype(np.float64), hidden_init, O0)
+    _, steps, isteps = R.hgru_forward(X.astype(np.float64), o0, wts, T, keep_inputs=True)
+    sO, sI = O.cpu().numpy(), weights["store_I"].cpu().numpy()
+    for t in range(T):
+        assert rel_inf(sO[:, t], steps[t]) <= FP32_REL_TOL, t
+        assert rel_inf(sI[:, t], isteps[t]) <= FP32_REL_TOL, t
+        if hidden_init == "random":
+            _checksums_close(sO[:, t], meta["step_checksums"][t])
+    # without store_states: the last O itself, bit-identical to the stack's last entry
+    aux2 = dict(aux, store_states=False)
+    cc2 = mp.hgru_module.ContextualCircuit(_cuda(X), timesteps=T, SRF=1, SSN=ssf, SSF=ssf, aux=aux2)
+    O2, _, _ = cc2.build(weights=wts, h2_init=_cuda(O0) if hidden_init == "random" else None,
+                         compute_dtype=dtype)
+    assert torch.equal(O2, O[:, T - 1])
