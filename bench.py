@@ -1,7 +1,10 @@
-"""Benchmark: depth-crops/s of the hGRU-8T pose forward (hgru_pose.model.build, 128x128 crops,
-batch 256 per GPU), one process per GPU, weak scaling (batch shards, no data-path collective).
+"""Benchmark: depth-crops/s of the hGRU-8T pose forward (hgru_pose.model.build, 128x128 crops),
+one process per GPU, batch shards, no data-path collective.  Default: batch 256 per GPU (weak
+scaling, SURVEY config 4's sharding); ``--global-batch 256`` reads the metric as one batch of 256
+over N GPUs (strong scaling, 256 / N per GPU).  At N > 1 the line also carries the other reading
+as ``other_scaling_row``.
 
-    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B] [--dtype f32|f32_split]
+    python bench.py [--gpus N] [--steps K] [--warmup W] [--batch B | --global-batch G] [--dtype ...]
     python -m torch.distributed.run --nproc-per-node N --master-addr 127.0.0.1 bench.py --gpus N
 
 A step = one forward of the whole hot path (conv_1 ... hGRU x8 ... fc_out) over B synthetic crops
@@ -35,7 +38,10 @@ def parse():
     p.add_argument("--gpus", type=int, default=1)
     p.add_argument("--steps", type=int, default=10)
     p.add_argument("--warmup", type=int, default=2)
-    p.add_argument("--batch", type=int, default=256, help="crops per GPU")
+    p.add_argument("--batch", type=int, default=256, help="crops per GPU (weak scaling, the default)")
+    p.add_argument("--global-batch", type=int, default=None,
+                   help="crops over all GPUs, sharded contiguously (strong scaling: each GPU gets "
+                        "global/N; the metric's 'batch 256 at 1/2/4/8 GPU' reading)")
     p.add_argument("--crop", type=int, default=128)
     p.add_argument("--timesteps", type=int, default=8)
     p.add_argument("--dtype", default="f32_fft", choices=["f32", "f32_split", "f32_fft", "bf16"],
@@ -168,6 +174,16 @@ def hbm_copy_gbps(dev, nbytes=2 << 30):
     return round(gbps, 1)
 
 
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
 def time_gpu(fn, steps, warmup):
     import torch
     for _ in range(warmup):
@@ -214,18 +230,23 @@ def extras(mp, dev, args):
             ctx.close()
         except Exception as e:  # noqa: BLE001
             out[key] = {"error": repr(e)}
-    try:   # config 2: hGRU pose fwd, T=8, batch 64, fp32-class (same context kind, B = 64)
+    try:   # config 2 (B = 64) and the metric's strong-scaling per-GPU batches (256 / N for N = 2, 4, 8)
         ctx = mp._lib.Context(mp._lib.MP_MODEL_HGRU_POSE, dev.index)
         T = args.timesteps
         for v in W.hgru_pose_vars(output_shape=69, timesteps=T, crop=128):
             ctx.set_weight(v.name, W.synth_value(v, 1234, T))
         ctx.finalize(mp._lib.dtype_code(args.dtype))
-        d64 = depth[:64].contiguous()
-        o64 = torch.from_numpy(W.synth_hidden((64, 64, 64, 64), seed=7)).to(dev)
-        out64 = torch.empty((64, 69), device=dev)
-        t = time_gpu(lambda: ctx.pose_fwd(d64, o64, out64, stream), 10, 2)
-        out["hgru_b64"] = {"crops_per_s": round(64 / t, 2), "ms_per_batch": round(t * 1e3, 3),
-                           "dtype": args.dtype}
+        o_all = torch.from_numpy(W.synth_hidden((128, 64, 64, 64), seed=7)).to(dev)
+        pts = {}
+        for b in (128, 64, 32):
+            db, ob = depth[:b].contiguous(), o_all[:b].contiguous()
+            outb = torch.empty((b, 69), device=dev)
+            t = time_gpu(lambda: ctx.pose_fwd(db, ob, outb, stream), 10, 2)
+            pts[f"b{b}"] = {"crops_per_s": round(b / t, 2), "ms_per_batch": round(t * 1e3, 3)}
+        out["hgru_b64"] = dict(pts["b64"], dtype=args.dtype)
+        out["strong_scaling_per_gpu"] = {"note": "one GPU at the per-GPU batch of global batch 256 over "
+                                                 "N = 2, 4, 8 GPUs; 'efficiency' = per-crop rate / the B=256 rate",
+                                         **pts}
         ctx.close()
     except Exception as e:  # noqa: BLE001
         out["hgru_b64"] = {"error": repr(e)}
@@ -397,28 +418,59 @@ def main():
     ctx.reserve(B)
 
     # ---- synthetic inputs resident in HBM (this rank's shard of the global batch) ----
+    strong = args.global_batch is not None
+    gb = args.global_batch if strong else world * B
+    s0, s1 = par.shard_range(gb, rank, world) if strong else (rank * B, rank * B + B)
+    B = s1 - s0
+    if B <= 0:
+        raise SystemExit("--global-batch must give every GPU at least one crop")
     depth = torch.from_numpy(W.synth_crops(B, seed=42 + rank, size=crop)).to(dev)
     o0 = torch.from_numpy(W.synth_hidden((B, crop // 2, crop // 2, 64), seed=7 + rank)).to(dev)
     out = torch.empty((B, 69), dtype=torch.float32, device=dev)
     stream = mp._lib.current_stream(dev)
 
-    for _ in range(args.warmup):
-        ctx.pose_fwd(depth, o0, out, stream)
-    torch.cuda.synchronize()
+    def timed(d, h, o, steps, warmup):
+        """warmup, barrier + sync, `steps` forwards, sync + barrier; the max over ranks"""
+        for _ in range(warmup):
+            ctx.pose_fwd(d, h, o, stream)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        for _ in range(steps):
+            ctx.pose_fwd(d, h, o, stream)
+        torch.cuda.synchronize()
+        if world > 1:
+            dist.barrier()
+        el = time.perf_counter() - t0
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64, device=dev)
+            dist.all_reduce(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el
+
+    elapsed = timed(depth, o0, out, args.steps, args.warmup)
+    # the other scaling reading of the metric, after the timed region (N > 1 only): the strong row
+    # (global batch 256 sharded) next to a weak headline, or the weak row (256 per GPU) next to a
+    # strong headline
+    other = None
     if world > 1:
-        dist.barrier()
-    torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    for _ in range(args.steps):
-        ctx.pose_fwd(depth, o0, out, stream)
-    torch.cuda.synchronize()
-    if world > 1:
-        dist.barrier()
-    elapsed = time.perf_counter() - t0
-    if world > 1:
-        t = torch.tensor([elapsed], dtype=torch.float64, device=dev)
-        dist.all_reduce(t, op=dist.ReduceOp.MAX)
-        elapsed = float(t.item())
+        if strong:
+            ob = 256
+        else:
+            a0, a1 = par.shard_range(256, rank, world)
+            ob = a1 - a0
+        d2 = torch.from_numpy(W.synth_crops(ob, seed=142 + rank, size=crop)).to(dev)
+        h2 = torch.from_numpy(W.synth_hidden((ob, crop // 2, crop // 2, 64), seed=107 + rank)).to(dev)
+        o2 = torch.empty((ob, 69), dtype=torch.float32, device=dev)
+        el2 = timed(d2, h2, o2, args.steps, 1)
+        tot = world * 256 if strong else 256
+        other = {"scaling": "weak" if strong else "strong", "global_batch": tot,
+                 "per_gpu_batch": 256 if strong else f"{256 // world}-{-(-256 // world)}",
+                 "value": round(tot * args.steps / el2, 3), "unit": "crops/s",
+                 "ms_per_step": round(el2 / args.steps * 1e3, 3)}
+        del d2, h2, o2
     # per-kernel HIP-event profile: a separate pass over the same inputs with profiling on.  The
     # timed pass runs the hGRU loop of the FFT path as two batch halves on two streams (their
     # kernels overlap); with profiling on the library keeps one stream, so each launch below is a
@@ -442,9 +494,14 @@ def main():
     fft = args.dtype in ("f32_fft", "bf16")
     kern = fft_kernels(ctx, B, px, prof_steps, args.dtype == "bf16") if fft else None
     hbm_meas = hbm_copy_gbps(dev) if fft else None   # after the timed region
-    value = world * B * args.steps / elapsed
+    value = gb * args.steps / elapsed
+    if strong:
+        metric = (f"depth-crops/sec hGRU-8T fwd @global batch {gb} over {world} GPU (strong scaling, "
+                  f"{crop}x{crop} crops)")
+    else:
+        metric = f"depth-crops/sec hGRU-8T fwd @batch{B} per GPU (weak scaling, {crop}x{crop} crops)"
     rec = {
-        "metric": "depth-crops/sec hGRU-8T fwd @batch256 per GPU (128x128 crops)",
+        "metric": metric,
         "value": round(value, 3),
         "unit": "crops/s",
         "n_gpus": world,
@@ -452,15 +509,19 @@ def main():
         "warmup": args.warmup,
         "ms_per_step": round(elapsed / args.steps * 1e3, 3),
         "higher_is_better": True,
-        "scaling": "weak",
+        "scaling": "strong" if strong else "weak",
         "vs_baseline": None,
         "dtype": {"f32": "f32", "f32_split": "f32 (f16x3 split MFMA, fp32 accumulate)",
                   "f32_fft": "f32 (fp32 FFT convolution, fp32-accurate f16x3 spectral GEMM)",
                   "bf16": "bf16 (bf16 spectra and hGRU maps, bf16 spectral / gate GEMMs, fp32 accumulate, fp32 FFTs and elementwise math)"}[args.dtype],
         "data": "synthetic crops + synthetic weights (splitmix64 stand-ins; reference publishes none)",
         "config": {"workload": f"hgru_pose.model.build fwd, T={T}, {crop}x{crop} crops, "
-                               f"batch {B} per GPU", "global_batch": world * B, "crop": crop,
-                   "timesteps": T, "parallelism": f"dp{world} (batch shards, one {'RCCL' if args.backend == 'nccl' else 'gloo'} weight broadcast)",
+                               + (f"global batch {gb} sharded over {world} GPU" if strong else f"batch {B} per GPU"),
+                   "global_batch": gb, "per_gpu_batch": B, "crop": crop,
+                   "timesteps": T,
+                   "parallelism": (f"dp{world} (contiguous batch shards, one {'RCCL' if args.backend == 'nccl' else 'gloo'} "
+                                   "weight broadcast before timing, no collective in the timed region)") if world > 1
+                   else "dp1 (single GPU, no collective)",
                    "hgru_streams": (int(os.environ.get("MP_STREAMS", "2")) if fft else 1)},
         "roofline": (fft_roofline(kern, args.dtype == "bf16", B, hbm_meas) if fft else
                      roofline(args.dtype, achieved_tf, conv_launch_ms, na + nb, conv15_flop)),
@@ -469,6 +530,8 @@ def main():
                                   "backbone": round(ms_bb / max(1, nbb), 3)},
         "weight_bcast_ms": round(bcast_s * 1e3, 3),
     }
+    if other:
+        rec["other_scaling_row"] = other
     if kern:
         rec["fft_kernels"] = kern
         rec["eCRF_conv_equiv_tflops"] = round(achieved_tf, 2)   # direct-conv FLOPs / FFT-conv time
@@ -496,16 +559,23 @@ def main():
                                  "gate": 1e-4 if args.dtype != "bf16" else BF16_REL_TOL}
             threads = max([t["num_threads"] for t in threadpool_info() if t["user_api"] == "blas"] or [1])
             rec["cpu_baseline"] = {"value": round(nc / cpu_s, 4), "unit": "crops/s", "cores": threads,
-                                   "kind": "port",
+                                   "kind": "port", "cpu": cpu_model(),
+                                   "cpus_available": len(os.sched_getaffinity(0)),
                                    "sample": f"{nc} crops of the same workload (numpy fp32 oracle, "
                                              f"OpenBLAS, batches of 4), {cpu_s:.1f} s"}
         if not args.no_extras:
+            head_rate = value
             try:
                 rec["extras"] = {"e2e_batch1_latency": e2e_latency(mp, ctx, dev, T)}
             except Exception as e:  # noqa: BLE001
                 rec["extras"] = {"e2e_batch1_latency": {"error": repr(e)}}
             ctx.close()
             rec["extras"].update(extras(mp, dev, args))
+            sp = rec["extras"].get("strong_scaling_per_gpu")
+            if sp and not strong and B == 256:
+                for k, v in sp.items():
+                    if isinstance(v, dict):
+                        v["efficiency"] = round(v["crops_per_s"] / head_rate, 3)
     if rank == 0:
         print(json.dumps(rec), flush=True)
     if world > 1:

@@ -347,11 +347,20 @@ int stream_count() {
   return v;
 }
 
+// smallest batch slice worth a stream of its own (MP_SLICE_MIN, A/B knob)
+int slice_min() {
+  static const int v = [] {
+    const char* e = std::getenv("MP_SLICE_MIN");
+    return e ? std::max(1, std::atoi(e)) : 32;
+  }();
+  return v;
+}
+
 void run_circuit(mp_ctx* c, int64_t n, int H, int W, int T, const float* o0_nhwc, float* final_dst2,
                  const StateOut* so, hipStream_t st) {
   // FFT path, not profiling: batch slices are independent, so they run on separate streams and
   // their latency-bound kernels overlap (the per-kernel HIP-event profile keeps one stream)
-  const int ns = std::min<int>(stream_count(), (int)(n / 32));
+  const int ns = std::min<int>(stream_count(), (int)(n / slice_min()));
   if (is_fft(c->dtype) && !c->prof && ns >= 2) {
     hip_check(launch_gate_init_x3(o0_nhwc, c->O.f(), c->Og.f(), c->ir_x3.p, c->ir_us, c->vecs.f(), (int)n, H, W,
                                   st, c->dtype == MP_DTYPE_BF16),
@@ -366,12 +375,13 @@ void run_circuit(mp_ctx* c, int64_t n, int H, int W, int T, const float* o0_nhwc
     }
     if (!c->ev_fork) hip_check(hipEventCreateWithFlags(&c->ev_fork, hipEventDisableTiming), "hipEventCreate");
     hip_check(hipEventRecord(c->ev_fork, st), "hipEventRecord");
-    // slices of whole 32-image GEMM groups
-    const int groups = (int)(n + 31) / 32;
+    // slices of whole GEMM groups (32 images; MP_SLICE_MIN below 32 splits a group)
+    const int gs = std::min(32, slice_min());
+    const int groups = (int)(n + gs - 1) / gs;
     int b0 = 0;
     for (int k = 0; k < ns; ++k) {
       const int g = groups / ns + (k < groups % ns ? 1 : 0);
-      const int cnt = std::min<int>(g * 32, (int)n - b0);
+      const int cnt = std::min<int>(g * gs, (int)n - b0);
       hipStream_t s = k == 0 ? st : c->sides[k - 1];
       if (k > 0) hip_check(hipStreamWaitEvent(s, c->ev_fork, 0), "hipStreamWaitEvent");
       fft_circuit_range(c, b0, cnt, H, W, T, final_dst2, so, s);
