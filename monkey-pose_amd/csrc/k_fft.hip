@@ -39,6 +39,10 @@
 namespace mp {
 
 constexpr int FX = FFT_N / 2 + 1;      // 37
+#ifndef FFT_NT
+#define FFT_NT 192                     // threads per FFT block (row phase 128, column phase 148)
+#endif
+constexpr int FNT = FFT_NT;
 constexpr int NF = FFT_N * FX;         // 2664 frequencies
 // scale of the input spectra before the f16 split: |S| <= 4096 max|x|, so activations up to
 // 1023 in magnitude stay inside f16 range (hGRU maps are tanh / sigmoid-gated, |x| <~ 1)
@@ -69,6 +73,26 @@ __device__ __forceinline__ uint32_t pack_bf2(float a, float b) {
 struct cpx {
   float x, y;
 };
+
+// streaming (non-temporal) access to the once-written, once-read spectra and P2 (A/B switches)
+#ifndef FFT_NT_STREAM
+#define FFT_NT_STREAM 0     // Y loads of the inverse column phase
+#endif
+#ifndef FFT_NT_ST
+#define FFT_NT_ST 1         // staged 16-B stores of S and Y (fft_fwd 0.198 -> 0.173 ms, spec_gemm -2 %)
+#endif
+#ifndef FFT_NT_MAP
+#define FFT_NT_MAP 0        // pixel-major stores of P2 and I
+#endif
+typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ void st16(uint4* p, uint4 v) {
+  if constexpr (FFT_NT_ST) {
+    __builtin_nontemporal_store(u32x4_t{v.x, v.y, v.z, v.w}, reinterpret_cast<u32x4_t*>(p));
+  } else {
+    *p = v;
+  }
+}
 __device__ __forceinline__ cpx unpack_bf2(uint32_t u) {   // bf16 -> fp32 is exact: the high half
   return {__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)};
 }
@@ -91,6 +115,21 @@ __device__ __forceinline__ void map_st4(float* base, size_t idx, f32x4 v) {
     *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(base) + idx) = uint2{pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])};
   else
     *reinterpret_cast<f32x4*>(base + idx) = v;
+}
+// the same for maps read exactly once by the next kernel (P2, I): non-temporal under FFT_NT_ST
+template <bool BM>
+__device__ __forceinline__ void map_st4_stream(float* base, size_t idx, f32x4 v) {
+  if constexpr (FFT_NT_MAP) {
+    if constexpr (BM) {
+      typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+      __builtin_nontemporal_store(u32x2_t{pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])},
+                                  reinterpret_cast<u32x2_t*>(reinterpret_cast<uint16_t*>(base) + idx));
+    } else {
+      __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(base + idx));
+    }
+  } else {
+    map_st4<BM>(base, idx, v);
+  }
 }
 template <bool BM>
 __device__ __forceinline__ cpx map_ld2(const float* base, size_t idx) {
@@ -250,9 +289,9 @@ __device__ __forceinline__ void fwd_cols_to_S(cpx* T, void* __restrict__ S, int 
         }
       }
       lds_barrier();
-      for (int i = tid; i < FX * 36; i += 192) {   // per fx: 36 groups x 16 B at f = fx*72 + 36*half
+      for (int i = tid; i < FX * 36; i += FNT) {   // per fx: 36 groups x 16 B at f = fx*72 + 36*half
         const int ffx = i / 36, w = i - ffx * 36;
-        dst[ffx * 72 + 36 * half + w] = *reinterpret_cast<const uint4*>(stg + ffx * STG_LD_B + w * 4);
+        st16(dst + ffx * 72 + 36 * half + w, *reinterpret_cast<const uint4*>(stg + ffx * STG_LD_B + w * 4));
       }
     }
     return;
@@ -274,9 +313,9 @@ __device__ __forceinline__ void fwd_cols_to_S(cpx* T, void* __restrict__ S, int 
     }
     lds_barrier();
     // per fx: 36 groups x 32 B = 72 uint4 at f = fx*72 + 36*half
-    for (int i = tid; i < FX * 72; i += 192) {
+    for (int i = tid; i < FX * 72; i += FNT) {
       const int ffx = i / 72, w = i - ffx * 72;
-      dst[(ffx * 72 + 36 * half) * 2 + w] = *reinterpret_cast<const uint4*>(stg + ffx * STG_LD + w * 4);
+      st16(dst + (ffx * 72 + 36 * half) * 2 + w, *reinterpret_cast<const uint4*>(stg + ffx * STG_LD + w * 4));
     }
   }
 }
@@ -296,7 +335,14 @@ __device__ __forceinline__ void inv_cols_to_T(const void* __restrict__ Y, int b,
     } else {
       const cpx* src = static_cast<const cpx*>(Y) + off;
 #pragma unroll
-      for (int fy = 0; fy < 72; ++fy) v[fy] = src[fy * 4];
+      for (int fy = 0; fy < 72; ++fy) {
+        if constexpr (FFT_NT_STREAM) {
+          const f32x2_t t = __builtin_nontemporal_load(reinterpret_cast<const f32x2_t*>(src + fy * 4));
+          v[fy] = {t[0], t[1]};
+        } else {
+          v[fy] = src[fy * 4];
+        }
+      }
     }
     fft72<1>(v);
 #pragma unroll
@@ -338,7 +384,7 @@ __device__ __forceinline__ int fft_block_cq(int blk) {
 // independent 8-byte loads in flight per thread): staging the tile through LDS pixel-major measured
 // slower (0.24 vs 0.18 ms at B = 256) -- the load pass and its barrier serialise ahead of the FFT.
 template <bool BF, bool BM>
-__global__ __launch_bounds__(192, 2) void fft_fwd_kernel(const float* __restrict__ src, void* __restrict__ S,
+__global__ __launch_bounds__(FNT, 2) void fft_fwd_kernel(const float* __restrict__ src, void* __restrict__ S,
                                                       int H, int W) {
   __shared__ cpx T[FFT_LDS];
   const int b = blockIdx.x >> 4, cq = fft_block_cq(blockIdx.x);
@@ -384,7 +430,7 @@ __global__ __launch_bounds__(192, 2) void fft_fwd_kernel(const float* __restrict
 
 // inverse 2-D FFT of Y -> the spatial conv result P (C8)
 template <bool BF, bool BM>
-__global__ __launch_bounds__(192, 2) void fft_inv_kernel(const void* __restrict__ Y, float* __restrict__ P,
+__global__ __launch_bounds__(FNT, 2) void fft_inv_kernel(const void* __restrict__ Y, float* __restrict__ P,
                                                       int H, int W) {
   __shared__ cpx T[FFT_LDS];
   const int b = blockIdx.x >> 4, cq = fft_block_cq(blockIdx.x);
@@ -405,10 +451,10 @@ __global__ __launch_bounds__(192, 2) void fft_inv_kernel(const void* __restrict_
   }
   lds_barrier();
 #pragma unroll 4
-  for (int i = tid; i < H * W; i += 192) {
+  for (int i = tid; i < H * W; i += FNT) {
     const int yy = i / W, x = i - yy * W;
     const cpx a = T[(2 * yy) * RLD + x], c = T[(2 * yy + 1) * RLD + x];
-    map_st4<BM>(P, c8_index(b, q, yy, x, e0, H, W), f32x4{a.x, a.y, c.x, c.y});
+    map_st4_stream<BM>(P, c8_index(b, q, yy, x, e0, H, W), f32x4{a.x, a.y, c.x, c.y});
   }
 }
 
@@ -418,7 +464,7 @@ __global__ __launch_bounds__(192, 2) void fft_inv_kernel(const void* __restrict_
 // over them (X, O in, I out: one float4 per lane), and the parked I rows are the forward row
 // transform's input.  p: the A-epilogue arguments (X, O, vecs; dst = I).
 template <bool BF, bool BM>
-__global__ __launch_bounds__(192, 2) void fft_inv_a_fwd_kernel(const void* __restrict__ Y, ConvArgs p,
+__global__ __launch_bounds__(FNT, 2) void fft_inv_a_fwd_kernel(const void* __restrict__ Y, ConvArgs p,
                                                             void* __restrict__ S) {
   __shared__ cpx T[FFT_LDS];
   const int H = p.H, W = p.W;
@@ -446,11 +492,11 @@ __global__ __launch_bounds__(192, 2) void fft_inv_a_fwd_kernel(const void* __res
     const f32x4 nu = *reinterpret_cast<const f32x4*>(p.vecs + V_NU * 64 + ch);
     // 64 x 64 pixels (zero padding included) in chunks of 8 per thread: the X / O loads of a
     // chunk are unconditional (clamped addresses) so all 16 are in flight together
-    for (int i0 = 0; i0 < 64 * 64; i0 += 8 * 192) {
+    for (int i0 = 0; i0 < 64 * 64; i0 += 8 * FNT) {
       f32x4 xv[8], ov[8];
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const int i = min(i0 + u * 192 + tid, 64 * 64 - 1);
+        const int i = min(i0 + u * FNT + tid, 64 * 64 - 1);
         const int yy = min(i >> 6, H - 1), x = min(i & 63, W - 1);
         const size_t idx = c8_index(b, q, yy, x, e0, H, W);
         xv[u] = map_ld4<BM>(p.X, idx);
@@ -458,7 +504,7 @@ __global__ __launch_bounds__(192, 2) void fft_inv_a_fwd_kernel(const void* __res
       }
 #pragma unroll
       for (int u = 0; u < 8; ++u) {
-        const int i = i0 + u * 192 + tid;
+        const int i = i0 + u * FNT + tid;
         if (i >= 64 * 64) break;
         const int yy = i >> 6, x = i & 63;
         cpx& ra = T[(2 * yy) * RLD + x];
@@ -468,7 +514,7 @@ __global__ __launch_bounds__(192, 2) void fft_inv_a_fwd_kernel(const void* __res
           f32x4 iv;
 #pragma unroll
           for (int j = 0; j < 4; ++j) iv[j] = tanhf(xv[u][j] - (be[j] * ov[u][j] + nu[j]) * (pv[j] + lat[j]));
-          map_st4<BM>(p.dst, c8_index(b, q, yy, x, e0, H, W), iv);
+          map_st4_stream<BM>(p.dst, c8_index(b, q, yy, x, e0, H, W), iv);
           ra = {iv[0], iv[1]};
           rc = {iv[2], iv[3]};
         } else {
@@ -596,7 +642,7 @@ __global__ __launch_bounds__(256, 2) void spec_gemm_kernel(const uint4* __restri
   for (int it = 0; it < 16; ++it) {
     const int idx = it * 256 + tid, line = idx >> 3, piece = idx & 7;
     const int bl = line >> 4, cqo = line & 15, b = img0 + bl;
-    if (b < B) Y[(((size_t)b * 16 + cqo) * NF + 4 * quad) * 2 + piece] = tile[bl * SG_YLD + cqo * 8 + piece];
+    if (b < B) st16(Y + (((size_t)b * 16 + cqo) * NF + 4 * quad) * 2 + piece, tile[bl * SG_YLD + cqo * 8 + piece]);
   }
 }
 
@@ -669,7 +715,7 @@ __global__ __launch_bounds__(256, 2) void spec_gemm_bf_kernel(const uint4* __res
   for (int it = 0; it < 8; ++it) {
     const int idx = it * 256 + tid, line = idx >> 2, piece = idx & 3;
     const int bl = line >> 4, cqo = line & 15, b = img0 + bl;
-    if (b < B) Y[((size_t)b * 16 + cqo) * NF + 4 * quad + piece] = tile[bl * SGB_YLD + cqo * 4 + piece];
+    if (b < B) st16(Y + ((size_t)b * 16 + cqo) * NF + 4 * quad + piece, tile[bl * SGB_YLD + cqo * 4 + piece]);
   }
 }
 
@@ -1055,21 +1101,21 @@ hipError_t build_spec_weights(const float* w, int ks, void* Gx, float* unscale, 
 
 hipError_t launch_fft_fwd(const float* act, void* S, int B, int H, int W, hipStream_t st, bool bf) {
   if (bf && fft_bf16_maps())
-    hipLaunchKernelGGL((fft_fwd_kernel<true, true>), dim3(B * 16), dim3(192), 0, st, act, S, H, W);
+    hipLaunchKernelGGL((fft_fwd_kernel<true, true>), dim3(B * 16), dim3(FNT), 0, st, act, S, H, W);
   else if (bf)
-    hipLaunchKernelGGL((fft_fwd_kernel<true, false>), dim3(B * 16), dim3(192), 0, st, act, S, H, W);
+    hipLaunchKernelGGL((fft_fwd_kernel<true, false>), dim3(B * 16), dim3(FNT), 0, st, act, S, H, W);
   else
-    hipLaunchKernelGGL((fft_fwd_kernel<false, false>), dim3(B * 16), dim3(192), 0, st, act, S, H, W);
+    hipLaunchKernelGGL((fft_fwd_kernel<false, false>), dim3(B * 16), dim3(FNT), 0, st, act, S, H, W);
   return hipGetLastError();
 }
 
 hipError_t launch_fft_inv_a_fwd(const void* Y, const ConvArgs& a, void* S, int B, hipStream_t st, bool bf) {
   if (bf && fft_bf16_maps())
-    hipLaunchKernelGGL((fft_inv_a_fwd_kernel<true, true>), dim3(B * 16), dim3(192), 0, st, Y, a, S);
+    hipLaunchKernelGGL((fft_inv_a_fwd_kernel<true, true>), dim3(B * 16), dim3(FNT), 0, st, Y, a, S);
   else if (bf)
-    hipLaunchKernelGGL((fft_inv_a_fwd_kernel<true, false>), dim3(B * 16), dim3(192), 0, st, Y, a, S);
+    hipLaunchKernelGGL((fft_inv_a_fwd_kernel<true, false>), dim3(B * 16), dim3(FNT), 0, st, Y, a, S);
   else
-    hipLaunchKernelGGL((fft_inv_a_fwd_kernel<false, false>), dim3(B * 16), dim3(192), 0, st, Y, a, S);
+    hipLaunchKernelGGL((fft_inv_a_fwd_kernel<false, false>), dim3(B * 16), dim3(FNT), 0, st, Y, a, S);
   return hipGetLastError();
 }
 
@@ -1087,11 +1133,11 @@ hipError_t launch_spec_gemm(const void* S, const void* Gx, void* Y, int B, float
 
 hipError_t launch_fft_inv(const void* Y, float* P, int B, int H, int W, hipStream_t st, bool bf) {
   if (bf && fft_bf16_maps())
-    hipLaunchKernelGGL((fft_inv_kernel<true, true>), dim3(B * 16), dim3(192), 0, st, Y, P, H, W);
+    hipLaunchKernelGGL((fft_inv_kernel<true, true>), dim3(B * 16), dim3(FNT), 0, st, Y, P, H, W);
   else if (bf)
-    hipLaunchKernelGGL((fft_inv_kernel<true, false>), dim3(B * 16), dim3(192), 0, st, Y, P, H, W);
+    hipLaunchKernelGGL((fft_inv_kernel<true, false>), dim3(B * 16), dim3(FNT), 0, st, Y, P, H, W);
   else
-    hipLaunchKernelGGL((fft_inv_kernel<false, false>), dim3(B * 16), dim3(192), 0, st, Y, P, H, W);
+    hipLaunchKernelGGL((fft_inv_kernel<false, false>), dim3(B * 16), dim3(FNT), 0, st, Y, P, H, W);
   return hipGetLastError();
 }
 
