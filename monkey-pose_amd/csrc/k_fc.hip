@@ -14,6 +14,7 @@
 
 #include <algorithm>
 #include <cmath>
+#include <cstdlib>
 #include <vector>
 
 namespace mp {
@@ -139,6 +140,7 @@ __global__ void fc_reduce_kernel(const float* __restrict__ part, int S, int M, i
 // 2^13..2^14, so the lo halves stay normal); activations are split unscaled when staged into LDS
 // (hi / lo planes [128 m][32 k] f16).
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
 
 __device__ __forceinline__ f32x16 mfma16(f16x8 a, f16x8 b, f32x16 c) {
   return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
@@ -228,12 +230,14 @@ __global__ __launch_bounds__(256, 3) void fc_gemm_x3_kernel(const float* __restr
 #pragma unroll
     for (int i = 0; i < MB; ++i) {
       const int e = tid + i * 256, row = e >> 3, k4 = (e & 7) * 4;
+      f16x4 hv, lv;
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        const _Float16 hh = (_Float16)av[i][s];
-        Ah[row * FCX_LD + k4 + s] = hh;
-        if constexpr (NP == 3) Al[row * FCX_LD + k4 + s] = (_Float16)(av[i][s] - (float)hh);
+        hv[s] = (_Float16)av[i][s];
+        lv[s] = (_Float16)(av[i][s] - (float)hv[s]);
       }
+      *reinterpret_cast<f16x4*>(Ah + row * FCX_LD + k4) = hv;   // one 8-byte LDS write per plane
+      if constexpr (NP == 3) *reinterpret_cast<f16x4*>(Al + row * FCX_LD + k4) = lv;
     }
     f16x8 wc[FC_BK / 16][2];
 #pragma unroll
@@ -334,7 +338,14 @@ hipError_t launch_pack_fc(const float* W, f32x4* out, int K, int N, hipStream_t 
 int fc_choose_splits(int M, int K, int N, int* kslice) {
   (void)M;
   (void)N;
-  int S = K >= 32768 ? K / 4096 : std::min(64, (K + 127) / 128);
+  // large K: slices of ~5.4k, i.e. 48 for fc_1 (K = 262,144): at batch 256 that is 2 x 8 x 48 = 768
+  // blocks = one full round of 3 blocks on each of the 256 CUs (64 slices left a 1/3-full second
+  // round); an env override exists for A/B only
+  static const int ksz = [] {
+    const char* e = std::getenv("MP_FC_KSLICE");
+    return e ? std::max(32, std::atoi(e)) : 5440;
+  }();
+  int S = K >= 32768 ? std::max(1, K / ksz) : std::min(64, (K + 127) / 128);
   if (S < 1) S = 1;
   int ks = (K + S - 1) / S;
   ks = (ks + FC_BK - 1) / FC_BK * FC_BK;
