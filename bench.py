@@ -116,6 +116,30 @@ PMC_KERNEL = {"fft_fwd": "fft_fwd_kernel<", "spec_gemm": "spec_gemm_kernel<", "i
               "fft_inv": "fft_inv_kernel<", "epi_b": "spec_epi_b_kernel<"}
 
 
+# MFMA utilisation per kernel from the committed PMC pass (tools/pmc_mfma.sh / .py: SQ_VALU_MFMA_BUSY_CYCLES
+# over GRBM_GUI_ACTIVE x 1024 SIMDs, the gfx950 MfmaUtil), same one-stream B = 256 workload
+PMC_MFMA = "profiles/r2_pmc/mfma_util_pose_fp32_b256.csv"
+MFMA_KERNELS = {"fc_gemm_x3 (fc_1, k_fc.hip)": "fc_gemm_x3_kernel", "conv64x3 (conv_2/3, k_conv64x3.hip)": "conv64x3_kernel",
+                "spec_gemm (k_fft.hip)": "spec_gemm_kernel", "spec_epi_b (gate GEMMs, k_fft.hip)": "spec_epi_b_kernel",
+                "gate_init_x3 (k_fft.hip)": "gate_init_x3_kernel"}
+
+
+def pmc_mfma_busy():
+    """{kernel: MFMA-busy fraction} of the MFMA kernels of the pose forward (fp32 path, B = 256)."""
+    import csv
+    full = os.path.join(os.path.dirname(os.path.abspath(__file__)), PMC_MFMA)
+    if not os.path.exists(full):
+        return None
+    rows = list(csv.DictReader(open(full)))
+    out = {}
+    for label, tag in MFMA_KERNELS.items():
+        for r in rows:
+            if tag in r["kernel"]:
+                out[label] = float(r["mfma_util"])
+                break
+    return {"source": PMC_MFMA, "mfma_busy": out}
+
+
 def pmc_traffic(name, bf16, batch):
     """(bytes per launch, source) of kernel `name` from the committed PMC summary, or (None, why)."""
     import csv
@@ -532,6 +556,10 @@ def main():
     }
     if other:
         rec["other_scaling_row"] = other
+    if args.dtype == "f32_fft":
+        mb = pmc_mfma_busy()
+        if mb:
+            rec["roofline"]["mfma_busy_pmc"] = mb
     if kern:
         rec["fft_kernels"] = kern
         rec["eCRF_conv_equiv_tflops"] = round(achieved_tf, 2)   # direct-conv FLOPs / FFT-conv time
