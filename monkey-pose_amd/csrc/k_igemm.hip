@@ -1009,9 +1009,11 @@ bool wide_path(const IgemmArgs& a) {
 }  // namespace
 
 int igemm_pm_splits(const IgemmArgs& a) {
-  // off by default: one stream, hier con_6 0.75 -> 0.47 ms, but the graph runtime already runs the
-  // five limbs' con_6 side by side on its streams and there the split lost (34.4k -> 32.6k crops/s)
-  static const int maxs = std::max(1, env_flag("MP_IGEMM_PM_SPLITS", 1));
+  // split K into 8 input-channel ranges by default: hier con_6 (5x5, 512 -> 1024 on 4x4 maps,
+  // 256 blocks of 128 x 128 otherwise: one wave per SIMD) 0.76 -> 0.40 ms on one stream (4 splits
+  // 0.42, 16 splits 0.43), and on the graph runtime's streams hier fp32 34.5k -> 37.7k crops/s,
+  // bf16 53.0k -> 56.3k (round 1 had measured 4 splits slower there; MP_IGEMM_PM_SPLITS=1 for A/B)
+  static const int maxs = std::max(1, env_flag("MP_IGEMM_PM_SPLITS", 8));
   if (a.K < 4 || !wide_path(a)) return 1;
   HaloGeom hg;
   size_t lds;
