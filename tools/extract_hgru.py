@@ -585,9 +585,8 @@ def circuit(n, h, w, ssf, timesteps, hidden_init="random", store_states=False):
     aux["hidden_init"] = hidden_init
     aux["store_states"] = store_states
     X = S.inp("X", (n, h, w, 64))
-    with make_tf(interp).variable_scope("contextual_circuit") if False else NullCtx():
-        c = cc(X=X, timesteps=timesteps, SRF=1, SSN=15, SSF=ssf, strides=[1, 1, 1, 1], padding="SAME", aux=aux)
-        res = c.get("build", interp)()
+    c = cc(X=X, timesteps=timesteps, SRF=1, SSN=15, SSF=ssf, strides=[1, 1, 1, 1], padding="SAME", aux=aux)
+    res = c.get("build", interp)()
     return interp, res, c
 
 
