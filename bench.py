@@ -110,8 +110,8 @@ def fft_kernels(ctx, B, hw, steps, bf16=False):
 # per-kernel HBM bytes per launch from rocprofv3 PMC passes (FETCH_SIZE x2 on gfx950 + WRITE_SIZE,
 # MI355X_MICROARCH.md), collected with the full-batch single-stream launches of this workload by
 # tools/pmc_bytes.py and committed under profiles/ (bench cannot profile itself)
-PMC_TRAFFIC = {False: "profiles/r1_last/pmc_traffic_fp32_b256.csv",
-               True: "profiles/r1_last/pmc_traffic_bf16_b256.csv"}
+PMC_TRAFFIC = {False: "profiles/r2_last/pmc_traffic_fp32_b256.csv",
+               True: "profiles/r2_last/pmc_traffic_bf16_b256.csv"}
 PMC_KERNEL = {"fft_fwd": "fft_fwd_kernel<", "spec_gemm": "spec_gemm_kernel<", "inv_a_fwd": "fft_inv_a_fwd_kernel<",
               "fft_inv": "fft_inv_kernel<", "epi_b": "spec_epi_b_kernel<"}
 

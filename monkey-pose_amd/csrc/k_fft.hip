@@ -43,6 +43,12 @@ constexpr int FX = FFT_N / 2 + 1;      // 37
 #define FFT_NT 192                     // threads per FFT block (row phase 128, column phase 148)
 #endif
 constexpr int FNT = FFT_NT;
+#ifndef FFT_MINB
+#define FFT_MINB 2                     // blocks per CU the FFT kernels are register-budgeted for
+#endif
+#ifndef FFT_MINB_BF
+#define FFT_MINB_BF 3                  // the bf16 kernels (f16 LDS tiles, 38.5 KB): 3 blocks per CU
+#endif
 constexpr int NF = FFT_N * FX;         // 2664 frequencies
 // scale of the input spectra before the f16 split: |S| <= 4096 max|x|, so activations up to
 // 1023 in magnitude stay inside f16 range (hGRU maps are tanh / sigmoid-gated, |x| <~ 1)
@@ -248,8 +254,38 @@ constexpr int STG_LD = 296;       // output staging pitch per fx, dwords (36 fy 
 constexpr int STG_LD_B = 148;     // the same for bf16 spectra (36 fy x 4 dwords + 4 pad)
 constexpr int FFT_LDS = FX * 4 * FWD_LD;   // complex elements of the block's LDS (76,960 B)
 
+// The block's LDS transpose / parking space.  fp32 path: complex64 entries.  bf16 path (H): complex
+// f16 entries (4 B) -- the spectra it feeds are bf16 (8-bit mantissa), so the f16 (11-bit)
+// intermediates add ~1/8 of that rounding, and the halved tile (38.5 KB) lets 3 blocks share a CU
+// instead of 2.  Values stay far inside f16 range (row-FFT outputs <= 64 max|map|, |map| <~ 2).
+template <bool H>
+struct Lds;
+template <>
+struct Lds<false> {
+  typedef cpx elem;
+  cpx* p;
+  __device__ __forceinline__ cpx get(int i) const { return p[i]; }
+  __device__ __forceinline__ void set(int i, cpx v) const { p[i] = v; }
+  __device__ __forceinline__ uint32_t* raw() const { return reinterpret_cast<uint32_t*>(p); }
+};
+template <>
+struct Lds<true> {
+  typedef uint32_t elem;
+  uint32_t* p;
+  __device__ __forceinline__ cpx get(int i) const {
+    const f16x2 h = __builtin_bit_cast(f16x2, p[i]);
+    return {(float)h[0], (float)h[1]};
+  }
+  __device__ __forceinline__ void set(int i, cpx v) const {
+    const f16x2 h = {(_Float16)v.x, (_Float16)v.y};
+    p[i] = __builtin_bit_cast(uint32_t, h);
+  }
+  __device__ __forceinline__ uint32_t* raw() const { return p; }
+};
+
 // forward row phase: the packed row v (a + ib, zero padded) -> half spectra of a and b in T
-__device__ __forceinline__ void fwd_rows_to_T(cpx (&v)[72], int y, int p, cpx* T) {
+template <bool H>
+__device__ __forceinline__ void fwd_rows_to_T(cpx (&v)[72], int y, int p, Lds<H> T) {
   fft72<-1>(v);
   // Z = FFT(a + i b):  A[k] = (Z[k] + conj Z[-k]) / 2,  B[k] = (Z[k] - conj Z[-k]) / (2i)
 #pragma unroll
@@ -257,8 +293,8 @@ __device__ __forceinline__ void fwd_rows_to_T(cpx (&v)[72], int y, int p, cpx* T
     const cpx zk = v[k], zm = v[(72 - k) % 72];
     const cpx A = {0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y)};
     const cpx B = {0.5f * (zk.y + zm.y), -0.5f * (zk.x - zm.x)};
-    T[(k * 4 + 2 * p) * FWD_LD + y] = A;
-    T[(k * 4 + 2 * p + 1) * FWD_LD + y] = B;
+    T.set((k * 4 + 2 * p) * FWD_LD + y, A);
+    T.set((k * 4 + 2 * p + 1) * FWD_LD + y, B);
   }
 }
 
@@ -266,16 +302,16 @@ __device__ __forceinline__ void fwd_rows_to_T(cpx (&v)[72], int y, int p, cpx* T
 // contiguous 85 KiB S run is written through LDS (T's space) in two fy halves, 1 KiB per
 // wave-instruction.  Called by ALL threads (contains barriers); T must be complete on entry.
 template <bool BF>
-__device__ __forceinline__ void fwd_cols_to_S(cpx* T, void* __restrict__ S, int b, int cq, int tid) {
+__device__ __forceinline__ void fwd_cols_to_S(Lds<BF> T, void* __restrict__ S, int b, int cq, int tid) {
   const bool col = tid < FX * 4;
   const int fx = tid >> 2, c = tid & 3;
   cpx v[72];
   if (col) {
 #pragma unroll
-    for (int y = 0; y < 72; ++y) v[y] = y < 64 ? T[tid * FWD_LD + y] : cpx{0.f, 0.f};
+    for (int y = 0; y < 72; ++y) v[y] = y < 64 ? T.get(tid * FWD_LD + y) : cpx{0.f, 0.f};
     fft72<-1>(v);
   }
-  uint32_t* stg = reinterpret_cast<uint32_t*>(T);
+  uint32_t* stg = T.raw();
   if constexpr (BF) {
     uint4* dst = reinterpret_cast<uint4*>(S) + ((size_t)b * 16 + cq) * NF;
 #pragma unroll
@@ -323,7 +359,7 @@ __device__ __forceinline__ void fwd_cols_to_S(cpx* T, void* __restrict__ S, int 
 // inverse column phase: Y[b][cq][f] -> T[y][c][fx] (rows y < 64).  Direct per-thread loads (72
 // independent 8-byte loads in flight per thread) measured faster than an LDS-staged read.
 template <bool BF>
-__device__ __forceinline__ void inv_cols_to_T(const void* __restrict__ Y, int b, int cq, int tid, cpx* T) {
+__device__ __forceinline__ void inv_cols_to_T(const void* __restrict__ Y, int b, int cq, int tid, Lds<BF> T) {
   if (tid < FX * 4) {
     const int fx = tid >> 2, c = tid & 3;
     const size_t off = (((size_t)b * 16 + cq) * NF + fx * 72) * 4 + c;
@@ -346,18 +382,18 @@ __device__ __forceinline__ void inv_cols_to_T(const void* __restrict__ Y, int b,
     }
     fft72<1>(v);
 #pragma unroll
-    for (int y = 0; y < 64; ++y) T[(y * 4 + c) * FX + fx] = v[y];   // rows >= H: unused
+    for (int y = 0; y < 64; ++y) T.set((y * 4 + c) * FX + fx, v[y]);   // rows >= H: unused
   }
 }
 
 // inverse row phase: the Hermitian-extended half spectra of rows (y, 2p) and (y, 2p+1) packed as
 // C = A + iB, one inverse FFT: v[x].x / v[x].y = the two real output rows
-__device__ __forceinline__ void inv_row_from_T(const cpx* T, int y, int p, cpx (&v)[72]) {
-  const cpx* ta = T + (y * 4 + 2 * p) * FX;
-  const cpx* tb = ta + FX;
+template <bool H>
+__device__ __forceinline__ void inv_row_from_T(Lds<H> T, int y, int p, cpx (&v)[72]) {
+  const int ta = (y * 4 + 2 * p) * FX, tb = ta + FX;
 #pragma unroll
   for (int k = 0; k < FX; ++k) {   // C[k] = A[k] + i B[k];  C[72-k] from A[72-k] = conj A[k] etc.
-    const cpx A = ta[k], B = tb[k];
+    const cpx A = T.get(ta + k), B = T.get(tb + k);
     v[k] = {A.x - B.y, A.y + B.x};
     if (k > 0 && k < FX - 1) v[72 - k] = {A.x + B.y, B.x - A.y};
   }
@@ -384,9 +420,10 @@ __device__ __forceinline__ int fft_block_cq(int blk) {
 // independent 8-byte loads in flight per thread): staging the tile through LDS pixel-major measured
 // slower (0.24 vs 0.18 ms at B = 256) -- the load pass and its barrier serialise ahead of the FFT.
 template <bool BF, bool BM>
-__global__ __launch_bounds__(FNT, 2) void fft_fwd_kernel(const float* __restrict__ src, void* __restrict__ S,
+__global__ __launch_bounds__(FNT, BF ? FFT_MINB_BF : FFT_MINB) void fft_fwd_kernel(const float* __restrict__ src, void* __restrict__ S,
                                                       int H, int W) {
-  __shared__ cpx T[FFT_LDS];
+  __shared__ typename Lds<BF>::elem Tbuf[FFT_LDS];
+  const Lds<BF> T{Tbuf};
   const int b = blockIdx.x >> 4, cq = fft_block_cq(blockIdx.x);
   const int q = cq >> 1, e0 = 4 * (cq & 1);
   const int tid = threadIdx.x;
@@ -430,9 +467,10 @@ __global__ __launch_bounds__(FNT, 2) void fft_fwd_kernel(const float* __restrict
 
 // inverse 2-D FFT of Y -> the spatial conv result P (C8)
 template <bool BF, bool BM>
-__global__ __launch_bounds__(FNT, 2) void fft_inv_kernel(const void* __restrict__ Y, float* __restrict__ P,
+__global__ __launch_bounds__(FNT, BF ? FFT_MINB_BF : FFT_MINB) void fft_inv_kernel(const void* __restrict__ Y, float* __restrict__ P,
                                                       int H, int W) {
-  __shared__ cpx T[FFT_LDS];
+  __shared__ typename Lds<BF>::elem Tbuf[FFT_LDS];
+  const Lds<BF> T{Tbuf};
   const int b = blockIdx.x >> 4, cq = fft_block_cq(blockIdx.x);
   const int q = cq >> 1, e0 = 4 * (cq & 1);
   const int tid = threadIdx.x;
@@ -446,14 +484,14 @@ __global__ __launch_bounds__(FNT, 2) void fft_inv_kernel(const void* __restrict_
     lds_barrier();   // every inverse row has read T
     if (live) {
 #pragma unroll
-      for (int x = 0; x < 64; ++x) T[tid * RLD + x] = v[x];
+      for (int x = 0; x < 64; ++x) T.set(tid * RLD + x, v[x]);
     }
   }
   lds_barrier();
 #pragma unroll 4
   for (int i = tid; i < H * W; i += FNT) {
     const int yy = i / W, x = i - yy * W;
-    const cpx a = T[(2 * yy) * RLD + x], c = T[(2 * yy + 1) * RLD + x];
+    const cpx a = T.get((2 * yy) * RLD + x), c = T.get((2 * yy + 1) * RLD + x);
     map_st4_stream<BM>(P, c8_index(b, q, yy, x, e0, H, W), f32x4{a.x, a.y, c.x, c.y});
   }
 }
@@ -464,9 +502,10 @@ __global__ __launch_bounds__(FNT, 2) void fft_inv_kernel(const void* __restrict_
 // over them (X, O in, I out: one float4 per lane), and the parked I rows are the forward row
 // transform's input.  p: the A-epilogue arguments (X, O, vecs; dst = I).
 template <bool BF, bool BM>
-__global__ __launch_bounds__(FNT, 2) void fft_inv_a_fwd_kernel(const void* __restrict__ Y, ConvArgs p,
+__global__ __launch_bounds__(FNT, BF ? FFT_MINB_BF : FFT_MINB) void fft_inv_a_fwd_kernel(const void* __restrict__ Y, ConvArgs p,
                                                             void* __restrict__ S) {
-  __shared__ cpx T[FFT_LDS];
+  __shared__ typename Lds<BF>::elem Tbuf[FFT_LDS];
+  const Lds<BF> T{Tbuf};
   const int H = p.H, W = p.W;
   const int b = blockIdx.x >> 4, cq = fft_block_cq(blockIdx.x);
   const int q = cq >> 1, e0 = 4 * (cq & 1);
@@ -481,7 +520,7 @@ __global__ __launch_bounds__(FNT, 2) void fft_inv_a_fwd_kernel(const void* __res
     lds_barrier();   // every inverse row has read T
     if (live) {
 #pragma unroll
-      for (int x = 0; x < 64; ++x) T[tid * RLD + x] = v[x];
+      for (int x = 0; x < 64; ++x) T.set(tid * RLD + x, v[x]);
     }
   }
   lds_barrier();
@@ -507,19 +546,19 @@ __global__ __launch_bounds__(FNT, 2) void fft_inv_a_fwd_kernel(const void* __res
         const int i = i0 + u * FNT + tid;
         if (i >= 64 * 64) break;
         const int yy = i >> 6, x = i & 63;
-        cpx& ra = T[(2 * yy) * RLD + x];
-        cpx& rc = T[(2 * yy + 1) * RLD + x];
+        const int ia = (2 * yy) * RLD + x, ic = (2 * yy + 1) * RLD + x;
         if (yy < H && x < W) {
+          const cpx ra = T.get(ia), rc = T.get(ic);
           const f32x4 pv = {ra.x, ra.y, rc.x, rc.y};
           f32x4 iv;
 #pragma unroll
           for (int j = 0; j < 4; ++j) iv[j] = tanhf(xv[u][j] - (be[j] * ov[u][j] + nu[j]) * (pv[j] + lat[j]));
           map_st4_stream<BM>(p.dst, c8_index(b, q, yy, x, e0, H, W), iv);
-          ra = {iv[0], iv[1]};
-          rc = {iv[2], iv[3]};
+          T.set(ia, {iv[0], iv[1]});
+          T.set(ic, {iv[2], iv[3]});
         } else {
-          ra = {0.f, 0.f};
-          rc = {0.f, 0.f};
+          T.set(ia, {0.f, 0.f});
+          T.set(ic, {0.f, 0.f});
         }
       }
     }
@@ -528,7 +567,7 @@ __global__ __launch_bounds__(FNT, 2) void fft_inv_a_fwd_kernel(const void* __res
   cpx v[72];
   if (tid < 128) {
 #pragma unroll
-    for (int x = 0; x < 72; ++x) v[x] = x < 64 ? T[tid * RLD + x] : cpx{0.f, 0.f};
+    for (int x = 0; x < 72; ++x) v[x] = x < 64 ? T.get(tid * RLD + x) : cpx{0.f, 0.f};
   }
   lds_barrier();   // parked rows read: T's space is free
   if (tid < 128) fwd_rows_to_T(v, y, pp, T);
