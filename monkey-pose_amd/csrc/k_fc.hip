@@ -168,7 +168,7 @@ __global__ void pack_fc_x3_kernel(const float* __restrict__ W, f16x8* out, int K
   dst[64] = lv;
 }
 
-constexpr int FCX_LD = FC_BK + 8;   // f16 pitch of the hi / lo activation planes (+16 B: conflict-free)
+
 
 // K steps are software-pipelined one step ahead: the activation float4s and the weight fragments
 // of step k+1 are loaded into registers while step k's MFMAs run; loads are unconditional (row
@@ -178,13 +178,16 @@ constexpr int FCX_LD = FC_BK + 8;   // f16 pitch of the hi / lo activation plane
 // mantissa, finer than bf16), fp32 accumulation
 // MB: 32-row m-blocks per block (4 = 128 rows; small batches take 1 or 2 so the MFMAs of empty rows
 // and their staging are not paid: fc_1 at batch 1 / 64)
-template <int NP, int MB>
+template <int NP, int MB, int BK = FC_BK>
 __global__ __launch_bounds__(256, 3) void fc_gemm_x3_kernel(const float* __restrict__ A, int lda,
                                                          const f16x8* __restrict__ Wpk,
                                                          float* __restrict__ part, int M, int K,
                                                          int N32, int kslice, float unscale, int S) {
   constexpr int BM = 32 * MB;
-  __shared__ _Float16 Ah[BM * FCX_LD], Al[BM * FCX_LD];
+  constexpr int LD = BK + 8;            // f16 pitch of the planes (+16 B: conflict-free b128 reads)
+  constexpr int RQ = BK / 4;            // float4s per activation row per K step
+  constexpr int NA = MB * BK / 32;      // activation float4s per thread per K step
+  __shared__ _Float16 Ah[BM * LD], Al[NP == 3 ? BM * LD : 1];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, col = lane & 31;
   const FcTile tl = fc_tile((M + BM - 1) / BM, (N32 + 3) / 4);
   if (tl.split >= S) return;
@@ -197,18 +200,18 @@ __global__ __launch_bounds__(256, 3) void fc_gemm_x3_kernel(const float* __restr
   const int kbeg = split * kslice;
   const int kend = min(K, kbeg + kslice);
 
-  auto load_act = [&](int k0, f32x4 (&v)[MB]) {
+  auto load_act = [&](int k0, f32x4 (&v)[NA]) {
 #pragma unroll
-    for (int i = 0; i < MB; ++i) {
-      const int e = tid + i * 256, row = e >> 3, k4 = (e & 7) * 4;
-      const int gm = mt * BM + row;   // K % FC_BK == 0 (launcher): every step is interior
+    for (int i = 0; i < NA; ++i) {
+      const int e = tid + i * 256, row = e / RQ, k4 = (e % RQ) * 4;
+      const int gm = mt * BM + row;   // K % BK == 0 (launcher): every step is interior
       v[i] = *reinterpret_cast<const f32x4*>(A + (size_t)min(gm, M - 1) * lda + k0 + k4);
       if (gm >= M) v[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
   };
-  auto load_w = [&](int k0, f16x8 (&w)[FC_BK / 16][2]) {
+  auto load_w = [&](int k0, f16x8 (&w)[BK / 16][2]) {
 #pragma unroll
-    for (int g = 0; g < FC_BK / 16; ++g) {
+    for (int g = 0; g < BK / 16; ++g) {
       const int kb = min((k0 >> 4) + g, K16 - 1);
       const f16x8* wp = Wpk + (((size_t)kb * N32 + nbc) * 2) * 64 + lane;
       w[g][0] = wp[0];
@@ -219,46 +222,46 @@ __global__ __launch_bounds__(256, 3) void fc_gemm_x3_kernel(const float* __restr
   f32x16 acc[MB];
 #pragma unroll
   for (int m = 0; m < MB; ++m) acc[m] = f32x16{};
-  f32x4 av[MB];
-  f16x8 wn[FC_BK / 16][2];
+  f32x4 av[NA];
+  f16x8 wn[BK / 16][2];
   if (kbeg < kend) {
     load_act(kbeg, av);
     load_w(kbeg, wn);
   }
-  for (int k0 = kbeg; k0 < kend; k0 += FC_BK) {
+  for (int k0 = kbeg; k0 < kend; k0 += BK) {
     lds_barrier();   // the previous step's LDS reads are done
 #pragma unroll
-    for (int i = 0; i < MB; ++i) {
-      const int e = tid + i * 256, row = e >> 3, k4 = (e & 7) * 4;
+    for (int i = 0; i < NA; ++i) {
+      const int e = tid + i * 256, row = e / RQ, k4 = (e % RQ) * 4;
       f16x4 hv, lv;
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
         hv[s] = (_Float16)av[i][s];
         lv[s] = (_Float16)(av[i][s] - (float)hv[s]);
       }
-      *reinterpret_cast<f16x4*>(Ah + row * FCX_LD + k4) = hv;   // one 8-byte LDS write per plane
-      if constexpr (NP == 3) *reinterpret_cast<f16x4*>(Al + row * FCX_LD + k4) = lv;
+      *reinterpret_cast<f16x4*>(Ah + row * LD + k4) = hv;   // one 8-byte LDS write per plane
+      if constexpr (NP == 3) *reinterpret_cast<f16x4*>(Al + row * LD + k4) = lv;
     }
-    f16x8 wc[FC_BK / 16][2];
+    f16x8 wc[BK / 16][2];
 #pragma unroll
-    for (int g = 0; g < FC_BK / 16; ++g) {
+    for (int g = 0; g < BK / 16; ++g) {
       wc[g][0] = wn[g][0];
       if constexpr (NP == 3) wc[g][1] = wn[g][1];
     }
-    if (k0 + FC_BK < kend) {   // prefetch the next step
-      load_act(k0 + FC_BK, av);
-      load_w(k0 + FC_BK, wn);
+    if (k0 + BK < kend) {   // prefetch the next step
+      load_act(k0 + BK, av);
+      load_w(k0 + BK, wn);
     }
     lds_barrier();
     if (wave_on) {
 #pragma unroll
-      for (int g = 0; g < FC_BK / 16; ++g) {
+      for (int g = 0; g < BK / 16; ++g) {
         if ((k0 >> 4) + g >= K16) break;
         const f16x8 wh = wc[g][0];
         [[maybe_unused]] const f16x8 wl = wc[g][1];
 #pragma unroll
         for (int m = 0; m < MB; ++m) {
-          const int o = (m * 32 + col) * FCX_LD + 16 * g + 8 * h;
+          const int o = (m * 32 + col) * LD + 16 * g + 8 * h;
           const f16x8 ah = *reinterpret_cast<const f16x8*>(Ah + o);
           if constexpr (NP == 3) {
             const f16x8 al = *reinterpret_cast<const f16x8*>(Al + o);
@@ -311,16 +314,30 @@ hipError_t launch_fc_gemm_x3(const float* A, int lda, const void* Wpk, float uns
 #define MP_FC_X3(NPV, MBV)                                                                                   \
   hipLaunchKernelGGL((fc_gemm_x3_kernel<NPV, MBV>), dim3(grid), dim3(256), 0, st, A, lda, w, part, M, K, N32, \
                      kslice, unscale, S)
-  if (nprod == 1) {
+#define MP_FC_X3K(NPV, MBV, BKV)                                                                                   \
+  hipLaunchKernelGGL((fc_gemm_x3_kernel<NPV, MBV, BKV>), dim3(grid), dim3(256), 0, st, A, lda, w, part, M, K, N32, \
+                     kslice, unscale, S)
+  static const int bk64 = [] {
+    const char* e = std::getenv("MP_FC_BK64");
+    return e ? std::atoi(e) : 1;
+  }();
+  // one product (bf16): 64-deep K steps, half the barriers and LDS staging passes per MFMA --
+  // bf16 fc_1 0.320 -> 0.263 ms at batch 256, 0.161 -> 0.129 at 32, 0.153 -> 0.106 at 1
+  if (nprod == 1 && bk64 && K % 64 == 0 && kslice % 64 == 0) {
+    if (mb == 1) MP_FC_X3K(1, 1, 64);
+    else if (mb == 2) MP_FC_X3K(1, 2, 64);
+    else MP_FC_X3K(1, 4, 64);
+  } else if (nprod == 1) {
     if (mb == 1) MP_FC_X3(1, 1);
     else if (mb == 2) MP_FC_X3(1, 2);
     else MP_FC_X3(1, 4);
-  } else {
+  } else {   // three products: 64-deep steps spill at 128 rows (160 B / lane, fc_1 0.46 -> 1.47 ms)
     if (mb == 1) MP_FC_X3(3, 1);
     else if (mb == 2) MP_FC_X3(3, 2);
     else MP_FC_X3(3, 4);
   }
 #undef MP_FC_X3
+#undef MP_FC_X3K
   return hipGetLastError();
 }
 
@@ -348,7 +365,8 @@ int fc_choose_splits(int M, int K, int N, int* kslice) {
   int S = K >= 32768 ? std::max(1, K / ksz) : std::min(64, (K + 127) / 128);
   if (S < 1) S = 1;
   int ks = (K + S - 1) / S;
-  ks = (ks + FC_BK - 1) / FC_BK * FC_BK;
+  const int q = K % 64 == 0 ? 64 : FC_BK;   // whole 64-deep steps where K allows (the one-product kernel)
+  ks = (ks + q - 1) / q * q;
   S = (K + ks - 1) / ks;
   *kslice = ks;
   return S;
