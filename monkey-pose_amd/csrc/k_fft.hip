@@ -18,11 +18,10 @@
 // scaled f16 hi + lo, three f16 MFMA products, fp32 accumulation, as k_conv64x3.hip), so the path
 // is fp32-class: error ~1e-6 of max|output| against the float64 oracle.
 //
-// Frequencies: f = fx * 72 + fy, fy in [0, 72), fx in [0, 37) (the real-input half spectrum), so
-// the 72 values one FFT thread writes / reads sit at a 32-byte stride (immediate offsets).
-// Spectra live image-major in HBM, [b][cq][f][32 B] (cq = channel / 4, f fastest), so every FFT
-// block reads / writes one contiguous 85 KiB run; the FFT kernels stage that run through LDS in two
-// halves so each wave-instruction moves 1 KiB of consecutive bytes.
+// Frequencies: f = fy * 37 + fx, fy in [0, 72), fx in [0, 37) (the real-input half spectrum), so
+// at one fy the column threads of a wave (16 fx x 4 channels) read / write 512 contiguous bytes
+// (bf16; spec_f<BF>() below: fp32 keeps f = fx * 72 + fy).  Spectra live image-major in HBM,
+// [b][cq][f][32 B] (cq = channel / 4, f fastest): every FFT block reads / writes one contiguous run.
 //   S (input spectra): 32 B = 8 f16 hi (re/im of the 4 channels, interleaved) + 8 f16 lo;
 //   Y (output spectra): 32 B = 4 x complex64.
 // The spectral GEMM needs, for ONE frequency, 32 images of one operand half side by side (an MFMA
@@ -43,6 +42,19 @@ constexpr int FX = FFT_N / 2 + 1;      // 37
 #define FFT_NT 192                     // threads per FFT block (row phase 128, column phase 148)
 #endif
 constexpr int FNT = FFT_NT;
+// phase timestamps (tools/fft_stamps.hip only; compiled out of the library): thread 0 of every
+// block records the shader clock at the phase boundaries of the FFT kernels
+#ifdef FFT_STAMP
+__device__ unsigned long long fft_stamp_buf[16384 * 8];
+#define FFT_STAMP_AT(k) \
+  do { \
+    if (threadIdx.x == 0) fft_stamp_buf[blockIdx.x * 8 + (k)] = __builtin_amdgcn_s_memtime(); \
+  } while (0)
+#else
+#define FFT_STAMP_AT(k) \
+  do { \
+  } while (0)
+#endif
 #ifndef FFT_MINB
 #define FFT_MINB 2                     // blocks per CU the FFT kernels are register-budgeted for
 #endif
@@ -50,6 +62,23 @@ constexpr int FNT = FFT_NT;
 #define FFT_MINB_BF 3                  // the bf16 kernels (f16 LDS tiles, 38.5 KB): 3 blocks per CU
 #endif
 constexpr int NF = FFT_N * FX;         // 2664 frequencies
+// frequency order of S, Y and the spectral weights, per dtype.  fy-major, f = fy * 37 + fx: at one
+// fy a wave of column threads (16 fx x 4 channels) reads / writes 512 (bf16: 256) contiguous bytes,
+// and the forward column phase stores straight from registers; fx-major, f = fx * 72 + fy: each
+// column thread's 72 values are contiguous (a wave-instruction touches 16 separate pieces) and S is
+// staged through LDS into 1-KiB stores.  Measured (same box, B = 256): bf16 inv_a_fwd 0.213 -> 0.200,
+// fft_fwd 0.100 -> 0.096 ms fy-major; fp32 the other way (inv_a_fwd 0.343 -> 0.352, fft_inv 0.138 ->
+// 0.144), so fp32 stays fx-major.  The spectral GEMM only sees quads of 4 consecutive f either way.
+#ifndef FFT_FYMAJOR_F32
+#define FFT_FYMAJOR_F32 0
+#endif
+#ifndef FFT_FYMAJOR_BF
+#define FFT_FYMAJOR_BF 1
+#endif
+template <bool BF>
+__host__ __device__ constexpr bool fy_major() { return BF ? FFT_FYMAJOR_BF : FFT_FYMAJOR_F32; }
+template <bool BF>
+__host__ __device__ constexpr int spec_f(int fx, int fy) { return fy_major<BF>() ? fy * FX + fx : fx * FFT_N + fy; }
 // scale of the input spectra before the f16 split: |S| <= 4096 max|x|, so activations up to
 // 1023 in magnitude stay inside f16 range (hGRU maps are tanh / sigmoid-gated, |x| <~ 1)
 constexpr float SPEC_SCALE = 1.0f / 64.0f;
@@ -76,9 +105,32 @@ __device__ __forceinline__ uint32_t pack_bf2(float a, float b) {
 }
 
 
+// complex fp32: a plain struct, every complex operation two scalar VALU instructions (default).
+// FFT_PACKED=1 (A/B only): a 2-float vector, complex adds one v_pk_add_f32 and twiddle products two
+// v_pk_fma_f32 / v_pk_mul_f32 (the swapped halves folded into op_sel): -8 % fft_fwd, -6 % fft_inv,
+// bf16 forward +6.5 %, BUT the two-stream hGRU schedule then gave run-to-run different bits (up to
+// ~1e-4 on I_1 of the second slice's crops; more often the more op_sel-swap forms were packed),
+// while every FFT kernel alone, two slices of it side by side, and beside the spectral GEMM stayed
+// bit-identical (tools/fft_det.hip, tools/split_probe.py) -- root cause not found, so it stays off
+#ifndef FFT_PACKED
+#define FFT_PACKED 0
+#endif
+#if FFT_PACKED
+typedef float cpx __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ cpx cfma(cpx a, cpx b, cpx c) { return __builtin_elementwise_fma(a, b, c); }
+__device__ __forceinline__ cpx swp(cpx a) { return a.yx; }
+#else
 struct cpx {
   float x, y;
 };
+__device__ __forceinline__ cpx operator+(cpx a, cpx b) { return {a.x + b.x, a.y + b.y}; }
+__device__ __forceinline__ cpx operator-(cpx a, cpx b) { return {a.x - b.x, a.y - b.y}; }
+__device__ __forceinline__ cpx operator-(cpx a) { return {-a.x, -a.y}; }
+__device__ __forceinline__ cpx operator*(cpx a, cpx b) { return {a.x * b.x, a.y * b.y}; }
+__device__ __forceinline__ cpx operator*(cpx a, float s) { return {a.x * s, a.y * s}; }
+__device__ __forceinline__ cpx cfma(cpx a, cpx b, cpx c) { return {fmaf(a.x, b.x, c.x), fmaf(a.y, b.y, c.y)}; }
+__device__ __forceinline__ cpx swp(cpx a) { return {a.y, a.x}; }
+#endif
 
 // streaming (non-temporal) access to the once-written, once-read spectra and P2 (A/B switches)
 #ifndef FFT_NT_STREAM
@@ -90,6 +142,9 @@ struct cpx {
 #ifndef FFT_NT_MAP
 #define FFT_NT_MAP 0        // pixel-major stores of P2 and I
 #endif
+#ifndef FFT_EPI_PIPE
+#define FFT_EPI_PIPE 1      // inv_a_fwd epilogue, bf16 maps: next chunk's X / O loads issued before this chunk's math
+#endif
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void st16(uint4* p, uint4 v) {
@@ -100,7 +155,7 @@ __device__ __forceinline__ void st16(uint4* p, uint4 v) {
   }
 }
 __device__ __forceinline__ cpx unpack_bf2(uint32_t u) {   // bf16 -> fp32 is exact: the high half
-  return {__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)};
+  return cpx{__uint_as_float(u << 16), __uint_as_float(u & 0xffff0000u)};
 }
 // hGRU maps of the FFT path (the drive X, the states O, I, Og and the B half-step's P2): fp32 C8,
 // or -- BM, the MP_DTYPE_BF16 default -- bf16 C8 at the same element index (half the bytes; round
@@ -143,7 +198,7 @@ __device__ __forceinline__ cpx map_ld2(const float* base, size_t idx) {
     return unpack_bf2(*reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint16_t*>(base) + idx));
   } else {
     const float2 t = *reinterpret_cast<const float2*>(base + idx);
-    return {t.x, t.y};
+    return cpx{t.x, t.y};
   }
 }
 // sigmoid / tanh on v_exp_f32 + v_rcp_f32 (absolute error ~1e-7).  The A epilogue keeps ocml's
@@ -151,19 +206,43 @@ __device__ __forceinline__ cpx map_ld2(const float* base, size_t idx) {
 // error 6.1e-7 -> 8.1e-7
 __device__ __forceinline__ float fsigmoid(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 __device__ __forceinline__ float ftanh(float x) { return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __expf(2.f * x)); }
-__device__ __forceinline__ cpx operator+(cpx a, cpx b) { return {a.x + b.x, a.y + b.y}; }
-__device__ __forceinline__ cpx operator-(cpx a, cpx b) { return {a.x - b.x, a.y - b.y}; }
-__device__ __forceinline__ cpx scale(cpx a, float s) { return {a.x * s, a.y * s}; }
+#ifndef FFT_TANH
+#define FFT_TANH 1
+#endif
+// tanh of the A epilogue.  0: ocml tanhf (a branch per lane: polynomial below |x| = 0.625, an
+// exp-based form above, both paths executed by a mixed wave); 1: ftanh; 2: odd rational minimax
+// (numerator degree 13, denominator 6, on |x| <= 7.9; one v_rcp_f32)
+__device__ __forceinline__ float rtanh(float x) {
+  const float c = __builtin_amdgcn_fmed3f(x, -7.90531110763549805f, 7.90531110763549805f);
+  const float x2 = c * c;
+  float p = fmaf(x2, -2.76076847742355e-16f, 2.00018790482477e-13f);
+  p = fmaf(x2, p, -8.60467152213735e-11f);
+  p = fmaf(x2, p, 5.12229709037114e-08f);
+  p = fmaf(x2, p, 1.48572235717979e-05f);
+  p = fmaf(x2, p, 6.37261928875436e-04f);
+  p = fmaf(x2, p, 4.89352455891786e-03f);
+  p *= c;
+  float q = fmaf(x2, 1.19825839466702e-06f, 1.18534705686654e-04f);
+  q = fmaf(x2, q, 2.26843463243900e-03f);
+  q = fmaf(x2, q, 4.89352518554385e-03f);
+  return p * __builtin_amdgcn_rcpf(q);
+}
+__device__ __forceinline__ float atanh_f(float x) {
+  if constexpr (FFT_TANH == 1) return ftanh(x);
+  else if constexpr (FFT_TANH == 2) return rtanh(x);
+  else return tanhf(x);
+}
+__device__ __forceinline__ cpx scale(cpx a, float s) { return a * s; }
 // a * e^{S i 2 pi m / 72}  (S = -1 forward, +1 inverse)
 template <int S>
 __device__ __forceinline__ cpx twid(cpx a, int m) {
   const float c = TW72_COS[m], s = S * TW72_SIN[m];
-  return {a.x * c - a.y * s, a.x * s + a.y * c};
+  return cfma(swp(a), cpx{-s, s}, a * c);   // (x c - y s, y c + x s)
 }
 // a * e^{S i pi / 2}
 template <int S>
 __device__ __forceinline__ cpx rotq(cpx a) {
-  return {-S * a.y, S * a.x};
+  return swp(a) * cpx{(float)-S, (float)S};
 }
 
 template <int S>
@@ -174,8 +253,8 @@ __device__ __forceinline__ void dft8(cpx (&x)[8]) {
   const cpx b0 = a0 + a2, b2 = a0 - a2, b1 = a1 + a3, b3 = a1 - a3;
   const cpx b4 = a4 + a6, b6 = a4 - a6, b5 = a5 + a7, b7 = a5 - a7;
   const cpx t6 = rotq<S>(b6);
-  const cpx t5 = {H * (b5.x - S * b5.y), H * (S * b5.x + b5.y)};      // b5 * W8^1
-  const cpx t7 = {-H * (b7.x + S * b7.y), H * (S * b7.x - b7.y)};     // b7 * W8^3
+  const cpx t5 = cfma(swp(b5), cpx{(float)-S, (float)S}, b5) * H;    // b5 * W8^1 = H (b5 + rotq b5)
+  const cpx t7 = cfma(swp(b7), cpx{(float)-S, (float)S}, -b7) * H;   // b7 * W8^3 = H (rotq b7 - b7)
   x[0] = b0 + b4;
   x[4] = b0 - b4;
   x[2] = b2 + t6;
@@ -191,7 +270,7 @@ __device__ __forceinline__ void dft3(cpx& z0, cpx& z1, cpx& z2) {
   constexpr float R3 = 0.86602540378443865f;
   const cpx t = z1 + z2, d = z1 - z2;
   const cpx m = z0 - scale(t, 0.5f);
-  const cpx s = {-S * R3 * d.y, S * R3 * d.x};
+  const cpx s = swp(d) * cpx{-S * R3, S * R3};
   z0 = z0 + t;
   z1 = m + s;
   z2 = m - s;
@@ -223,6 +302,9 @@ __device__ __forceinline__ void dft9(cpx (&x)[9]) {
 // 72 = 8 x 9: n = 9 n1 + n2, k = k1 + 8 k2
 template <int S>
 __device__ __forceinline__ void fft72(cpx (&v)[72]) {
+#ifdef FFT_PROBE_NOFFT   // timing probe (tools/fft_stamps.hip): data movement without the transforms
+  return;
+#endif
   cpx a[9][8];
 #pragma unroll
   for (int n2 = 0; n2 < 9; ++n2) {
@@ -274,7 +356,7 @@ struct Lds<true> {
   uint32_t* p;
   __device__ __forceinline__ cpx get(int i) const {
     const f16x2 h = __builtin_bit_cast(f16x2, p[i]);
-    return {(float)h[0], (float)h[1]};
+    return cpx{(float)h[0], (float)h[1]};
   }
   __device__ __forceinline__ void set(int i, cpx v) const {
     const f16x2 h = {(_Float16)v.x, (_Float16)v.y};
@@ -291,21 +373,65 @@ __device__ __forceinline__ void fwd_rows_to_T(cpx (&v)[72], int y, int p, Lds<H>
 #pragma unroll
   for (int k = 0; k < FX; ++k) {
     const cpx zk = v[k], zm = v[(72 - k) % 72];
-    const cpx A = {0.5f * (zk.x + zm.x), 0.5f * (zk.y - zm.y)};
-    const cpx B = {0.5f * (zk.y + zm.y), -0.5f * (zk.x - zm.x)};
+    const cpx A = cfma(zm, cpx{1.f, -1.f}, zk) * 0.5f;               // (zk.x + zm.x, zk.y - zm.y) / 2
+    const cpx B = cfma(swp(zk), cpx{1.f, -1.f}, swp(zm)) * 0.5f;     // (zk.y + zm.y, zm.x - zk.x) / 2
     T.set((k * 4 + 2 * p) * FWD_LD + y, A);
     T.set((k * 4 + 2 * p + 1) * FWD_LD + y, B);
   }
 }
 
-// forward column phase: T -> S[b][cq][fx*72+fy] (scaled, split to f16 hi / lo).  The block's
-// contiguous 85 KiB S run is written through LDS (T's space) in two fy halves, 1 KiB per
-// wave-instruction.  Called by ALL threads (contains barriers); T must be complete on entry.
+// forward column phase: T -> S[b][cq][f] (scaled, split to f16 hi / lo).  T must be complete on
+// entry.  Fy-major (f = fy * 37 + fx, fy_major<BF>) the column threads store straight to HBM: at one fy
+// the wave's 16 columns x 4 channels are 512 contiguous bytes (fp32: the quad's hi / lo halves are
+// regrouped by two DPP quad_perms so each lane stores 8 contiguous bytes), no LDS staging and no
+// barrier (the last phase of its kernels).  Otherwise (f = fx * 72 + fy) the block's contiguous
+// 85 KiB S run is written through LDS (T's space) in two fy halves, 1 KiB per wave-instruction;
+// that form is called by ALL threads (it contains barriers).
 template <bool BF>
 __device__ __forceinline__ void fwd_cols_to_S(Lds<BF> T, void* __restrict__ S, int b, int cq, int tid) {
   const bool col = tid < FX * 4;
   const int fx = tid >> 2, c = tid & 3;
   cpx v[72];
+  if constexpr (fy_major<BF>()) {
+    if (!col) return;
+#pragma unroll
+    for (int y = 0; y < 72; ++y) v[y] = y < 64 ? T.get(tid * FWD_LD + y) : cpx{0.f, 0.f};
+    fft72<-1>(v);
+    typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
+    if constexpr (BF) {
+      uint32_t* dst = static_cast<uint32_t*>(S) + (((size_t)b * 16 + cq) * NF + fx) * 4 + c;
+#pragma unroll
+      for (int fy = 0; fy < 72; ++fy) {
+        const uint32_t w = pack_bf2(v[fy].x, v[fy].y);
+        if constexpr (FFT_NT_ST)
+          __builtin_nontemporal_store(w, dst + fy * FX * 4);
+        else
+          dst[fy * FX * 4] = w;
+      }
+    } else {
+      // 32-B group of (f, cq): [hi c0 | hi c1 | hi c2 | hi c3 | lo c0 | lo c1 | lo c2 | lo c3] (4 B
+      // each = f16 re, im); lane c of the quad stores bytes 8c .. 8c+7
+      u32x2_t* dst = reinterpret_cast<u32x2_t*>(S) + (((size_t)b * 16 + cq) * NF + fx) * 4 + c;
+      const bool hi_half = c < 2;
+#pragma unroll
+      for (int fy = 0; fy < 72; ++fy) {
+        const float re = v[fy].x * SPEC_SCALE, im = v[fy].y * SPEC_SCALE;
+        const _Float16 hr = (_Float16)re, hm = (_Float16)im;
+        const f16x2 hv = {hr, hm}, lv = {(_Float16)(re - (float)hr), (_Float16)(im - (float)hm)};
+        const int hb = __builtin_bit_cast(int, hv), lb = __builtin_bit_cast(int, lv);
+        const int h0 = __builtin_amdgcn_mov_dpp(hb, 0x88, 0xF, 0xF, false);   // quad_perm [0,2,0,2]
+        const int l0 = __builtin_amdgcn_mov_dpp(lb, 0x88, 0xF, 0xF, false);
+        const int h1 = __builtin_amdgcn_mov_dpp(hb, 0xDD, 0xF, 0xF, false);   // quad_perm [1,3,1,3]
+        const int l1 = __builtin_amdgcn_mov_dpp(lb, 0xDD, 0xF, 0xF, false);
+        const u32x2_t w = {(unsigned)(hi_half ? h0 : l0), (unsigned)(hi_half ? h1 : l1)};
+        if constexpr (FFT_NT_ST)
+          __builtin_nontemporal_store(w, dst + fy * FX * 4);
+        else
+          dst[fy * FX * 4] = w;
+      }
+    }
+    return;
+  }
   if (col) {
 #pragma unroll
     for (int y = 0; y < 72; ++y) v[y] = y < 64 ? T.get(tid * FWD_LD + y) : cpx{0.f, 0.f};
@@ -362,21 +488,22 @@ template <bool BF>
 __device__ __forceinline__ void inv_cols_to_T(const void* __restrict__ Y, int b, int cq, int tid, Lds<BF> T) {
   if (tid < FX * 4) {
     const int fx = tid >> 2, c = tid & 3;
-    const size_t off = (((size_t)b * 16 + cq) * NF + fx * 72) * 4 + c;
+    const size_t off = (((size_t)b * 16 + cq) * NF + spec_f<BF>(fx, 0)) * 4 + c;
+    constexpr int FS = spec_f<BF>(0, 1) * 4;   // element stride of one fy step
     cpx v[72];
     if constexpr (BF) {
       const uint32_t* src = static_cast<const uint32_t*>(Y) + off;
 #pragma unroll
-      for (int fy = 0; fy < 72; ++fy) v[fy] = unpack_bf2(src[fy * 4]);
+      for (int fy = 0; fy < 72; ++fy) v[fy] = unpack_bf2(src[fy * FS]);
     } else {
       const cpx* src = static_cast<const cpx*>(Y) + off;
 #pragma unroll
       for (int fy = 0; fy < 72; ++fy) {
         if constexpr (FFT_NT_STREAM) {
-          const f32x2_t t = __builtin_nontemporal_load(reinterpret_cast<const f32x2_t*>(src + fy * 4));
+          const f32x2_t t = __builtin_nontemporal_load(reinterpret_cast<const f32x2_t*>(src + fy * FS));
           v[fy] = {t[0], t[1]};
         } else {
-          v[fy] = src[fy * 4];
+          v[fy] = src[fy * FS];
         }
       }
     }
@@ -394,8 +521,8 @@ __device__ __forceinline__ void inv_row_from_T(Lds<H> T, int y, int p, cpx (&v)[
 #pragma unroll
   for (int k = 0; k < FX; ++k) {   // C[k] = A[k] + i B[k];  C[72-k] from A[72-k] = conj A[k] etc.
     const cpx A = T.get(ta + k), B = T.get(tb + k);
-    v[k] = {A.x - B.y, A.y + B.x};
-    if (k > 0 && k < FX - 1) v[72 - k] = {A.x + B.y, B.x - A.y};
+    v[k] = cfma(swp(B), cpx{-1.f, 1.f}, A);                               // (A.x - B.y, A.y + B.x)
+    if (k > 0 && k < FX - 1) v[72 - k] = cfma(A, cpx{1.f, -1.f}, swp(B));   // (A.x + B.y, B.x - A.y)
   }
   fft72<1>(v);
 }
@@ -427,6 +554,7 @@ __global__ __launch_bounds__(FNT, BF ? FFT_MINB_BF : FFT_MINB) void fft_fwd_kern
   const int b = blockIdx.x >> 4, cq = fft_block_cq(blockIdx.x);
   const int q = cq >> 1, e0 = 4 * (cq & 1);
   const int tid = threadIdx.x;
+  FFT_STAMP_AT(0);
   if (tid < 128) {
     const int y = tid >> 1, p = tid & 1;
     cpx v[72];
@@ -462,7 +590,9 @@ __global__ __launch_bounds__(FNT, BF ? FFT_MINB_BF : FFT_MINB) void fft_fwd_kern
     fwd_rows_to_T(v, y, p, T);
   }
   lds_barrier();
+  FFT_STAMP_AT(1);
   fwd_cols_to_S<BF>(T, S, b, cq, tid);
+  FFT_STAMP_AT(5);
 }
 
 // inverse 2-D FFT of Y -> the spatial conv result P (C8)
@@ -474,8 +604,10 @@ __global__ __launch_bounds__(FNT, BF ? FFT_MINB_BF : FFT_MINB) void fft_inv_kern
   const int b = blockIdx.x >> 4, cq = fft_block_cq(blockIdx.x);
   const int q = cq >> 1, e0 = 4 * (cq & 1);
   const int tid = threadIdx.x;
+  FFT_STAMP_AT(0);
   inv_cols_to_T<BF>(Y, b, cq, tid, T);
   lds_barrier();
+  FFT_STAMP_AT(1);
   const int y = tid >> 1, p = tid & 1;
   const bool live = tid < 128 && y < H;
   {
@@ -488,12 +620,14 @@ __global__ __launch_bounds__(FNT, BF ? FFT_MINB_BF : FFT_MINB) void fft_inv_kern
     }
   }
   lds_barrier();
+  FFT_STAMP_AT(2);
 #pragma unroll 4
   for (int i = tid; i < H * W; i += FNT) {
     const int yy = i / W, x = i - yy * W;
     const cpx a = T.get((2 * yy) * RLD + x), c = T.get((2 * yy + 1) * RLD + x);
     map_st4_stream<BM>(P, c8_index(b, q, yy, x, e0, H, W), f32x4{a.x, a.y, c.x, c.y});
   }
+  FFT_STAMP_AT(5);
 }
 
 // The A half-step's tail and the B half-step's head in one pass (hgru_module.py:657, 797-799):
@@ -510,8 +644,10 @@ __global__ __launch_bounds__(FNT, BF ? FFT_MINB_BF : FFT_MINB) void fft_inv_a_fw
   const int b = blockIdx.x >> 4, cq = fft_block_cq(blockIdx.x);
   const int q = cq >> 1, e0 = 4 * (cq & 1);
   const int tid = threadIdx.x;
+  FFT_STAMP_AT(0);
   inv_cols_to_T<BF>(Y, b, cq, tid, T);
   lds_barrier();
+  FFT_STAMP_AT(1);
   const int y = tid >> 1, pp = tid & 1;
   const bool live = tid < 128 && y < H;
   {
@@ -524,26 +660,42 @@ __global__ __launch_bounds__(FNT, BF ? FFT_MINB_BF : FFT_MINB) void fft_inv_a_fw
     }
   }
   lds_barrier();
+  FFT_STAMP_AT(2);
   {
     const int ch = 8 * q + e0;
     const f32x4 lat = *reinterpret_cast<const f32x4*>(p.vecs + V_LAT * 64 + ch);
     const f32x4 be = *reinterpret_cast<const f32x4*>(p.vecs + V_BETA * 64 + ch);
     const f32x4 nu = *reinterpret_cast<const f32x4*>(p.vecs + V_NU * 64 + ch);
-    // 64 x 64 pixels (zero padding included) in chunks of 8 per thread: the X / O loads of a
-    // chunk are unconditional (clamped addresses) so all 16 are in flight together
-    for (int i0 = 0; i0 < 64 * 64; i0 += 8 * FNT) {
-      f32x4 xv[8], ov[8];
+    // 64 x 64 pixels (zero padding included) in chunks of EU per thread: the X / O loads of a
+    // chunk are unconditional (clamped addresses) so all 2 EU are in flight together.  With bf16
+    // maps (PIPE) the next chunk's loads are issued before this chunk's math: the phase is ~45k of
+    // the block's ~100k cycles (tools/fft_stamps.hip); with fp32 maps the second register set
+    // measured 2-4 % slower (inv_a_fwd 0.338 -> 0.351 ms), so there it stays one chunk at a time
+    constexpr int EU = 8, ECH = EU * FNT, NECH = (64 * 64 + ECH - 1) / ECH;
+    constexpr bool PIPE = FFT_EPI_PIPE && BM;
+    f32x4 xv[2][EU], ov[2][EU];
+    auto load_chunk = [&](int k, f32x4 (&xs)[EU], f32x4 (&os)[EU]) {
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int i = min(i0 + u * FNT + tid, 64 * 64 - 1);
+      for (int u = 0; u < EU; ++u) {
+        const int i = min(k * ECH + u * FNT + tid, 64 * 64 - 1);
         const int yy = min(i >> 6, H - 1), x = min(i & 63, W - 1);
         const size_t idx = c8_index(b, q, yy, x, e0, H, W);
-        xv[u] = map_ld4<BM>(p.X, idx);
-        ov[u] = map_ld4<BM>(p.O, idx);
+        xs[u] = map_ld4<BM>(p.X, idx);
+        os[u] = map_ld4<BM>(p.O, idx);
+      }
+    };
+    if constexpr (PIPE) load_chunk(0, xv[0], ov[0]);
+#pragma unroll
+    for (int k = 0; k < NECH; ++k) {
+      const int cur = PIPE ? (k & 1) : 0;
+      if constexpr (PIPE) {
+        if (k + 1 < NECH) load_chunk(k + 1, xv[cur ^ 1], ov[cur ^ 1]);
+      } else {
+        load_chunk(k, xv[0], ov[0]);
       }
 #pragma unroll
-      for (int u = 0; u < 8; ++u) {
-        const int i = i0 + u * FNT + tid;
+      for (int u = 0; u < EU; ++u) {
+        const int i = k * ECH + u * FNT + tid;
         if (i >= 64 * 64) break;
         const int yy = i >> 6, x = i & 63;
         const int ia = (2 * yy) * RLD + x, ic = (2 * yy + 1) * RLD + x;
@@ -552,7 +704,13 @@ __global__ __launch_bounds__(FNT, BF ? FFT_MINB_BF : FFT_MINB) void fft_inv_a_fw
           const f32x4 pv = {ra.x, ra.y, rc.x, rc.y};
           f32x4 iv;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) iv[j] = tanhf(xv[u][j] - (be[j] * ov[u][j] + nu[j]) * (pv[j] + lat[j]));
+          for (int j = 0; j < 4; ++j) {
+#ifdef FFT_PROBE_NOTANH   // timing probe: the A epilogue without tanhf
+            iv[j] = xv[cur][u][j] - (be[j] * ov[cur][u][j] + nu[j]) * (pv[j] + lat[j]);
+#else
+            iv[j] = atanh_f(xv[cur][u][j] - (be[j] * ov[cur][u][j] + nu[j]) * (pv[j] + lat[j]));
+#endif
+          }
           map_st4_stream<BM>(p.dst, c8_index(b, q, yy, x, e0, H, W), iv);
           T.set(ia, {iv[0], iv[1]});
           T.set(ic, {iv[2], iv[3]});
@@ -564,6 +722,7 @@ __global__ __launch_bounds__(FNT, BF ? FFT_MINB_BF : FFT_MINB) void fft_inv_a_fw
     }
   }
   lds_barrier();
+  FFT_STAMP_AT(3);
   cpx v[72];
   if (tid < 128) {
 #pragma unroll
@@ -572,7 +731,9 @@ __global__ __launch_bounds__(FNT, BF ? FFT_MINB_BF : FFT_MINB) void fft_inv_a_fw
   lds_barrier();   // parked rows read: T's space is free
   if (tid < 128) fwd_rows_to_T(v, y, pp, T);
   lds_barrier();
+  FFT_STAMP_AT(4);
   fwd_cols_to_S<BF>(T, S, b, cq, tid);
+  FFT_STAMP_AT(5);
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -760,7 +921,7 @@ __global__ __launch_bounds__(256, 2) void spec_gemm_bf_kernel(const uint4* __res
 
 // spectral weights, once per weight set: G[f][ci][co] (complex, 1/N^2 folded in), one thread per
 // (f, ci, co), float64 accumulation
-__global__ void spec_weights_kernel(const float* __restrict__ w, cpx* __restrict__ G, int KS) {
+__global__ void spec_weights_kernel(const float* __restrict__ w, cpx* __restrict__ G, int KS, int fym) {
   __shared__ double tc[FFT_N], ts[FFT_N];
   for (int m = threadIdx.x; m < FFT_N; m += blockDim.x) {
     double s, c;
@@ -772,7 +933,7 @@ __global__ void spec_weights_kernel(const float* __restrict__ w, cpx* __restrict
   const int idx = blockIdx.x * blockDim.x + threadIdx.x;
   if (idx >= NF * 4096) return;
   const int co = idx & 63, ci = (idx >> 6) & 63, f = idx >> 12;
-  const int fx = f / FFT_N, fy = f - fx * FFT_N, R = KS / 2;
+  const int fx = fym ? f % FX : f / FFT_N, fy = fym ? f / FX : f % FFT_N, R = KS / 2;   // spec_f<BF> order
   double gr = 0.0, gi = 0.0;
   for (int ky = 0; ky < KS; ++ky)
     for (int kx = 0; kx < KS; ++kx) {
@@ -1109,7 +1270,8 @@ hipError_t build_spec_weights(const float* w, int ks, void* Gx, float* unscale, 
   if (e == hipSuccess) e = hipMalloc(&mx, sizeof(unsigned));
   if (e == hipSuccess) e = hipMemset(mx, 0, sizeof(unsigned));
   if (e == hipSuccess) {
-    hipLaunchKernelGGL(spec_weights_kernel, dim3(NF * 4096 / 256), dim3(256), 0, 0, w, G, ks);
+    hipLaunchKernelGGL(spec_weights_kernel, dim3(NF * 4096 / 256), dim3(256), 0, 0, w, G, ks,
+                       (int)(bf ? fy_major<true>() : fy_major<false>()));
     hipLaunchKernelGGL(absmax_kernel, dim3(1024), dim3(256), 0, 0, reinterpret_cast<const float*>(G),
                        (size_t)NF * 4096 * 2, mx);
     e = hipGetLastError();
