@@ -298,8 +298,15 @@ __device__ __forceinline__ void dft9(cpx (&x)[9]) {
   }
 }
 
-// in-register 72-point DFT, X[k] = sum_n v[n] e^{S 2 pi i n k / 72} (unnormalised);
-// 72 = 8 x 9: n = 9 n1 + n2, k = k1 + 8 k2
+// in-register 72-point DFT, X[k] = sum_n v[n] e^{S 2 pi i n k / 72} (unnormalised).
+// FFT_PFA (default): Good-Thomas prime-factor form of 72 = 8 x 9 (gcd 1): n = (9 n1 + 8 n2) mod 72,
+// k = (9 k1 + 64 k2) mod 72 makes e^{2 pi i n k / 72} = e^{2 pi i n1 k1 / 8} e^{2 pi i n2 k2 / 9}, so
+// the 8-point and 9-point passes need no twiddles between them (56 complex products fewer per
+// transform; both index maps are register renamings).  0: Cooley-Tukey n = 9 n1 + n2, k = k1 + 8 k2
+// with a twiddle per (n2, k1).
+#ifndef FFT_PFA
+#define FFT_PFA 1
+#endif
 template <int S>
 __device__ __forceinline__ void fft72(cpx (&v)[72]) {
 #ifdef FFT_PROBE_NOFFT   // timing probe (tools/fft_stamps.hip): data movement without the transforms
@@ -310,10 +317,10 @@ __device__ __forceinline__ void fft72(cpx (&v)[72]) {
   for (int n2 = 0; n2 < 9; ++n2) {
     cpx t[8];
 #pragma unroll
-    for (int n1 = 0; n1 < 8; ++n1) t[n1] = v[9 * n1 + n2];
+    for (int n1 = 0; n1 < 8; ++n1) t[n1] = FFT_PFA ? v[(9 * n1 + 8 * n2) % 72] : v[9 * n1 + n2];
     dft8<S>(t);
 #pragma unroll
-    for (int k1 = 0; k1 < 8; ++k1) a[n2][k1] = (n2 * k1 == 0) ? t[k1] : twid<S>(t[k1], n2 * k1);
+    for (int k1 = 0; k1 < 8; ++k1) a[n2][k1] = (FFT_PFA || n2 * k1 == 0) ? t[k1] : twid<S>(t[k1], n2 * k1);
   }
 #pragma unroll
   for (int k1 = 0; k1 < 8; ++k1) {
@@ -322,7 +329,7 @@ __device__ __forceinline__ void fft72(cpx (&v)[72]) {
     for (int n2 = 0; n2 < 9; ++n2) u[n2] = a[n2][k1];
     dft9<S>(u);
 #pragma unroll
-    for (int k2 = 0; k2 < 9; ++k2) v[k1 + 8 * k2] = u[k2];
+    for (int k2 = 0; k2 < 9; ++k2) v[FFT_PFA ? (9 * k1 + 64 * k2) % 72 : k1 + 8 * k2] = u[k2];
   }
 }
 
@@ -538,6 +545,13 @@ constexpr int RLD = 73;
 // (separate L2s), so blocks i and i+8 share an XCD: giving them the two halves of a chunk lets one
 // L2 fetch (or write back) each line once instead of two XCDs each moving the whole line
 // (rocprofv3 FETCH/WRITE_SIZE showed 2x the algorithmic bytes on these maps otherwise).
+__device__ __forceinline__ int fft_block_img(int blk) {
+#ifdef FFT_PROBE_WRAP   // timing probe (tools/fft_stamps.hip): every block works on one of WRAP images
+  return (blk >> 4) % FFT_PROBE_WRAP;
+#else
+  return blk >> 4;
+#endif
+}
 __device__ __forceinline__ int fft_block_cq(int blk) {
   const int p = blk & 15;
   return 2 * (p & 7) + (p >> 3);
@@ -551,7 +565,7 @@ __global__ __launch_bounds__(FNT, BF ? FFT_MINB_BF : FFT_MINB) void fft_fwd_kern
                                                       int H, int W) {
   __shared__ typename Lds<BF>::elem Tbuf[FFT_LDS];
   const Lds<BF> T{Tbuf};
-  const int b = blockIdx.x >> 4, cq = fft_block_cq(blockIdx.x);
+  const int b = fft_block_img(blockIdx.x), cq = fft_block_cq(blockIdx.x);
   const int q = cq >> 1, e0 = 4 * (cq & 1);
   const int tid = threadIdx.x;
   FFT_STAMP_AT(0);
@@ -601,7 +615,7 @@ __global__ __launch_bounds__(FNT, BF ? FFT_MINB_BF : FFT_MINB) void fft_inv_kern
                                                       int H, int W) {
   __shared__ typename Lds<BF>::elem Tbuf[FFT_LDS];
   const Lds<BF> T{Tbuf};
-  const int b = blockIdx.x >> 4, cq = fft_block_cq(blockIdx.x);
+  const int b = fft_block_img(blockIdx.x), cq = fft_block_cq(blockIdx.x);
   const int q = cq >> 1, e0 = 4 * (cq & 1);
   const int tid = threadIdx.x;
   FFT_STAMP_AT(0);
@@ -641,7 +655,7 @@ __global__ __launch_bounds__(FNT, BF ? FFT_MINB_BF : FFT_MINB) void fft_inv_a_fw
   __shared__ typename Lds<BF>::elem Tbuf[FFT_LDS];
   const Lds<BF> T{Tbuf};
   const int H = p.H, W = p.W;
-  const int b = blockIdx.x >> 4, cq = fft_block_cq(blockIdx.x);
+  const int b = fft_block_img(blockIdx.x), cq = fft_block_cq(blockIdx.x);
   const int q = cq >> 1, e0 = 4 * (cq & 1);
   const int tid = threadIdx.x;
   FFT_STAMP_AT(0);
