@@ -91,7 +91,9 @@ def fft_kernels(ctx, B, hw, steps, bf16=False):
         "epi_b": (5 * sm, 0.0),                        # P, I, O in; O', Og' out
     }
     out = {}
-    mfma_peak = PEAK_F16_TFLOPS if bf16 else PEAK_FP32_TFLOPS
+    # the fp32 path's spectral GEMM is f16x3 (three f16 MFMA products per fp32-accurate MAC): its
+    # ceiling is the dense f16 peak / 3, not the fp32 MFMA peak; bf16 is one product per MAC
+    mfma_peak = PEAK_F16_TFLOPS if bf16 else round(PEAK_F16_TFLOPS / 3, 1)
     for name, (byt, flop) in algo.items():
         ms, n = ctx.profile_read(name)
         if n == 0:
@@ -163,7 +165,7 @@ def fft_roofline(kern, bf16=False, batch=256, hbm_meas=None):
     r = {"kernel": name + " (k_fft.hip)", "avg_launch_ms": k["avg_launch_ms"], "launches": k["launches"],
          "traffic": traffic, "traffic_source": src, "algo_bytes": k["algo_bytes"]}
     t_hbm = k["algo_bytes"] / (PEAK_HBM_GBPS * 1e9)
-    peak = k.get("mfma_peak", PEAK_FP32_TFLOPS)
+    peak = k.get("mfma_peak", round(PEAK_F16_TFLOPS / 3, 1))
     t_mfma = k.get("algo_flop", 0.0) / (peak * 1e12)
     if t_mfma > t_hbm:
         r.update(bound="mfma", achieved=k["achieved_tflops"], peak=peak, unit="TFLOP/s",

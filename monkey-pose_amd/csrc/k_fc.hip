@@ -286,6 +286,179 @@ __global__ __launch_bounds__(256, 3) void fc_gemm_x3_kernel(const float* __restr
   }
 }
 
+// ---------------------------------------------------------------------------------------------
+// fc_1 on pre-split activations (the hGRU pose head, FFT dtypes): the last hGRU epilogue
+// (k_fft.hip spec_epi_b_kernel, mode 2) writes the BN'd NHWC activations as f16 hi / lo planes
+// Ah, Al [M][K] with exactly fc_gemm_x3_kernel's split (hi = (f16)a, lo = (f16)(a - hi)), so the K
+// loop here has no conversion work and no register staging: every K step's activation tile is
+// copied HBM -> LDS by global_load_lds_dwordx4 (1 KiB per wave-instruction, lane-linear in LDS),
+// double-buffered, one barrier per step, while the weights stream to registers one step ahead as
+// before.  The LDS image of a plane is [BM rows][BK k] f16 with the 16-byte chunks of each row
+// XOR-swizzled by row (the swizzle is applied to the global source address, since the DMA writes
+// LDS lane-linearly), so the 32 consecutive rows one ds_read_b128 fragment load touches hit
+// distinct banks.  MFMA order per output is fc_gemm_x3_kernel's: bit-identical results.
+#ifndef FC_P_MINB
+#define FC_P_MINB 3   // blocks per CU the pre-split kernel is register-budgeted for (one product)
+#endif
+#ifndef FC_P_BK3
+#define FC_P_BK3 32   // K step of the three-product kernel
+#endif
+#ifndef FC_P_MINB3
+#define FC_P_MINB3 3
+#endif
+#ifndef FC_P_NW3
+#define FC_P_NW3 4    // waves per block of the three-product kernel (each 32 output columns)
+#endif
+template <int BK>
+__device__ __forceinline__ int fcp_swz(int row) {   // 16-B chunk swizzle of a row (BK = 32: 4 chunks, 64: 8)
+  return BK == 32 ? (row >> 2) & 3 : (row >> 1) & 7;
+}
+
+template <int NP, int MB, int BK, int MINB, int NW = 4>
+__global__ __launch_bounds__(64 * NW, MINB) void fc_gemm_x3p_kernel(const _Float16* __restrict__ Ah,
+                                                               const _Float16* __restrict__ Al, int lda,
+                                                               const f16x8* __restrict__ Wpk,
+                                                               float* __restrict__ part, int M, int K, int N32,
+                                                               int kslice, float unscale, int S) {
+  constexpr int BM = 32 * MB;
+  constexpr int NPL = NP == 3 ? 2 : 1;         // activation planes staged (hi, lo)
+  constexpr int CH = BK / 8;                   // 16-B chunks per row
+  constexpr int PLANE = BM * BK;               // f16 per plane per stage
+  constexpr int STAGE = NPL * PLANE;
+  constexpr int RPI = 1024 / (BK * 2);         // rows per glds wave-instruction
+  constexpr int NI = NPL * BM / RPI;           // glds wave-instructions per stage
+  constexpr int NIW = (NI + NW - 1) / NW;      // per wave
+  __shared__ _Float16 lds[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, col = lane & 31;
+  const FcTile tl = fc_tile((M + BM - 1) / BM, (N32 + NW - 1) / NW);
+  if (tl.split >= S) return;
+  const int mt = tl.mt, ntile = tl.nt, split = tl.split;
+  const int K16 = (K + 15) / 16;
+  const int Npad = N32 * 32;
+  const int nb = ntile * NW + wv;
+  const bool wave_on = nb < N32;   // wave-uniform
+  const int nbc = min(nb, N32 - 1);
+  const int kbeg = split * kslice;
+  const int kend = min(K, kbeg + kslice);
+
+  // this lane's glds sources (k offset added per step) and the wave-uniform LDS destinations (a
+  // wave past the NI-th instruction repeats the last one: the same bytes to the same place)
+  const _Float16* src[NIW];
+  int dst[NIW];
+#pragma unroll
+  for (int j = 0; j < NIW; ++j) {
+    const int i = min(wv + NW * j, NI - 1);
+    const int pl = i / (BM / RPI), r0 = (i % (BM / RPI)) * RPI;
+    const int row = r0 + lane / CH, c = (lane % CH) ^ fcp_swz<BK>(row);
+    const int gm = min(mt * BM + row, M - 1);   // rows past M: valid addresses, outputs never stored
+    src[j] = (pl ? Al : Ah) + (size_t)gm * lda + 8 * c;
+    dst[j] = pl * PLANE + r0 * BK;
+  }
+  auto issue = [&](int k0, int stg) {
+#pragma unroll
+    for (int j = 0; j < NIW; ++j)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src[j] + k0),
+                                       (__attribute__((address_space(3))) void*)(lds + stg * STAGE + dst[j]), 16, 0, 0);
+  };
+  auto load_w = [&](int k0, f16x8 (&w)[BK / 16][2]) {
+#pragma unroll
+    for (int g = 0; g < BK / 16; ++g) {
+      const int kb = min((k0 >> 4) + g, K16 - 1);
+      const f16x8* wp = Wpk + (((size_t)kb * N32 + nbc) * 2) * 64 + lane;
+      w[g][0] = wp[0];
+      if constexpr (NP == 3) w[g][1] = wp[64];
+    }
+  };
+
+  f32x16 acc[MB];
+#pragma unroll
+  for (int m = 0; m < MB; ++m) acc[m] = f32x16{};
+  f16x8 wn[BK / 16][2];
+  if (kbeg < kend) {
+    issue(kbeg, 0);
+    load_w(kbeg, wn);
+  }
+  int stg = 0;
+  for (int k0 = kbeg; k0 < kend; k0 += BK, stg ^= 1) {
+    // this step's tile (DMA'd by every wave) and weights have landed; every wave is done reading
+    // the other stage (its previous step)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+    f16x8 wc[BK / 16][2];
+#pragma unroll
+    for (int g = 0; g < BK / 16; ++g) {
+      wc[g][0] = wn[g][0];
+      if constexpr (NP == 3) wc[g][1] = wn[g][1];
+    }
+    if (k0 + BK < kend) {
+      issue(k0 + BK, stg ^ 1);
+      load_w(k0 + BK, wn);
+    }
+    if (wave_on) {
+      const _Float16* tile = lds + stg * STAGE;
+#pragma unroll
+      for (int g = 0; g < BK / 16; ++g) {
+        const f16x8 wh = wc[g][0];
+        [[maybe_unused]] const f16x8 wl = wc[g][1];
+#pragma unroll
+        for (int m = 0; m < MB; ++m) {
+          const int row = m * 32 + col;
+          const int o = row * BK + 8 * ((2 * g + h) ^ fcp_swz<BK>(row));
+          const f16x8 ah = *reinterpret_cast<const f16x8*>(tile + o);
+          if constexpr (NP == 3) {
+            const f16x8 al = *reinterpret_cast<const f16x8*>(tile + PLANE + o);
+            acc[m] = mfma16(wl, ah, acc[m]);
+            acc[m] = mfma16(wh, al, acc[m]);
+          }
+          acc[m] = mfma16(wh, ah, acc[m]);
+        }
+      }
+    }
+  }
+  if (!wave_on) return;
+#pragma unroll
+  for (int m = 0; m < MB; ++m) {
+    const int gm = mt * BM + m * 32 + col;
+    if (gm >= M) continue;
+    float* dstp = part + ((size_t)split * M + gm) * Npad + 32 * nb + 4 * h;
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      *reinterpret_cast<f32x4*>(dstp + 8 * g) =
+          f32x4{acc[m][4 * g], acc[m][4 * g + 1], acc[m][4 * g + 2], acc[m][4 * g + 3]} * unscale;
+  }
+}
+
+hipError_t launch_fc_gemm_x3p(const void* Ah, const void* Al, int lda, const void* Wpk, float unscale, float* part,
+                              int M, int K, int N, int S, int kslice, hipStream_t st, int nprod) {
+  const int BK = nprod == 1 ? 64 : FC_P_BK3;
+  if (K % BK || kslice % BK || lda % 8 || (nprod == 3 && !Al)) return hipErrorInvalidValue;
+  const int N32 = (N + 31) / 32;
+  const int mb = M <= 32 ? 1 : (M <= 64 ? 2 : 4);
+  const int nw = nprod == 3 ? FC_P_NW3 : 4;   // waves (32-column groups) per block
+  const int grid = fc_grid((M + 32 * mb - 1) / (32 * mb), (N32 + nw - 1) / nw, S);
+  const _Float16* h = static_cast<const _Float16*>(Ah);
+  const _Float16* l = static_cast<const _Float16*>(Al);
+  const f16x8* w = static_cast<const f16x8*>(Wpk);
+#define MP_FCP(NPV, MBV, BKV, MINBV)                                                                                   \
+  hipLaunchKernelGGL((fc_gemm_x3p_kernel<NPV, MBV, BKV, MINBV>), dim3(grid), dim3(256), 0, st, h, l, lda, w, part, M, K, \
+                     N32, kslice, unscale, S)
+#define MP_FCP3(MBV)                                                                                                   \
+  hipLaunchKernelGGL((fc_gemm_x3p_kernel<3, MBV, FC_P_BK3, FC_P_MINB3, FC_P_NW3>), dim3(grid), dim3(64 * FC_P_NW3), 0, \
+                     st, h, l, lda, w, part, M, K, N32, kslice, unscale, S)
+  if (nprod == 1) {
+    if (mb == 1) MP_FCP(1, 1, 64, FC_P_MINB);
+    else if (mb == 2) MP_FCP(1, 2, 64, FC_P_MINB);
+    else MP_FCP(1, 4, 64, FC_P_MINB);
+  } else {
+    if (mb == 1) MP_FCP3(1);
+    else if (mb == 2) MP_FCP3(2);
+    else MP_FCP3(4);
+  }
+#undef MP_FCP
+#undef MP_FCP3
+  return hipGetLastError();
+}
+
 size_t fc_x3_bytes(int K, int N) { return (size_t)(K + 15) / 16 * ((N + 31) / 32) * 2 * 64 * sizeof(f16x8); }
 
 hipError_t launch_pack_fc_x3(const float* W, void* out, int K, int N, float* unscale, hipStream_t st) {

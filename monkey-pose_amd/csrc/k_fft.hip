@@ -1147,7 +1147,20 @@ __global__ __launch_bounds__(256) void spec_epi_b_kernel(ConvArgs p, const float
         f32x4 o;
 #pragma unroll
         for (int j = 0; j < 4; ++j) o[j] = Ov[n][4 * g + j] * ss[j] + tt[j];
-        *reinterpret_cast<f32x4*>(p.dst2 + (((size_t)b * H + y) * W + x) * C + c) = o;
+        const size_t e = (((size_t)b * H + y) * W + x) * C + c;
+        if (p.mode == 1) {
+          *reinterpret_cast<f32x4*>(p.dst2 + e) = o;
+        } else {   // mode 2: fc_1's f16 hi / lo planes, split exactly as fc_gemm_x3_kernel splits (k_fc.hip)
+          typedef _Float16 f16x4_t __attribute__((ext_vector_type(4)));
+          f16x4_t hv, lv;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            hv[j] = (_Float16)o[j];
+            lv[j] = (_Float16)(o[j] - (float)hv[j]);
+          }
+          *reinterpret_cast<f16x4_t*>(reinterpret_cast<_Float16*>(p.dst2) + e) = hv;
+          if (p.dst3) *reinterpret_cast<f16x4_t*>(reinterpret_cast<_Float16*>(p.dst3) + e) = lv;
+        }
       }
   }
 }

@@ -298,9 +298,30 @@ void store_step(const StateOut* so, const float* Omap, const float* Imap, int b0
   if (so->I) hip_check(launch_c8_to_nhwc(Imap, so->I + off, n, H, W, st, bf, stride), "store_states I");
 }
 
+// fc_1's pre-split activation planes (FFT path, k_fc.hip launch_fc_gemm_x3p): the last B epilogue
+// writes the BN'd NHWC output as f16 hi (and, for the three-product fc_1, lo) planes [batch][K]
+struct SplitOut {
+  _Float16* hi = nullptr;
+  _Float16* lo = nullptr;   // null: hi plane only (dtype bf16's one-product fc_1)
+};
+
+// final-step output arguments of the B epilogue for images from b0 on: NHWC fp32 (mode 1) or the
+// split planes (mode 2)
+void final_out(ConvArgs& b, float* final_dst2, const SplitOut* sp, int b0, int H, int W) {
+  const size_t m = (size_t)b0 * 64 * H * W;
+  if (sp) {
+    b.mode = 2;
+    b.dst2 = reinterpret_cast<float*>(sp->hi + m);
+    b.dst3 = sp->lo ? reinterpret_cast<float*>(sp->lo + m) : nullptr;
+  } else {
+    b.mode = 1;
+    b.dst2 = final_dst2 + m;
+  }
+}
+
 // the hGRU loop of images [b0, b0 + n) on stream st (FFT path), all state pointers offset
 void fft_circuit_range(mp_ctx* c, int b0, int n, int H, int W, int T, float* final_dst2, const StateOut* so,
-                       hipStream_t st) {
+                       const SplitOut* sp, hipStream_t st) {
   const size_t m = (size_t)b0 * 64 * H * W;              // elements per image of a C8 / NHWC map
   void* S = static_cast<char*>(c->specS.p) + fft_spec_bytes(b0);
   void* Y = static_cast<char*>(c->specY.p) + fft_spec_bytes(b0);
@@ -326,8 +347,9 @@ void fft_circuit_range(mp_ctx* c, int b0, int n, int H, int W, int T, float* fin
     b.I = map(c->I);
     b.vecs = c->vecs.f();
     b.rho = c->rho[t];
-    b.mode = (t == T - 1) ? 1 : 0;
-    b.dst2 = (t == T - 1) ? final_dst2 + m : map(c->Og);
+    b.mode = 0;
+    b.dst2 = map(c->Og);
+    if (t == T - 1) final_out(b, final_dst2, sp, b0, H, W);
     const bool bf = c->dtype == MP_DTYPE_BF16;
     hip_check(launch_fft_fwd(a.src, S, n, H, W, st, bf), "fft_fwd");
     hip_check(launch_spec_gemm(S, c->spec_g.p, Y, n, c->p_unscale, st, bf), "spec_gemm");
@@ -337,6 +359,15 @@ void fft_circuit_range(mp_ctx* c, int b0, int n, int H, int W, int T, float* fin
     hip_check(launch_spec_epi_b(b, P, c->or_x3.p, c->or_us, c->ir_x3.p, c->ir_us, n, st, bf), "B epilogue");
     store_step(so, b.O, b.I, b0, n, H, W, t, bm, st);
   }
+}
+
+// fc_1 on pre-split activation planes (MP_FC_PRESPLIT=0: the fp32 map + in-loop split, for A/B)
+bool fc_presplit() {
+  static const bool v = [] {
+    const char* e = std::getenv("MP_FC_PRESPLIT");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  return v;
 }
 
 int stream_count() {
@@ -357,7 +388,8 @@ int slice_min() {
 }
 
 void run_circuit(mp_ctx* c, int64_t n, int H, int W, int T, const float* o0_nhwc, float* final_dst2,
-                 const StateOut* so, hipStream_t st) {
+                 const StateOut* so, hipStream_t st, const SplitOut* sp = nullptr) {
+  if (sp && !is_fft(c->dtype)) fail(MP_ERR_STATE, "split fc_1 planes are an FFT-path output");
   // FFT path, not profiling: batch slices are independent, so they run on separate streams and
   // their latency-bound kernels overlap (the per-kernel HIP-event profile keeps one stream)
   const int ns = std::min<int>(stream_count(), (int)(n / slice_min()));
@@ -384,7 +416,7 @@ void run_circuit(mp_ctx* c, int64_t n, int H, int W, int T, const float* o0_nhwc
       const int cnt = std::min<int>(g * gs, (int)n - b0);
       hipStream_t s = k == 0 ? st : c->sides[k - 1];
       if (k > 0) hip_check(hipStreamWaitEvent(s, c->ev_fork, 0), "hipStreamWaitEvent");
-      fft_circuit_range(c, b0, cnt, H, W, T, final_dst2, so, s);
+      fft_circuit_range(c, b0, cnt, H, W, T, final_dst2, so, sp, s);
       b0 += cnt;
     }
     for (int k = 1; k < ns; ++k) {
@@ -420,8 +452,9 @@ void run_circuit(mp_ctx* c, int64_t n, int H, int W, int T, const float* o0_nhwc
     b.gpk_or = c->or_pk.v4();
     b.gpk_ir = c->ir_pk.v4();
     b.rho = c->rho[t];
-    b.mode = (t == T - 1) ? 1 : 0;
-    b.dst2 = (t == T - 1) ? final_dst2 : c->Og.f();
+    b.mode = 0;
+    b.dst2 = c->Og.f();
+    if (t == T - 1) final_out(b, final_dst2, sp, 0, H, W);
     if (is_fft(c->dtype)) {
       fft_step(c, a, b, (int)n, st);
     } else {
@@ -710,7 +743,18 @@ int mp_hgru_pose_fwd_taps(mp_ctx* ctx, const float* depth, int64_t n, int64_t h,
     so.O = tp.states_O;
     so.I = tp.states_I;
     so.T = ctx->timesteps;
-    run_circuit(ctx, n, H, W, ctx->timesteps, h0, ctx->fcin.f(), (so.O || so.I) ? &so : nullptr, st);
+    // FFT dtypes: the last B epilogue writes fc_1's f16 hi / lo activation planes into fcin (same
+    // bytes as the fp32 map), so fc_1 stages them by LDS-DMA with no conversion (bit-identical); the
+    // hgru tap needs the fp32 map, and MP_FC_PRESPLIT=0 restores that form for A/B
+    SplitOut sp;
+    const bool presplit = is_fft(ctx->dtype) && !tp.hgru && fc_presplit();
+    const int fc_np = ctx->dtype == MP_DTYPE_BF16 ? 1 : 3;   // bf16: one f16 product
+    if (presplit) {
+      sp.hi = reinterpret_cast<_Float16*>(ctx->fcin.p);
+      sp.lo = fc_np == 3 ? sp.hi + (size_t)N * ctx->fc1_in : nullptr;
+    }
+    run_circuit(ctx, n, H, W, ctx->timesteps, h0, ctx->fcin.f(), (so.O || so.I) ? &so : nullptr, st,
+                presplit ? &sp : nullptr);
     if (tp.hgru)
       hip_check(hipMemcpyAsync(tp.hgru, ctx->fcin.f(), (size_t)N * ctx->fc1_in * sizeof(float),
                                hipMemcpyDeviceToDevice, st),
@@ -722,9 +766,10 @@ int mp_hgru_pose_fwd_taps(mp_ctx* ctx, const float* depth, int64_t n, int64_t h,
       hip_check(ctx->dtype == MP_DTYPE_F32
                     ? launch_fc_gemm(ctx->fcin.f(), ctx->fc1_in, ctx->fc1_pk.v4(), ctx->part.f(), N, ctx->fc1_in,
                                      ctx->fc1_out, S, ks, st)
-                    : launch_fc_gemm_x3(ctx->fcin.f(), ctx->fc1_in, ctx->fc1_pk.p, ctx->fc1_unscale, ctx->part.f(),
-                                        N, ctx->fc1_in, ctx->fc1_out, S, ks, st,
-                                        ctx->dtype == MP_DTYPE_BF16 ? 1 : 3),   // bf16: one f16 product
+                : presplit ? launch_fc_gemm_x3p(sp.hi, sp.lo, ctx->fc1_in, ctx->fc1_pk.p, ctx->fc1_unscale,
+                                                ctx->part.f(), N, ctx->fc1_in, ctx->fc1_out, S, ks, st, fc_np)
+                           : launch_fc_gemm_x3(ctx->fcin.f(), ctx->fc1_in, ctx->fc1_pk.p, ctx->fc1_unscale,
+                                               ctx->part.f(), N, ctx->fc1_in, ctx->fc1_out, S, ks, st, fc_np),
                 "fc_1 gemm");
       if (tp.fc1)   // fc_1 + bias before the relu (same partial sums)
         hip_check(launch_fc_reduce(ctx->part.f(), S, N, ctx->fc1_out, ctx->fc1_b.f(), 0, nullptr, nullptr, tp.fc1,

@@ -23,9 +23,10 @@ struct ConvArgs {
   const float* vecs;      // [V_COUNT][64]
   const f32x4* gpk_or;    // B: packed o_r
   const f32x4* gpk_ir;    // B: packed i_r (next step's input gate)
-  float* dst2;            // B mode 0: Og' (C8);  mode 1: affine(O') NHWC
+  float* dst2;            // B mode 0: Og' (C8);  mode 1: affine(O') NHWC;  mode 2: its f16 hi plane
+  float* dst3;            // B mode 2 (FFT path): the f16 lo plane of affine(O') NHWC (null: hi only)
   float rho;              // B: rho[t]
-  int mode;               // B: 0 = next-step gate, 1 = final step
+  int mode;               // B: 0 = next-step gate, 1 = final step, 2 = final step as fc_1's split planes
   int H, W, tiles_x, tiles_y;
   float ascale;           // f16x3 kernel: activation split scale (0 = the hGRU default 2^10)
   int dst_bf16;           // BB: dst is a bf16 C8 map (MP_DTYPE_BF16's hGRU drive X)
@@ -114,6 +115,10 @@ size_t fc_x3_bytes(int K, int N);
 hipError_t launch_pack_fc_x3(const float* W, void* out, int K, int N, float* unscale, hipStream_t st);
 hipError_t launch_fc_gemm_x3(const float* A, int lda, const void* Wpk, float unscale, float* part, int M, int K,
                              int N, int S, int kslice, hipStream_t st, int nprod = 3);
+// the same GEMM on activations already split into f16 hi / lo planes [M][lda] (Al unused when
+// nprod = 1): bit-identical partial sums, no conversion in the K loop (LDS-DMA staging)
+hipError_t launch_fc_gemm_x3p(const void* Ah, const void* Al, int lda, const void* Wpk, float unscale, float* part,
+                              int M, int K, int N, int S, int kslice, hipStream_t st, int nprod = 3);
 // k_frame.hip (frame -> CoM -> crop chain)
 hipError_t launch_resize_bilinear(const float* x, int N, int H, int W, int C, float* out, int Ho, int Wo,
                                   hipStream_t st);

@@ -1,5 +1,5 @@
-"""The A/B switches read once at library load (MP_BF16_MAPS, MP_IGEMM_PM_SPLITS, MP_IGEMM_XCD,
-MP_IGEMM_HALO) keep their paths correct: each case runs in one child process with the switch set
+"""The A/B switches read once at library load (MP_BF16_MAPS, MP_FC_PRESPLIT, MP_IGEMM_PM_SPLITS,
+MP_IGEMM_XCD, MP_IGEMM_HALO) keep their paths correct: each case runs in one child process with the switch set
 (the parent's library already made its choice), against the committed golden vectors."""
 import json
 import os
@@ -41,6 +41,8 @@ print(json.dumps({{"err": float(rel_inf(out, ref))}}))
 CASES = [
     # (env, model, dtype, gate)
     ({"MP_BF16_MAPS": "0"}, "pose", "bf16", 5e-3),
+    ({"MP_FC_PRESPLIT": "0"}, "pose", "fp32_fft", 1e-4),
+    ({"MP_FC_PRESPLIT": "0"}, "pose", "bf16", 5e-3),
     ({"MP_IGEMM_PM_SPLITS": "1"}, "hier", "fp32_split", 1e-4),
     ({"MP_IGEMM_PM_SPLITS": "1"}, "hier", "bf16", 5e-3),
     ({"MP_IGEMM_XCD": "0", "MP_IGEMM_HALO": "0"}, "hier", "fp32_split", 1e-4),

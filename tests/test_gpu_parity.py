@@ -96,6 +96,26 @@ def test_pose_intermediates_match_oracle(dtype):
         assert np.array_equal(getattr(m, k).cpu().numpy(), lazy[k]), k
 
 
+@pytest.mark.parametrize("n", [1, 33, 130])
+@pytest.mark.parametrize("dtype", ["fp32_fft", "bf16"])
+def test_fc1_presplit_planes_bit_identical(dtype, n):
+    """fc_1 on the f16 hi / lo planes the last B epilogue writes (spec_epi_b mode 2 ->
+    k_fc.hip fc_gemm_x3p_kernel, LDS-DMA staging) equals fc_1 on the fp32 map (the hgru-tap path,
+    fc_gemm_x3_kernel's in-loop split) bit for bit: 32-, 64- and 128-row tiles, a partial tile."""
+    mp = pkg()
+    W = mp.weights
+    crop = 64
+    wts = W.synth_weights(W.hgru_pose_vars(crop=crop), seed=11)
+    depth = W.synth_crops(n, seed=12, size=crop)
+    O0 = W.synth_hidden((n, crop // 2, crop // 2, 64), seed=13)
+    m = mp.hgru_pose.model()
+    m.compute_dtype = dtype
+    m.load_weights(wts)
+    plain = m.build(_cuda(depth), 69, h2_init=_cuda(O0)).cpu().numpy()
+    tapped = m.build(_cuda(depth), 69, h2_init=_cuda(O0), keep_intermediates=True).cpu().numpy()
+    assert np.array_equal(plain, tapped)
+
+
 @pytest.mark.parametrize("dtype", DTYPES)
 def test_batch_invariance_and_determinism(dtype):
     """Each crop's output is bit-identical alone or inside a batch, and run to run."""
