@@ -243,7 +243,9 @@ int mp_crop3d_dev(const mp_camera* cam, const float* frames, int64_t n, int64_t 
 /* read a model property: "output_shape", "timesteps", "ssf", "finalized", "workspace_bytes",
  * "weight_bytes"; graph contexts also "graph_kernels" (kernel launches per forward),
  * "graph_streams" (streams the schedule uses), "graph_captured" (1 once a hipGraph was built, MP_GRAPH_EXEC=1),
- * "graph_buffers" (activation buffers after concat placement) -- as planned by the last forward */
+ * "graph_buffers" (activation buffers after concat placement), "graph_fused_pools" (2x2 max pools
+ * computed inside their conv's kernel: MP_GRAPH_FUSE / MP_GRAPH_FUSE_POOL) -- as planned by the
+ * last forward */
 int mp_info(mp_ctx* ctx, const char* key, int64_t* value);
 
 /* per-kernel device timing with HIP events recorded on the launch stream around every launch of

@@ -142,6 +142,9 @@ __device__ __forceinline__ cpx swp(cpx a) { return {a.y, a.x}; }
 #ifndef FFT_NT_MAP
 #define FFT_NT_MAP 0        // pixel-major stores of P2 and I
 #endif
+#ifndef FFT_EPI_EU
+#define FFT_EPI_EU 8        // inv_a_fwd epilogue, fp32 maps: pixels per thread per load chunk
+#endif
 #ifndef FFT_EPI_PIPE
 #define FFT_EPI_PIPE 1      // inv_a_fwd epilogue, bf16 maps: next chunk's X / O loads issued before this chunk's math
 #endif
@@ -685,7 +688,7 @@ __global__ __launch_bounds__(FNT, BF ? FFT_MINB_BF : FFT_MINB) void fft_inv_a_fw
     // maps (PIPE) the next chunk's loads are issued before this chunk's math: the phase is ~45k of
     // the block's ~100k cycles (tools/fft_stamps.hip); with fp32 maps the second register set
     // measured 2-4 % slower (inv_a_fwd 0.338 -> 0.351 ms), so there it stays one chunk at a time
-    constexpr int EU = 8, ECH = EU * FNT, NECH = (64 * 64 + ECH - 1) / ECH;
+    constexpr int EU = BM ? 8 : FFT_EPI_EU, ECH = EU * FNT, NECH = (64 * 64 + ECH - 1) / ECH;
     constexpr bool PIPE = FFT_EPI_PIPE && BM;
     f32x4 xv[2][EU], ov[2][EU];
     auto load_chunk = [&](int k, f32x4 (&xs)[EU], f32x4 (&os)[EU]) {

@@ -548,9 +548,29 @@ __global__ __launch_bounds__(256) void igemm_pm_reduce_kernel(IgemmArgs p, int S
   if (i >= (size_t)M * nq) return;
   const int gm = (int)(i / nq), c = (int)(i - (size_t)gm * nq) * 4;
   if (c >= p.Cout) return;
-  const float* src = p.part + (size_t)gm * (N32 * 32) + c;
-  f32x4 s = *reinterpret_cast<const f32x4*>(src);
-  for (int z = 1; z < S; ++z) s += *reinterpret_cast<const f32x4*>(src + (size_t)z * M * (N32 * 32));
+  auto sum = [&](int row) {
+    const float* src = p.part + (size_t)row * (N32 * 32) + c;
+    f32x4 s = *reinterpret_cast<const f32x4*>(src);
+    for (int z = 1; z < S; ++z) s += *reinterpret_cast<const f32x4*>(src + (size_t)z * M * (N32 * 32));
+    return s;
+  };
+  if (p.pool) {   // fused 2x2/2 max pool: this thread = pooled position q (the top-left window row)
+    const int n = gm % p.N, pos = gm / p.N, y = pos / p.Wo, x = pos - y * p.Wo;
+    if ((y & 1) || (x & 1)) return;
+    float best[4] = {-INFINITY, -INFINITY, -INFINITY, -INFINITY};
+#pragma unroll
+    for (int d = 0; d < 4; ++d) {
+      const f32x4 s = sum(((y + (d >> 1)) * p.Wo + x + (d & 1)) * p.N + n);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) best[j] = fmaxf(best[j], fmaxf(s[j] * unscale + (c + j < p.Cout ? p.bias[c + j] : 0.f), 0.f));
+    }
+    float* dst = p.out + (((size_t)n * (p.Ho / 2) + y / 2) * (p.Wo / 2) + x / 2) * p.ldo + p.coff + c;
+#pragma unroll
+    for (int j = 0; j < 4; ++j)
+      if (c + j < p.Cout) dst[j] = best[j];
+    return;
+  }
+  const f32x4 s = sum(gm);
   float* dst = p.out + ((size_t)(gm % p.N) * HWo + gm / p.N) * p.ldo + p.coff + c;
 #pragma unroll
   for (int j = 0; j < 4; ++j) {
@@ -743,6 +763,96 @@ struct HaloGeom {
   int R, NI, HH, WW, PH;   // rows per tile, images per tile, halo rows / cols per image, halo pixels
 };
 
+// The halo kernel's epilogue with the 2x2/2 max pool of relu(conv + bias) fused (hier: every conv
+// feeds exactly one max_pool, train_hier_networks.py:536-569): the pre-pool map is never written.
+// A tile is R (even) whole rows of W (even) pixels, so every pool window lies in one tile: lane
+// pairs (col, col ^ 1) hold its two columns; its two rows are lanes (col, col ^ W) of one 32-pixel
+// block (W <= 16), the two blocks of one wave (W = 32), or the two wave rows (W = 64, exchanged
+// through LDS).  max is exact, so the pooled values are bit-identical to conv -> pool2_kernel.
+__device__ __forceinline__ float dpp_xor1(float v) {   // lane ^ 1 (quad_perm [1,0,3,2])
+  return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
+}
+__device__ void halo_pool_epilogue(const IgemmArgs& p, const HaloGeom& hg, f32x16 (&acc)[2][2], bool wave_on,
+                                   float unscale, int m0, int nb0, _Float16* lds) {
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, col = lane & 31;
+  const int wm = wv & 1, wn = wv >> 1;
+  const int N32 = (p.Cout + 31) / 32, W = p.W, HW = p.H * W;
+  // relu(acc * unscale + bias), then the max over the column pair
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      const int cb = min(nb0 + 2 * wn + nb, N32 - 1);
+#pragma unroll
+      for (int e = 0; e < 16; ++e) {
+        const int c = cb * 32 + 8 * (e >> 2) + 4 * h + (e & 3);
+        const float v = fmaxf(acc[mb][nb][e] * unscale + (c < p.Cout ? p.bias[c] : 0.f), 0.f);
+        acc[mb][nb][e] = fmaxf(v, dpp_xor1(v));
+      }
+    }
+  // the max over the row pair
+  if (W <= 16) {
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[mb][nb][e] = fmaxf(acc[mb][nb][e], __shfl_xor(acc[mb][nb][e], W));
+  } else if (W == 32) {
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+      for (int e = 0; e < 16; ++e) acc[0][nb][e] = fmaxf(acc[0][nb][e], acc[1][nb][e]);
+  } else {   // W = 64: wave row wm = 1 hands its values to wm = 0 through LDS (the halo buffers are free
+             // once every wave is past its last MFMA)
+    float* x = reinterpret_cast<float*>(lds);
+    lds_barrier();
+    if (wm == 1) {
+#pragma unroll
+      for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+          for (int e = 0; e < 16; ++e) x[(((wn * 2 + mb) * 2 + nb) * 16 + e) * 64 + lane] = acc[mb][nb][e];
+    }
+    lds_barrier();
+    if (wm == 0) {
+#pragma unroll
+      for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb)
+#pragma unroll
+          for (int e = 0; e < 16; ++e)
+            acc[mb][nb][e] = fmaxf(acc[mb][nb][e], x[(((wn * 2 + mb) * 2 + nb) * 16 + e) * 64 + lane]);
+    }
+  }
+  if (!wave_on) return;
+  const int Ho = p.H / 2, Wo = W / 2;
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb) {
+    const int pp = (2 * wm + mb) * 32 + col;   // pixel of the tile
+    const int gm = m0 + pp;
+    const int n = gm / HW, y = (gm - n * HW) / W, xx = gm % W;
+    // the window's top-left lane writes: even column, even row, and (W = 32) block 0 / (W = 64) wave row 0
+    const bool top = (W <= 16) ? ((y & 1) == 0) : (W == 32 ? mb == 0 : wm == 0);
+    if ((xx & 1) || !top || gm >= p.N * HW) continue;
+    float* dst = p.out + (((size_t)n * Ho + y / 2) * Wo + xx / 2) * p.ldo + p.coff;
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      const int cb = nb0 + 2 * wn + nb;
+      if (cb >= N32) break;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int c = cb * 32 + 8 * g + 4 * h;
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (c + j < p.Cout) dst[c + j] = acc[mb][nb][4 * g + j];
+      }
+    }
+  }
+  (void)hg;
+}
+
 template <int KS, int NP>
 __global__ __launch_bounds__(256, 2) void igemm_x3h_kernel(IgemmArgs p, HaloGeom hg, const f16x8* __restrict__ wpk,
                                                           float unscale) {
@@ -872,6 +982,10 @@ __global__ __launch_bounds__(256, 2) void igemm_x3h_kernel(IgemmArgs p, HaloGeom
       store_halo((c + 1) & 1, hv);   // that buffer was last read in chunk c - 1, before the last barrier
       lds_barrier();
     }
+  }
+  if (p.pool) {   // fused 2x2/2 max pool (uniform branch): the pooled map goes to the output view
+    halo_pool_epilogue(p, hg, acc, wave_on, unscale, m0, nb0, hs);
+    return;
   }
   if (!wave_on) return;
   const bool vst = (p.ldo % 4 == 0) && (p.coff % 4 == 0) && (p.Cout % 4 == 0);
@@ -1028,8 +1142,17 @@ size_t igemm_pm_part_floats(const IgemmArgs& a) {
   return S > 1 ? (size_t)S * a.N * a.Ho * a.Wo * ((a.Cout + 31) / 32 * 32) : 0;
 }
 
+bool igemm_can_pool(const IgemmArgs& a) {
+  if (!a.relu || a.Ho % 2 || a.Wo % 2 || !wide_path(a)) return false;
+  HaloGeom hg;
+  size_t lds;
+  if (halo_geom(a, hg, lds)) return hg.R % 2 == 0 && a.W <= 64 && 4096 * sizeof(float) <= lds;   // W = 64 exchange
+  return pm_path(a) && a.part && igemm_pm_splits(a) > 1;   // the split-K reduce pools
+}
+
 hipError_t launch_igemm_x3(const IgemmArgs& a, const void* wpk, float unscale, hipStream_t st) {
   if (a.K < 4) return hipErrorInvalidValue;   // the clamped vector load needs K >= 4
+  if (a.pool && !igemm_can_pool(a)) return hipErrorInvalidValue;
   const int M = a.N * a.Ho * a.Wo;
   const int N32 = (a.Cout + 31) / 32;
   const int nb = N32 >= 4 ? 4 : (N32 >= 2 ? 2 : 1);

@@ -329,6 +329,21 @@ void plan(mp_ctx* c, G& g, int64_t n, int64_t h, int64_t w) {
         }
       }
     }
+  // conv -> 2x2 max pool pairs where the pool is the conv's only consumer: the f16x3 conv kernels
+  // can write the pooled map themselves (k_igemm.hip igemm_can_pool; decided per conv below)
+  std::vector<int> pool_after(g.ops.size(), -1);
+  if (env_int("MP_GRAPH_FUSE_POOL", 1))
+    for (size_t i = 0; i < g.ops.size(); ++i) {
+      const auto& op = g.ops[i];
+      if (op.kind != MP_OP_CONV || fused_pool[i] >= 0 || uses[op.out] != 1) continue;
+      for (size_t j = i + 1; j < g.ops.size(); ++j) {
+        const auto& pj = g.ops[j];
+        if (pj.kind == MP_OP_MAXPOOL && pj.ksize == 2 && pj.src[0] == op.out && root(pj.out) == pj.out) {
+          pool_after[i] = (int)j;
+          break;
+        }
+      }
+    }
   // kernels and their producers
   for (size_t i = 0; i < g.ops.size(); ++i) {
     const auto& op = g.ops[i];
@@ -406,6 +421,16 @@ void plan(mp_ctx* c, G& g, int64_t n, int64_t h, int64_t w) {
           k->part.alloc(pf * sizeof(float));
           a.part = k->part.f();
         }
+      }
+      const int pj = pool_after[i];
+      if (L.x3 && pj >= 0 && igemm_can_pool(a)) {
+        // conv + relu + max pool in one kernel: the pre-pool map is never written
+        a.pool = 1;
+        a.out = base(g.ops[pj].out);
+        a.ldo = ld(g.ops[pj].out);
+        a.coff = coff(g.ops[pj].out);
+        fused_away[pj] = 1;
+        T[g.ops[pj].out].prod = {(int)g.kerns.size()};
       }
     } else if (op.kind == MP_OP_MAXPOOL || op.kind == MP_OP_AVGPOOL) {
       if (op.ksize != 2) fail(MP_ERR_UNSUPPORTED, "pool window " + std::to_string(op.ksize) + " (only 2x2/2)");
@@ -711,6 +736,11 @@ bool graph_info(mp_ctx* c, const std::string& k, int64_t* v) {
     *v = g.captured ? 1 : 0;
   else if (k == "graph_buffers")
     *v = (int64_t)g.groups.size();
+  else if (k == "graph_fused_pools") {   // max pools computed inside their conv's kernel
+    int64_t f = 0;
+    for (const auto& kk : g.kerns) f += (kk->kind == MP_OP_CONV && kk->ia.pool) || kk->kind == KIND_CONV1_POOL;
+    *v = f;
+  }
   else
     fail(MP_ERR_ARG, "unknown info key: " + k);
   return true;

@@ -93,7 +93,13 @@ struct IgemmArgs {
                            // floats, caller-owned); null: no split
   int nprod = 3;           // f16 split kernels: 3 = fp32-accurate f16x3, 1 = hi x hi only (bf16 dtype)
   int xcd = 0;             // set by the launcher: XCD-aware tile order (k_igemm.hip xcd_tile)
+  int pool = 0;            // 1: a 2x2/2 max pool of relu(conv) is fused into the epilogue, and the
+                           // output view (out, ldo, coff) is the pooled (Ho/2 x Wo/2) map;
+                           // only where igemm_can_pool(a) holds
 };
+// whether launch_igemm_x3 can fuse the conv's 2x2 max pool (the halo and the split-K position-major
+// paths, even output sizes, relu on)
+bool igemm_can_pool(const IgemmArgs& a);
 // input-channel splits of the position-major tap-skipping path for this conv (1 = none); a property
 // of the layer alone (never of the batch), so every crop's sums group the same way at any batch
 int igemm_pm_splits(const IgemmArgs& a);

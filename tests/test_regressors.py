@@ -150,3 +150,26 @@ def test_regressors_bf16_within_bf16_gate(kind, engine):
     assert err <= BF16_REL_TOL
     one = model.forward(torch.from_numpy(depth[1:2]).cuda()).cpu().numpy()
     assert np.array_equal(one[0], out[1])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["fp32_split", "bf16"])
+def test_hier_fused_conv_pool_bit_identical(dtype, monkeypatch):
+    """The graph runtime fuses every hier conv -> 2x2 max pool pair into the conv kernel (halo
+    epilogue for conv_2 / con_3 / con_4 / con_5 at W = 64 / 32 / 16 / 8, the split-K reduce for
+    con_6): all six outputs are bit-identical to the unfused conv + pool2_kernel schedule
+    (MP_GRAPH_FUSE_POOL=0), at an odd batch (a partial last tile of two-image con_5 tiles)."""
+    torch = pytest.importorskip("torch")
+    W = pkg().weights
+    outs = {}
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("MP_GRAPH_FUSE_POOL", fuse)
+        model = pkg().train_hier_networks.hier_model_struct()
+        model.compute_dtype = dtype
+        g = model.record(128, 128, *MG.HIER_HEADS)
+        model.load_weights(W.synth_weights(model._table(g), seed=21))
+        depth = torch.from_numpy(W.synth_crops(5, seed=22, size=128)).cuda()
+        main = model.build(depth, *MG.HIER_HEADS, train_mode=False)
+        outs[fuse] = [main.cpu().numpy()] + [getattr(model, f"{f}_output").cpu().numpy() for f in "prmit"]
+    for a, b in zip(outs["1"], outs["0"]):
+        assert np.array_equal(a, b)

@@ -5,6 +5,9 @@ set -e
 cd "$(dirname "$0")/../monkey-pose_amd/csrc"
 src=$1; out=$2; shift 2
 obj=/tmp/exp_$(basename "$out" .so).o
-/opt/rocm/bin/hipcc --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result "$@" -c "$src" -o "$obj"
+# the Makefile's per-source flags (k_fft.hip: -fno-slp-vectorize -- without it the FFT kernels are
+# SLP-packed, spill, and round differently)
+extra=""; [ "$src" = k_fft.hip ] && extra="-fno-slp-vectorize"
+/opt/rocm/bin/hipcc $extra --offload-arch=gfx950 -O3 -std=c++17 -fPIC -Wall -Wno-unused-result "$@" -c "$src" -o "$obj"
 objs=$(ls build/*.o | grep -v "build/${src%.hip}.o")
 /opt/rocm/bin/hipcc --offload-arch=gfx950 -shared -fPIC -o "$out" $objs "$obj" -Wl,-rpath,/opt/rocm/lib
