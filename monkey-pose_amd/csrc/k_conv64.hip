@@ -186,6 +186,69 @@ __global__ __launch_bounds__(256) void conv1_pool_bn_kernel(const float* __restr
   }
 }
 
+// The same fused 1-channel conv_layer + 2x2/2 max pool for any Cout % 4 == 0 (the dense regressor's
+// conv_0: 1 -> 12, train_dense_networks.py:229-236), written to an NHWC view (ldo, coff) -- the
+// graph runtime's concat buffers.  Exact fp32 FMAs, relu before the max; one thread per pooled
+// pixel and 4 output channels.
+__global__ __launch_bounds__(256) void conv1_pool_any_kernel(const float* __restrict__ in,
+                                                             const float* __restrict__ w,   // [9][Cout]
+                                                             const float* __restrict__ bias, float* out,
+                                                             int ldo, int coff, int B, int Hin, int Win, int Cout) {
+  const int Ho = Hin / 2, Wo = Win / 2, nq = Cout / 4;
+  const size_t total = (size_t)B * Ho * Wo * nq;
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int q = i % nq;
+  const size_t pix = i / nq;
+  const int x = pix % Wo;
+  const int y = (pix / Wo) % Ho;
+  const int b = pix / ((size_t)Wo * Ho);
+  float pt[4][4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int c = 0; c < 4; ++c) {
+      const int yy = 2 * y - 1 + r, xx = 2 * x - 1 + c;
+      const bool ok = yy >= 0 && yy < Hin && xx >= 0 && xx < Win;
+      const float v = in[((size_t)b * Hin + min(max(yy, 0), Hin - 1)) * Win + min(max(xx, 0), Win - 1)];
+      pt[r][c] = ok ? v : 0.f;
+    }
+  f32x4 o;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    const int ch = 4 * q + e;
+    float best = 0.f;   // relu output >= 0, so 0 is the identity of the max
+#pragma unroll
+    for (int dy = 0; dy < 2; ++dy)
+#pragma unroll
+      for (int dx = 0; dx < 2; ++dx) {
+        float sacc = 0.f;
+#pragma unroll
+        for (int ky = 0; ky < 3; ++ky)
+#pragma unroll
+          for (int kx = 0; kx < 3; ++kx) sacc = fmaf(pt[dy + ky][dx + kx], w[(ky * 3 + kx) * Cout + ch], sacc);
+        best = fmaxf(best, fmaxf(sacc + bias[ch], 0.f));
+      }
+    o[e] = best;
+  }
+  float* dst = out + pix * ldo + coff + 4 * q;
+  if ((ldo | coff) % 4 == 0) {
+    *reinterpret_cast<f32x4*>(dst) = o;
+  } else {
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dst[e] = o[e];
+  }
+}
+
+hipError_t launch_conv1_pool_any(const float* in, const float* w, const float* bias, float* out, int ldo, int coff,
+                                 int B, int Hin, int Win, int Cout, hipStream_t st) {
+  if (Cout % 4 || Hin % 2 || Win % 2) return hipErrorInvalidValue;
+  const size_t total = (size_t)B * (Hin / 2) * (Win / 2) * (Cout / 4);
+  hipLaunchKernelGGL(conv1_pool_any_kernel, dim3((total + 255) / 256), dim3(256), 0, st, in, w, bias, out, ldo, coff, B,
+                     Hin, Win, Cout);
+  return hipGetLastError();
+}
+
 // layout conversions (standalone ContextualCircuit API, debug taps)
 __global__ void nhwc_to_c8_kernel(const float* __restrict__ in, float* out, int B, int H, int W, bool bf) {
   const size_t total = (size_t)B * H * W * NQ;

@@ -314,14 +314,13 @@ void plan(mp_ctx* c, G& g, int64_t n, int64_t h, int64_t w) {
   if (env_int("MP_GRAPH_FUSE", 1))
     for (size_t i = 0; i < g.ops.size(); ++i) {
       const auto& op = g.ops[i];
-      if (op.kind != MP_OP_CONV || op.ksize != 3 || op.stride != 1 || op.cout != 64) continue;
+      if (op.kind != MP_OP_CONV || op.ksize != 3 || op.stride != 1 || op.cout % 4 || op.cout > 64) continue;
       const int s = op.src[0];
       if (root(s) != s || T[s].C != 1 || T[s].H % 2 || T[s].W % 2 || ld(s) != 1 || coff(s) != 0) continue;
       if (uses[op.out] != 1) continue;
       for (size_t j = i + 1; j < g.ops.size(); ++j) {
         const auto& pj = g.ops[j];
-        if (pj.kind == MP_OP_MAXPOOL && pj.ksize == 2 && pj.src[0] == op.out && root(pj.out) == pj.out &&
-            ld(pj.out) == 64 && coff(pj.out) == 0) {
+        if (pj.kind == MP_OP_MAXPOOL && pj.ksize == 2 && pj.src[0] == op.out && root(pj.out) == pj.out) {
           fused_pool[i] = (int)j;
           fused_away[j] = 1;
           // the pre-pool map is never materialised: drop its (singleton) buffer
@@ -355,7 +354,7 @@ void plan(mp_ctx* c, G& g, int64_t n, int64_t h, int64_t w) {
       k->op = (int)i;
       k->kind = KIND_CONV1_POOL;
       const auto& L = c->layers.at(op.name);
-      if (L.cin != 1 || L.cout != 64 || L.k != 3) fail(MP_ERR_SHAPE, "conv " + op.name + ": weights mismatch");
+      if (L.cin != 1 || L.cout != op.cout || L.k != 3) fail(MP_ERR_SHAPE, "conv " + op.name + ": weights mismatch");
       k->L = &L;
       k->px = base(op.src[0]);
       k->cH = T[op.src[0]].H;
@@ -363,6 +362,9 @@ void plan(mp_ctx* c, G& g, int64_t n, int64_t h, int64_t w) {
       k->cw = c->raw.at(op.name + "/" + op.name + "_filters").dev->f();
       k->cb = L.b.f();
       k->pout = base(pj.out);
+      k->pldo = ld(pj.out);
+      k->pcoff = coff(pj.out);
+      k->pC = op.cout;
       std::vector<float> one(64, 1.f), zero(64, 0.f);
       upload(k->ones, one);
       upload(k->zeros, zero);
@@ -547,9 +549,15 @@ void launch_kern(mp_ctx* c, G& g, G::Kern& k, hipStream_t st) {
     case KIND_CONV1_POOL: {
       ProfScope ps(c, st, "graph_conv");
       ProfScope pl(c, st, g.ops[k.op].name.c_str());
-      hip_check(launch_conv1_pool_bn(k.px, k.cw, k.cb, k.ones.f(), k.zeros.f(), k.pout, (int)g.pn, k.cH, k.cW, st,
-                                     true),
-                g.ops[k.op].name.c_str());
+      // the hGRU backbone's conv_1 kernel for a dense 64-channel output (hier conv_1), else the
+      // any-width form writing into the pool output's view (dense conv_0: 12 channels)
+      if (k.pC == 64 && k.pldo == 64 && k.pcoff == 0)
+        hip_check(launch_conv1_pool_bn(k.px, k.cw, k.cb, k.ones.f(), k.zeros.f(), k.pout, (int)g.pn, k.cH, k.cW, st,
+                                       true),
+                  g.ops[k.op].name.c_str());
+      else
+        hip_check(launch_conv1_pool_any(k.px, k.cw, k.cb, k.pout, k.pldo, k.pcoff, (int)g.pn, k.cH, k.cW, k.pC, st),
+                  g.ops[k.op].name.c_str());
       break;
     }
     case MP_OP_CONV: {

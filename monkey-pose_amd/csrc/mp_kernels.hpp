@@ -39,6 +39,9 @@ hipError_t launch_gate_init(const float* O0, float* O, float* Og, const f32x4* g
 hipError_t launch_conv1_pool_bn(const float* in, const float* w, const float* bias, const float* s,
                                 const float* t, float* out, int B, int Hin, int Win, hipStream_t st,
                                 bool nhwc = false);
+// 1-channel 3x3 SAME conv + relu + 2x2/2 max pool for Cout % 4 == 0, NHWC output view (ldo, coff)
+hipError_t launch_conv1_pool_any(const float* in, const float* w, const float* bias, float* out, int ldo, int coff,
+                                 int B, int Hin, int Win, int Cout, hipStream_t st);
 // bf: the C8 side is a bf16 map
 hipError_t launch_nhwc_to_c8(const float* in, float* out, int B, int H, int W, hipStream_t st, bool bf = false);
 hipError_t launch_c8_to_nhwc(const float* in, float* out, int B, int H, int W, hipStream_t st, bool bf = false,
