@@ -459,6 +459,22 @@ hipError_t launch_fc_gemm_x3p(const void* Ah, const void* Al, int lda, const voi
   return hipGetLastError();
 }
 
+__global__ void pad_cin_kernel(const float* __restrict__ w, float* __restrict__ out, int taps, int Cin, int cinp,
+                               int Cout) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (size_t)taps * cinp * Cout) return;
+  const int co = i % Cout;
+  const size_t r = i / Cout;
+  const int ci = r % cinp, t = r / cinp;
+  out[i] = ci < Cin ? w[((size_t)t * Cin + ci) * Cout + co] : 0.f;
+}
+
+hipError_t launch_pad_cin(const float* w, float* out, int taps, int Cin, int cinp, int Cout, hipStream_t st) {
+  const size_t total = (size_t)taps * cinp * Cout;
+  hipLaunchKernelGGL(pad_cin_kernel, dim3((total + 255) / 256), dim3(256), 0, st, w, out, taps, Cin, cinp, Cout);
+  return hipGetLastError();
+}
+
 size_t fc_x3_bytes(int K, int N) { return (size_t)(K + 15) / 16 * ((N + 31) / 32) * 2 * 64 * sizeof(f16x8); }
 
 hipError_t launch_pack_fc_x3(const float* W, void* out, int K, int N, float* unscale, hipStream_t st) {

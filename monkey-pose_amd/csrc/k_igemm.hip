@@ -853,12 +853,15 @@ __device__ void halo_pool_epilogue(const IgemmArgs& p, const HaloGeom& hg, f32x1
   (void)hg;
 }
 
-template <int KS, int NP>
+// NARROW (Cout <= 64): the four waves side by side along the pixels, each 32 pixels x 64 couts
+// (one 32-pixel block), instead of the 2 x 2 grid whose second wave column would idle
+template <int KS, int NP, bool NARROW = false>
 __global__ __launch_bounds__(256, 2) void igemm_x3h_kernel(IgemmArgs p, HaloGeom hg, const f16x8* __restrict__ wpk,
                                                           float unscale) {
+  constexpr int MBW = NARROW ? 1 : 2;   // 32-pixel blocks per wave
   extern __shared__ _Float16 hs[];   // [2][PH][HX_PITCH]
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, col = lane & 31;
-  const int wm = wv & 1, wn = wv >> 1;
+  const int wm = NARROW ? wv : (wv & 1), wn = NARROW ? 0 : (wv >> 1);
   const int HW = p.H * p.W;
   const int M = p.N * HW;
   int mt_, nt_;
@@ -868,7 +871,8 @@ __global__ __launch_bounds__(256, 2) void igemm_x3h_kernel(IgemmArgs p, HaloGeom
   const int N32 = (p.Cout + 31) / 32;
   const int pad = KS / 2;
   const int n0 = m0 / HW, y0 = (m0 - n0 * HW) / p.W;   // first image / row of the tile
-  const int nchunk = p.Cin / 32;
+  const int cinp = p.cinp ? p.cinp : p.Cin;   // channels per tap of the weight packing (% 32 == 0)
+  const int nchunk = cinp / 32;
   const int bufsz = hg.PH * HX_PITCH;
 
   // halo staging: item e = (halo pixel e / 8, channel quad e % 8)
@@ -880,10 +884,10 @@ __global__ __launch_bounds__(256, 2) void igemm_x3h_kernel(IgemmArgs p, HaloGeom
       const int i = hp / (hg.HH * hg.WW), r = hp - i * hg.HH * hg.WW;
       const int hy = r / hg.WW, hx = r - hy * hg.WW;
       const int n = n0 + i, y = y0 + hy - pad, x = hx - pad;
-      const bool ok = hp < hg.PH && n < p.N && y >= 0 && y < p.H && x >= 0 && x < p.W;
+      const bool ok = hp < hg.PH && n < p.N && y >= 0 && y < p.H && x >= 0 && x < p.W && c * 32 + 4 * q < p.Cin;
       const int cn = min(n, p.N - 1), cy = min(max(y, 0), p.H - 1), cx = min(max(x, 0), p.W - 1);
       const f32x4 t = *reinterpret_cast<const f32x4*>(p.x + (((size_t)cn * p.H + cy) * p.W + cx) * p.ldx + p.cix +
-                                                      c * 32 + 4 * q);
+                                                      min(c * 32 + 4 * q, p.Cin - 4));
       v[u] = ok ? t : f32x4{0.f, 0.f, 0.f, 0.f};
     }
   };
@@ -910,7 +914,7 @@ __global__ __launch_bounds__(256, 2) void igemm_x3h_kernel(IgemmArgs p, HaloGeom
     for (int g = 0; g < 2; ++g)
 #pragma unroll
       for (int nb = 0; nb < 2; ++nb) {
-        const int kb = (t * p.Cin + c * 32) / 16 + g, nbc = min(nb0 + 2 * wn + nb, N32 - 1);
+        const int kb = (t * cinp + c * 32) / 16 + g, nbc = min(nb0 + 2 * wn + nb, N32 - 1);
         const f16x8* src = wpk + ((size_t)kb * N32 + nbc) * 2 * 64 + lane;
         w[g][nb][0] = src[0];
         if constexpr (NP == 3) w[g][nb][1] = src[64];
@@ -918,17 +922,17 @@ __global__ __launch_bounds__(256, 2) void igemm_x3h_kernel(IgemmArgs p, HaloGeom
   };
 
   // halo offset (in f16) of this lane's output pixel in each of its two 32-pixel blocks
-  int pbase[2];
+  int pbase[MBW];
 #pragma unroll
-  for (int mb = 0; mb < 2; ++mb) {
-    const int pp = (2 * wm + mb) * 32 + col;
+  for (int mb = 0; mb < MBW; ++mb) {
+    const int pp = (MBW * wm + mb) * 32 + col;
     const int i = pp / (hg.R * p.W), r = (pp / p.W) % hg.R, x = pp % p.W;
     pbase[mb] = ((i * hg.HH + r) * hg.WW + x) * HX_PITCH + 8 * h;
   }
 
-  f32x16 acc[2][2];
+  f32x16 acc[MBW][2];
 #pragma unroll
-  for (int mb = 0; mb < 2; ++mb)
+  for (int mb = 0; mb < MBW; ++mb)
 #pragma unroll
     for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = f32x16{};
   const bool wave_on = nb0 + 2 * wn < N32;   // wave-uniform
@@ -959,16 +963,16 @@ __global__ __launch_bounds__(256, 2) void igemm_x3h_kernel(IgemmArgs p, HaloGeom
       if (wave_on) {
 #pragma unroll
         for (int g = 0; g < 2; ++g) {
-          f16x8 ah[2], al[2];
+          f16x8 ah[MBW], al[MBW];
 #pragma unroll
-          for (int mb = 0; mb < 2; ++mb) {
+          for (int mb = 0; mb < MBW; ++mb) {
             ah[mb] = *reinterpret_cast<const f16x8*>(hb + pbase[mb] + toff + 16 * g);
             al[mb] = *reinterpret_cast<const f16x8*>(hb + pbase[mb] + toff + 32 + 16 * g);
           }
 #pragma unroll
           for (int nb = 0; nb < 2; ++nb)
 #pragma unroll
-            for (int mb = 0; mb < 2; ++mb) {
+            for (int mb = 0; mb < MBW; ++mb) {
               if constexpr (NP == 3) {
                 acc[mb][nb] = mfma16(wc[g][nb][1], ah[mb], acc[mb][nb]);
                 acc[mb][nb] = mfma16(wc[g][nb][0], al[mb], acc[mb][nb]);
@@ -983,15 +987,17 @@ __global__ __launch_bounds__(256, 2) void igemm_x3h_kernel(IgemmArgs p, HaloGeom
       lds_barrier();
     }
   }
-  if (p.pool) {   // fused 2x2/2 max pool (uniform branch): the pooled map goes to the output view
-    halo_pool_epilogue(p, hg, acc, wave_on, unscale, m0, nb0, hs);
-    return;
+  if constexpr (!NARROW) {
+    if (p.pool) {   // fused 2x2/2 max pool (uniform branch): the pooled map goes to the output view
+      halo_pool_epilogue(p, hg, acc, wave_on, unscale, m0, nb0, hs);
+      return;
+    }
   }
   if (!wave_on) return;
   const bool vst = (p.ldo % 4 == 0) && (p.coff % 4 == 0) && (p.Cout % 4 == 0);
 #pragma unroll
-  for (int mb = 0; mb < 2; ++mb) {
-    const int gm = m0 + (2 * wm + mb) * 32 + col;
+  for (int mb = 0; mb < MBW; ++mb) {
+    const int gm = m0 + (MBW * wm + mb) * 32 + col;
     if (gm >= M) continue;
     float* dst = p.out + (size_t)gm * p.ldo + p.coff;
 #pragma unroll
@@ -1077,7 +1083,8 @@ int env_flag(const char* name, int dflt) {
 bool halo_geom(const IgemmArgs& a, HaloGeom& hg, size_t& lds) {
   static const int halo = env_flag("MP_IGEMM_HALO", 1);
   if (!(halo && a.stride == 1 && (a.KS == 3 || a.KS == 5) && a.pad_t == a.KS / 2 && a.pad_l == a.KS / 2 &&
-        a.Ho == a.H && a.Wo == a.W && a.Cin % 32 == 0 && a.ldx % 4 == 0 && a.cix % 4 == 0 && a.W <= IG_BM &&
+        a.Ho == a.H && a.Wo == a.W && a.ldx % 4 == 0 && a.cix % 4 == 0 && a.W <= IG_BM &&
+        (a.Cin % 32 == 0 || (a.wpad && a.cinp % 32 == 0 && a.cinp >= a.Cin && a.Cin % 4 == 0)) &&
         IG_BM % a.W == 0))
     return false;
   const int HW = a.H * a.W;
@@ -1160,15 +1167,25 @@ hipError_t launch_igemm_x3(const IgemmArgs& a, const void* wpk, float unscale, h
   const f16x8* w = static_cast<const f16x8*>(wpk);
   const bool one = a.nprod == 1;   // MP_DTYPE_BF16: one f16 product per MAC
   static const int xcd = env_flag("MP_IGEMM_XCD", 1);
-  if (wide_path(a)) {
-    HaloGeom hg;
-    size_t lds = 0;
-    if (halo_geom(a, hg, lds)) {
+  HaloGeom hg;
+  size_t lds = 0;
+  // halo tiles for Cout > 64, and (MP_IGEMM_HALO_NARROW, on by default) for Cout <= 64 with the
+  // four waves along the pixels (igemm_x3h_kernel<.., NARROW>): the im2col kernel gathers every
+  // input element KS^2 times
+  static const int narrow = env_flag("MP_IGEMM_HALO_NARROW", 1);
+  // (zero-padding Cin to the 32-channel chunk costs up to 2.7x the MFMAs at Cin = 12: the narrow
+  // halo path is taken from Cin = 32 on, where the padding is at most 1.5x)
+  if ((wide_path(a) || (narrow && a.Cin >= 32)) && halo_geom(a, hg, lds)) {
+    {
       static const bool attr = [] {
         for (const void* f : {reinterpret_cast<const void*>(igemm_x3h_kernel<3, 3>),
                               reinterpret_cast<const void*>(igemm_x3h_kernel<5, 3>),
                               reinterpret_cast<const void*>(igemm_x3h_kernel<3, 1>),
-                              reinterpret_cast<const void*>(igemm_x3h_kernel<5, 1>)})
+                              reinterpret_cast<const void*>(igemm_x3h_kernel<5, 1>),
+                              reinterpret_cast<const void*>(igemm_x3h_kernel<3, 3, true>),
+                              reinterpret_cast<const void*>(igemm_x3h_kernel<5, 3, true>),
+                              reinterpret_cast<const void*>(igemm_x3h_kernel<3, 1, true>),
+                              reinterpret_cast<const void*>(igemm_x3h_kernel<5, 1, true>)})
           (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
         return true;
       }();
@@ -1176,16 +1193,29 @@ hipError_t launch_igemm_x3(const IgemmArgs& a, const void* wpk, float unscale, h
       const dim3 hgrid((M + IG_BM - 1) / IG_BM, (N32 + 3) / 4);
       IgemmArgs h = a;
       h.xcd = xcd;
-      if (a.KS == 3 && one)
-        hipLaunchKernelGGL((igemm_x3h_kernel<3, 1>), hgrid, dim3(256), lds, st, h, hg, w, unscale);
-      else if (a.KS == 3)
-        hipLaunchKernelGGL((igemm_x3h_kernel<3, 3>), hgrid, dim3(256), lds, st, h, hg, w, unscale);
-      else if (one)
-        hipLaunchKernelGGL((igemm_x3h_kernel<5, 1>), hgrid, dim3(256), lds, st, h, hg, w, unscale);
-      else
-        hipLaunchKernelGGL((igemm_x3h_kernel<5, 3>), hgrid, dim3(256), lds, st, h, hg, w, unscale);
+      if (a.Cin % 32) {
+        w = static_cast<const f16x8*>(a.wpad);   // per-tap Cin rows padded to cinp (halo_geom checked)
+      } else {
+        h.cinp = 0;
+      }
+#define MP_HALO(KSV, NPV, NARV) \
+  hipLaunchKernelGGL((igemm_x3h_kernel<KSV, NPV, NARV>), hgrid, dim3(256), lds, st, h, hg, w, unscale)
+      if (N32 <= 2) {   // Cout <= 64
+        if (a.KS == 3 && one) MP_HALO(3, 1, true);
+        else if (a.KS == 3) MP_HALO(3, 3, true);
+        else if (one) MP_HALO(5, 1, true);
+        else MP_HALO(5, 3, true);
+      } else {
+        if (a.KS == 3 && one) MP_HALO(3, 1, false);
+        else if (a.KS == 3) MP_HALO(3, 3, false);
+        else if (one) MP_HALO(5, 1, false);
+        else MP_HALO(5, 3, false);
+      }
+#undef MP_HALO
       return hipGetLastError();
     }
+  }
+  if (wide_path(a)) {
     IgemmArgs b = a;
     b.xcd = xcd;
     b.pmajor = pm_path(a) ? 1 : 0;

@@ -416,6 +416,10 @@ void plan(mp_ctx* c, G& g, int64_t n, int64_t h, int64_t w) {
       a.pad_l = same_pad_before(S.W, L.k, op.stride);
       a.relu = 1;
       a.nprod = L.nprod;
+      if (L.cinp) {   // the Cin-padded packing for the halo kernel (k_igemm.hip halo_geom)
+        a.wpad = L.wpad.p;
+        a.cinp = L.cinp;
+      }
       k->L = &L;
       if (L.x3) {   // split-K workspace of the position-major small-map path (k_igemm.hip)
         const size_t pf = igemm_pm_part_floats(a);

@@ -96,6 +96,8 @@ struct IgemmArgs {
                            // floats, caller-owned); null: no split
   int nprod = 3;           // f16 split kernels: 3 = fp32-accurate f16x3, 1 = hi x hi only (bf16 dtype)
   int xcd = 0;             // set by the launcher: XCD-aware tile order (k_igemm.hip xcd_tile)
+  const void* wpad = nullptr;   // halo path for Cin % 32 != 0: the same weights packed with every
+  int cinp = 0;                 // tap's Cin rows zero-padded to cinp (% 32 == 0; launch_pack_cin_pad)
   int pool = 0;            // 1: a 2x2/2 max pool of relu(conv) is fused into the epilogue, and the
                            // output view (out, ldo, coff) is the pooled (Ho/2 x Wo/2) map;
                            // only where igemm_can_pool(a) holds
@@ -122,6 +124,8 @@ hipError_t launch_fc_gemm(const float* A, int lda, const f32x4* Wpk, float* part
 // product only (single f16 MFMA, hi weight planes only -- MP_DTYPE_BF16's fc_1)
 size_t fc_x3_bytes(int K, int N);
 hipError_t launch_pack_fc_x3(const float* W, void* out, int K, int N, float* unscale, hipStream_t st);
+// HWIO [taps][Cin][Cout] -> [taps][cinp][Cout] with zero rows ci >= Cin (fp32, device)
+hipError_t launch_pad_cin(const float* w, float* out, int taps, int Cin, int cinp, int Cout, hipStream_t st);
 hipError_t launch_fc_gemm_x3(const float* A, int lda, const void* Wpk, float unscale, float* part, int M, int K,
                              int N, int S, int kslice, hipStream_t st, int nprod = 3);
 // the same GEMM on activations already split into f16 hi / lo planes [M][lda] (Al unused when

@@ -141,6 +141,10 @@ void conv(mp_ctx* c, const std::string& name, int n, const View& in, const View&
   a.pad_l = same_pad_before(in.W, L.k, stride);
   a.relu = 1;
   a.nprod = L.nprod;
+  if (L.cinp) {   // the Cin-padded packing for the halo kernel
+    a.wpad = L.wpad.p;
+    a.cinp = L.cinp;
+  }
   hip_check(L.x3 ? launch_igemm_x3(a, L.w.p, L.wus, st) : launch_igemm_conv(a, st), name.c_str());
 }
 
@@ -360,6 +364,21 @@ void pack_matrix(mp_ctx* c, mp_ctx::PackedLayer& L, const float* w, bool x3_ok) 
   if (L.x3) {
     L.w.alloc(fc_x3_bytes(L.K, L.cout));
     hip_check(launch_pack_fc_x3(w, L.w.p, L.K, L.cout, &L.wus, nullptr), "pack (f16x3)");
+    // 3x3 / 5x5 convs whose Cin is not a multiple of 32: a second packing with each tap's rows
+    // zero-padded to a multiple of 32, for the halo kernel (zero rows leave max|W|, so the scale, and
+    // every real weight's hi / lo split unchanged)
+    if ((L.k == 3 || L.k == 5) && L.cin % 32 && L.cin % 4 == 0 && L.K == L.k * L.k * L.cin) {
+      L.cinp = (L.cin + 31) / 32 * 32;
+      const int taps = L.k * L.k, Kp = taps * L.cinp;
+      DevBuf tmp;
+      tmp.alloc((size_t)Kp * L.cout * sizeof(float));
+      hip_check(launch_pad_cin(w, tmp.f(), taps, L.cin, L.cinp, L.cout, nullptr), "pad Cin");
+      L.wpad.alloc(fc_x3_bytes(Kp, L.cout));
+      float us = 0.f;
+      hip_check(launch_pack_fc_x3(tmp.f(), L.wpad.p, Kp, L.cout, &us, nullptr), "pack (f16x3, Cin padded)");
+      hip_check(hipDeviceSynchronize(), "pad Cin sync");
+      if (us != L.wus) fail(MP_ERR_STATE, "padded packing changed the weight scale");
+    }
   } else {
     L.w.alloc((size_t)((L.K + 7) / 8) * ((L.cout + 31) / 32) * 64 * 16);
     hip_check(launch_pack_fc(w, L.w.v4(), L.K, L.cout, nullptr), "pack");

@@ -146,6 +146,8 @@ struct mp_ctx {
     bool x3 = false;      // MP_DTYPE_F32_SPLIT / _BF16: w holds the f16x3 packing (launch_pack_fc_x3)
     float wus = 1.f;      // its 1 / weight scale
     int nprod = 3;        // products per MAC: 3 (fp32-accurate split) or 1 (MP_DTYPE_BF16: hi x hi)
+    DevBuf wpad;          // x3 convs with Cin % 32 != 0: the packing with Cin zero-padded to cinp per
+    int cinp = 0;         // tap (the halo kernel's 32-channel chunks; same scale as w)
   };
   std::map<std::string, PackedLayer> layers;   // keyed by layer name ("conv_3_1", "p_fc_2", ...)
   std::map<std::string, DevBuf> ws;            // named activation buffers
