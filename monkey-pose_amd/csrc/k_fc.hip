@@ -543,15 +543,17 @@ hipError_t launch_pack_fc(const float* W, f32x4* out, int K, int N, hipStream_t 
 // over enough blocks (fc_out, K = 1,024: 8 slices instead of 1).
 int fc_choose_splits(int M, int K, int N, int* kslice) {
   (void)M;
-  (void)N;
   // large K: slices of ~5.4k, i.e. 48 for fc_1 (K = 262,144): at batch 256 that is 2 x 8 x 48 = 768
   // blocks = one full round of 3 blocks on each of the 256 CUs (64 slices left a 1/3-full second
-  // round); an env override exists for A/B only
-  static const int ksz = [] {
-    const char* e = std::getenv("MP_FC_KSLICE");
-    return e ? std::max(32, std::atoi(e)) : 5440;
-  }();
+  // round); and at least 384 blocks per 128-row tile whatever N is (the dense head's fc_1_1 / fc_1_2,
+  // N = 512: 18 / 12 slices gave 192 / 128 blocks at batch 256 and 0.25 ms each).  A function of
+  // K and N only, so a crop's sums group the same way at every batch.  MP_FC_KSLICE (A/B only)
+  // fixes the slice length.
+  static const char* kenv = std::getenv("MP_FC_KSLICE");
+  static const int ksz = kenv ? std::max(32, std::atoi(kenv)) : 5440;
+  const int nt = ((N + 31) / 32 + 3) / 4;   // 128-column tiles
   int S = K >= 32768 ? std::max(1, K / ksz) : std::min(64, (K + 127) / 128);
+  if (K >= 32768 && !kenv) S = std::min(std::max(S, (384 + nt - 1) / nt), K / 512);
   if (S < 1) S = 1;
   int ks = (K + S - 1) / S;
   const int q = K % 64 == 0 ? 64 : FC_BK;   // whole 64-deep steps where K allows (the one-product kernel)
