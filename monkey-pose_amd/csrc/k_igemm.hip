@@ -746,6 +746,130 @@ __global__ __launch_bounds__(256, 3) void igemm_x3w_kernel(IgemmArgs p, const f1
   }
 }
 
+// Pointwise (1x1, stride 1) f16x3 conv for K = Cin <= 192 and Cout <= 128 (the dense regressors'
+// bottlenecks, train_dense_networks.py:248-373: 40 .. 184 -> 24 .. 96 channels on 64 x 64 maps).
+// These are HBM-bound GEMMs with a short K loop: the im2col kernels' one-step-ahead prefetch left a
+// load latency exposed in every one of their 2 - 6 K steps.  Here every thread issues its whole
+// K extent of the activation tile (NCH chunks x 4 float4) up front, then the chunk loop only splits,
+// stages and multiplies; weights stay one chunk ahead (L2-resident).  Block / wave geometry, operand
+// split and epilogue are igemm_x3w_kernel's (128 pixels x 128 couts, 2 x 2 waves of 64 x 64), and
+// so are the per-output K order and the result, bit for bit.
+template <int NP, int NCH>
+__global__ __launch_bounds__(256, 2) void igemm_x3pw_kernel(IgemmArgs p, const f16x8* __restrict__ wpk, float unscale) {
+  __shared__ _Float16 Ah[IG_BM * IGX_LD], Al[IG_BM * IGX_LD];
+  __shared__ f16x8 Ws[2 * 4 * 2 * 64];   // [k16 g][cout block nb][part][lane]
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, col = lane & 31;
+  const int wm = wv & 1, wn = wv >> 1;
+  const int M = p.N * p.Ho * p.Wo;
+  const int m0 = blockIdx.x * IG_BM;
+  const int N32 = (p.Cout + 31) / 32;
+  const int K16 = (p.K + 15) / 16;
+  const int k4 = (tid & 7) * 4;
+  f32x4 av[NCH][4];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int gm = m0 + (tid >> 3) + 32 * i, k = 32 * c + k4;
+      const f32x4 t =
+          *reinterpret_cast<const f32x4*>(p.x + (size_t)min(gm, M - 1) * p.ldx + p.cix + min(k, p.K - 4));
+      av[c][i] = (gm < M && k < p.K) ? t : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  auto load_w = [&](int k0, f16x8 (&w)[4]) {
+#pragma unroll
+    for (int u = 0; u < 4; ++u) {
+      const int e = tid + 256 * u, l = e & 63, part = (e >> 6) & 1, nb = (e >> 7) & 3, g = e >> 9;
+      const int kb = min((k0 >> 4) + g, K16 - 1), nbc = min(nb, N32 - 1);
+      if (NP == 3 || part == 0) w[u] = wpk[(((size_t)kb * N32 + nbc) * 2 + part) * 64 + l];
+    }
+  };
+  f32x16 acc[2][2];
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = f32x16{};
+  f16x8 wnx[4];
+  load_w(0, wnx);
+  const bool wave_on = 2 * wn < N32;   // wave-uniform
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int k0 = 32 * c;
+    lds_barrier();   // the previous chunk's LDS reads are done
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = (tid >> 3) + 32 * i;
+      f16x4 hv, lv;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        hv[s] = (_Float16)av[c][i][s];
+        lv[s] = (_Float16)(av[c][i][s] - (float)hv[s]);
+      }
+      *reinterpret_cast<f16x4*>(Ah + row * IGX_LD + k4) = hv;
+      if constexpr (NP == 3) *reinterpret_cast<f16x4*>(Al + row * IGX_LD + k4) = lv;
+    }
+#pragma unroll
+    for (int u = 0; u < 4; ++u) Ws[tid + 256 * u] = wnx[u];
+    if (c + 1 < NCH) load_w(k0 + IG_BK, wnx);
+    lds_barrier();
+    if (wave_on) {
+#pragma unroll
+      for (int g = 0; g < 2; ++g) {
+        if ((k0 >> 4) + g >= K16) break;   // block-uniform
+        f16x8 ah[2], al[2];
+#pragma unroll
+        for (int mb = 0; mb < 2; ++mb) {
+          const int o = ((2 * wm + mb) * 32 + col) * IGX_LD + 16 * g + 8 * h;
+          ah[mb] = *reinterpret_cast<const f16x8*>(Ah + o);
+          al[mb] = *reinterpret_cast<const f16x8*>(Al + o);
+        }
+#pragma unroll
+        for (int nb = 0; nb < 2; ++nb) {
+          const f16x8 wh = Ws[((g * 4 + 2 * wn + nb) * 2 + 0) * 64 + lane];
+          const f16x8 wl = Ws[((g * 4 + 2 * wn + nb) * 2 + 1) * 64 + lane];
+#pragma unroll
+          for (int mb = 0; mb < 2; ++mb) {
+            if constexpr (NP == 3) {
+              acc[mb][nb] = mfma16(wl, ah[mb], acc[mb][nb]);
+              acc[mb][nb] = mfma16(wh, al[mb], acc[mb][nb]);
+            }
+            acc[mb][nb] = mfma16(wh, ah[mb], acc[mb][nb]);
+          }
+        }
+      }
+    }
+  }
+  if (!wave_on) return;
+  const bool vst = (p.ldo % 4 == 0) && (p.coff % 4 == 0) && (p.Cout % 4 == 0);
+#pragma unroll
+  for (int mb = 0; mb < 2; ++mb) {
+    const int gm = m0 + (2 * wm + mb) * 32 + col;
+    if (gm >= M) continue;
+    float* dst = p.out + (size_t)gm * p.ldo + p.coff;
+#pragma unroll
+    for (int nb = 0; nb < 2; ++nb) {
+      const int cb = 2 * wn + nb;
+      if (cb >= N32) break;
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int c = cb * 32 + 8 * g + 4 * h;
+        f32x4 o;
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const float v = acc[mb][nb][4 * g + j] * unscale + (c + j < p.Cout ? p.bias[c + j] : 0.f);
+          o[j] = p.relu ? fmaxf(v, 0.f) : v;
+        }
+        if (vst) {
+          if (c < p.Cout) *reinterpret_cast<f32x4*>(dst + c) = o;
+        } else {
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (c + j < p.Cout) dst[c + j] = o[j];
+        }
+      }
+    }
+  }
+}
+
 // Halo-tiled f16x3 convolution (stride 1, odd KS, SAME, Cin % 32 == 0, Cout > 64): the im2col
 // kernels above gather, split and stage every input element once per tap (9x for 3x3); here a
 // block's 128 output pixels are whole rows (NI images x R rows x W cols, 128 % W == 0) and the
@@ -1167,6 +1291,27 @@ hipError_t launch_igemm_x3(const IgemmArgs& a, const void* wpk, float unscale, h
   const f16x8* w = static_cast<const f16x8*>(wpk);
   const bool one = a.nprod == 1;   // MP_DTYPE_BF16: one f16 product per MAC
   static const int xcd = env_flag("MP_IGEMM_XCD", 1);
+  static const int pw = env_flag("MP_IGEMM_PW", 1);
+  if (pw && a.KS == 1 && a.stride == 1 && a.Ho == a.H && a.Wo == a.W && a.pad_t == 0 && a.pad_l == 0 &&
+      a.K == a.Cin && a.K <= 192 && a.Cin % 4 == 0 && a.cix % 4 == 0 && a.ldx % 4 == 0 && N32 <= 4 && !a.pool) {
+    const int nch = (a.K + 31) / 32;
+    const dim3 pgrid((M + IG_BM - 1) / IG_BM);
+#define MP_PW(NPV, NCHV) hipLaunchKernelGGL((igemm_x3pw_kernel<NPV, NCHV>), pgrid, dim3(256), 0, st, a, w, unscale)
+#define MP_PWN(NCHV)     \
+  if (one) MP_PW(1, NCHV); \
+  else MP_PW(3, NCHV)
+    switch (nch) {
+      case 1: MP_PWN(1); break;
+      case 2: MP_PWN(2); break;
+      case 3: MP_PWN(3); break;
+      case 4: MP_PWN(4); break;
+      case 5: MP_PWN(5); break;
+      default: MP_PWN(6); break;
+    }
+#undef MP_PWN
+#undef MP_PW
+    return hipGetLastError();
+  }
   HaloGeom hg;
   size_t lds = 0;
   // halo tiles for Cout > 64, and (MP_IGEMM_HALO_NARROW, on by default) for Cout <= 64 with the
