@@ -114,14 +114,18 @@ def fft_kernels(ctx, B, hw, steps, bf16=False):
 # tools/pmc_bytes.py and committed under profiles/ (bench cannot profile itself)
 PMC_TRAFFIC = {False: "profiles/r2_last/pmc_traffic_fp32_b256.csv",
                True: "profiles/r2_last/pmc_traffic_bf16_b256.csv"}
-PMC_KERNEL = {"fft_fwd": "fft_fwd_kernel<", "spec_gemm": "spec_gemm_kernel<", "inv_a_fwd": "fft_inv_a_fwd_kernel<",
-              "fft_inv": "fft_inv_kernel<", "epi_b": "spec_epi_b_kernel<"}
+PMC_KERNEL = {   # name: (fp32 path's kernel, bf16 path's kernel) as rocprofv3 names them
+    "fft_fwd": ("fft_fwd_kernel<false, false>", "fft_fwd_kernel<true, true>"),
+    "spec_gemm": ("spec_gemm_kernel<0>", "spec_gemm_bf_kernel"),
+    "inv_a_fwd": ("fft_inv_a_fwd_kernel<false, false>", "fft_inv_a_fwd_kernel<true, true>"),
+    "fft_inv": ("fft_inv_kernel<false, false>", "fft_inv_kernel<true, true>"),
+    "epi_b": ("spec_epi_b_kernel<false, false, false>", "spec_epi_b_kernel<true, true, false>")}
 
 
 # MFMA utilisation per kernel from the committed PMC pass (tools/pmc_mfma.sh / .py: SQ_VALU_MFMA_BUSY_CYCLES
 # over GRBM_GUI_ACTIVE x 1024 SIMDs, the gfx950 MfmaUtil), same one-stream B = 256 workload
 PMC_MFMA = "profiles/r2_pmc/mfma_util_pose_fp32_b256.csv"
-MFMA_KERNELS = {"fc_gemm_x3 (fc_1, k_fc.hip)": "fc_gemm_x3_kernel", "conv64x3 (conv_2/3, k_conv64x3.hip)": "conv64x3_kernel",
+MFMA_KERNELS = {"fc_gemm_x3p (fc_1 on split planes, k_fc.hip)": "fc_gemm_x3p_kernel", "conv64x3 (conv_2/3, k_conv64x3.hip)": "conv64x3_kernel",
                 "spec_gemm (k_fft.hip)": "spec_gemm_kernel", "spec_epi_b (gate GEMMs, k_fft.hip)": "spec_epi_b_kernel",
                 "gate_init_x3 (k_fft.hip)": "gate_init_x3_kernel"}
 
@@ -149,7 +153,7 @@ def pmc_traffic(name, bf16, batch):
     full = os.path.join(os.path.dirname(os.path.abspath(__file__)), path) if path else None
     if batch != 256 or not full or not os.path.exists(full):
         return None, "no PMC summary for this dtype / batch"
-    tag = PMC_KERNEL[name] + ("true" if bf16 else "false")
+    tag = PMC_KERNEL[name][1 if bf16 else 0]
     for r in csv.DictReader(open(full)):
         if tag in r["kernel"]:
             return round(float(r["traffic_MB"]) * 1e6), path

@@ -1070,7 +1070,10 @@ __device__ __forceinline__ void gate_any(const void* gpk, const f32x16 (&V)[2], 
     gate_x3(static_cast<const f16x8*>(gpk), V, Y, lane, us);
 }
 
-template <bool BF, bool BM>
+// FINAL: the last step's instantiation (p.mode 1 / 2: BN_3(O_T) as the NHWC fp32 map or as fc_1's
+// split planes); the other steps' (p.mode 0: the next step's gated state) carries no final-step code,
+// so its register budget stays under 128 VGPRs (4 waves per SIMD)
+template <bool BF, bool BM, bool FINAL = false>
 __global__ __launch_bounds__(256) void spec_epi_b_kernel(ConvArgs p, const float* __restrict__ P,
                                                          const void* __restrict__ or_x3, float or_us,
                                                          const void* __restrict__ ir_x3, float ir_us, int nseg) {
@@ -1126,7 +1129,7 @@ __global__ __launch_bounds__(256) void spec_epi_b_kernel(ConvArgs p, const float
       map_st4<BM>(p.dst, idx, o);
     }
   f32x16 (&Ov)[2] = Iv;
-  if (p.mode == 0) {
+  if constexpr (!FINAL) {
     gate_any<BF>(ir_x3, Ov, Y, lane, ir_us);
 #pragma unroll
     for (int n = 0; n < 2; ++n)
@@ -1151,7 +1154,7 @@ __global__ __launch_bounds__(256) void spec_epi_b_kernel(ConvArgs p, const float
 #pragma unroll
         for (int j = 0; j < 4; ++j) o[j] = Ov[n][4 * g + j] * ss[j] + tt[j];
         const size_t e = (((size_t)b * H + y) * W + x) * C + c;
-        if (p.mode == 1) {
+        if (p.mode != 2) {
           *reinterpret_cast<f32x4*>(p.dst2 + e) = o;
         } else {   // mode 2: fc_1's f16 hi / lo planes, split exactly as fc_gemm_x3_kernel splits (k_fc.hip)
           typedef _Float16 f16x4_t __attribute__((ext_vector_type(4)));
@@ -1411,15 +1414,21 @@ hipError_t launch_gate_init_x3(const float* O0, float* O, float* Og, const void*
 hipError_t launch_spec_epi_b(const ConvArgs& a, const float* P, const void* or_x3, float or_us, const void* ir_x3,
                              float ir_us, int B, hipStream_t st, bool bf) {
   const int nseg = B * a.H * (a.W / 32);
-  if (bf && fft_bf16_maps())
-    hipLaunchKernelGGL((spec_epi_b_kernel<true, true>), dim3((nseg + 3) / 4), dim3(256), 0, st, a, P, or_x3, or_us, ir_x3,
-                       ir_us, nseg);
-  else if (bf)
-    hipLaunchKernelGGL((spec_epi_b_kernel<true, false>), dim3((nseg + 3) / 4), dim3(256), 0, st, a, P, or_x3, or_us, ir_x3,
-                       ir_us, nseg);
-  else
-    hipLaunchKernelGGL((spec_epi_b_kernel<false, false>), dim3((nseg + 3) / 4), dim3(256), 0, st, a, P, or_x3, or_us, ir_x3,
-                       ir_us, nseg);
+#define MP_EPIB(BFV, BMV, FV)                                                                                     \
+  hipLaunchKernelGGL((spec_epi_b_kernel<BFV, BMV, FV>), dim3((nseg + 3) / 4), dim3(256), 0, st, a, P, or_x3, or_us, \
+                     ir_x3, ir_us, nseg)
+  const bool fin = a.mode != 0;
+  if (bf && fft_bf16_maps()) {
+    if (fin) MP_EPIB(true, true, true);
+    else MP_EPIB(true, true, false);
+  } else if (bf) {
+    if (fin) MP_EPIB(true, false, true);
+    else MP_EPIB(true, false, false);
+  } else {
+    if (fin) MP_EPIB(false, false, true);
+    else MP_EPIB(false, false, false);
+  }
+#undef MP_EPIB
   return hipGetLastError();
 }
 
