@@ -896,17 +896,27 @@ struct HaloGeom {
 __device__ __forceinline__ float dpp_xor1(float v) {   // lane ^ 1 (quad_perm [1,0,3,2])
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
 }
-__device__ void halo_pool_epilogue(const IgemmArgs& p, const HaloGeom& hg, f32x16 (&acc)[2][2], bool wave_on,
-                                   float unscale, int m0, int nb0, _Float16* lds) {
+// WR: the wave layout of igemm_x3h_kernel (wave rows; MBW 32-pixel blocks x NBW cout blocks per wave)
+template <int WR>
+struct HaloLayout {
+  static constexpr int MBW = 4 / WR;                 // 32-pixel blocks per wave (the tile has 4)
+  static constexpr int NBW = WR == 1 ? 1 : 2;        // 32-cout blocks per wave
+  static constexpr int NT = (4 / WR) * NBW;          // 32-cout blocks per tile (WR = 4: 2, else 4)
+};
+
+template <int WR>
+__device__ void halo_pool_epilogue(const IgemmArgs& p, f32x16 (&acc)[HaloLayout<WR>::MBW][HaloLayout<WR>::NBW],
+                                   bool wave_on, float unscale, int m0, int nb0, _Float16* lds) {
+  constexpr int MBW = HaloLayout<WR>::MBW, NBW = HaloLayout<WR>::NBW;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, col = lane & 31;
-  const int wm = wv & 1, wn = wv >> 1;
+  const int wm = wv % WR, wn = wv / WR;
   const int N32 = (p.Cout + 31) / 32, W = p.W, HW = p.H * W;
   // relu(acc * unscale + bias), then the max over the column pair
 #pragma unroll
-  for (int mb = 0; mb < 2; ++mb)
+  for (int mb = 0; mb < MBW; ++mb)
 #pragma unroll
-    for (int nb = 0; nb < 2; ++nb) {
-      const int cb = min(nb0 + 2 * wn + nb, N32 - 1);
+    for (int nb = 0; nb < NBW; ++nb) {
+      const int cb = min(nb0 + NBW * wn + nb, N32 - 1);
 #pragma unroll
       for (int e = 0; e < 16; ++e) {
         const int c = cb * 32 + 8 * (e >> 2) + 4 * h + (e & 3);
@@ -914,56 +924,66 @@ __device__ void halo_pool_epilogue(const IgemmArgs& p, const HaloGeom& hg, f32x1
         acc[mb][nb][e] = fmaxf(v, dpp_xor1(v));
       }
     }
-  // the max over the row pair
+  // the max over the row pair: lanes col ^ W (W <= 16), blocks b, b + 1 (W = 32) or b, b + 2 (W = 64)
+  // of the tile's four 32-pixel blocks b = MBW wm + mb -- in-lane when one wave holds both
   if (W <= 16) {
 #pragma unroll
-    for (int mb = 0; mb < 2; ++mb)
+    for (int mb = 0; mb < MBW; ++mb)
 #pragma unroll
-      for (int nb = 0; nb < 2; ++nb)
+      for (int nb = 0; nb < NBW; ++nb)
 #pragma unroll
         for (int e = 0; e < 16; ++e) acc[mb][nb][e] = fmaxf(acc[mb][nb][e], __shfl_xor(acc[mb][nb][e], W));
   } else if (W == 32) {
 #pragma unroll
-    for (int nb = 0; nb < 2; ++nb)
+    for (int mb = 0; mb + 1 < MBW; mb += 2)
 #pragma unroll
-      for (int e = 0; e < 16; ++e) acc[0][nb][e] = fmaxf(acc[0][nb][e], acc[1][nb][e]);
-  } else {   // W = 64: wave row wm = 1 hands its values to wm = 0 through LDS (the halo buffers are free
-             // once every wave is past its last MFMA)
+      for (int nb = 0; nb < NBW; ++nb)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[mb][nb][e] = fmaxf(acc[mb][nb][e], acc[mb + 1][nb][e]);
+  } else if constexpr (MBW == 4) {   // W = 64, one wave holds both rows
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb)
+#pragma unroll
+      for (int nb = 0; nb < NBW; ++nb)
+#pragma unroll
+        for (int e = 0; e < 16; ++e) acc[mb][nb][e] = fmaxf(acc[mb][nb][e], acc[mb + 2][nb][e]);
+  } else {   // W = 64, 2 x 2 waves: wave row wm = 1 hands its values to wm = 0 through LDS (the halo
+             // buffers are free once every wave is past its last MFMA)
     float* x = reinterpret_cast<float*>(lds);
     lds_barrier();
     if (wm == 1) {
 #pragma unroll
-      for (int mb = 0; mb < 2; ++mb)
+      for (int mb = 0; mb < MBW; ++mb)
 #pragma unroll
-        for (int nb = 0; nb < 2; ++nb)
+        for (int nb = 0; nb < NBW; ++nb)
 #pragma unroll
-          for (int e = 0; e < 16; ++e) x[(((wn * 2 + mb) * 2 + nb) * 16 + e) * 64 + lane] = acc[mb][nb][e];
+          for (int e = 0; e < 16; ++e) x[(((wn * MBW + mb) * NBW + nb) * 16 + e) * 64 + lane] = acc[mb][nb][e];
     }
     lds_barrier();
     if (wm == 0) {
 #pragma unroll
-      for (int mb = 0; mb < 2; ++mb)
+      for (int mb = 0; mb < MBW; ++mb)
 #pragma unroll
-        for (int nb = 0; nb < 2; ++nb)
+        for (int nb = 0; nb < NBW; ++nb)
 #pragma unroll
           for (int e = 0; e < 16; ++e)
-            acc[mb][nb][e] = fmaxf(acc[mb][nb][e], x[(((wn * 2 + mb) * 2 + nb) * 16 + e) * 64 + lane]);
+            acc[mb][nb][e] = fmaxf(acc[mb][nb][e], x[(((wn * MBW + mb) * NBW + nb) * 16 + e) * 64 + lane]);
     }
   }
   if (!wave_on) return;
   const int Ho = p.H / 2, Wo = W / 2;
 #pragma unroll
-  for (int mb = 0; mb < 2; ++mb) {
-    const int pp = (2 * wm + mb) * 32 + col;   // pixel of the tile
+  for (int mb = 0; mb < MBW; ++mb) {
+    const int b = MBW * wm + mb, pp = b * 32 + col;   // block and pixel of the tile
     const int gm = m0 + pp;
     const int n = gm / HW, y = (gm - n * HW) / W, xx = gm % W;
-    // the window's top-left lane writes: even column, even row, and (W = 32) block 0 / (W = 64) wave row 0
-    const bool top = (W <= 16) ? ((y & 1) == 0) : (W == 32 ? mb == 0 : wm == 0);
+    // the window's top-left lane writes: even column, even row (the first block of its pair)
+    const bool top = (W <= 16) ? ((y & 1) == 0) : (W == 32 ? (b & 1) == 0 : b < 2);
     if ((xx & 1) || !top || gm >= p.N * HW) continue;
     float* dst = p.out + (((size_t)n * Ho + y / 2) * Wo + xx / 2) * p.ldo + p.coff;
 #pragma unroll
-    for (int nb = 0; nb < 2; ++nb) {
-      const int cb = nb0 + 2 * wn + nb;
+    for (int nb = 0; nb < NBW; ++nb) {
+      const int cb = nb0 + NBW * wn + nb;
       if (cb >= N32) break;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
@@ -974,24 +994,26 @@ __device__ void halo_pool_epilogue(const IgemmArgs& p, const HaloGeom& hg, f32x1
       }
     }
   }
-  (void)hg;
 }
 
-// NARROW (Cout <= 64): the four waves side by side along the pixels, each 32 pixels x 64 couts
-// (one 32-pixel block), instead of the 2 x 2 grid whose second wave column would idle
-template <int KS, int NP, bool NARROW = false>
+// Wave layouts (WR = wave rows along the 128 pixels): 2 = the 2 x 2 grid of 64 px x 64 couts;
+// 4 = NARROW (Cout <= 64): four waves of 32 px x 64 couts, instead of a 2 x 2 grid whose second wave
+// column would idle; 1 = TALL: four waves of 128 px x 32 couts -- every wave loads only its own
+// cout block's weight fragments (the 2 x 2 grid has two waves load each), half the per-tap weight
+// traffic from L2 / L1 for twice the LDS fragment reads
+template <int KS, int NP, int WR = 2>
 __global__ __launch_bounds__(256, 2) void igemm_x3h_kernel(IgemmArgs p, HaloGeom hg, const f16x8* __restrict__ wpk,
                                                           float unscale) {
-  constexpr int MBW = NARROW ? 1 : 2;   // 32-pixel blocks per wave
+  constexpr int MBW = HaloLayout<WR>::MBW, NBW = HaloLayout<WR>::NBW;
   extern __shared__ _Float16 hs[];   // [2][PH][HX_PITCH]
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, col = lane & 31;
-  const int wm = NARROW ? wv : (wv & 1), wn = NARROW ? 0 : (wv >> 1);
+  const int wm = wv % WR, wn = wv / WR;
   const int HW = p.H * p.W;
   const int M = p.N * HW;
   int mt_, nt_;
   xcd_tile(p, false, mt_, nt_);   // neighbouring row tiles share halo rows
   const int m0 = mt_ * IG_BM;
-  const int nb0 = nt_ * 4;
+  const int nb0 = nt_ * HaloLayout<WR>::NT;
   const int N32 = (p.Cout + 31) / 32;
   const int pad = KS / 2;
   const int n0 = m0 / HW, y0 = (m0 - n0 * HW) / p.W;   // first image / row of the tile
@@ -1033,12 +1055,12 @@ __global__ __launch_bounds__(256, 2) void igemm_x3h_kernel(IgemmArgs p, HaloGeom
     }
   };
   // this wave's weight fragments of (chunk c, tap t): [g][nb][hi|lo]
-  auto load_w = [&](int c, int t, f16x8 (&w)[2][2][2]) {
+  auto load_w = [&](int c, int t, f16x8 (&w)[2][NBW][2]) {
 #pragma unroll
     for (int g = 0; g < 2; ++g)
 #pragma unroll
-      for (int nb = 0; nb < 2; ++nb) {
-        const int kb = (t * cinp + c * 32) / 16 + g, nbc = min(nb0 + 2 * wn + nb, N32 - 1);
+      for (int nb = 0; nb < NBW; ++nb) {
+        const int kb = (t * cinp + c * 32) / 16 + g, nbc = min(nb0 + NBW * wn + nb, N32 - 1);
         const f16x8* src = wpk + ((size_t)kb * N32 + nbc) * 2 * 64 + lane;
         w[g][nb][0] = src[0];
         if constexpr (NP == 3) w[g][nb][1] = src[64];
@@ -1054,17 +1076,17 @@ __global__ __launch_bounds__(256, 2) void igemm_x3h_kernel(IgemmArgs p, HaloGeom
     pbase[mb] = ((i * hg.HH + r) * hg.WW + x) * HX_PITCH + 8 * h;
   }
 
-  f32x16 acc[MBW][2];
+  f32x16 acc[MBW][NBW];
 #pragma unroll
   for (int mb = 0; mb < MBW; ++mb)
 #pragma unroll
-    for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = f32x16{};
-  const bool wave_on = nb0 + 2 * wn < N32;   // wave-uniform
+    for (int nb = 0; nb < NBW; ++nb) acc[mb][nb] = f32x16{};
+  const bool wave_on = nb0 + NBW * wn < N32;   // wave-uniform
 
   f32x4 hv[HX_ITEMS];
   load_halo(0, hv);
   store_halo(0, hv);
-  f16x8 wc[2][2][2], wnx[2][2][2];
+  f16x8 wc[2][NBW][2], wnx[2][NBW][2];
   load_w(0, 0, wnx);
   lds_barrier();
   for (int c = 0; c < nchunk; ++c) {
@@ -1075,7 +1097,7 @@ __global__ __launch_bounds__(256, 2) void igemm_x3h_kernel(IgemmArgs p, HaloGeom
 #pragma unroll
       for (int g = 0; g < 2; ++g)
 #pragma unroll
-        for (int nb = 0; nb < 2; ++nb) {
+        for (int nb = 0; nb < NBW; ++nb) {
           wc[g][nb][0] = wnx[g][nb][0];
           wc[g][nb][1] = wnx[g][nb][1];
         }
@@ -1094,7 +1116,7 @@ __global__ __launch_bounds__(256, 2) void igemm_x3h_kernel(IgemmArgs p, HaloGeom
             al[mb] = *reinterpret_cast<const f16x8*>(hb + pbase[mb] + toff + 32 + 16 * g);
           }
 #pragma unroll
-          for (int nb = 0; nb < 2; ++nb)
+          for (int nb = 0; nb < NBW; ++nb)
 #pragma unroll
             for (int mb = 0; mb < MBW; ++mb) {
               if constexpr (NP == 3) {
@@ -1111,9 +1133,9 @@ __global__ __launch_bounds__(256, 2) void igemm_x3h_kernel(IgemmArgs p, HaloGeom
       lds_barrier();
     }
   }
-  if constexpr (!NARROW) {
+  if constexpr (WR != 4) {
     if (p.pool) {   // fused 2x2/2 max pool (uniform branch): the pooled map goes to the output view
-      halo_pool_epilogue(p, hg, acc, wave_on, unscale, m0, nb0, hs);
+      halo_pool_epilogue<WR>(p, acc, wave_on, unscale, m0, nb0, hs);
       return;
     }
   }
@@ -1125,8 +1147,8 @@ __global__ __launch_bounds__(256, 2) void igemm_x3h_kernel(IgemmArgs p, HaloGeom
     if (gm >= M) continue;
     float* dst = p.out + (size_t)gm * p.ldo + p.coff;
 #pragma unroll
-    for (int nb = 0; nb < 2; ++nb) {
-      const int cb = nb0 + 2 * wn + nb;
+    for (int nb = 0; nb < NBW; ++nb) {
+      const int cb = nb0 + NBW * wn + nb;
       if (cb >= N32) break;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
@@ -1323,19 +1345,24 @@ hipError_t launch_igemm_x3(const IgemmArgs& a, const void* wpk, float unscale, h
   if ((wide_path(a) || (narrow && a.Cin >= 32)) && halo_geom(a, hg, lds)) {
     {
       static const bool attr = [] {
-        for (const void* f : {reinterpret_cast<const void*>(igemm_x3h_kernel<3, 3>),
-                              reinterpret_cast<const void*>(igemm_x3h_kernel<5, 3>),
-                              reinterpret_cast<const void*>(igemm_x3h_kernel<3, 1>),
-                              reinterpret_cast<const void*>(igemm_x3h_kernel<5, 1>),
-                              reinterpret_cast<const void*>(igemm_x3h_kernel<3, 3, true>),
-                              reinterpret_cast<const void*>(igemm_x3h_kernel<5, 3, true>),
-                              reinterpret_cast<const void*>(igemm_x3h_kernel<3, 1, true>),
-                              reinterpret_cast<const void*>(igemm_x3h_kernel<5, 1, true>)})
+        for (const void* f : {reinterpret_cast<const void*>(igemm_x3h_kernel<3, 3, 2>),
+                              reinterpret_cast<const void*>(igemm_x3h_kernel<5, 3, 2>),
+                              reinterpret_cast<const void*>(igemm_x3h_kernel<3, 1, 2>),
+                              reinterpret_cast<const void*>(igemm_x3h_kernel<5, 1, 2>),
+                              reinterpret_cast<const void*>(igemm_x3h_kernel<3, 3, 4>),
+                              reinterpret_cast<const void*>(igemm_x3h_kernel<5, 3, 4>),
+                              reinterpret_cast<const void*>(igemm_x3h_kernel<3, 1, 4>),
+                              reinterpret_cast<const void*>(igemm_x3h_kernel<5, 1, 4>),
+                              reinterpret_cast<const void*>(igemm_x3h_kernel<3, 3, 1>),
+                              reinterpret_cast<const void*>(igemm_x3h_kernel<5, 3, 1>),
+                              reinterpret_cast<const void*>(igemm_x3h_kernel<3, 1, 1>),
+                              reinterpret_cast<const void*>(igemm_x3h_kernel<5, 1, 1>)})
           (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
         return true;
       }();
       (void)attr;
-      const dim3 hgrid((M + IG_BM - 1) / IG_BM, (N32 + 3) / 4);
+      static const int tall = env_flag("MP_IGEMM_HALO_TALL", 1);
+      const dim3 hgrid((M + IG_BM - 1) / IG_BM, N32 <= 2 ? 1 : (N32 + 3) / 4);
       IgemmArgs h = a;
       h.xcd = xcd;
       if (a.Cin % 32) {
@@ -1343,19 +1370,21 @@ hipError_t launch_igemm_x3(const IgemmArgs& a, const void* wpk, float unscale, h
       } else {
         h.cinp = 0;
       }
-#define MP_HALO(KSV, NPV, NARV) \
-  hipLaunchKernelGGL((igemm_x3h_kernel<KSV, NPV, NARV>), hgrid, dim3(256), lds, st, h, hg, w, unscale)
+#define MP_HALO(KSV, NPV, WRV) \
+  hipLaunchKernelGGL((igemm_x3h_kernel<KSV, NPV, WRV>), hgrid, dim3(256), lds, st, h, hg, w, unscale)
+#define MP_HALO_WR(WRV)                    \
+  if (a.KS == 3 && one) MP_HALO(3, 1, WRV); \
+  else if (a.KS == 3) MP_HALO(3, 3, WRV);   \
+  else if (one) MP_HALO(5, 1, WRV);         \
+  else MP_HALO(5, 3, WRV)
       if (N32 <= 2) {   // Cout <= 64
-        if (a.KS == 3 && one) MP_HALO(3, 1, true);
-        else if (a.KS == 3) MP_HALO(3, 3, true);
-        else if (one) MP_HALO(5, 1, true);
-        else MP_HALO(5, 3, true);
+        MP_HALO_WR(4);
+      } else if (tall) {
+        MP_HALO_WR(1);
       } else {
-        if (a.KS == 3 && one) MP_HALO(3, 1, false);
-        else if (a.KS == 3) MP_HALO(3, 3, false);
-        else if (one) MP_HALO(5, 1, false);
-        else MP_HALO(5, 3, false);
+        MP_HALO_WR(2);
       }
+#undef MP_HALO_WR
 #undef MP_HALO
       return hipGetLastError();
     }
