@@ -1,7 +1,8 @@
 """The A/B switches read once at library load or plan time (MP_BF16_MAPS, MP_FC_PRESPLIT,
 MP_GRAPH_FUSE_POOL, MP_IGEMM_PM_SPLITS, MP_IGEMM_XCD, MP_IGEMM_HALO, MP_IGEMM_HALO_NARROW,
-MP_IGEMM_PW) keep their paths correct: each case runs in one child process with the switch set
-(the parent's library already made its choice), against the committed golden vectors."""
+MP_IGEMM_HALO_TALL, MP_IGEMM_PW) keep their paths correct: each case runs in one child process
+with the switch set (the parent's library already made its choice), against the committed golden
+vectors."""
 import json
 import os
 import subprocess
@@ -56,6 +57,7 @@ CASES = [
     ({"MP_IGEMM_PM_SPLITS": "1"}, "hier", "bf16", 5e-3),
     ({"MP_IGEMM_XCD": "0", "MP_IGEMM_HALO": "0"}, "hier", "fp32_split", 1e-4),
     ({"MP_GRAPH_FUSE_POOL": "0"}, "hier", "bf16", 5e-3),
+    ({"MP_IGEMM_HALO_TALL": "0"}, "hier", "fp32_split", 1e-4),
     ({"MP_IGEMM_PW": "0", "MP_IGEMM_HALO_NARROW": "0"}, "dense", "fp32_split", 1e-4),
     ({"MP_IGEMM_PW": "0", "MP_IGEMM_HALO_NARROW": "0"}, "dense", "bf16", 5e-3),
 ]
