@@ -552,7 +552,11 @@ int fc_choose_splits(int M, int K, int N, int* kslice) {
   static const char* kenv = std::getenv("MP_FC_KSLICE");
   static const int ksz = kenv ? std::max(32, std::atoi(kenv)) : 5440;
   const int nt = ((N + 31) / 32 + 3) / 4;   // 128-column tiles
-  int S = K >= 32768 ? std::max(1, K / ksz) : std::min(64, (K + 127) / 128);
+  static const int smallk = [] {   // K per slice below 32k (A/B knob MP_FC_SMALLK)
+    const char* e = std::getenv("MP_FC_SMALLK");
+    return e ? std::max(32, std::atoi(e)) : 128;
+  }();
+  int S = K >= 32768 ? std::max(1, K / ksz) : std::min(64, (K + smallk - 1) / smallk);
   if (K >= 32768 && !kenv) S = std::min(std::max(S, (384 + nt - 1) / nt), K / 512);
   if (S < 1) S = 1;
   int ks = (K + S - 1) / S;
