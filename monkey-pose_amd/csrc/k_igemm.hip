@@ -661,12 +661,17 @@ __global__ __launch_bounds__(256, 3) void igemm_x3w_kernel(IgemmArgs p, const f1
   for (int mb = 0; mb < 2; ++mb)
 #pragma unroll
     for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = f32x16{};
+  // split-K (p.part, gridDim.z ranges, tiny maps: igemm_x3w_splits): this block sums K steps
+  // [kb0, kb1) into raw partials; igemm_split_reduce_kernel adds them in z order with the epilogue
+  const int nz = p.part ? (int)gridDim.z : 1;
+  const int kspan = ((p.K + nz - 1) / nz + IG_BK - 1) / IG_BK * IG_BK;
+  const int kb0 = (int)blockIdx.z * kspan, kb1 = min(p.K, kb0 + kspan);
   f32x4 av[4];
   f16x8 wnx[4];
-  load_act(0, av);
-  load_w(0, wnx);
+  load_act(kb0, av);
+  load_w(kb0, wnx);
   const bool wave_on = nb0 + 2 * wn < N32;   // wave-uniform
-  for (int k0 = 0; k0 < p.K; k0 += IG_BK) {
+  for (int k0 = kb0; k0 < kb1; k0 += IG_BK) {
     lds_barrier();   // the previous step's LDS reads are done
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -682,7 +687,7 @@ __global__ __launch_bounds__(256, 3) void igemm_x3w_kernel(IgemmArgs p, const f1
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) Ws[tid + 256 * u] = wnx[u];
-    if (k0 + IG_BK < p.K) {   // prefetch the next step
+    if (k0 + IG_BK < kb1) {   // prefetch the next step
       load_act(k0 + IG_BK, av);
       load_w(k0 + IG_BK, wnx);
     }
@@ -715,6 +720,24 @@ __global__ __launch_bounds__(256, 3) void igemm_x3w_kernel(IgemmArgs p, const f1
     }
   }
   if (!wave_on) return;
+  if (nz > 1) {   // raw partial sums [z][gm][N32 * 32]
+#pragma unroll
+    for (int mb = 0; mb < 2; ++mb) {
+      const int gm = m0 + (2 * wm + mb) * 32 + col;
+      if (gm >= M) continue;
+      float* dst = p.part + ((size_t)blockIdx.z * M + gm) * (N32 * 32);
+#pragma unroll
+      for (int nb = 0; nb < 2; ++nb) {
+        const int cb = nb0 + 2 * wn + nb;
+        if (cb >= N32) break;
+#pragma unroll
+        for (int g = 0; g < 4; ++g)
+          *reinterpret_cast<f32x4*>(dst + cb * 32 + 8 * g + 4 * h) =
+              f32x4{acc[mb][nb][4 * g], acc[mb][nb][4 * g + 1], acc[mb][nb][4 * g + 2], acc[mb][nb][4 * g + 3]};
+      }
+    }
+    return;
+  }
   const bool vst = (p.ldo % 4 == 0) && (p.coff % 4 == 0) && (p.Cout % 4 == 0);
 #pragma unroll
   for (int mb = 0; mb < 2; ++mb) {
@@ -743,6 +766,26 @@ __global__ __launch_bounds__(256, 3) void igemm_x3w_kernel(IgemmArgs p, const f1
         }
       }
     }
+  }
+}
+
+// the split-K reduce of igemm_x3w_kernel (row-major rows): out = relu?((sum_z part[z]) * unscale +
+// bias), z in order; one thread per 4 output channels of one row
+__global__ __launch_bounds__(256) void igemm_split_reduce_kernel(IgemmArgs p, int S, float unscale) {
+  const int M = p.N * p.Ho * p.Wo, N32 = (p.Cout + 31) / 32, nq = N32 * 8;
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (size_t)M * nq) return;
+  const int gm = (int)(i / nq), c = (int)(i - (size_t)gm * nq) * 4;
+  if (c >= p.Cout) return;
+  const float* src = p.part + (size_t)gm * (N32 * 32) + c;
+  f32x4 s = *reinterpret_cast<const f32x4*>(src);
+  for (int z = 1; z < S; ++z) s += *reinterpret_cast<const f32x4*>(src + (size_t)z * M * (N32 * 32));
+  float* dst = p.out + (size_t)gm * p.ldo + p.coff + c;
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    if (c + j >= p.Cout) break;
+    const float v = s[j] * unscale + p.bias[c + j];
+    dst[j] = p.relu ? fmaxf(v, 0.f) : v;
   }
 }
 
@@ -1290,8 +1333,23 @@ int igemm_pm_splits(const IgemmArgs& a) {
   return S;
 }
 
+// K splits of the wide im2col kernel on small output maps (<= 8 x 8: the dense-hier scale-2 / 3
+// convs, whose Cin is often not a multiple of 32 so neither the halo nor the tap-skipping path
+// applies; at 4 x 4, 32 pixel tiles x 2 cout tiles = 64 blocks at B = 256 otherwise).  A property of
+// the layer alone (K, map size), never of the batch.
+int igemm_x3w_splits(const IgemmArgs& a) {
+  static const int on = env_flag("MP_IGEMM_SMALL_SPLITK", 1);
+  if (!on || !wide_path(a) || a.Ho * a.Wo > 64 || pm_path(a)) return 1;
+  HaloGeom hg;
+  size_t lds;
+  if (halo_geom(a, hg, lds)) return 1;
+  // <= 4 x 4: up to 8 slices of >= 256; 8 x 8 (128 pixel tiles x 2 cout tiles = 256 blocks at
+  // B = 256, a third of the resident slots): up to 4 of >= 512
+  return a.Ho * a.Wo <= 16 ? std::max(1, std::min(8, a.K / 256)) : std::max(1, std::min(4, a.K / 512));
+}
+
 size_t igemm_pm_part_floats(const IgemmArgs& a) {
-  const int S = igemm_pm_splits(a);
+  const int S = std::max(igemm_pm_splits(a), igemm_x3w_splits(a));
   return S > 1 ? (size_t)S * a.N * a.Ho * a.Wo * ((a.Cout + 31) / 32 * 32) : 0;
 }
 
@@ -1405,6 +1463,17 @@ hipError_t launch_igemm_x3(const IgemmArgs& a, const void* wpk, float unscale, h
         hipLaunchKernelGGL(igemm_x3w_pm_kernel<3>, sgrid, dim3(256), 0, st, b, w, unscale);
       const size_t total = (size_t)M * (N32 * 8);
       hipLaunchKernelGGL(igemm_pm_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, b, S, unscale);
+      return hipGetLastError();
+    }
+    const int S2 = !b.pmajor && a.part ? igemm_x3w_splits(a) : 1;
+    if (S2 > 1) {
+      const dim3 sgrid((M + IG_BM - 1) / IG_BM, (N32 + 3) / 4, S2);
+      if (one)
+        hipLaunchKernelGGL(igemm_x3w_kernel<1>, sgrid, dim3(256), 0, st, b, w, unscale);
+      else
+        hipLaunchKernelGGL(igemm_x3w_kernel<3>, sgrid, dim3(256), 0, st, b, w, unscale);
+      const size_t total = (size_t)M * (N32 * 8);
+      hipLaunchKernelGGL(igemm_split_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, b, S2, unscale);
       return hipGetLastError();
     }
     b.part = nullptr;
