@@ -1333,19 +1333,19 @@ int igemm_pm_splits(const IgemmArgs& a) {
   return S;
 }
 
-// K splits of the wide im2col kernel on small output maps (<= 8 x 8: the dense-hier scale-2 / 3
-// convs, whose Cin is often not a multiple of 32 so neither the halo nor the tap-skipping path
-// applies; at 4 x 4, 32 pixel tiles x 2 cout tiles = 64 blocks at B = 256 otherwise).  A property of
-// the layer alone (K, map size), never of the batch.
+// K splits of the wide im2col kernel on tiny output maps (<= 4 x 4: the dense-hier scale-3 convs,
+// whose Cin is often not a multiple of 32 so neither the halo nor the tap-skipping path applies:
+// 32 pixel tiles x 2 cout tiles = 64 blocks at B = 256 otherwise).  A property of the layer alone
+// (K, map size), never of the batch.
 int igemm_x3w_splits(const IgemmArgs& a) {
   static const int on = env_flag("MP_IGEMM_SMALL_SPLITK", 1);
-  if (!on || !wide_path(a) || a.Ho * a.Wo > 64 || pm_path(a)) return 1;
+  if (!on || !wide_path(a) || a.Ho * a.Wo > 16 || pm_path(a)) return 1;
   HaloGeom hg;
   size_t lds;
   if (halo_geom(a, hg, lds)) return 1;
-  // <= 4 x 4: up to 8 slices of >= 256; 8 x 8 (128 pixel tiles x 2 cout tiles = 256 blocks at
-  // B = 256, a third of the resident slots): up to 4 of >= 512
-  return a.Ho * a.Wo <= 16 ? std::max(1, std::min(8, a.K / 256)) : std::max(1, std::min(4, a.K / 512));
+  // up to 8 slices of >= 256 (on 8 x 8 maps, up to 4 slices of >= 512 measured flat in the
+  // multi-stream dense-hier schedule: 20.1k vs 20.0k crops/s)
+  return std::max(1, std::min(8, a.K / 256));
 }
 
 size_t igemm_pm_part_floats(const IgemmArgs& a) {

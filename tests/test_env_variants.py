@@ -1,8 +1,8 @@
 """The A/B switches read once at library load or plan time (MP_BF16_MAPS, MP_FC_PRESPLIT,
 MP_GRAPH_FUSE_POOL, MP_IGEMM_PM_SPLITS, MP_IGEMM_XCD, MP_IGEMM_HALO, MP_IGEMM_HALO_NARROW,
-MP_IGEMM_HALO_TALL, MP_IGEMM_PW) keep their paths correct: each case runs in one child process
-with the switch set (the parent's library already made its choice), against the committed golden
-vectors."""
+MP_IGEMM_HALO_TALL, MP_IGEMM_PW, MP_IGEMM_SMALL_SPLITK) keep their paths correct: each case runs in
+one child process with the switch set (the parent's library already made its choice), against the
+committed golden vectors."""
 import json
 import os
 import subprocess
@@ -37,6 +37,14 @@ elif kind == "dense":
     model.load_weights(wts)
     out = model.build(torch.from_numpy(depth).cuda(), 69, train_mode=False).cpu().numpy()
     ref = golden_array("dense_c128", "out")
+elif kind == "dense_hier":
+    m = meta["dense_hier_c128"]
+    wts, depth = MG.regressor_inputs("dense_hier", m["n"], m["crop"], m["weight_seed"], m["crop_seed"])
+    model = P.train_dense_hier_networks.dense_hier_model_struct()
+    model.compute_dtype = dtype
+    model.load_weights(wts)
+    out = model.build(torch.from_numpy(depth).cuda(), *MG.HIER_HEADS, train_mode=False).cpu().numpy()
+    ref = golden_array("dense_hier_c128", "out")
 else:
     m = meta["hier_c128"]
     wts, depth = MG.regressor_inputs(m["kind"], m["n"], m["crop"], m["weight_seed"], m["crop_seed"])
@@ -58,6 +66,7 @@ CASES = [
     ({"MP_IGEMM_XCD": "0", "MP_IGEMM_HALO": "0"}, "hier", "fp32_split", 1e-4),
     ({"MP_GRAPH_FUSE_POOL": "0"}, "hier", "bf16", 5e-3),
     ({"MP_IGEMM_HALO_TALL": "0"}, "hier", "fp32_split", 1e-4),
+    ({"MP_IGEMM_SMALL_SPLITK": "0"}, "dense_hier", "fp32_split", 1e-4),
     ({"MP_IGEMM_PW": "0", "MP_IGEMM_HALO_NARROW": "0"}, "dense", "fp32_split", 1e-4),
     ({"MP_IGEMM_PW": "0", "MP_IGEMM_HALO_NARROW": "0"}, "dense", "bf16", 5e-3),
 ]
