@@ -190,18 +190,26 @@ __global__ __launch_bounds__(256, NB == 4 ? 2 : 3) void igemm_x3_kernel(IgemmArg
   }
   const int k4 = (tid & 7) * 4;
 
+  // this thread's im2col column k = k0 + k4 as (ky, kx, ci), advanced by one K step per load_act
+  // call (the calls come in K order) instead of two integer divisions per step; past K the tap
+  // runs off the image (clamped address, masked value)
+  int ici = 0, ikx = 0, iky = 0;
+  auto im2col_start = [&](int k) {
+    const int tap = k / p.Cin;
+    ici = k - tap * p.Cin;
+    iky = tap / p.KS;
+    ikx = tap - iky * p.KS;
+  };
   auto load_act = [&](int k0, f32x4 (&v)[4]) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int kk = k0 + k4;
       if (vec) {
-        const int kc = min(kk, p.K - 4);
-        const int tap = kc / p.Cin, ci = kc - tap * p.Cin;
-        const int iy = sy[i] + tap / p.KS, ix = sx[i] + tap % p.KS;
+        const int iy = sy[i] + iky, ix = sx[i] + ikx;
         const bool ok = sok[i] && kk < p.K && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
         const int cy = min(max(iy, 0), p.H - 1), cx = min(max(ix, 0), p.W - 1);
         const f32x4 t =
-            *reinterpret_cast<const f32x4*>(p.x + (((size_t)sn[i] * p.H + cy) * p.W + cx) * p.ldx + p.cix + ci);
+            *reinterpret_cast<const f32x4*>(p.x + (((size_t)sn[i] * p.H + cy) * p.W + cx) * p.ldx + p.cix + ici);
         v[i] = ok ? t : f32x4{0.f, 0.f, 0.f, 0.f};
       } else {
 #pragma unroll
@@ -214,6 +222,16 @@ __global__ __launch_bounds__(256, NB == 4 ? 2 : 3) void igemm_x3_kernel(IgemmArg
           const int cy = min(max(iy, 0), p.H - 1), cx = min(max(ix, 0), p.W - 1);
           const float t = p.x[(((size_t)sn[i] * p.H + cy) * p.W + cx) * p.ldx + p.cix + ci];
           v[i][s] = ok ? t : 0.f;
+        }
+      }
+    }
+    if (vec) {   // the next K step: ci += 32, carrying into the tap (at most 32 / Cin carries)
+      ici += IG_BK;
+      while (ici >= p.Cin) {
+        ici -= p.Cin;
+        if (++ikx == p.KS) {
+          ikx = 0;
+          ++iky;
         }
       }
     }
@@ -237,6 +255,7 @@ __global__ __launch_bounds__(256, NB == 4 ? 2 : 3) void igemm_x3_kernel(IgemmArg
   for (int nb = 0; nb < NB; ++nb) acc[nb] = f32x16{};
   f32x4 av[4];
   f16x8 wn[2][NB][2];
+  im2col_start(k4);
   load_act(0, av);
   load_w(0, wn);
   for (int k0 = 0; k0 < p.K; k0 += IG_BK) {
@@ -616,18 +635,26 @@ __global__ __launch_bounds__(256, 3) void igemm_x3w_kernel(IgemmArgs p, const f1
   }
   const int k4 = (tid & 7) * 4;
 
+  // this thread's im2col column k = k0 + k4 as (ky, kx, ci), advanced by one K step per load_act
+  // call (the calls come in K order) instead of two integer divisions per step; past K the tap
+  // runs off the image (clamped address, masked value)
+  int ici = 0, ikx = 0, iky = 0;
+  auto im2col_start = [&](int k) {
+    const int tap = k / p.Cin;
+    ici = k - tap * p.Cin;
+    iky = tap / p.KS;
+    ikx = tap - iky * p.KS;
+  };
   auto load_act = [&](int k0, f32x4 (&v)[4]) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int kk = k0 + k4;
       if (vec) {
-        const int kc = min(kk, p.K - 4);
-        const int tap = kc / p.Cin, ci = kc - tap * p.Cin;
-        const int iy = sy[i] + tap / p.KS, ix = sx[i] + tap % p.KS;
+        const int iy = sy[i] + iky, ix = sx[i] + ikx;
         const bool ok = sok[i] && kk < p.K && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
         const int cy = min(max(iy, 0), p.H - 1), cx = min(max(ix, 0), p.W - 1);
         const f32x4 t =
-            *reinterpret_cast<const f32x4*>(p.x + (((size_t)sn[i] * p.H + cy) * p.W + cx) * p.ldx + p.cix + ci);
+            *reinterpret_cast<const f32x4*>(p.x + (((size_t)sn[i] * p.H + cy) * p.W + cx) * p.ldx + p.cix + ici);
         v[i] = ok ? t : f32x4{0.f, 0.f, 0.f, 0.f};
       } else {
 #pragma unroll
@@ -640,6 +667,16 @@ __global__ __launch_bounds__(256, 3) void igemm_x3w_kernel(IgemmArgs p, const f1
           const int cy = min(max(iy, 0), p.H - 1), cx = min(max(ix, 0), p.W - 1);
           const float t = p.x[(((size_t)sn[i] * p.H + cy) * p.W + cx) * p.ldx + p.cix + ci];
           v[i][s] = ok ? t : 0.f;
+        }
+      }
+    }
+    if (vec) {   // the next K step: ci += 32, carrying into the tap (at most 32 / Cin carries)
+      ici += IG_BK;
+      while (ici >= p.Cin) {
+        ici -= p.Cin;
+        if (++ikx == p.KS) {
+          ikx = 0;
+          ++iky;
         }
       }
     }
@@ -668,6 +705,7 @@ __global__ __launch_bounds__(256, 3) void igemm_x3w_kernel(IgemmArgs p, const f1
   const int kb0 = (int)blockIdx.z * kspan, kb1 = min(p.K, kb0 + kspan);
   f32x4 av[4];
   f16x8 wnx[4];
+  im2col_start(kb0 + k4);
   load_act(kb0, av);
   load_w(kb0, wnx);
   const bool wave_on = nb0 + 2 * wn < N32;   // wave-uniform
