@@ -961,7 +961,6 @@ __global__ __launch_bounds__(256, 2) void igemm_x3pw_kernel(IgemmArgs p, const f
 // are in flight during chunk c's MFMAs and are written to the other buffer after them (one barrier
 // per chunk).  Weight fragments come straight from L2 / L1 (packed [k/16][n/32][hi|lo][lane], each
 // wave-load one contiguous KiB), one tap ahead.  Waves: 2 x 2 grid of 64 pixels x 64 couts.
-constexpr int HX_PITCH = 72;   // f16 per staged pixel
 constexpr int HX_ITEMS = 9;    // f32x4 halo items per thread per chunk (<= 2304 = 288 pixels)
 
 struct HaloGeom {
@@ -1082,11 +1081,15 @@ __device__ void halo_pool_epilogue(const IgemmArgs& p, f32x16 (&acc)[HaloLayout<
 // column would idle; 1 = TALL: four waves of 128 px x 32 couts -- every wave loads only its own
 // cout block's weight fragments (the 2 x 2 grid has two waves load each), half the per-tap weight
 // traffic from L2 / L1 for twice the LDS fragment reads
-template <int KS, int NP, int WR = 2>
+// CH: input channels per staged chunk, 32 or 16 (Cin 12 / 16 / 40 / 48 ...: the weights' per-tap rows
+// padded to 16 instead of 32); a staged pixel is [hi CH][lo CH][8 pad] f16 (72 / 40: conflict-free
+// b128 reads of 32 consecutive pixels either way)
+template <int KS, int NP, int WR = 2, int CH = 32>
 __global__ __launch_bounds__(256, 2) void igemm_x3h_kernel(IgemmArgs p, HaloGeom hg, const f16x8* __restrict__ wpk,
                                                           float unscale) {
   constexpr int MBW = HaloLayout<WR>::MBW, NBW = HaloLayout<WR>::NBW;
-  extern __shared__ _Float16 hs[];   // [2][PH][HX_PITCH]
+  constexpr int PITCH = 2 * CH + 8, QPP = CH / 4, NG = CH / 16;
+  extern __shared__ _Float16 hs[];   // [2][PH][PITCH]
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, col = lane & 31;
   const int wm = wv % WR, wn = wv / WR;
   const int HW = p.H * p.W;
@@ -1098,23 +1101,23 @@ __global__ __launch_bounds__(256, 2) void igemm_x3h_kernel(IgemmArgs p, HaloGeom
   const int N32 = (p.Cout + 31) / 32;
   const int pad = KS / 2;
   const int n0 = m0 / HW, y0 = (m0 - n0 * HW) / p.W;   // first image / row of the tile
-  const int cinp = p.cinp ? p.cinp : p.Cin;   // channels per tap of the weight packing (% 32 == 0)
-  const int nchunk = cinp / 32;
-  const int bufsz = hg.PH * HX_PITCH;
+  const int cinp = p.cinp ? p.cinp : p.Cin;   // channels per tap of the weight packing (% CH == 0)
+  const int nchunk = cinp / CH;
+  const int bufsz = hg.PH * PITCH;
 
-  // halo staging: item e = (halo pixel e / 8, channel quad e % 8)
+  // halo staging: item e = (halo pixel e / QPP, channel quad e % QPP)
   auto load_halo = [&](int c, f32x4 (&v)[HX_ITEMS]) {
 #pragma unroll
     for (int u = 0; u < HX_ITEMS; ++u) {
       const int e = tid + 256 * u;
-      const int hp = e >> 3, q = e & 7;
+      const int hp = e / QPP, q = e % QPP;
       const int i = hp / (hg.HH * hg.WW), r = hp - i * hg.HH * hg.WW;
       const int hy = r / hg.WW, hx = r - hy * hg.WW;
       const int n = n0 + i, y = y0 + hy - pad, x = hx - pad;
-      const bool ok = hp < hg.PH && n < p.N && y >= 0 && y < p.H && x >= 0 && x < p.W && c * 32 + 4 * q < p.Cin;
+      const bool ok = hp < hg.PH && n < p.N && y >= 0 && y < p.H && x >= 0 && x < p.W && c * CH + 4 * q < p.Cin;
       const int cn = min(n, p.N - 1), cy = min(max(y, 0), p.H - 1), cx = min(max(x, 0), p.W - 1);
       const f32x4 t = *reinterpret_cast<const f32x4*>(p.x + (((size_t)cn * p.H + cy) * p.W + cx) * p.ldx + p.cix +
-                                                      min(c * 32 + 4 * q, p.Cin - 4));
+                                                      min(c * CH + 4 * q, p.Cin - 4));
       v[u] = ok ? t : f32x4{0.f, 0.f, 0.f, 0.f};
     }
   };
@@ -1122,7 +1125,7 @@ __global__ __launch_bounds__(256, 2) void igemm_x3h_kernel(IgemmArgs p, HaloGeom
 #pragma unroll
     for (int u = 0; u < HX_ITEMS; ++u) {
       const int e = tid + 256 * u;
-      const int hp = e >> 3, q = e & 7;
+      const int hp = e / QPP, q = e % QPP;
       if (hp >= hg.PH) continue;
       f16x4 hv, lv;
 #pragma unroll
@@ -1130,18 +1133,18 @@ __global__ __launch_bounds__(256, 2) void igemm_x3h_kernel(IgemmArgs p, HaloGeom
         hv[s] = (_Float16)v[u][s];
         lv[s] = (_Float16)(v[u][s] - (float)hv[s]);
       }
-      _Float16* d = hs + buf * bufsz + hp * HX_PITCH + 4 * q;
+      _Float16* d = hs + buf * bufsz + hp * PITCH + 4 * q;
       *reinterpret_cast<f16x4*>(d) = hv;
-      if constexpr (NP == 3) *reinterpret_cast<f16x4*>(d + 32) = lv;
+      if constexpr (NP == 3) *reinterpret_cast<f16x4*>(d + CH) = lv;
     }
   };
   // this wave's weight fragments of (chunk c, tap t): [g][nb][hi|lo]
   auto load_w = [&](int c, int t, f16x8 (&w)[2][NBW][2]) {
 #pragma unroll
-    for (int g = 0; g < 2; ++g)
+    for (int g = 0; g < NG; ++g)
 #pragma unroll
       for (int nb = 0; nb < NBW; ++nb) {
-        const int kb = (t * cinp + c * 32) / 16 + g, nbc = min(nb0 + NBW * wn + nb, N32 - 1);
+        const int kb = (t * cinp + c * CH) / 16 + g, nbc = min(nb0 + NBW * wn + nb, N32 - 1);
         const f16x8* src = wpk + ((size_t)kb * N32 + nbc) * 2 * 64 + lane;
         w[g][nb][0] = src[0];
         if constexpr (NP == 3) w[g][nb][1] = src[64];
@@ -1154,7 +1157,7 @@ __global__ __launch_bounds__(256, 2) void igemm_x3h_kernel(IgemmArgs p, HaloGeom
   for (int mb = 0; mb < MBW; ++mb) {
     const int pp = (MBW * wm + mb) * 32 + col;
     const int i = pp / (hg.R * p.W), r = (pp / p.W) % hg.R, x = pp % p.W;
-    pbase[mb] = ((i * hg.HH + r) * hg.WW + x) * HX_PITCH + 8 * h;
+    pbase[mb] = ((i * hg.HH + r) * hg.WW + x) * PITCH + 8 * h;
   }
 
   f32x16 acc[MBW][NBW];
@@ -1176,7 +1179,7 @@ __global__ __launch_bounds__(256, 2) void igemm_x3h_kernel(IgemmArgs p, HaloGeom
 #pragma unroll
     for (int t = 0; t < KS * KS; ++t) {
 #pragma unroll
-      for (int g = 0; g < 2; ++g)
+      for (int g = 0; g < NG; ++g)
 #pragma unroll
         for (int nb = 0; nb < NBW; ++nb) {
           wc[g][nb][0] = wnx[g][nb][0];
@@ -1186,15 +1189,15 @@ __global__ __launch_bounds__(256, 2) void igemm_x3h_kernel(IgemmArgs p, HaloGeom
         load_w(c, t + 1, wnx);
       else if (c + 1 < nchunk)
         load_w(c + 1, 0, wnx);
-      const int toff = ((t / KS) * hg.WW + t % KS) * HX_PITCH;
+      const int toff = ((t / KS) * hg.WW + t % KS) * PITCH;
       if (wave_on) {
 #pragma unroll
-        for (int g = 0; g < 2; ++g) {
+        for (int g = 0; g < NG; ++g) {
           f16x8 ah[MBW], al[MBW];
 #pragma unroll
           for (int mb = 0; mb < MBW; ++mb) {
             ah[mb] = *reinterpret_cast<const f16x8*>(hb + pbase[mb] + toff + 16 * g);
-            al[mb] = *reinterpret_cast<const f16x8*>(hb + pbase[mb] + toff + 32 + 16 * g);
+            al[mb] = *reinterpret_cast<const f16x8*>(hb + pbase[mb] + toff + CH + 16 * g);
           }
 #pragma unroll
           for (int nb = 0; nb < NBW; ++nb)
@@ -1307,11 +1310,15 @@ int env_flag(const char* name, int dflt) {
 
 // halo tiles: stride 1, SAME, odd KS in {3, 5}, Cin % 32 == 0, tiles of whole rows of one image (or
 // whole images), halo within HX_ITEMS per thread and two buffers within 80 KiB
+// channels per staged chunk of the halo kernel: 32 unless the weights are padded to a multiple of 16
+// that is not one of 32
+int halo_ch(const IgemmArgs& a) { return (a.Cin % 32 == 0 || a.cinp % 32 == 0) ? 32 : 16; }
+
 bool halo_geom(const IgemmArgs& a, HaloGeom& hg, size_t& lds) {
   static const int halo = env_flag("MP_IGEMM_HALO", 1);
   if (!(halo && a.stride == 1 && (a.KS == 3 || a.KS == 5) && a.pad_t == a.KS / 2 && a.pad_l == a.KS / 2 &&
         a.Ho == a.H && a.Wo == a.W && a.ldx % 4 == 0 && a.cix % 4 == 0 && a.W <= IG_BM &&
-        (a.Cin % 32 == 0 || (a.wpad && a.cinp % 32 == 0 && a.cinp >= a.Cin && a.Cin % 4 == 0)) &&
+        (a.Cin % 32 == 0 || (a.wpad && a.cinp % 16 == 0 && a.cinp >= a.Cin && a.Cin % 4 == 0)) &&
         IG_BM % a.W == 0))
     return false;
   const int HW = a.H * a.W;
@@ -1328,8 +1335,10 @@ bool halo_geom(const IgemmArgs& a, HaloGeom& hg, size_t& lds) {
   hg.HH = hg.R + a.KS - 1;
   hg.WW = a.W + a.KS - 1;
   hg.PH = hg.NI * hg.HH * hg.WW;
-  lds = 2 * (size_t)hg.PH * HX_PITCH * sizeof(_Float16);
-  return ok && hg.PH * 8 <= 256 * HX_ITEMS && lds <= 80 * 1024;
+  const int ch = halo_ch(a);
+  if (ch == 16 && a.Cout > 64) return false;   // 16-channel chunks exist for the NARROW layout only
+  lds = 2 * (size_t)hg.PH * (2 * ch + 8) * sizeof(_Float16);
+  return ok && hg.PH * (ch / 4) <= 256 * HX_ITEMS && lds <= 80 * 1024;
 }
 
 // small maps (<= 8 x 8) where at least 40 % of the im2col taps are padding: position-major tiles so
@@ -1436,9 +1445,11 @@ hipError_t launch_igemm_x3(const IgemmArgs& a, const void* wpk, float unscale, h
   // four waves along the pixels (igemm_x3h_kernel<.., NARROW>): the im2col kernel gathers every
   // input element KS^2 times
   static const int narrow = env_flag("MP_IGEMM_HALO_NARROW", 1);
-  // (zero-padding Cin to the 32-channel chunk costs up to 2.7x the MFMAs at Cin = 12: the narrow
-  // halo path is taken from Cin = 32 on, where the padding is at most 1.5x)
-  if ((wide_path(a) || (narrow && a.Cin >= 32)) && halo_geom(a, hg, lds)) {
+  // (zero-padded Cin costs MFMAs: Cin = 12 padded to 32 was 2.7x and lost; the narrow halo path is
+  // taken where the padded channels are at most 4/3 of Cin -- 16-channel chunks make that 12 -> 16,
+  // 24 -> 32, 40 / 48 -> 48)
+  if ((wide_path(a) || (narrow && (a.Cin % 32 == 0 || 3 * (a.cinp ? a.cinp : a.Cin) <= 4 * a.Cin))) &&
+      halo_geom(a, hg, lds)) {
     {
       static const bool attr = [] {
         for (const void* f : {reinterpret_cast<const void*>(igemm_x3h_kernel<3, 3, 2>),
@@ -1452,7 +1463,11 @@ hipError_t launch_igemm_x3(const IgemmArgs& a, const void* wpk, float unscale, h
                               reinterpret_cast<const void*>(igemm_x3h_kernel<3, 3, 1>),
                               reinterpret_cast<const void*>(igemm_x3h_kernel<5, 3, 1>),
                               reinterpret_cast<const void*>(igemm_x3h_kernel<3, 1, 1>),
-                              reinterpret_cast<const void*>(igemm_x3h_kernel<5, 1, 1>)})
+                              reinterpret_cast<const void*>(igemm_x3h_kernel<5, 1, 1>),
+                              reinterpret_cast<const void*>(igemm_x3h_kernel<3, 3, 4, 16>),
+                              reinterpret_cast<const void*>(igemm_x3h_kernel<5, 3, 4, 16>),
+                              reinterpret_cast<const void*>(igemm_x3h_kernel<3, 1, 4, 16>),
+                              reinterpret_cast<const void*>(igemm_x3h_kernel<5, 1, 4, 16>)})
           (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
         return true;
       }();
@@ -1466,14 +1481,17 @@ hipError_t launch_igemm_x3(const IgemmArgs& a, const void* wpk, float unscale, h
       } else {
         h.cinp = 0;
       }
-#define MP_HALO(KSV, NPV, WRV) \
-  hipLaunchKernelGGL((igemm_x3h_kernel<KSV, NPV, WRV>), hgrid, dim3(256), lds, st, h, hg, w, unscale)
-#define MP_HALO_WR(WRV)                    \
-  if (a.KS == 3 && one) MP_HALO(3, 1, WRV); \
-  else if (a.KS == 3) MP_HALO(3, 3, WRV);   \
-  else if (one) MP_HALO(5, 1, WRV);         \
-  else MP_HALO(5, 3, WRV)
-      if (N32 <= 2) {   // Cout <= 64
+#define MP_HALO(KSV, NPV, WRV, CHV) \
+  hipLaunchKernelGGL((igemm_x3h_kernel<KSV, NPV, WRV, CHV>), hgrid, dim3(256), lds, st, h, hg, w, unscale)
+#define MP_HALO_WRC(WRV, CHV)                    \
+  if (a.KS == 3 && one) MP_HALO(3, 1, WRV, CHV); \
+  else if (a.KS == 3) MP_HALO(3, 3, WRV, CHV);   \
+  else if (one) MP_HALO(5, 1, WRV, CHV);         \
+  else MP_HALO(5, 3, WRV, CHV)
+#define MP_HALO_WR(WRV) MP_HALO_WRC(WRV, 32)
+      if (N32 <= 2 && halo_ch(a) == 16) {   // Cout <= 64, 16-channel chunks
+        MP_HALO_WRC(4, 16);
+      } else if (N32 <= 2) {   // Cout <= 64
         MP_HALO_WR(4);
       } else if (tall) {
         MP_HALO_WR(1);
@@ -1481,6 +1499,7 @@ hipError_t launch_igemm_x3(const IgemmArgs& a, const void* wpk, float unscale, h
         MP_HALO_WR(2);
       }
 #undef MP_HALO_WR
+#undef MP_HALO_WRC
 #undef MP_HALO
       return hipGetLastError();
     }

@@ -365,10 +365,11 @@ void pack_matrix(mp_ctx* c, mp_ctx::PackedLayer& L, const float* w, bool x3_ok) 
     L.w.alloc(fc_x3_bytes(L.K, L.cout));
     hip_check(launch_pack_fc_x3(w, L.w.p, L.K, L.cout, &L.wus, nullptr), "pack (f16x3)");
     // 3x3 / 5x5 convs whose Cin is not a multiple of 32: a second packing with each tap's rows
-    // zero-padded to a multiple of 32, for the halo kernel (zero rows leave max|W|, so the scale, and
+    // zero-padded to a multiple of 16 or 32, for the halo kernel (zero rows leave max|W|, so the scale, and
     // every real weight's hi / lo split unchanged)
     if ((L.k == 3 || L.k == 5) && L.cin % 32 && L.cin % 4 == 0 && L.K == L.k * L.k * L.cin) {
-      L.cinp = (L.cin + 31) / 32 * 32;
+      // the smaller of the 16- and 32-multiples (16-channel halo chunks when that is not one of 32)
+      L.cinp = (L.cin + 15) / 16 * 16 < (L.cin + 31) / 32 * 32 ? (L.cin + 15) / 16 * 16 : (L.cin + 31) / 32 * 32;
       const int taps = L.k * L.k, Kp = taps * L.cinp;
       DevBuf tmp;
       tmp.alloc((size_t)Kp * L.cout * sizeof(float));
