@@ -72,8 +72,11 @@ enum { MP_MEM_HOST = 0, MP_MEM_DEVICE = 1 };
  *                       error ~1e-6 of max|output|.  Needs map height <= 64, width 32 or 64.
  *   MP_DTYPE_BF16       the FFT path with bf16 spectra (input and output), bf16 spectral weights and
  *                       bf16 1x1 gate weights: one v_mfma_f32_32x32x16_bf16 product per MAC, fp32
- *                       accumulation, fp32 FFTs and elementwise math; backbone and fc_1 stay
- *                       fp32-class.  Error ~1e-3..1e-2 of max|output| (SURVEY config 4). */
+ *                       accumulation, fp32 FFTs and elementwise math; the hGRU maps O / I / Og / P2
+ *                       and the drive X stored as bf16; conv_2 / conv_3 and fc_1 run one f16
+ *                       product per MAC (hi x hi of the f16x3 split, fp32 accumulation); conv_1,
+ *                       the BNs and the fc_1 output stay fp32.  Error ~1e-3 of max|output| on the
+ *                       pose (gate 5e-3), a few 1e-3 on the raw circuit state (SURVEY config 4). */
 enum { MP_DTYPE_F32 = 0, MP_DTYPE_F32_SPLIT = 1, MP_DTYPE_F32_FFT = 2, MP_DTYPE_BF16 = 3 };
 
 /* library version, (major << 16) | minor */

@@ -26,6 +26,29 @@ __device__ __forceinline__ void gate_mm(const f32x4* __restrict__ gpk, const f32
   }
 }
 
+// backbone epilogue of output block n (32 channels): relu(conv + b), folded BN, C8 store
+__device__ __forceinline__ void bb_epilogue_n(const ConvArgs& p, const f32x16& acc, int n, int b, int y, int x,
+                                              int h) {
+#pragma unroll
+  for (int g = 0; g < 4; ++g) {
+    const int c = 32 * n + 8 * g + 4 * h;
+    const f32x4 bb = *reinterpret_cast<const f32x4*>(p.bias + c);
+    const f32x4 ss = *reinterpret_cast<const f32x4*>(p.bn_s + c);
+    const f32x4 tt = *reinterpret_cast<const f32x4*>(p.bn_t + c);
+    f32x4 o;
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const float v = fmaxf(acc[4 * g + j] + bb[j], 0.f);   // relu(conv + b)
+      o[j] = v * ss[j] + tt[j];                             // folded BN
+    }
+    const size_t idx = c8_index(b, 4 * n + g, y, x, 4 * h, p.H, p.W);
+    if (p.dst_bf16)
+      *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(p.dst) + idx) = bf16x4_pack(o);
+    else
+      *reinterpret_cast<f32x4*>(p.dst + idx) = o;
+  }
+}
+
 template <int EPI>
 __device__ __forceinline__ void conv_epilogue(const ConvArgs& p, const f32x16& acc0, const f32x16& acc1,
                                               int b, int y, int x, int h, int lane, float scale) {
@@ -33,25 +56,7 @@ __device__ __forceinline__ void conv_epilogue(const ConvArgs& p, const f32x16& a
   f32x16 acc[2] = {acc0 * scale, acc1 * scale};
   if constexpr (EPI == EPI_BB) {
 #pragma unroll
-    for (int n = 0; n < 2; ++n)
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int c = 32 * n + 8 * g + 4 * h;
-        const f32x4 bb = *reinterpret_cast<const f32x4*>(p.bias + c);
-        const f32x4 ss = *reinterpret_cast<const f32x4*>(p.bn_s + c);
-        const f32x4 tt = *reinterpret_cast<const f32x4*>(p.bn_t + c);
-        f32x4 o;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const float v = fmaxf(acc[n][4 * g + j] + bb[j], 0.f);   // relu(conv + b)
-          o[j] = v * ss[j] + tt[j];                                    // folded BN
-        }
-        const size_t idx = c8_index(b, 4 * n + g, y, x, 4 * h, H, W);
-        if (p.dst_bf16)
-          *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(p.dst) + idx) = bf16x4_pack(o);
-        else
-          *reinterpret_cast<f32x4*>(p.dst + idx) = o;
-      }
+    for (int n = 0; n < 2; ++n) bb_epilogue_n(p, acc[n], n, b, y, x, h);
   } else if constexpr (EPI == EPI_HGRU_A) {
     // I = tanh(X - (beta*O + nu) * (P1 + lateral_bias))      hgru_module.py:657, 797-799
 #pragma unroll

@@ -19,6 +19,8 @@
 // pre-packed in fragment order (two 16-byte loads per lane per tap per 32 output channels).
 #include "conv_epi.hpp"
 
+#include <cstdlib>
+
 typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
 
 namespace mp {
@@ -35,29 +37,37 @@ __device__ __forceinline__ f32x16 mfma16(f16x8 a, f16x8 b, f32x16 c) {
 // after its MFMAs (sched_group_barrier).
 // NP = 3: the fp32-accurate split (hi*lo, lo*hi, hi*hi); NP = 1: hi*hi only (MP_DTYPE_BF16's
 // backbone: one f16 product per MAC, 11-bit operands, fp32 accumulation)
-template <int KS, int EPI, int NW, int SCHED, int NP = 3>
+// TH rows per tile (TH3 = 32; 8 for small backbone batches) and NN of the two 32-channel output
+// blocks per block (1: the block's n-half is blockIdx.x % 2; EPI_BB only).  Each accumulator's
+// MFMA sequence (chunks, taps, lo/hi order) is the same for every TH / NN, so the outputs are
+// bit-identical across the variants and a batch-size-dependent choice keeps batch invariance.
+template <int KS, int EPI, int NW, int SCHED, int NP = 3, int TH = TH3, int NN = 2>
 __global__ __launch_bounds__(NW * 64, 1) void conv64x3_kernel(ConvArgs p, const f16x8* __restrict__ wpk,
                                                               float unscale) {
+  static_assert(NN == 2 || EPI == EPI_BB, "split output blocks only for the backbone epilogue");
   constexpr int R = KS / 2;
-  constexpr int HY = TH3 + KS - 1, HX = TW + KS - 1;
+  constexpr int HY = TH + KS - 1, HX = TW + KS - 1;
   constexpr int KK = KS * KS;
   constexpr int NQ16 = 4;                // 16-channel chunks
-  constexpr int MB = TH3 / NW;           // M-blocks (rows of 32 pixels) per wave
+  constexpr int MB = TH / NW;            // M-blocks (rows of 32 pixels) per wave
+  static_assert(MB >= 1 && MB * NW == TH, "rows per tile must be a multiple of the wave count");
   constexpr int NT = NW * 64;
   __shared__ f16x8 halo[HY * 4 * HX];
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, col = lane & 31;
   const int H = p.H, W = p.W;
   int bid = blockIdx.x;
+  const int n0 = NN == 2 ? 0 : bid % 2;   // first output block of this block
+  if constexpr (NN == 1) bid >>= 1;
   const int tx = bid % p.tiles_x;
   bid /= p.tiles_x;
   const int ty = bid % p.tiles_y;
   const int b = bid / p.tiles_y;
-  const int y0 = ty * TH3, x0 = tx * TW;
+  const int y0 = ty * TH, x0 = tx * TW;
 
-  f32x16 acc[2][MB];
+  f32x16 acc[NN][MB];
 #pragma unroll
-  for (int n = 0; n < 2; ++n)
+  for (int n = 0; n < NN; ++n)
 #pragma unroll
     for (int m = 0; m < MB; ++m) acc[n][m] = f32x16{};
 
@@ -89,6 +99,7 @@ __global__ __launch_bounds__(NW * 64, 1) void conv64x3_kernel(ConvArgs p, const 
     const f16x8* wq = wpk + (size_t)Q * KK * 4 * 64 + lane;
     const f16x8* hb = halo + ((wv * MB) * 4 + h) * HX + col;
     if constexpr (SCHED == 0) {
+      static_assert(NN == 2, "the SCHED 0 tap loop covers both output blocks");
       for (int ky = 0; ky < KS; ++ky) {
         const f16x8* hrow = hb + ky * 4 * HX;
 #pragma unroll 1
@@ -114,9 +125,11 @@ __global__ __launch_bounds__(NW * 64, 1) void conv64x3_kernel(ConvArgs p, const 
       // one-tap-ahead prefetch: the weights of tap t+1 are requested at the top of tap t, the
       // halo fragments of M-block m for tap t+1 right after M-block m's MFMAs of tap t.  The "next
       // tap" of the last tap wraps to tap 0 so every address stays in bounds.
-      f16x8 w[4], bh[MB], bl[MB];
+      constexpr int NWF = 2 * NN;   // weight fragments per tap: (hi, lo) of each output block
+      f16x8 w[NWF], bh[MB], bl[MB];
+      const f16x8* wq0 = wq + 2 * n0 * 64;
 #pragma unroll
-      for (int i = 0; i < 4; ++i) w[i] = wq[i * 64];
+      for (int i = 0; i < NWF; ++i) w[i] = wq0[i * 64];
 #pragma unroll
       for (int m = 0; m < MB; ++m) {
         bh[m] = hb[m * 4 * HX];
@@ -129,29 +142,29 @@ __global__ __launch_bounds__(NW * 64, 1) void conv64x3_kernel(ConvArgs p, const 
           nkx = 0;
           nky = (nky + 1 == KS) ? 0 : nky + 1;
         }
-        f16x8 cw[4];
+        f16x8 cw[NWF];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) cw[i] = w[i];
-        const f16x8* wn = wq + ntap * 4 * 64;
+        for (int i = 0; i < NWF; ++i) cw[i] = w[i];
+        const f16x8* wn = wq0 + ntap * 4 * 64;
 #pragma unroll
-        for (int i = 0; i < 4; ++i) w[i] = wn[i * 64];
+        for (int i = 0; i < NWF; ++i) w[i] = wn[i * 64];
         const f16x8* hn = hb + nky * 4 * HX + nkx;
 #pragma unroll
         for (int m = 0; m < MB; ++m) {
           const f16x8 ch = bh[m], cl = bl[m];
           if constexpr (NP == 3) {
-            acc[0][m] = mfma16(cw[0], cl, acc[0][m]);
-            acc[1][m] = mfma16(cw[2], cl, acc[1][m]);
-            acc[0][m] = mfma16(cw[1], ch, acc[0][m]);
-            acc[1][m] = mfma16(cw[3], ch, acc[1][m]);
+#pragma unroll
+            for (int n = 0; n < NN; ++n) acc[n][m] = mfma16(cw[2 * n], cl, acc[n][m]);
+#pragma unroll
+            for (int n = 0; n < NN; ++n) acc[n][m] = mfma16(cw[2 * n + 1], ch, acc[n][m]);
           }
-          acc[0][m] = mfma16(cw[0], ch, acc[0][m]);
-          acc[1][m] = mfma16(cw[2], ch, acc[1][m]);
+#pragma unroll
+          for (int n = 0; n < NN; ++n) acc[n][m] = mfma16(cw[2 * n], ch, acc[n][m]);
           bh[m] = hn[m * 4 * HX];
           if constexpr (NP == 3) bl[m] = hn[m * 4 * HX + 2 * HX];
-          if (m == 0) __builtin_amdgcn_sched_group_barrier(0x020, 4, 0);   // the 4 weight loads
-          __builtin_amdgcn_sched_group_barrier(0x008, 2 * NP, 0);          // 6 (2) MFMA
-          __builtin_amdgcn_sched_group_barrier(0x100, NP == 3 ? 2 : 1, 0); // 2 (1) ds_read
+          if (m == 0) __builtin_amdgcn_sched_group_barrier(0x020, NWF, 0);   // the weight loads
+          __builtin_amdgcn_sched_group_barrier(0x008, NN * NP, 0);           // 6 (2) MFMA at NN = 2
+          __builtin_amdgcn_sched_group_barrier(0x100, NP == 3 ? 2 : 1, 0);   // 2 (1) ds_read
         }
       }
     }
@@ -163,7 +176,10 @@ __global__ __launch_bounds__(NW * 64, 1) void conv64x3_kernel(ConvArgs p, const 
     // one M-block at a time: keeps the scheduler from hoisting every block's epilogue loads
     // beside the live accumulators
     __builtin_amdgcn_sched_barrier(0);
-    conv_epilogue<EPI>(p, acc[0][m], acc[1][m], b, y0 + wv * MB + m, x, h, lane, unscale);
+    if constexpr (NN == 2)
+      conv_epilogue<EPI>(p, acc[0][m], acc[1][m], b, y0 + wv * MB + m, x, h, lane, unscale);
+    else
+      bb_epilogue_n(p, acc[0][m] * unscale, n0, b, y0 + wv * MB + m, x, h);
   }
 }
 
@@ -189,10 +205,11 @@ __global__ void pack_conv64x3_kernel(const float* __restrict__ w, f16x8* out, in
   dst[64] = lv;
 }
 
-template <int KS, int EPI, int NW, int SCHED, int NP = 3>
-static hipError_t launch_x3_t(const ConvArgs& a, const void* wpk, float unscale, int B, hipStream_t st) {
-  const int nblk = B * a.tiles_x * a.tiles_y;
-  hipLaunchKernelGGL((conv64x3_kernel<KS, EPI, NW, SCHED, NP>), dim3(nblk), dim3(NW * 64), 0, st, a,
+template <int KS, int EPI, int NW, int SCHED, int NP = 3, int TH = TH3, int NN = 2>
+static hipError_t launch_x3_t(ConvArgs a, const void* wpk, float unscale, int B, hipStream_t st) {
+  a.tiles_y = a.H / TH;
+  const int nblk = B * a.tiles_x * a.tiles_y * (2 / NN);
+  hipLaunchKernelGGL((conv64x3_kernel<KS, EPI, NW, SCHED, NP, TH, NN>), dim3(nblk), dim3(NW * 64), 0, st, a,
                      static_cast<const f16x8*>(wpk), unscale);
   return hipGetLastError();
 }
@@ -200,15 +217,30 @@ static hipError_t launch_x3_t(const ConvArgs& a, const void* wpk, float unscale,
 // the production variant per kernel size (chosen with tools/bench_conv.hip)
 constexpr int X3_NW = 8, X3_SCHED = 1;
 
+// Backbone convs of small batches: 8-row tiles with one 32-channel output block per block (8x the
+// blocks: a batch-1 conv is 32 blocks instead of 4), bit-identical to the 32-row tiles.  Taken
+// below 128 blocks of the default tiling (B < 32 at 64 x 64); MP_CONV_SMALL=0 keeps the default.
+static bool conv_small_tiles(const ConvArgs& a, int B) {
+  static const int on = [] {
+    const char* e = std::getenv("MP_CONV_SMALL");
+    return e ? std::atoi(e) : 1;
+  }();
+  return on && a.H % 8 == 0 && (long)B * (a.W / TW) * (a.H / TH3) < 128;
+}
+
 hipError_t launch_conv64x3(int ks, int epi, ConvArgs a, const void* wpk, float unscale, int B, hipStream_t st,
                            int nprod) {
   a.tiles_x = a.W / TW;
   a.tiles_y = a.H / TH3;
   if (a.ascale == 0.f) a.ascale = ACT_SCALE;
+  const bool small = epi == EPI_BB && ks == 3 && conv_small_tiles(a, B);
   if (nprod == 1) {
-    if (ks == 3 && epi == EPI_BB) return launch_x3_t<3, EPI_BB, X3_NW, X3_SCHED, 1>(a, wpk, unscale, B, st);
+    if (ks == 3 && epi == EPI_BB)
+      return small ? launch_x3_t<3, EPI_BB, X3_NW, X3_SCHED, 1, 8, 1>(a, wpk, unscale, B, st)
+                   : launch_x3_t<3, EPI_BB, X3_NW, X3_SCHED, 1>(a, wpk, unscale, B, st);
     return hipErrorInvalidValue;
   }
+  if (small) return launch_x3_t<3, EPI_BB, X3_NW, X3_SCHED, 3, 8, 1>(a, wpk, unscale, B, st);
 #define MP_CASE(K, E) \
   if (ks == K && epi == E) return launch_x3_t<K, E, X3_NW, X3_SCHED>(a, wpk, unscale, B, st);
   MP_CASE(15, EPI_HGRU_A)

@@ -60,6 +60,7 @@ CASES = [
     # (env, model, dtype, gate)
     ({"MP_BF16_MAPS": "0"}, "pose", "bf16", 5e-3),
     ({"MP_FC_PRESPLIT": "0"}, "pose", "fp32_fft", 1e-4),
+    ({"MP_CONV_SMALL": "0"}, "pose", "fp32_fft", 1e-4),
     ({"MP_FC_PRESPLIT": "0"}, "pose", "bf16", 5e-3),
     ({"MP_IGEMM_PM_SPLITS": "1"}, "hier", "fp32_split", 1e-4),
     ({"MP_IGEMM_PM_SPLITS": "1"}, "hier", "bf16", 5e-3),
