@@ -112,8 +112,8 @@ def fft_kernels(ctx, B, hw, steps, bf16=False):
 # per-kernel HBM bytes per launch from rocprofv3 PMC passes (FETCH_SIZE x2 on gfx950 + WRITE_SIZE,
 # MI355X_MICROARCH.md), collected with the full-batch single-stream launches of this workload by
 # tools/pmc_bytes.py and committed under profiles/ (bench cannot profile itself)
-PMC_TRAFFIC = {False: "profiles/r2c/pmc_traffic_fp32_b256.csv",
-               True: "profiles/r2c/pmc_traffic_bf16_b256.csv"}
+PMC_TRAFFIC = {False: "profiles/r2d/pmc_traffic_fp32_b256.csv",
+               True: "profiles/r2d/pmc_traffic_bf16_b256.csv"}
 PMC_KERNEL = {   # name: (fp32 path's kernel, bf16 path's kernel) as rocprofv3 names them
     "fft_fwd": ("fft_fwd_kernel<false, false>", "fft_fwd_kernel<true, true>"),
     "spec_gemm": ("spec_gemm_kernel<0>", "spec_gemm_bf_kernel"),
@@ -124,7 +124,7 @@ PMC_KERNEL = {   # name: (fp32 path's kernel, bf16 path's kernel) as rocprofv3 n
 
 # MFMA utilisation per kernel from the committed PMC pass (tools/pmc_mfma.sh / .py: SQ_VALU_MFMA_BUSY_CYCLES
 # over GRBM_GUI_ACTIVE x 1024 SIMDs, the gfx950 MfmaUtil), same one-stream B = 256 workload
-PMC_MFMA = "profiles/r2c/mfma_util_pose_fp32_b256.csv"
+PMC_MFMA = "profiles/r2d/mfma_util_pose_fp32_b256.csv"
 MFMA_KERNELS = {"fc_gemm_x3p (fc_1 on split planes, k_fc.hip)": "fc_gemm_x3p_kernel", "conv64x3 (conv_2/3, k_conv64x3.hip)": "conv64x3_kernel",
                 "spec_gemm (k_fft.hip)": "spec_gemm_kernel", "spec_epi_b (gate GEMMs, k_fft.hip)": "spec_epi_b_kernel<false, false, false>",
                 "gate_init_x3 (k_fft.hip)": "gate_init_x3_kernel"}
@@ -238,7 +238,7 @@ def extras(mp, dev, args):
         hm = mp.train_hier_networks.hier_model_struct()
         hm.load_weights({v.name: W.synth_value(v, 5) for v in W.hier_vars()})
         hm.build(depth, 108, 39, 39, 39, 39, 36)
-        t = time_gpu(lambda: hm.forward(depth), 5, 1)
+        t = time_gpu(lambda: hm.forward(depth), 20, 3)
         out["hier_b256"] = {"crops_per_s": round(B / t, 2), "ms_per_batch": round(t * 1e3, 3),
                             "gflop_per_crop": 7.97, "tflops": round(7.97e9 * B / t / 1e12, 2),
                             "dtype": "fp32_split", "engine": "layer-graph runtime (mp_graph_fwd)",
@@ -284,7 +284,7 @@ def extras(mp, dev, args):
         dm = mp.train_dense_networks.dense_model_struct()
         dm.load_weights({v.name: W.synth_value(v, 6) for v in W.dense_vars()})
         dm.build(depth, 69)
-        t = time_gpu(lambda: dm.forward(depth), 5, 1)
+        t = time_gpu(lambda: dm.forward(depth), 20, 3)
         out["dense_b256"] = {"crops_per_s": round(B / t, 2), "ms_per_batch": round(t * 1e3, 3),
                              "gflop_per_crop": 3.22, "tflops": round(3.22e9 * B / t / 1e12, 2),
                              "dtype": "fp32_split", "engine": "layer-graph runtime (mp_graph_fwd)"}
@@ -317,7 +317,7 @@ def extras(mp, dev, args):
                "buffers": model._ctx.info("graph_buffers")}
         for mode in ("1", "0"):   # hipGraph replay, then eager multi-stream launches (the default)
             _os.environ["MP_GRAPH_EXEC"] = mode
-            t = time_gpu(lambda: model.forward(depth), 5, 1)
+            t = time_gpu(lambda: model.forward(depth), 10, 2)
             k = "hipgraph_replay" if mode == "1" else "eager_multistream"
             rec[k] = {"crops_per_s": round(B / t, 2), "ms_per_batch": round(t * 1e3, 3),
                       "tflops": round(gf * 1e9 * B / t / 1e12, 2)}
