@@ -827,7 +827,7 @@ __global__ __launch_bounds__(256) void igemm_split_reduce_kernel(IgemmArgs p, in
   }
 }
 
-// Pointwise (1x1, stride 1) f16x3 conv for K = Cin <= 192 and Cout <= 128 (the dense regressors'
+// Pointwise (1x1, stride 1) f16x3 conv for K = Cin <= 192 and Cout <= 256 (the dense regressors'
 // bottlenecks, train_dense_networks.py:248-373: 40 .. 184 -> 24 .. 96 channels on 64 x 64 maps).
 // These are HBM-bound GEMMs with a short K loop: the im2col kernels' one-step-ahead prefetch left a
 // load latency exposed in every one of their 2 - 6 K steps.  Here every thread issues its whole
@@ -842,7 +842,10 @@ __global__ __launch_bounds__(256, 2) void igemm_x3pw_kernel(IgemmArgs p, const f
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, col = lane & 31;
   const int wm = wv & 1, wn = wv >> 1;
   const int M = p.N * p.Ho * p.Wo;
-  const int m0 = blockIdx.x * IG_BM;
+  int mt_, nt_;
+  xcd_tile(p, false, mt_, nt_);   // the N tiles of one pixel tile run on one XCD: one HBM read of it
+  const int m0 = mt_ * IG_BM;
+  const int nb0 = nt_ * 4;        // first 32-channel block of this block's 128 output channels
   const int N32 = (p.Cout + 31) / 32;
   const int K16 = (p.K + 15) / 16;
   const int k4 = (tid & 7) * 4;
@@ -860,7 +863,7 @@ __global__ __launch_bounds__(256, 2) void igemm_x3pw_kernel(IgemmArgs p, const f
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
       const int e = tid + 256 * u, l = e & 63, part = (e >> 6) & 1, nb = (e >> 7) & 3, g = e >> 9;
-      const int kb = min((k0 >> 4) + g, K16 - 1), nbc = min(nb, N32 - 1);
+      const int kb = min((k0 >> 4) + g, K16 - 1), nbc = min(nb0 + nb, N32 - 1);
       if (NP == 3 || part == 0) w[u] = wpk[(((size_t)kb * N32 + nbc) * 2 + part) * 64 + l];
     }
   };
@@ -871,7 +874,7 @@ __global__ __launch_bounds__(256, 2) void igemm_x3pw_kernel(IgemmArgs p, const f
     for (int nb = 0; nb < 2; ++nb) acc[mb][nb] = f32x16{};
   f16x8 wnx[4];
   load_w(0, wnx);
-  const bool wave_on = 2 * wn < N32;   // wave-uniform
+  const bool wave_on = nb0 + 2 * wn < N32;   // wave-uniform
 #pragma unroll
   for (int c = 0; c < NCH; ++c) {
     const int k0 = 32 * c;
@@ -928,7 +931,7 @@ __global__ __launch_bounds__(256, 2) void igemm_x3pw_kernel(IgemmArgs p, const f
     float* dst = p.out + (size_t)gm * p.ldo + p.coff;
 #pragma unroll
     for (int nb = 0; nb < 2; ++nb) {
-      const int cb = 2 * wn + nb;
+      const int cb = nb0 + 2 * wn + nb;
       if (cb >= N32) break;
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
@@ -1420,10 +1423,12 @@ hipError_t launch_igemm_x3(const IgemmArgs& a, const void* wpk, float unscale, h
   static const int xcd = env_flag("MP_IGEMM_XCD", 1);
   static const int pw = env_flag("MP_IGEMM_PW", 1);
   if (pw && a.KS == 1 && a.stride == 1 && a.Ho == a.H && a.Wo == a.W && a.pad_t == 0 && a.pad_l == 0 &&
-      a.K == a.Cin && a.K <= 192 && a.Cin % 4 == 0 && a.cix % 4 == 0 && a.ldx % 4 == 0 && N32 <= 4 && !a.pool) {
+      a.K == a.Cin && a.K <= 192 && a.Cin % 4 == 0 && a.cix % 4 == 0 && a.ldx % 4 == 0 && N32 <= 8 && !a.pool) {
     const int nch = (a.K + 31) / 32;
-    const dim3 pgrid((M + IG_BM - 1) / IG_BM);
-#define MP_PW(NPV, NCHV) hipLaunchKernelGGL((igemm_x3pw_kernel<NPV, NCHV>), pgrid, dim3(256), 0, st, a, w, unscale)
+    const dim3 pgrid((M + IG_BM - 1) / IG_BM, (N32 + 3) / 4);   // 128-channel output tiles
+    IgemmArgs pa = a;
+    pa.xcd = xcd;
+#define MP_PW(NPV, NCHV) hipLaunchKernelGGL((igemm_x3pw_kernel<NPV, NCHV>), pgrid, dim3(256), 0, st, pa, w, unscale)
 #define MP_PWN(NCHV)     \
   if (one) MP_PW(1, NCHV); \
   else MP_PW(3, NCHV)

@@ -19,6 +19,7 @@
 // Activations: x is copied into a graph-owned input buffer and outputs copied out, so the captured
 // graph only ever sees its own pointers.
 #include <algorithm>
+#include <map>
 #include <cstdio>
 #include <cstdlib>
 #include <numeric>
@@ -75,6 +76,9 @@ struct GraphState {
     int cH = 0, cW = 0;
     mpr::DevBuf ones, zeros;
   };
+  // concatenated packings of fused 1x1 sibling convs, keyed by their names; kept across re-plans
+  std::map<std::string, std::unique_ptr<mp_ctx::PackedLayer>> fused1x1;
+  int n_fused_1x1 = 0;   // this plan's 1x1 convs computed by a sibling's kernel
   int64_t pn = 0, ph = 0, pw = 0;
   bool planned = false;
   std::vector<Tensor> t;
@@ -163,6 +167,49 @@ using G = GraphState;
 // written (the hGRU backbone's conv_1 kernel, NHWC out, unit affine)
 constexpr int KIND_CONV1_POOL = 100;
 
+// 1x1 sibling fusion: the one packing of several 1x1 convs over the same input, output channels
+// concatenated in member order (weights [Cin][sum Cout], one power-of-two scale from their joint
+// max|W|: the split stays 22 bits relative to that max, i.e. fp32-accurate, but not bit-identical to
+// the separate packings)
+const mp_ctx::PackedLayer& fused_1x1_pack(mp_ctx* c, G& g, const std::vector<int>& mem) {
+  std::string key;
+  int tot = 0;
+  for (int m : mem) {
+    key += g.ops[m].name + "+";
+    tot += g.ops[m].cout;
+  }
+  auto& slot = g.fused1x1[key];
+  if (slot) return *slot;
+  slot = std::make_unique<mp_ctx::PackedLayer>();
+  auto& F = *slot;
+  const auto& L0 = c->layers.at(g.ops[mem[0]].name);
+  F.k = 1;
+  F.cin = L0.cin;
+  F.K = L0.cin;
+  F.cout = tot;
+  F.x3 = true;
+  F.nprod = L0.nprod;
+  mpr::DevBuf tmp;
+  tmp.alloc((size_t)F.K * tot * sizeof(float));
+  F.b.alloc((size_t)tot * sizeof(float));
+  int off = 0;
+  for (int m : mem) {
+    const auto& op = g.ops[m];
+    const float* w = c->raw.at(op.name + "/" + op.name + "_filters").dev->f();   // HWIO [1][1][Cin][Cout]
+    hip_check(hipMemcpy2D(tmp.f() + off, (size_t)tot * sizeof(float), w, (size_t)op.cout * sizeof(float),
+                          (size_t)op.cout * sizeof(float), F.K, hipMemcpyDeviceToDevice),
+              "fused 1x1 weights");
+    hip_check(hipMemcpy(F.b.f() + off, c->layers.at(op.name).b.p, (size_t)op.cout * sizeof(float),
+                        hipMemcpyDeviceToDevice),
+              "fused 1x1 bias");
+    off += op.cout;
+  }
+  F.w.alloc(fc_x3_bytes(F.K, tot));
+  hip_check(launch_pack_fc_x3(tmp.f(), F.w.p, F.K, tot, &F.wus, nullptr), "pack fused 1x1");
+  hip_check(hipDeviceSynchronize(), "pack fused 1x1");
+  return F;
+}
+
 void plan(mp_ctx* c, G& g, int64_t n, int64_t h, int64_t w) {
   g.drop_exec();
   g.planned = false;
@@ -250,8 +297,57 @@ void plan(mp_ctx* c, G& g, int64_t n, int64_t h, int64_t w) {
     if (o.H <= 0 || o.W <= 0 || o.C <= 0) fail(MP_ERR_SHAPE, "empty tensor in the graph");
   }
   GDBG("plan: shapes done (%d tensors, %zu ops)", NT, g.ops.size());
+  // 1x1 siblings: stride-1 1x1 f16x3 convs reading the same tensor (the dense regressors'
+  // conv_L_1_1x1 / conv_L_2_1x1_1 and conv_L_2_1x1_2 / conv_L_3_1x1_2 pairs,
+  // train_dense_networks.py:248-373) run as one conv over their concatenated weights while the
+  // pointwise kernel takes it (Cin <= 192, Cout <= 256): the input is read once instead of once per
+  // conv.  Their outputs become adjacent channel ranges of one buffer (placement constraints like a
+  // concat's), so each consumer reads its slice in place.  MP_GRAPH_FUSE_1X1=0 keeps them apart.
+  std::vector<int> sib_lead(g.ops.size(), -1);        // op -> the op whose kernel computes it
+  std::vector<std::vector<int>> sib_mem(g.ops.size());  // lead -> members (lead first)
+  g.n_fused_1x1 = 0;
+  if (env_int("MP_GRAPH_FUSE_1X1", 1)) {
+    std::vector<char> in_concat(NT, 0);
+    for (const auto& op : g.ops)
+      if (op.kind == MP_OP_CONCAT)
+        for (int s : op.src) in_concat[root(s)] = 1;
+    std::map<int, std::vector<int>> by_src;
+    for (size_t i = 0; i < g.ops.size(); ++i) {
+      const auto& op = g.ops[i];
+      if (op.kind != MP_OP_CONV || op.ksize != 1 || op.stride != 1) continue;
+      const auto it = c->layers.find(op.name);
+      if (it == c->layers.end() || !it->second.x3 || in_concat[op.out] || root(op.out) != op.out) continue;
+      const int s = root(op.src[0]);
+      if (s == 0 || T[s].C > 192 || T[s].C % 4) continue;
+      by_src[s].push_back((int)i);
+    }
+    for (auto& kv : by_src) {
+      const auto& v = kv.second;
+      for (size_t a = 0; a < v.size();) {   // runs in op order, at most 256 output channels each
+        int tot = g.ops[v[a]].cout;
+        size_t b = a + 1;
+        while (b < v.size() && tot + g.ops[v[b]].cout <= 256) tot += g.ops[v[b++]].cout;
+        if (b - a >= 2) g.n_fused_1x1 += (int)(b - a) - 1;
+        if (b - a >= 2)
+          for (size_t q = a; q < b; ++q) {
+            sib_lead[v[q]] = v[a];
+            sib_mem[v[a]].push_back(v[q]);
+          }
+        a = b;
+      }
+    }
+  }
   // 3: placement of concat groups
   UF uf(NT);
+  for (size_t i = 0; i < g.ops.size(); ++i) {
+    if (sib_lead[i] != (int)i) continue;
+    int off = 0;
+    for (int m : sib_mem[i]) {
+      if (m != (int)i && !uf.unite(g.ops[m].out, g.ops[i].out, off))
+        fail(MP_ERR_UNSUPPORTED, "1x1 sibling placement conflict at " + g.ops[m].name);
+      off += g.ops[m].cout;
+    }
+  }
   for (const auto& op : g.ops) {
     if (op.kind != MP_OP_CONCAT) continue;
     int off = 0;
@@ -334,7 +430,7 @@ void plan(mp_ctx* c, G& g, int64_t n, int64_t h, int64_t w) {
   if (env_int("MP_GRAPH_FUSE_POOL", 1))
     for (size_t i = 0; i < g.ops.size(); ++i) {
       const auto& op = g.ops[i];
-      if (op.kind != MP_OP_CONV || fused_pool[i] >= 0 || uses[op.out] != 1) continue;
+      if (op.kind != MP_OP_CONV || fused_pool[i] >= 0 || uses[op.out] != 1 || sib_lead[i] >= 0) continue;
       for (size_t j = i + 1; j < g.ops.size(); ++j) {
         const auto& pj = g.ops[j];
         if (pj.kind == MP_OP_MAXPOOL && pj.ksize == 2 && pj.src[0] == op.out && root(pj.out) == pj.out) {
@@ -380,6 +476,10 @@ void plan(mp_ctx* c, G& g, int64_t n, int64_t h, int64_t w) {
       continue;
     }
     if (op.kind == MP_OP_RELU || op.kind == MP_OP_IDENTITY) continue;
+    if (sib_lead[i] >= 0 && sib_lead[i] != (int)i) {   // computed by its lead's kernel
+      o.prod = T[g.ops[sib_lead[i]].out].prod;
+      continue;
+    }
     auto k = std::make_unique<G::Kern>();
     k->op = (int)i;
     k->kind = op.kind;
@@ -388,11 +488,12 @@ void plan(mp_ctx* c, G& g, int64_t n, int64_t h, int64_t w) {
     if (op.kind == MP_OP_CONV) {
       auto it = c->layers.find(op.name);
       if (it == c->layers.end()) fail(MP_ERR_STATE, "conv layer not finalized: " + op.name);
-      const auto& L = it->second;
-      if (L.cin != S.C || L.cout != op.cout || L.k != op.ksize)
-        fail(MP_ERR_SHAPE, "conv " + op.name + ": weights [" + std::to_string(L.k) + "," + std::to_string(L.k) + "," +
-                               std::to_string(L.cin) + "," + std::to_string(L.cout) + "] vs input channels " +
+      const auto& L1 = it->second;
+      if (L1.cin != S.C || L1.cout != op.cout || L1.k != op.ksize)
+        fail(MP_ERR_SHAPE, "conv " + op.name + ": weights [" + std::to_string(L1.k) + "," + std::to_string(L1.k) + "," +
+                               std::to_string(L1.cin) + "," + std::to_string(L1.cout) + "] vs input channels " +
                                std::to_string(S.C));
+      const auto& L = sib_lead[i] == (int)i ? fused_1x1_pack(c, g, sib_mem[i]) : L1;
       IgemmArgs& a = k->ia;
       a.x = base(s);
       a.ldx = ld(s);
@@ -690,6 +791,8 @@ void finalize_graph(mp_ctx* c) {
   auto& g = *c->graph;
   g.drop_exec();
   g.planned = false;
+  g.kerns.clear();
+  g.fused1x1.clear();   // packed from the previous weights
   c->layers.clear();
   // input channels per conv from a channel-only pass (spatial sizes come at plan time)
   std::vector<int> ch(g.n_tensors, 0);
@@ -748,7 +851,9 @@ bool graph_info(mp_ctx* c, const std::string& k, int64_t* v) {
     *v = g.captured ? 1 : 0;
   else if (k == "graph_buffers")
     *v = (int64_t)g.groups.size();
-  else if (k == "graph_fused_pools") {   // max pools computed inside their conv's kernel
+  else if (k == "graph_fused_1x1") {   // 1x1 convs computed by a sibling's kernel
+    *v = g.n_fused_1x1;
+  } else if (k == "graph_fused_pools") {   // max pools computed inside their conv's kernel
     int64_t f = 0;
     for (const auto& kk : g.kerns) f += (kk->kind == MP_OP_CONV && kk->ia.pool) || kk->kind == KIND_CONV1_POOL;
     *v = f;

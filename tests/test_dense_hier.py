@@ -128,8 +128,10 @@ def test_dense_hier_gpu_matches_golden_and_oracle(dtype):
         assert rel_inf(got, golden_array("dense_hier_c128", f"{f}_out")) <= FP32_REL_TOL
     ctx = model._ctx
     assert ctx.info("graph_streams") > 1
-    # 365 convs + 28 pools + 52 FC (gemm + reduce); pools fused into their conv's kernel launch nothing
-    assert ctx.info("graph_kernels") + ctx.info("graph_fused_pools") == 365 + 28 + 2 * 52
+    # 365 convs + 28 pools + 52 FC (gemm + reduce); pools fused into their conv's kernel and 1x1
+    # convs computed by a sibling's kernel launch nothing
+    assert (ctx.info("graph_kernels") + ctx.info("graph_fused_pools") + ctx.info("graph_fused_1x1")
+            == 365 + 28 + 2 * 52)
     # 169 concats placed in place: fewer buffers than tensors
     assert ctx.info("graph_buffers") < 365 + 28 + 52
     again = model.forward(x).cpu().numpy()

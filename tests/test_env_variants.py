@@ -70,6 +70,8 @@ CASES = [
     ({"MP_IGEMM_SMALL_SPLITK": "0"}, "dense_hier", "fp32_split", 1e-4),
     ({"MP_IGEMM_PW": "0", "MP_IGEMM_HALO_NARROW": "0"}, "dense", "fp32_split", 1e-4),
     ({"MP_IGEMM_PW": "0", "MP_IGEMM_HALO_NARROW": "0"}, "dense", "bf16", 5e-3),
+    ({"MP_GRAPH_FUSE_1X1": "0"}, "dense", "fp32_split", 1e-4),
+    ({"MP_GRAPH_FUSE_1X1": "0"}, "dense_hier", "fp32_split", 1e-4),
 ]
 
 

@@ -53,6 +53,11 @@ def test_dense_gpu_matches_golden_and_oracle(dtype, engine):
     assert np.array_equal(out, again)
     one = model.forward(torch.from_numpy(depth[1:2]).cuda()).cpu().numpy()
     assert np.array_equal(one[0], out[1])
+    if engine == "graph" and dtype == "fp32_split":
+        # the 1x1 sibling pairs over one input (conv_L_1_1x1 + conv_L_2_1x1_1 at L = 3..6, and
+        # conv_L_2_1x1_2 + conv_L_3_1x1_2 where the 32x32 input is <= 192 channels: L = 3, 4) run
+        # as one conv each (mp_graph.hip plan: 1x1 siblings)
+        assert model._ctx.info("graph_fused_1x1") == 6
 
 
 @pytest.mark.gpu
