@@ -428,134 +428,6 @@ __global__ __launch_bounds__(64 * NW, MINB) void fc_gemm_x3p_kernel(const _Float
   }
 }
 
-// The three-product fc_1 kernel with a 2 x 2 wave grid (MP_FC_WL22): wave (wm, wn) owns rows
-// 64 wm .. 64 wm + 63 (two 32-row m-blocks) and output columns of blocks 4 nt + 2 wn, + 1, instead of
-// all 128 rows x one 32-column block.  Each A fragment pair (hi, lo) read from LDS then feeds two
-// column blocks: half the ds_read_b128 per MFMA (4 instead of 8 per 12 MFMAs per 16-deep k group),
-// for twice the weight fragments per wave (the two m-halves' waves read the same ones, from L1).
-// Per output the MFMA sequence (g order; lo_w*hi_a, hi_w*lo_a, hi_w*hi_a) is fc_gemm_x3p_kernel's:
-// bit-identical results.  Staging (LDS-DMA, swizzle, double buffer) is unchanged.
-template <int BK, int MINB>
-__global__ __launch_bounds__(256, MINB) void fc_gemm_x3p22_kernel(const _Float16* __restrict__ Ah,
-                                                               const _Float16* __restrict__ Al, int lda,
-                                                               const f16x8* __restrict__ Wpk,
-                                                               float* __restrict__ part, int M, int K, int N32,
-                                                               int kslice, float unscale, int S) {
-  constexpr int NW = 4, MB = 4, BM = 128, NPL = 2;
-  constexpr int CH = BK / 8;
-  constexpr int PLANE = BM * BK;
-  constexpr int STAGE = NPL * PLANE;
-  constexpr int RPI = 1024 / (BK * 2);
-  constexpr int NI = NPL * BM / RPI;
-  constexpr int NIW = (NI + NW - 1) / NW;
-  __shared__ _Float16 lds[2 * STAGE];
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, col = lane & 31;
-  const int wm = wv & 1, wn = wv >> 1;
-  const FcTile tl = fc_tile((M + BM - 1) / BM, (N32 + NW - 1) / NW);
-  if (tl.split >= S) return;
-  const int mt = tl.mt, ntile = tl.nt, split = tl.split;
-  const int K16 = (K + 15) / 16;
-  const int Npad = N32 * 32;
-  const int nbw = ntile * NW + 2 * wn;   // this wave's first column block
-  const bool on0 = nbw < N32, on1 = nbw + 1 < N32;   // wave-uniform
-  const int nbc0 = min(nbw, N32 - 1), nbc1 = min(nbw + 1, N32 - 1);
-  const int kbeg = split * kslice;
-  const int kend = min(K, kbeg + kslice);
-  (void)MB;
-
-  const _Float16* src[NIW];
-  int dst[NIW];
-#pragma unroll
-  for (int j = 0; j < NIW; ++j) {
-    const int i = min(wv + NW * j, NI - 1);
-    const int pl = i / (BM / RPI), r0 = (i % (BM / RPI)) * RPI;
-    const int row = r0 + lane / CH, c = (lane % CH) ^ fcp_swz<BK>(row);
-    const int gm = min(mt * BM + row, M - 1);
-    src[j] = (pl ? Al : Ah) + (size_t)gm * lda + 8 * c;
-    dst[j] = pl * PLANE + r0 * BK;
-  }
-  auto issue = [&](int k0, int stg) {
-#pragma unroll
-    for (int j = 0; j < NIW; ++j)
-      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src[j] + k0),
-                                       (__attribute__((address_space(3))) void*)(lds + stg * STAGE + dst[j]), 16, 0, 0);
-  };
-  auto load_w = [&](int k0, f16x8 (&w)[BK / 16][2][2]) {
-#pragma unroll
-    for (int g = 0; g < BK / 16; ++g) {
-      const int kb = min((k0 >> 4) + g, K16 - 1);
-      const f16x8* w0 = Wpk + (((size_t)kb * N32 + nbc0) * 2) * 64 + lane;
-      const f16x8* w1 = Wpk + (((size_t)kb * N32 + nbc1) * 2) * 64 + lane;
-      w[g][0][0] = w0[0];
-      w[g][0][1] = w0[64];
-      w[g][1][0] = w1[0];
-      w[g][1][1] = w1[64];
-    }
-  };
-
-  f32x16 acc[2][2];   // [m-block of the wave][column block]
-#pragma unroll
-  for (int a = 0; a < 2; ++a)
-#pragma unroll
-    for (int c = 0; c < 2; ++c) acc[a][c] = f32x16{};
-  f16x8 wn_[BK / 16][2][2];
-  if (kbeg < kend) {
-    issue(kbeg, 0);
-    load_w(kbeg, wn_);
-  }
-  int stg = 0;
-  for (int k0 = kbeg; k0 < kend; k0 += BK, stg ^= 1) {
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    lds_barrier();
-    f16x8 wc[BK / 16][2][2];
-#pragma unroll
-    for (int g = 0; g < BK / 16; ++g)
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        wc[g][c][0] = wn_[g][c][0];
-        wc[g][c][1] = wn_[g][c][1];
-      }
-    if (k0 + BK < kend) {
-      issue(k0 + BK, stg ^ 1);
-      load_w(k0 + BK, wn_);
-    }
-    if (on0) {
-      const _Float16* tile = lds + stg * STAGE;
-#pragma unroll
-      for (int g = 0; g < BK / 16; ++g) {
-#pragma unroll
-        for (int a = 0; a < 2; ++a) {
-          const int row = (2 * wm + a) * 32 + col;
-          const int o = row * BK + 8 * ((2 * g + h) ^ fcp_swz<BK>(row));
-          const f16x8 ah = *reinterpret_cast<const f16x8*>(tile + o);
-          const f16x8 al = *reinterpret_cast<const f16x8*>(tile + PLANE + o);
-#pragma unroll
-          for (int c = 0; c < 2; ++c) {
-            acc[a][c] = mfma16(wc[g][c][1], ah, acc[a][c]);
-            acc[a][c] = mfma16(wc[g][c][0], al, acc[a][c]);
-            acc[a][c] = mfma16(wc[g][c][0], ah, acc[a][c]);
-          }
-        }
-      }
-    }
-  }
-  if (!on0) return;
-#pragma unroll
-  for (int a = 0; a < 2; ++a) {
-    const int gm = mt * BM + (2 * wm + a) * 32 + col;
-    if (gm >= M) continue;
-#pragma unroll
-    for (int c = 0; c < 2; ++c) {
-      if (c == 1 && !on1) break;
-      float* dstp = part + ((size_t)split * M + gm) * Npad + 32 * (nbw + c) + 4 * h;
-#pragma unroll
-      for (int q = 0; q < 4; ++q)
-        *reinterpret_cast<f32x4*>(dstp + 8 * q) =
-            f32x4{acc[a][c][4 * q], acc[a][c][4 * q + 1], acc[a][c][4 * q + 2], acc[a][c][4 * q + 3]} * unscale;
-    }
-  }
-}
-
 hipError_t launch_fc_gemm_x3p(const void* Ah, const void* Al, int lda, const void* Wpk, float unscale, float* part,
                               int M, int K, int N, int S, int kslice, hipStream_t st, int nprod) {
   const int BK = nprod == 1 ? 64 : FC_P_BK3;
@@ -578,15 +450,8 @@ hipError_t launch_fc_gemm_x3p(const void* Ah, const void* Al, int lda, const voi
     else if (mb == 2) MP_FCP(1, 2, 64, FC_P_MINB);
     else MP_FCP(1, 4, 64, FC_P_MINB);
   } else {
-    static const int wl22 = [] {
-      const char* e = std::getenv("MP_FC_WL22");
-      return e ? std::atoi(e) : 0;
-    }();
     if (mb == 1) MP_FCP3(1);
     else if (mb == 2) MP_FCP3(2);
-    else if (wl22)
-      hipLaunchKernelGGL((fc_gemm_x3p22_kernel<FC_P_BK3, FC_P_MINB3>), dim3(fc_grid((M + 127) / 128, (N32 + 3) / 4, S)),
-                         dim3(256), 0, st, h, l, lda, w, part, M, K, N32, kslice, unscale, S);
     else MP_FCP3(4);
   }
 #undef MP_FCP
