@@ -40,37 +40,96 @@ float pairwise_sum_f32(const float* a, int64_t n) {
 }
 
 // numpy sum of the thresholded frame: float32 pairwise for a float32 frame, exact for uint16
-double frame_sum(const std::vector<float>& dc) { return (double)pairwise_sum_f32(dc.data(), (int64_t)dc.size()); }
-double frame_sum(const std::vector<uint16_t>& dc) {
+double frame_sum(const float* dc, int64_t n) { return (double)pairwise_sum_f32(dc, n); }
+double frame_sum(const uint16_t* dc, int64_t n) {
   uint64_t s = 0;
-  for (uint16_t v : dc) s += v;
+  for (int64_t i = 0; i < n; ++i) s += dc[i];
   return (double)s;
 }
 
+// numpy's calculateCoM (monkeydetector.py:66-84) in one pass: the thresholded frame dc goes to a
+// per-thread buffer reused across calls (no 0.9 MB allocation and page faults per frame), and the
+// mask sums are integer per row (the original's double sums of integers are exact, so this is
+// bit-identical), a branch-free loop the compiler vectorises.  frame_sum keeps numpy's pairwise
+// float32 order.
+// float thresholds equivalent to the double comparisons for every float v: v < lo <=> v < lo_f
+// (the smallest float >= lo), v > hi <=> v > hi_f (the largest float <= hi); NaN compares false
+// either way.  With them the row loop runs in float SIMD lanes.
+inline float float_at_least(double x) {
+  float f = (float)x;
+  if ((double)f < x) f = std::nextafter(f, INFINITY);
+  return f;
+}
+inline float float_at_most(double x) {
+  float f = (float)x;
+  if ((double)f > x) f = std::nextafter(f, -INFINITY);
+  return f;
+}
+template <typename T>
+struct Thresh {
+  double lo, hi;
+  explicit Thresh(const mp_camera& c) : lo(c.min_depth), hi(c.max_depth) {}
+  bool out(T v) const { return (double)v < lo || (double)v > hi; }
+};
+template <>
+struct Thresh<float> {
+  float lo, hi;
+  explicit Thresh(const mp_camera& c) : lo(float_at_least(c.min_depth)), hi(float_at_most(c.max_depth)) {}
+  bool out(float v) const { return v < lo || v > hi; }
+};
+
+// numpy's calculateCoM (monkeydetector.py:66-84) in one pass: the thresholded frame dc goes to a
+// per-thread buffer reused across calls (no 0.9 MB allocation and page faults per frame), and the
+// mask sums are integer per row (the original's double sums of integers are exact, so this is
+// bit-identical), a branch-free loop the compiler vectorises.  frame_sum keeps numpy's pairwise
+// float32 order.
 template <typename T>
 void center_of_mass(const mp_camera& cam, const T* dpt, int64_t h, int64_t w, double com[3]) {
-  std::vector<T> dc(dpt, dpt + h * w);
-  double sr = 0, sc = 0;   // integer sums, exact in double (center_of_mass of the mask)
-  int64_t num = 0, npos = 0;
-  for (int64_t y = 0; y < h; ++y)
-    for (int64_t x = 0; x < w; ++x) {
-      T& v = dc[y * w + x];
-      if ((double)v < cam.min_depth) v = 0;
-      if ((double)v > cam.max_depth) v = 0;
-      if (v > 0) {
-        sr += (double)y;
-        sc += (double)x;
-        ++npos;
+  thread_local std::vector<T> buf;
+  buf.resize((size_t)(h * w));
+  T* dc = buf.data();
+  const Thresh<T> th(cam);
+  const bool narrow = w < 46000;   // a row's sum of x fits int32
+  int64_t sr = 0, sc = 0, num = 0, npos = 0;
+  for (int64_t y = 0; y < h; ++y) {
+    const T* src = dpt + y * w;
+    T* d = dc + y * w;
+    int64_t rpos = 0, rx = 0, rnum = 0;
+    if (narrow) {
+      int32_t p32 = 0, x32 = 0, n32 = 0;
+      for (int32_t x = 0; x < (int32_t)w; ++x) {
+        const T v = th.out(src[x]) ? T(0) : src[x];   // dc[dc < min] = 0; dc[dc > max] = 0
+        d[x] = v;
+        const int32_t pos = v > T(0);
+        p32 += pos;
+        x32 += pos ? x : 0;
+        n32 += v != T(0);
       }
-      if (v != 0) ++num;
+      rpos = p32;
+      rx = x32;
+      rnum = n32;
+    } else {
+      for (int64_t x = 0; x < w; ++x) {
+        const T v = th.out(src[x]) ? T(0) : src[x];
+        d[x] = v;
+        const int64_t pos = v > T(0);
+        rpos += pos;
+        rx += pos ? x : 0;
+        rnum += v != T(0);
+      }
     }
+    sr += y * rpos;
+    sc += rx;
+    npos += rpos;
+    num += rnum;
+  }
   if (num == 0) {
     com[0] = com[1] = com[2] = 0.0;
     return;
   }
-  const double cc0 = sr / (double)npos, cc1 = sc / (double)npos;   // ndimage.center_of_mass(dc > 0)
-  const double s = frame_sum(dc);
-  com[0] = (cc1 * (double)num) / (double)num;                       // numpy.array(...) / num
+  const double cc0 = (double)sr / (double)npos, cc1 = (double)sc / (double)npos;   // ndimage.center_of_mass(dc > 0)
+  const double s = frame_sum(dc, h * w);
+  com[0] = (cc1 * (double)num) / (double)num;                                       // numpy.array(...) / num
   com[1] = (cc0 * (double)num) / (double)num;
   com[2] = s / (double)num;
 }
@@ -104,13 +163,17 @@ void crop_one(const mp_camera& cam, const T* dpt, int64_t h, int64_t w, const do
     return (float)v;
   };
   for (int64_t i = 0; i < dsz * dsz; ++i) out[i] = (float)cam.max_depth;
+  // the output columns inside the patch and their nearest-neighbour source columns, once per crop
+  const int64_t x0 = std::max<int64_t>(0, -g.offx), x1 = std::min<int64_t>(g.szw, dsz - g.offx);
+  thread_local std::vector<int64_t> colmap;
+  colmap.resize((size_t)std::max<int64_t>(0, x1 - x0));
+  for (int64_t x = x0; x < x1; ++x) colmap[x - x0] = mpgeom::nn_col(g, x);
   for (int64_t y = 0; y < g.szh; ++y) {
+    const int64_t oy = g.offy + y;
+    if (oy < 0 || oy >= dsz) continue;
     const int64_t sy = mpgeom::nn_row(g, y);
-    for (int64_t x = 0; x < g.szw; ++x) {
-      const int64_t sx = mpgeom::nn_col(g, x);
-      const int64_t oy = g.offy + y, ox = g.offx + x;
-      if (oy >= 0 && oy < dsz && ox >= 0 && ox < dsz) out[oy * dsz + ox] = crop_at(sy, sx);
-    }
+    float* orow = out + oy * dsz + g.offx;
+    for (int64_t x = x0; x < x1; ++x) orow[x] = crop_at(sy, colmap[x - x0]);
   }
   mpgeom::crop_matrix(g, M);
   std::memcpy(com_out, com, sizeof(com));
