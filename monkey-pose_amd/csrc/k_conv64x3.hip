@@ -217,15 +217,18 @@ static hipError_t launch_x3_t(ConvArgs a, const void* wpk, float unscale, int B,
 // the production variant per kernel size (chosen with tools/bench_conv.hip)
 constexpr int X3_NW = 8, X3_SCHED = 1;
 
-// Backbone convs of small batches: 8-row tiles with one 32-channel output block per block (8x the
-// blocks: a batch-1 conv is 32 blocks instead of 4), bit-identical to the 32-row tiles.  Taken
-// below 128 blocks of the default tiling (B < 32 at 64 x 64); MP_CONV_SMALL=0 keeps the default.
+// Backbone convs of small batches: 8-row tiles with one 32-channel output block per workgroup (8x
+// the workgroups: a batch-1 conv is 32 instead of 4), bit-identical to the 32-row tiles.  Measured
+// (one MI355X, tools/ab_th.sh, backbone ms with 32 / 16 / 8 rows): B = 8 0.118 / - / 0.059, B = 16
+// 0.125 / 0.088 / 0.068, B = 24 0.129 / 0.099 / 0.088, B = 32 0.133 / 0.108 / 0.105, B = 48
+// 0.145 / 0.160 / -.  Hence 8 rows up to 128 workgroups of the 32-row tiling (B <= 32 at 64 x 64),
+// else 32.  MP_CONV_SMALL=0 keeps 32.
 static bool conv_small_tiles(const ConvArgs& a, int B) {
   static const int on = [] {
     const char* e = std::getenv("MP_CONV_SMALL");
     return e ? std::atoi(e) : 1;
   }();
-  return on && a.H % 8 == 0 && (long)B * (a.W / TW) * (a.H / TH3) < 128;
+  return on && a.H % 8 == 0 && (long)B * (a.W / TW) * (a.H / TH3) <= 128;
 }
 
 hipError_t launch_conv64x3(int ks, int epi, ConvArgs a, const void* wpk, float unscale, int B, hipStream_t st,

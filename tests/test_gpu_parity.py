@@ -138,13 +138,13 @@ def test_batch_invariance_and_determinism(dtype):
 
 @pytest.mark.parametrize("dtype", ["fp32_fft", "bf16"])
 def test_backbone_small_batch_tiles_bit_identical(dtype):
-    """Backbone conv_2 / conv_3 below 128 default tiles (B < 32 at 64 x 64) run 8-row tiles with one
-    32-channel output block per workgroup (k_conv64x3.hip conv_small_tiles); a batch of 34 takes
-    the 32-row tiles.  The pool1 / conv2 / conv3 taps and the output of a crop alone equal its
-    slice of the batch bit for bit."""
+    """Backbone conv_2 / conv_3 of batches <= 32 (at 64 x 64) run 8-row tiles with one 32-channel
+    output block per workgroup (k_conv64x3.hip conv_small_tiles); a batch of 66 takes the 32-row
+    tiles.  The conv2 / conv3 taps and the outputs of single crops and of a 20-crop slice equal
+    their part of the batch bit for bit."""
     mp = pkg()
     W = mp.weights
-    n, crop = 34, 128
+    n, crop = 66, 128
     wts = W.synth_weights(W.hgru_pose_vars(crop=crop), seed=21)
     depth = W.synth_crops(n, seed=22, size=crop)
     O0 = W.synth_hidden((n, crop // 2, crop // 2, 64), seed=23)
@@ -153,11 +153,15 @@ def test_backbone_small_batch_tiles_bit_identical(dtype):
     m.load_weights(wts)
     full = m.build(_cuda(depth), 69, h2_init=_cuda(O0), keep_intermediates=True).cpu().numpy()
     taps = {k: getattr(m, k).cpu().numpy() for k in ("conv2", "conv3")}
-    for i in (0, 17, 33):
+    for i in (0, 33, 65):
         one = m.build(_cuda(depth[i:i + 1]), 69, h2_init=_cuda(O0[i:i + 1]), keep_intermediates=True)
         for k, v in taps.items():
             assert np.array_equal(getattr(m, k).cpu().numpy()[0], v[i]), (k, i)
         assert np.array_equal(one.cpu().numpy()[0], full[i]), i
+    part = m.build(_cuda(depth[40:60]), 69, h2_init=_cuda(O0[40:60]), keep_intermediates=True)
+    for k, v in taps.items():
+        assert np.array_equal(getattr(m, k).cpu().numpy(), v[40:60]), k
+    assert np.array_equal(part.cpu().numpy(), full[40:60])
 
 
 def test_rejects_training_and_bad_shapes():
