@@ -112,12 +112,16 @@ int mp_finalize_weights(mp_ctx* ctx, int compute_dtype);
 int mp_reserve(mp_ctx* ctx, int64_t max_batch);
 
 /* ContextualCircuit aux 'hidden_init' (hgru_module.py:875-892): the initial output state O0.
- * ('random' draws a fresh xavier tensor per sess.run, hgru_module.py:879-887: the caller draws it
- * and passes it as o0.)  The initial I is never read by the hgru_pose aux (795-804). */
+ * The initial I is never read by the hgru_pose aux (795-804). */
 enum {
-  MP_HIDDEN_GIVEN = 0,    /* o0 as passed (hidden_init='random', made explicit)            */
+  MP_HIDDEN_GIVEN = 0,    /* o0 as passed ('random' with the caller's draw, e.g. for parity)  */
   MP_HIDDEN_ZEROS = 1,    /* O0 = zeros_like(X)                      (888-890); o0 unused */
-  MP_HIDDEN_IDENTITY = 2  /* O0 = X, the circuit's drive             (876-878); o0 unused */
+  MP_HIDDEN_IDENTITY = 2, /* O0 = X, the circuit's drive             (876-878); o0 unused */
+  MP_HIDDEN_RANDOM = 3    /* 'random' (879-887): a fresh draw on the device per call, xavier-uniform
+                             with limit sqrt(6 / (k + k)); element i of the NHWC O0 is
+                             f32((2u - 1) * limit), u = splitmix64(i * 0x9E3779B97F4A7C15 + key) >> 11
+                             scaled by 2^-53, key = fnv1a64("h2_init") ^ (s * 0x2545F4914F6CDD1D),
+                             s = rng_seed + rng_call (monkey-pose_amd/weights.py synth_hidden(seed=s)) */
 };
 
 /* hgru_pose.model.build (hgru_pose.py:47-105), inference:
@@ -130,7 +134,7 @@ int mp_hgru_pose_fwd(mp_ctx* ctx, const float* depth, int64_t n, int64_t h, int6
 
 /* the reference model's readable intermediates (hgru_pose.py:50-103: m.conv1, m.pool1, m.conv2,
  * m.conv3, m.hgru, m.fc1, m.relu1); each a caller-owned device buffer, NULL = not wanted.
- * NHWC fp32 like the reference tensors; [n, 1024] for fc1 / relu1. */
+ * NHWC fp32 like the reference tensors; [n, 1024] for fc1 / relu1.  (The 0.1 layout; 0.2 keeps it.) */
 typedef struct {
   float* conv1;  /* [n, h, w, 64]      relu(conv_1)                       (50)      */
   float* pool1;  /* [n, h/2, w/2, 64]  BN(max_pool(conv1))                (51-60)   */
@@ -139,15 +143,30 @@ typedef struct {
   float* hgru;   /* [n, h/2, w/2, 64]  BN(O_T), the fc_1 input            (81-90)   */
   float* fc1;    /* [n, 1024]          fc_1 + bias (pre-activation)       (91)      */
   float* relu1;  /* [n, 1024]          BN(relu(fc1))                      (92-103)  */
+} mp_pose_taps;
+
+/* per-call options of mp_hgru_pose_fwd_ex / mp_hgru_circuit_fwd_opts (since 0.2).  struct_size =
+ * sizeof(mp_fwd_opts) as the caller was compiled: the library reads that many bytes and no more,
+ * and fields added by later versions keep their defaults for older callers.  Zero-initialise. */
+typedef struct {
+  uint64_t struct_size;
+  int32_t hidden_init;        /* MP_HIDDEN_*; o0 may be NULL unless MP_HIDDEN_GIVEN */
+  int32_t reserved;
+  uint64_t rng_seed;          /* MP_HIDDEN_RANDOM: the draw of seed rng_seed + rng_call */
+  uint64_t rng_call;          /*   (the caller's per-call counter: the reference re-draws per run) */
   /* store_states (hgru_module.py:889-915): every timestep's states, [n, T, h/2, w/2, 64] NHWC
    * (the reference's stack transposed to batch-major, 909-912).  states_O[:, t] = O_t after the
    * rho gain, states_I[:, t] = I_t.  (The reference's own stacks swap O and I on alternate steps:
    * full() takes (store_O, store_I) where the loop passes (store_I, store_O), hgru_module.py:825,
-   * 897-908; here each stack holds what its name says.) */
+   * 897-908; here each stack holds what its name says.)  NULL = not wanted. */
   float* states_O;
   float* states_I;
-  int32_t hidden_init; /* MP_HIDDEN_*: the initial state; o0 may be NULL unless MP_HIDDEN_GIVEN */
-} mp_pose_taps;
+  const mp_pose_taps* taps;   /* pose model only: the intermediates, or NULL */
+} mp_fwd_opts;
+
+/* mp_hgru_pose_fwd with options (opts may be NULL: the mp_hgru_pose_fwd defaults) */
+int mp_hgru_pose_fwd_ex(mp_ctx* ctx, const float* depth, int64_t n, int64_t h, int64_t w, const float* o0,
+                        float* out, const mp_fwd_opts* opts, void* stream);
 
 /* mp_hgru_pose_fwd that also writes the requested intermediates (taps may be NULL) */
 int mp_hgru_pose_fwd_taps(mp_ctx* ctx, const float* depth, int64_t n, int64_t h, int64_t w,
@@ -159,12 +178,16 @@ int mp_hgru_pose_fwd_taps(mp_ctx* ctx, const float* depth, int64_t n, int64_t h,
 int mp_hgru_circuit_fwd(mp_ctx* ctx, const float* x, const float* o0, int64_t n, int64_t h,
                         int64_t w, int64_t k, int timesteps, float* o_out, void* stream);
 
-/* mp_hgru_circuit_fwd with the aux 'hidden_init' (MP_HIDDEN_*; o0 may be NULL unless
- * MP_HIDDEN_GIVEN) and 'store_states' (hgru_module.py:889-915): states_O / states_I, each
- * [n, timesteps, h, w, k] NHWC or NULL, receive every step's O_t (after the rho gain) and I_t */
+/* mp_hgru_circuit_fwd with the aux 'hidden_init' (MP_HIDDEN_GIVEN / _ZEROS / _IDENTITY; o0 may be
+ * NULL unless MP_HIDDEN_GIVEN) and 'store_states' (hgru_module.py:889-915): states_O / states_I,
+ * each [n, timesteps, h, w, k] NHWC or NULL, receive every step's O_t (after the rho gain) and I_t */
 int mp_hgru_circuit_fwd_ex(mp_ctx* ctx, const float* x, const float* o0, int64_t n, int64_t h, int64_t w,
                            int64_t k, int timesteps, int hidden_init, float* o_out, float* states_O,
                            float* states_I, void* stream);
+
+/* mp_hgru_circuit_fwd with every option of mp_fwd_opts except taps (since 0.2) */
+int mp_hgru_circuit_fwd_opts(mp_ctx* ctx, const float* x, const float* o0, int64_t n, int64_t h, int64_t w,
+                             int64_t k, int timesteps, float* o_out, const mp_fwd_opts* opts, void* stream);
 
 /* dense_model_struct.build(depth, output_shape) -> .output  (train_dense_networks.py:223-408):
  *   depth [n, h, w, 1] (h, w multiples of 32 in the reference's 128x128), out [n, output_shape] */
@@ -218,6 +241,14 @@ int mp_center_of_mass(const mp_camera* cam, const void* depth, int depth_dtype, 
  *   info    optional {xstart, xend, ystart, yend, sz_w, sz_h, off_x, off_y} (integers of the crop) */
 int mp_crop3d(const mp_camera* cam, const void* depth, int depth_dtype, int64_t h, int64_t w, const double* com,
               int64_t dsize, float* out, double M[9], double com_out[3], int32_t info[8]);
+
+/* mp_crop3d with cropArea3D's other options (since 0.2):
+ *   flags  MP_CROP_DOCOM: docom=True, the second refinement (monkeydetector.py:287-300) -- the CoM of
+ *          the first crop (+ xstart / ystart), falling back to the crop's centre depth and then to
+ *          300 mm when that CoM is (0,0,0), and a second crop around it; com_out is the refined CoM */
+enum { MP_CROP_DOCOM = 1 };
+int mp_crop3d_ex(const mp_camera* cam, const void* depth, int depth_dtype, int64_t h, int64_t w, const double* com,
+                 int flags, int64_t dsize, float* out, double M[9], double com_out[3], int32_t info[8]);
 
 /* prepare_data_test (train_cnn_networks_hgru.py:61-74) for n frames [n][h][w]: patches
  * [n][dsize][dsize][1] = crop / max_depth (the model input), Ms [n][9], coms_out [n][3];

@@ -11,6 +11,8 @@ The directory name carries a hyphen, so import it with ``importlib.import_module
   as a layer graph (``_graph``) and run by the native graph runtime (``mp_graph_*``)
 * ``train_cnn_networks_hgru`` -- ``attn_model_struct`` (the attention CoM regressor),
   ``prepare_data_test`` (device batch crop) and ``FramePosePipeline`` (frame -> CoM -> crop -> pose)
+* ``monkeydetector`` -- ``MonkeyDetector`` / ``tfMonkeyDetector``: CoM, crop (native), joint transforms
+* ``pose_evaluation`` -- the host metrics (``getMeanError_np`` ...)
 * ``weights``     -- TF variable-name tables and deterministic synthetic initialisers
 * ``tf_checkpoint`` -- TF1 V2 checkpoint reader / writer (no TensorFlow needed)
 * ``data_loader`` -- TFRecord ingestion (``inputs`` / ``read_and_decode``, ``create_tf_record``)
@@ -25,6 +27,7 @@ from . import train_hier_networks  # noqa: F401
 from . import train_dense_hier_networks  # noqa: F401
 from . import train_cnn_networks_hgru  # noqa: F401
 from . import monkeydetector  # noqa: F401
+from . import pose_evaluation  # noqa: F401
 from . import parallel  # noqa: F401
 from . import tf_checkpoint  # noqa: F401
 from . import data_loader  # noqa: F401

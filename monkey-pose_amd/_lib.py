@@ -79,6 +79,13 @@ _SIGS = {
                                               ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
                                               ctypes.c_int64, ctypes.c_int, ctypes.c_int, ctypes.c_void_p,
                                               ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "mp_hgru_pose_fwd_ex": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64,
+                                           ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
+                                           ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "mp_hgru_circuit_fwd_opts": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
+                                                ctypes.c_int64, ctypes.c_int64, ctypes.c_int64,
+                                                ctypes.c_int64, ctypes.c_int, ctypes.c_void_p,
+                                                ctypes.c_void_p, ctypes.c_void_p]),
     "mp_dense_fwd": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
                                     ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p]),
     "mp_hier_fwd": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
@@ -116,12 +123,34 @@ _lib: Optional[ctypes.CDLL] = None
 TAP_NAMES = ("conv1", "pool1", "conv2", "conv3", "hgru", "fc1", "relu1")
 STATE_NAMES = ("states_O", "states_I")      # store_states stacks [n, T, h/2, w/2, 64]
 
-# ContextualCircuit aux 'hidden_init' (hgru_module.py:875-892) -> MP_HIDDEN_*
+# ContextualCircuit aux 'hidden_init' (hgru_module.py:875-892) -> MP_HIDDEN_*: 'random' with an
+# explicit draw is MP_HIDDEN_GIVEN; without one the library draws it on the device (MP_HIDDEN_RANDOM)
 MP_HIDDEN = {"random": 0, "zeros": 1, "identity": 2}
+MP_HIDDEN_GIVEN, MP_HIDDEN_RANDOM = 0, 3
+MP_ABI_VERSION = (0, 2)
 
 
 class PoseTaps(ctypes.Structure):
-    _fields_ = [(n, ctypes.c_void_p) for n in TAP_NAMES + STATE_NAMES] + [("hidden_init", ctypes.c_int32)]
+    _fields_ = [(n, ctypes.c_void_p) for n in TAP_NAMES]
+
+
+class FwdOpts(ctypes.Structure):
+    """``mp_fwd_opts`` (include/monkeypose.h, since 0.2)."""
+    _fields_ = [("struct_size", ctypes.c_uint64), ("hidden_init", ctypes.c_int32), ("reserved", ctypes.c_int32),
+                ("rng_seed", ctypes.c_uint64), ("rng_call", ctypes.c_uint64), ("states_O", ctypes.c_void_p),
+                ("states_I", ctypes.c_void_p), ("taps", ctypes.c_void_p)]
+
+
+def fwd_opts(hidden_init: int = 0, rng_seed: int = 0, rng_call: int = 0, states_O=None, states_I=None,
+             taps: Optional[PoseTaps] = None) -> FwdOpts:
+    o = FwdOpts()
+    o.struct_size = ctypes.sizeof(FwdOpts)
+    o.hidden_init = int(hidden_init)
+    o.rng_seed = int(rng_seed) & 0xFFFFFFFFFFFFFFFF
+    o.rng_call = int(rng_call) & 0xFFFFFFFFFFFFFFFF
+    o.states_O, o.states_I = _ptr(states_O), _ptr(states_I)
+    o.taps = None if taps is None else ctypes.addressof(taps)
+    return o
 
 
 class MonkeyPoseError(RuntimeError):
@@ -145,6 +174,10 @@ def load() -> ctypes.CDLL:
             fn = getattr(lib, name)
             fn.restype = res
             fn.argtypes = args
+        v = lib.mp_version()
+        if (v >> 16, v & 0xFFFF) < MP_ABI_VERSION:
+            raise RuntimeError(f"{LIB_PATH} is ABI {v >> 16}.{v & 0xFFFF}, this package needs "
+                               f"{MP_ABI_VERSION[0]}.{MP_ABI_VERSION[1]}: rebuild it")
         _lib = lib
     return _lib
 
@@ -217,21 +250,25 @@ class Context:
         check(self.lib.mp_hgru_pose_fwd(self.h, _ptr(depth), n, h, w, _ptr(o0), _ptr(out),
                                         ctypes.c_void_p(stream)))
 
-    def pose_fwd_taps(self, depth, o0, out, taps: dict, stream: int, hidden_init: int = 0) -> None:
-        """mp_hgru_pose_fwd_taps; ``taps`` maps names of TAP_NAMES / STATE_NAMES to CUDA output
-        tensors; ``o0`` may be None unless ``hidden_init`` is MP_HIDDEN['random']."""
+    def pose_fwd_taps(self, depth, o0, out, taps: dict, stream: int, hidden_init: int = 0, rng_seed: int = 0,
+                      rng_call: int = 0) -> None:
+        """mp_hgru_pose_fwd_ex; ``taps`` maps names of TAP_NAMES / STATE_NAMES to CUDA output
+        tensors; ``o0`` may be None unless ``hidden_init`` is MP_HIDDEN_GIVEN; MP_HIDDEN_RANDOM
+        draws O0 on the device from (rng_seed + rng_call)."""
         n, h, w, c = depth.shape
-        t = PoseTaps(*[ctypes.c_void_p(_ptr(taps[k]) if k in taps else None) for k in TAP_NAMES + STATE_NAMES],
-                     int(hidden_init))
-        check(self.lib.mp_hgru_pose_fwd_taps(self.h, _ptr(depth), n, h, w, _ptr(o0), _ptr(out),
-                                             ctypes.byref(t), ctypes.c_void_p(stream)))
+        t = None
+        if any(k in taps for k in TAP_NAMES):
+            t = PoseTaps(*[ctypes.c_void_p(_ptr(taps[k]) if k in taps else None) for k in TAP_NAMES])
+        o = fwd_opts(hidden_init, rng_seed, rng_call, taps.get("states_O"), taps.get("states_I"), t)
+        check(self.lib.mp_hgru_pose_fwd_ex(self.h, _ptr(depth), n, h, w, _ptr(o0), _ptr(out), ctypes.byref(o),
+                                           ctypes.c_void_p(stream)))
 
     def circuit_fwd(self, x, o0, out, timesteps: int, stream: int, hidden_init: int = 0, states_O=None,
-                    states_I=None) -> None:
+                    states_I=None, rng_seed: int = 0, rng_call: int = 0) -> None:
         n, h, w, k = x.shape
-        check(self.lib.mp_hgru_circuit_fwd_ex(self.h, _ptr(x), _ptr(o0), n, h, w, k, int(timesteps),
-                                              int(hidden_init), _ptr(out), _ptr(states_O), _ptr(states_I),
-                                              ctypes.c_void_p(stream)))
+        o = fwd_opts(hidden_init, rng_seed, rng_call, states_O, states_I)
+        check(self.lib.mp_hgru_circuit_fwd_opts(self.h, _ptr(x), _ptr(o0), n, h, w, k, int(timesteps), _ptr(out),
+                                                ctypes.byref(o), ctypes.c_void_p(stream)))
 
     def dense_fwd(self, depth, out, stream: int) -> None:
         n, h, w, c = depth.shape

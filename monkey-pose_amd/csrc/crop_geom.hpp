@@ -89,6 +89,23 @@ __host__ __device__ inline int crop_geometry(const mp_camera& cam, const double 
   return CROP_OK;
 }
 
+// The reference ran on Python 2.7, i.e. NumPy <= 1.16, whose value-based casting compares a float32
+// array with a float64 scalar (getCrop's `cropped < zstart` / `cropped > zend`,
+// monkeydetector.py:209-210; calculateCoM's `dc < self.minDepth` / `dc > self.maxDepth`, 74-75)
+// IN FLOAT32, against f32(scalar), whenever min_scalar_type(scalar) is at most float32, i.e.
+// -3.4e38 < scalar < 3.4e38 (numpy/core/src/multiarray/convert_datatype.c, min_scalar_type_num);
+// otherwise (NaN, inf, beyond that range) in float64.  A uint16 frame against a float scalar
+// promotes to float64 (the scalar's kind is higher), so those comparisons stay in double.
+// (NumPy 2's NEP 50 would compare in float64: a pixel equal to f32(zend) with zend < f32(zend) is
+// kept by the reference and would be zeroed.)
+__host__ __device__ inline bool legacy_in_f32(double s) { return s > -3.4e38 && s < 3.4e38; }
+__host__ __device__ inline bool f32_lt(float v, double s) {
+  return legacy_in_f32(s) ? v < (float)s : (double)v < s;
+}
+__host__ __device__ inline bool f32_gt(float v, double s) {
+  return legacy_in_f32(s) ? v > (float)s : (double)v > s;
+}
+
 // nearest-neighbour source row / column of resized pixel y / x
 __host__ __device__ inline int64_t nn_row(const CropGeom& g, int64_t y) {
   return gmin((int64_t)floor((double)y * g.ify), g.rows - 1);

@@ -118,7 +118,15 @@ __device__ __forceinline__ uint32_t pack_bf2(float a, float b) {
 #if FFT_PACKED
 typedef float cpx __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ cpx cfma(cpx a, cpx b, cpx c) { return __builtin_elementwise_fma(a, b, c); }
+#if FFT_PACKED == 2   // probe: the half swap as two plain moves the compiler cannot fold into op_sel
+__device__ __forceinline__ cpx swp(cpx a) {
+  float x, y;
+  asm("v_mov_b32 %0, %2\n\tv_mov_b32 %1, %3" : "=&v"(x), "=&v"(y) : "v"(a.y), "v"(a.x));
+  return cpx{x, y};
+}
+#else
 __device__ __forceinline__ cpx swp(cpx a) { return a.yx; }
+#endif
 #else
 struct cpx {
   float x, y;

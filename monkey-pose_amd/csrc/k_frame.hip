@@ -101,9 +101,10 @@ __global__ __launch_bounds__(256) void crop3d_kernel(mp_camera cam, const float*
         v = 0.f;
         if (sy >= 0 && sy < g.r1 - g.r0 && sx >= 0 && sx < g.c1 - g.c0) {
           const float d = fr[(g.r0 + sy) * W + (g.c0 + sx)] * frame_scale;   // image * max_depth (float32)
-          if ((double)d < g.zstart && d != 0.f)
+          // float32 frame vs float64 bounds: compared in float32 (NumPy 1.x rule, crop_geom.hpp)
+          if (mpgeom::f32_lt(d, g.zstart) && d != 0.f)
             v = (float)g.zstart;
-          else if ((double)d > g.zend && d != 0.f)
+          else if (mpgeom::f32_gt(d, g.zend) && d != 0.f)
             v = 0.f;
           else
             v = d;
@@ -120,6 +121,52 @@ hipError_t launch_crop3d(const mp_camera& cam, const float* frames, int N, int H
   const int nb = (dsz * dsz + CROP_PIX_PER_BLOCK - 1) / CROP_PIX_PER_BLOCK;
   hipLaunchKernelGGL(crop3d_kernel, dim3(nb, N), dim3(256), 0, st, cam, frames, H, W, frame_scale, com_norm,
                      com_scale[0], com_scale[1], com_scale[2], dsz, patches, Ms, coms_out, status);
+  return hipGetLastError();
+}
+
+// hidden_init 'random' (hgru_module.py:879-887) drawn on the device: element i of O0 is
+// f32((2u - 1) * limit), u = (splitmix64(i * golden + key) >> 11) * 2^-53 -- the counter-based
+// generator of monkey-pose_amd/weights.py (uniform01 / sym_uniform), so a draw is reproducible on the
+// host bit for bit.  Double arithmetic with contraction off, as numpy evaluates it.
+__device__ __forceinline__ uint64_t splitmix_mix(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+
+__global__ __launch_bounds__(256) void hidden_uniform_kernel(float* __restrict__ out, int64_t n, uint64_t key,
+                                                             double limit) {
+#pragma clang fp contract(off)
+  const int64_t i0 = ((int64_t)blockIdx.x * 256 + threadIdx.x) * 4;
+  if (i0 >= n) return;
+  float v[4];
+#pragma unroll
+  for (int k = 0; k < 4; ++k) {
+    const uint64_t z = splitmix_mix((uint64_t)(i0 + k) * 0x9E3779B97F4A7C15ull + key);
+    const double u = (double)(z >> 11) * (1.0 / 9007199254740992.0);
+    v[k] = (float)((2.0 * u - 1.0) * limit);
+  }
+  if (i0 + 4 <= n) {
+    *reinterpret_cast<float4*>(out + i0) = make_float4(v[0], v[1], v[2], v[3]);
+  } else {
+    for (int k = 0; i0 + k < n; ++k) out[i0 + k] = v[k];
+  }
+}
+
+static uint64_t fnv1a64(const char* s) {
+  uint64_t h = 0xCBF29CE484222325ull;
+  for (; *s; ++s) {
+    h ^= (uint8_t)*s;
+    h *= 0x100000001B3ull;
+  }
+  return h;
+}
+
+hipError_t launch_hidden_uniform(float* out, int64_t n, uint64_t seed, double limit, hipStream_t st) {
+  if (n <= 0) return hipSuccess;
+  const uint64_t key = fnv1a64("h2_init") ^ (seed * 0x2545F4914F6CDD1Dull);
+  const int64_t nb = (n + 1023) / 1024;
+  hipLaunchKernelGGL(hidden_uniform_kernel, dim3((unsigned)nb), dim3(256), 0, st, out, n, key, limit);
   return hipGetLastError();
 }
 

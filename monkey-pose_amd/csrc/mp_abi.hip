@@ -12,7 +12,9 @@
 //   fc_gemm + fc_reduce      fc_out                                   (104-105)
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <cmath>
+#include <cstddef>
 #include <cstdlib>
 #include <cstring>
 #include <functional>
@@ -473,9 +475,15 @@ void run_circuit(mp_ctx* c, int64_t n, int H, int W, int T, const float* o0_nhwc
 // MP_HIDDEN_GIVEN -> the caller's o0; ZEROS -> a zeroed workspace map; IDENTITY -> X (the
 // caller's NHWC x for the circuit, the C8 drive converted into a workspace map for the pose model)
 const float* hidden_state(mp_ctx* c, int hidden_init, const float* o0, const float* x_nhwc, int64_t n, int H, int W,
-                          hipStream_t st) {
+                          hipStream_t st, uint64_t rng_seed = 0) {
   const size_t bytes = (size_t)n * H * W * 64 * sizeof(float);
   switch (hidden_init) {
+    case MP_HIDDEN_RANDOM:
+      // a fresh xavier-uniform draw on the device (hgru_module.py:884-887), limit sqrt(6 / (k + k))
+      c->h0.alloc(bytes);
+      hip_check(launch_hidden_uniform(c->h0.f(), (int64_t)n * H * W * 64, rng_seed, std::sqrt(6.0 / (2 * 64)), st),
+                "hidden_init random");
+      return c->h0.f();
     case MP_HIDDEN_GIVEN:
       if (!o0) fail(MP_ERR_ARG, "o0 is NULL (hidden_init = MP_HIDDEN_GIVEN)");
       return o0;
@@ -489,7 +497,7 @@ const float* hidden_state(mp_ctx* c, int hidden_init, const float* o0, const flo
       hip_check(launch_c8_to_nhwc(c->X.f(), c->h0.f(), (int)n, H, W, st, bf16_maps(c)), "hidden_init identity");
       return c->h0.f();
     default:
-      fail(MP_ERR_ARG, "hidden_init must be MP_HIDDEN_GIVEN, MP_HIDDEN_ZEROS or MP_HIDDEN_IDENTITY");
+      fail(MP_ERR_ARG, "hidden_init must be MP_HIDDEN_GIVEN, _ZEROS, _IDENTITY or _RANDOM");
   }
   return nullptr;
 }
@@ -501,7 +509,10 @@ const float* hidden_state(mp_ctx* c, int hidden_init, const float* o0, const flo
 
 extern "C" {
 
-int mp_version(void) { return (0 << 16) | 1; }
+// 0.2: mp_pose_taps back to its 0.1 layout (the 0.1 header's seven pointers); the per-step states,
+// hidden_init and the device O0 draw moved to the size-checked mp_fwd_opts (mp_hgru_pose_fwd_ex,
+// mp_hgru_circuit_fwd_opts); mp_crop3d_ex (docom)
+int mp_version(void) { return (0 << 16) | 2; }
 
 const char* mp_last_error(void) { return g_err.c_str(); }
 
@@ -660,12 +671,44 @@ int mp_reserve(mp_ctx* ctx, int64_t max_batch) {
   });
 }
 
-int mp_hgru_pose_fwd_taps(mp_ctx* ctx, const float* depth, int64_t n, int64_t h, int64_t w, const float* o0,
-                          float* out, const mp_pose_taps* taps, void* stream) {
+}  // extern "C"
+
+namespace {
+
+// the per-call options of a forward, from mp_fwd_opts (or their 0.1 defaults)
+struct FwdOpts {
+  mp_pose_taps tp{};
+  float* states_O = nullptr;
+  float* states_I = nullptr;
+  int hidden_init = MP_HIDDEN_GIVEN;
+  uint64_t rng_seed = 0;
+};
+
+// mp_fwd_opts as the caller compiled it: only struct_size bytes are read (fields the caller does not
+// know keep their defaults), so a smaller, older struct never makes the library read past it
+FwdOpts read_opts(const mp_fwd_opts* o, bool pose) {
+  FwdOpts f;
+  if (!o) return f;
+  if (o->struct_size < offsetof(mp_fwd_opts, rng_call) + sizeof(uint64_t))
+    fail(MP_ERR_ARG, "mp_fwd_opts.struct_size is smaller than the 0.2 layout");
+  mp_fwd_opts c{};
+  std::memcpy(&c, o, std::min<size_t>((size_t)o->struct_size, sizeof(c)));
+  f.hidden_init = c.hidden_init;
+  f.rng_seed = c.rng_seed + c.rng_call;
+  f.states_O = c.states_O;
+  f.states_I = c.states_I;
+  if (c.taps) {
+    if (!pose) fail(MP_ERR_ARG, "mp_fwd_opts.taps is for the pose model only");
+    f.tp = *c.taps;
+  }
+  return f;
+}
+
+int pose_fwd(mp_ctx* ctx, const float* depth, int64_t n, int64_t h, int64_t w, const float* o0, float* out,
+             const FwdOpts& fo, void* stream) {
   return guard([&] {
-    mp_pose_taps tp{};
-    if (taps) tp = *taps;
-    if (!ctx || !depth || !out || (!o0 && tp.hidden_init == MP_HIDDEN_GIVEN))
+    const mp_pose_taps& tp = fo.tp;
+    if (!ctx || !depth || !out || (!o0 && fo.hidden_init == MP_HIDDEN_GIVEN))
       fail(MP_ERR_ARG, "mp_hgru_pose_fwd: null pointer");
     if (ctx->model != MP_MODEL_HGRU_POSE) fail(MP_ERR_STATE, "context is not an hgru_pose model");
     if (!ctx->finalized) fail(MP_ERR_STATE, "weights not finalized");
@@ -738,10 +781,10 @@ int mp_hgru_pose_fwd_taps(mp_ctx* ctx, const float* depth, int64_t n, int64_t h,
     if (tp.pool1) hip_check(launch_c8_to_nhwc(ctx->bufA.f(), tp.pool1, N, H, W, st), "pool1 tap");
     if (tp.conv2) hip_check(launch_c8_to_nhwc(ctx->bufB.f(), tp.conv2, N, H, W, st), "conv2 tap");
     if (tp.conv3) hip_check(launch_c8_to_nhwc(ctx->X.f(), tp.conv3, N, H, W, st, bf16_maps(ctx)), "conv3 tap");
-    const float* h0 = hidden_state(ctx, tp.hidden_init, o0, nullptr, n, H, W, st);
+    const float* h0 = hidden_state(ctx, fo.hidden_init, o0, nullptr, n, H, W, st, fo.rng_seed);
     StateOut so;
-    so.O = tp.states_O;
-    so.I = tp.states_I;
+    so.O = fo.states_O;
+    so.I = fo.states_I;
     so.T = ctx->timesteps;
     // FFT dtypes: the last B epilogue writes fc_1's f16 hi / lo activation planes into fcin (same
     // bytes as the fp32 map), so fc_1 stages them by LDS-DMA with no conversion (bit-identical); the
@@ -797,6 +840,25 @@ int mp_hgru_pose_fwd_taps(mp_ctx* ctx, const float* depth, int64_t n, int64_t h,
   });
 }
 
+}  // namespace
+
+extern "C" {
+
+int mp_hgru_pose_fwd_taps(mp_ctx* ctx, const float* depth, int64_t n, int64_t h, int64_t w, const float* o0,
+                          float* out, const mp_pose_taps* taps, void* stream) {
+  FwdOpts fo;
+  if (taps) fo.tp = *taps;   // the seven pointers of the 0.1 struct, nothing past them
+  return pose_fwd(ctx, depth, n, h, w, o0, out, fo, stream);
+}
+
+int mp_hgru_pose_fwd_ex(mp_ctx* ctx, const float* depth, int64_t n, int64_t h, int64_t w, const float* o0,
+                        float* out, const mp_fwd_opts* opts, void* stream) {
+  FwdOpts fo;
+  const int rc = guard([&] { fo = read_opts(opts, true); });
+  if (rc != MP_OK) return rc;
+  return pose_fwd(ctx, depth, n, h, w, o0, out, fo, stream);
+}
+
 int mp_hgru_pose_fwd(mp_ctx* ctx, const float* depth, int64_t n, int64_t h, int64_t w, const float* o0,
                      float* out, void* stream) {
   return mp_hgru_pose_fwd_taps(ctx, depth, n, h, w, o0, out, nullptr, stream);
@@ -811,7 +873,21 @@ int mp_hgru_circuit_fwd(mp_ctx* ctx, const float* x, const float* o0, int64_t n,
 int mp_hgru_circuit_fwd_ex(mp_ctx* ctx, const float* x, const float* o0, int64_t n, int64_t h, int64_t w,
                            int64_t k, int timesteps, int hidden_init, float* o_out, float* states_O,
                            float* states_I, void* stream) {
+  mp_fwd_opts o{};
+  o.struct_size = sizeof(o);
+  o.hidden_init = hidden_init;
+  o.states_O = states_O;
+  o.states_I = states_I;
+  return mp_hgru_circuit_fwd_opts(ctx, x, o0, n, h, w, k, timesteps, o_out, &o, stream);
+}
+
+int mp_hgru_circuit_fwd_opts(mp_ctx* ctx, const float* x, const float* o0, int64_t n, int64_t h, int64_t w,
+                             int64_t k, int timesteps, float* o_out, const mp_fwd_opts* opts, void* stream) {
   return guard([&] {
+    const FwdOpts fo = read_opts(opts, false);
+    const int hidden_init = fo.hidden_init;
+    float* states_O = fo.states_O;
+    float* states_I = fo.states_I;
     if (!ctx || !x || !o_out || (!o0 && hidden_init == MP_HIDDEN_GIVEN))
       fail(MP_ERR_ARG, "mp_hgru_circuit_fwd: null pointer");
     if (!ctx->finalized) fail(MP_ERR_STATE, "weights not finalized");
@@ -828,7 +904,7 @@ int mp_hgru_circuit_fwd_ex(mp_ctx* ctx, const float* x, const float* o0, int64_t
       // the pose context's output affine is BN_3: use identity by running with a temporary copy
       fail(MP_ERR_UNSUPPORTED, "use an MP_MODEL_HGRU_CIRCUIT context for the standalone circuit");
     }
-    const float* h0 = hidden_state(ctx, hidden_init, o0, x, n, (int)h, (int)w, st);
+    const float* h0 = hidden_state(ctx, hidden_init, o0, x, n, (int)h, (int)w, st, fo.rng_seed);
     StateOut so;
     so.O = states_O;
     so.I = states_I;

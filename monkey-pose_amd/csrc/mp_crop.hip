@@ -47,14 +47,12 @@ double frame_sum(const uint16_t* dc, int64_t n) {
   return (double)s;
 }
 
-// numpy's calculateCoM (monkeydetector.py:66-84) in one pass: the thresholded frame dc goes to a
-// per-thread buffer reused across calls (no 0.9 MB allocation and page faults per frame), and the
-// mask sums are integer per row (the original's double sums of integers are exact, so this is
-// bit-identical), a branch-free loop the compiler vectorises.  frame_sum keeps numpy's pairwise
-// float32 order.
-// float thresholds equivalent to the double comparisons for every float v: v < lo <=> v < lo_f
-// (the smallest float >= lo), v > hi <=> v > hi_f (the largest float <= hi); NaN compares false
-// either way.  With them the row loop runs in float SIMD lanes.
+// calculateCoM's `dc[dc < self.minDepth] = 0; dc[dc > self.maxDepth] = 0` (74-75).  A uint16 frame
+// compares in double (NumPy 1.x promotes it with the float scalar to float64); a float32 frame
+// compares in float32 against f32(threshold) (NumPy 1.x value-based casting, crop_geom.hpp), or,
+// for a threshold beyond min_scalar_type's float32 range, in double -- expressed as the float
+// bound equivalent to the double comparison (v < lo <=> v < the smallest float >= lo), so the
+// row loop runs in float SIMD lanes either way.
 inline float float_at_least(double x) {
   float f = (float)x;
   if ((double)f < x) f = std::nextafter(f, INFINITY);
@@ -74,7 +72,9 @@ struct Thresh {
 template <>
 struct Thresh<float> {
   float lo, hi;
-  explicit Thresh(const mp_camera& c) : lo(float_at_least(c.min_depth)), hi(float_at_most(c.max_depth)) {}
+  explicit Thresh(const mp_camera& c)
+      : lo(mpgeom::legacy_in_f32(c.min_depth) ? (float)c.min_depth : float_at_least(c.min_depth)),
+        hi(mpgeom::legacy_in_f32(c.max_depth) ? (float)c.max_depth : float_at_most(c.max_depth)) {}
   bool out(float v) const { return v < lo || v > hi; }
 };
 
@@ -138,13 +138,49 @@ struct CropInfo {
   int32_t xstart, xend, ystart, yend, szw, szh, offx, offy;
 };
 
-// getCrop's "cropped[msk1] = zstart" stores zstart in the frame's dtype (float32 rounds, uint16
-// truncates); the crop itself is float32 (ret = ones(dsize, float32) * maxDepth; ret[...] = rz)
-inline float store_as(float, double z) { return (float)z; }
-inline float store_as(uint16_t, double z) { return (float)(uint16_t)(int64_t)z; }
+// getCrop's thresholding (monkeydetector.py:208-212) of one frame pixel, in the frame's dtype:
+// "cropped[msk1] = zstart" stores zstart as float32 (rounded) or uint16 (truncated); the
+// comparisons run in float32 for a float32 frame (NumPy 1.x value-based casting, crop_geom.hpp)
+// and in float64 for a uint16 frame
+inline float crop_px(float v, const mpgeom::CropGeom& g) {
+  if (mpgeom::f32_lt(v, g.zstart) && v != 0.f) return (float)g.zstart;
+  if (mpgeom::f32_gt(v, g.zend) && v != 0.f) return 0.f;
+  return v;
+}
+inline uint16_t crop_px(uint16_t v, const mpgeom::CropGeom& g) {
+  if ((double)v < g.zstart && v != 0) return (uint16_t)(int64_t)g.zstart;
+  if ((double)v > g.zend && v != 0) return 0;
+  return v;
+}
+
+// the padded, thresholded crop (getCrop's return value) at crop row y, column x
+template <typename T>
+inline T crop_at(const mpgeom::CropGeom& g, const T* dpt, int64_t w, int64_t y, int64_t x) {
+  const int64_t sy = y - g.pt, sx = x - g.pl;
+  if (sy < 0 || sy >= g.r1 - g.r0 || sx < 0 || sx >= g.c1 - g.c0) return T(0);
+  return crop_px(dpt[(g.r0 + sy) * w + (g.c0 + sx)], g);
+}
+
+// cropArea3D's docom refinement (monkeydetector.py:287-300): the CoM of the first crop, shifted back
+// to frame coordinates; numpy.allclose(com, 0.) (|c| <= 1e-8 each) falls back to the crop's centre
+// pixel as the depth and then to 300 mm (numpy.isclose(com[2], 0))
+template <typename T>
+void refine_com(const mp_camera& cam, const mpgeom::CropGeom& g, const T* dpt, int64_t w, double com[3]) {
+  thread_local std::vector<T> cb;
+  cb.resize((size_t)(g.rows * g.cols));
+  for (int64_t y = 0; y < g.rows; ++y)
+    for (int64_t x = 0; x < g.cols; ++x) cb[(size_t)(y * g.cols + x)] = crop_at(g, dpt, w, y, x);
+  center_of_mass(cam, cb.data(), g.rows, g.cols, com);
+  if (std::fabs(com[0]) <= 1e-8 && std::fabs(com[1]) <= 1e-8 && std::fabs(com[2]) <= 1e-8) {
+    com[2] = (double)cb[(size_t)((g.rows / 2) * g.cols + g.cols / 2)];
+    if (std::fabs(com[2]) <= 1e-8) com[2] = 300.;
+  }
+  com[0] += (double)g.xstart;
+  com[1] += (double)g.ystart;
+}
 
 template <typename T>
-void crop_one(const mp_camera& cam, const T* dpt, int64_t h, int64_t w, const double* com_in,
+void crop_one(const mp_camera& cam, const T* dpt, int64_t h, int64_t w, const double* com_in, bool docom,
               int64_t dsz, float* out, double M[9], double com_out[3], CropInfo* info) {
   double com[3];
   if (com_in)
@@ -152,16 +188,13 @@ void crop_one(const mp_camera& cam, const T* dpt, int64_t h, int64_t w, const do
   else
     center_of_mass(cam, dpt, h, w, com);
   mpgeom::CropGeom g;
-  const int st = mpgeom::crop_geometry(cam, com, h, w, dsz, &g);
+  int st = mpgeom::crop_geometry(cam, com, h, w, dsz, &g);
   if (st != mpgeom::CROP_OK) fail(MP_ERR_ARG, mpgeom::crop_status_msg(st));
-  auto crop_at = [&](int64_t y, int64_t x) -> float {   // padded, thresholded crop value (getCrop)
-    const int64_t sy = y - g.pt, sx = x - g.pl;
-    if (sy < 0 || sy >= g.r1 - g.r0 || sx < 0 || sx >= g.c1 - g.c0) return 0.f;
-    const T v = dpt[(g.r0 + sy) * w + (g.c0 + sx)];
-    if ((double)v < g.zstart && v != 0) return store_as(v, g.zstart);
-    if ((double)v > g.zend && v != 0) return 0.f;
-    return (float)v;
-  };
+  if (docom) {
+    refine_com(cam, g, dpt, w, com);
+    st = mpgeom::crop_geometry(cam, com, h, w, dsz, &g);
+    if (st != mpgeom::CROP_OK) fail(MP_ERR_ARG, mpgeom::crop_status_msg(st));
+  }
   for (int64_t i = 0; i < dsz * dsz; ++i) out[i] = (float)cam.max_depth;
   // the output columns inside the patch and their nearest-neighbour source columns, once per crop
   const int64_t x0 = std::max<int64_t>(0, -g.offx), x1 = std::min<int64_t>(g.szw, dsz - g.offx);
@@ -172,8 +205,8 @@ void crop_one(const mp_camera& cam, const T* dpt, int64_t h, int64_t w, const do
     const int64_t oy = g.offy + y;
     if (oy < 0 || oy >= dsz) continue;
     const int64_t sy = mpgeom::nn_row(g, y);
-    float* orow = out + oy * dsz + g.offx;
-    for (int64_t x = x0; x < x1; ++x) orow[x] = crop_at(sy, colmap[x - x0]);
+    float* orow = out + oy * dsz + (g.offx + x0);   // in-range base: output column offx + x0 >= 0
+    for (int64_t x = x0; x < x1; ++x) orow[x - x0] = (float)crop_at(g, dpt, w, sy, colmap[x - x0]);
   }
   mpgeom::crop_matrix(g, M);
   std::memcpy(com_out, com, sizeof(com));
@@ -207,15 +240,22 @@ int mp_center_of_mass(const mp_camera* cam, const void* depth, int depth_dtype, 
 
 int mp_crop3d(const mp_camera* cam, const void* depth, int depth_dtype, int64_t h, int64_t w, const double* com,
               int64_t dsize, float* out, double M[9], double com_out[3], int32_t info[8]) {
+  return mp_crop3d_ex(cam, depth, depth_dtype, h, w, com, 0, dsize, out, M, com_out, info);
+}
+
+int mp_crop3d_ex(const mp_camera* cam, const void* depth, int depth_dtype, int64_t h, int64_t w, const double* com,
+                 int flags, int64_t dsize, float* out, double M[9], double com_out[3], int32_t info[8]) {
   return guard([&] {
+    if (flags & ~MP_CROP_DOCOM) fail(MP_ERR_ARG, "mp_crop3d_ex: unknown flags");
+    const bool docom = (flags & MP_CROP_DOCOM) != 0;
     check_cam(cam);
     if (!depth || !out || !M || !com_out || h <= 0 || w <= 0 || dsize <= 0)
       fail(MP_ERR_ARG, "mp_crop3d: bad argument");
     CropInfo ci;
     if (depth_dtype == MP_DEPTH_F32)
-      crop_one(*cam, static_cast<const float*>(depth), h, w, com, dsize, out, M, com_out, &ci);
+      crop_one(*cam, static_cast<const float*>(depth), h, w, com, docom, dsize, out, M, com_out, &ci);
     else if (depth_dtype == MP_DEPTH_U16)
-      crop_one(*cam, static_cast<const uint16_t*>(depth), h, w, com, dsize, out, M, com_out, &ci);
+      crop_one(*cam, static_cast<const uint16_t*>(depth), h, w, com, docom, dsize, out, M, com_out, &ci);
     else
       fail(MP_ERR_ARG, "unknown depth dtype");
     if (info) std::memcpy(info, &ci, sizeof(ci));
@@ -238,11 +278,11 @@ int mp_crop3d_batch(const mp_camera* cam, const void* frames, int depth_dtype, i
         codes[t] = guard([&] {
           const double* ci = coms ? coms + 3 * i : nullptr;
           if (depth_dtype == MP_DEPTH_F32)
-            crop_one(*cam, static_cast<const float*>(frames) + i * h * w, h, w, ci, dsize, dst, Ms + 9 * i,
-                     coms_out + 3 * i, nullptr);
+            crop_one(*cam, static_cast<const float*>(frames) + i * h * w, h, w, ci, false, dsize, dst,
+                     Ms + 9 * i, coms_out + 3 * i, nullptr);
           else
-            crop_one(*cam, static_cast<const uint16_t*>(frames) + i * h * w, h, w, ci, dsize, dst, Ms + 9 * i,
-                     coms_out + 3 * i, nullptr);
+            crop_one(*cam, static_cast<const uint16_t*>(frames) + i * h * w, h, w, ci, false, dsize, dst,
+                     Ms + 9 * i, coms_out + 3 * i, nullptr);
         });
         if (codes[t] != MP_OK) {
           errs[t] = "frame " + std::to_string(i) + ": " + g_err;

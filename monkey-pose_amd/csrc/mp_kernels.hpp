@@ -135,6 +135,7 @@ hipError_t launch_fc_gemm_x3p(const void* Ah, const void* Al, int lda, const voi
 // k_frame.hip (frame -> CoM -> crop chain)
 hipError_t launch_resize_bilinear(const float* x, int N, int H, int W, int C, float* out, int Ho, int Wo,
                                   hipStream_t st);
+hipError_t launch_hidden_uniform(float* out, int64_t n, uint64_t seed, double limit, hipStream_t st);
 hipError_t launch_crop3d(const mp_camera& cam, const float* frames, int N, int H, int W, float frame_scale,
                          const float* com_norm, const double com_scale[3], int dsz, float* patches, double* Ms,
                          double* coms_out, int32_t* status, hipStream_t st);

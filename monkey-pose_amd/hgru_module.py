@@ -91,6 +91,8 @@ class ContextualCircuit(object):
         self.bias_shape = [1, 1, 1, self.k]
         self.weights: Optional[Dict[str, np.ndarray]] = None
         self.weight_seed = 1234
+        self.hidden_seed = 7        # hidden_init 'random': call c draws synth_hidden(seed=hidden_seed + c)
+        self._calls = 0
         self.scope = "contextual_circuit"
 
     def prepare_tensors(self, weights: Optional[Dict[str, np.ndarray]] = None,
@@ -111,19 +113,23 @@ class ContextualCircuit(object):
         return out
 
     def build(self, weights: Optional[Dict[str, np.ndarray]] = None, h2_init=None,
-              compute_dtype: str = 'auto'):
+              compute_dtype: str = 'auto', reference_stack_order: bool = False):
         """Run the circuit; returns ``(O, weights, activities)`` like the reference with
         ``return_weights=True`` (hgru_module.py:939-954).  ``compute_dtype``: 'auto' (the FFT
         path when the map allows), 'fp32_fft', 'fp32_split', 'fp32' or 'bf16' (see
         include/monkeypose.h and _lib.resolve_dtype).
 
-        hidden_init (875-892): 'random' -> O0 = ``h2_init`` (default: a seeded xavier-like draw;
-        the reference redraws it every sess.run), 'zeros' -> zeros_like(X), 'identity' -> X.
+        hidden_init (875-892): 'random' -> O0 = ``h2_init`` if given, else a fresh xavier-uniform
+        draw made on the device for every call, as the reference redraws it every sess.run (the
+        draw of call c is ``weights.synth_hidden(shape, seed=self.hidden_seed + c)``, bit for bit);
+        'zeros' -> zeros_like(X), 'identity' -> X.
         store_states (889-915): O is the per-step stack ``[n, T, h, w, k]`` (O_t after the rho
         gain, 909-912) and ``weights['store_O']`` / ``weights['store_I']`` hold the O_t / I_t
         stacks.  (The reference's TensorArrays trade places every step -- ``full`` takes
         ``(store_O, store_I)`` where the loop passes ``(store_I, store_O)``, 825 vs 897-908 -- so
-        its stacked "O" alternates O_t and I_t; here each stack holds what its name says.)"""
+        its stacked "O" alternates O_t and I_t; here each stack holds what its name says.
+        ``reference_stack_order=True`` returns the reference's interleaved stacks instead, see
+        ``reference_stacks``.)"""
         import torch
         X = self.X
         if not isinstance(X, torch.Tensor) or not X.is_cuda:
@@ -134,12 +140,17 @@ class ContextualCircuit(object):
             ctx.set_weight(name, val)
         ctx.finalize(_lib.dtype_code(_lib.resolve_dtype(compute_dtype, X.shape[1], X.shape[2])))
         X = X.detach().float().contiguous()
+        hidden = _lib.MP_HIDDEN[self.hidden_init]
+        call = 0
         if self.hidden_init == 'random':
             if h2_init is None:
-                h2_init = torch.from_numpy(W.synth_hidden(tuple(X.shape))).to(X.device)
-            h2_init = h2_init.detach().float().contiguous()
-            if h2_init.shape != X.shape:
-                raise ValueError("h2_init must have the shape of X")
+                hidden = _lib.MP_HIDDEN_RANDOM          # drawn on the device, per call
+                call = self._calls
+                self._calls += 1
+            else:
+                h2_init = h2_init.detach().float().contiguous()
+                if h2_init.shape != X.shape:
+                    raise ValueError("h2_init must have the shape of X")
         elif h2_init is not None:
             raise ValueError(f"h2_init is only used with hidden_init='random' (got {self.hidden_init!r})")
         O = torch.empty_like(X)
@@ -148,14 +159,32 @@ class ContextualCircuit(object):
             sO = torch.empty((X.shape[0], self.timesteps) + tuple(X.shape[1:]), dtype=torch.float32,
                              device=X.device)
             sI = torch.empty_like(sO)
-        ctx.circuit_fwd(X, h2_init, O, self.timesteps, _lib.current_stream(X.device),
-                        _lib.MP_HIDDEN[self.hidden_init], sO, sI)
+        ctx.circuit_fwd(X, h2_init, O, self.timesteps, _lib.current_stream(X.device), hidden, sO, sI,
+                        rng_seed=self.hidden_seed, rng_call=call)
         torch.cuda.current_stream(X.device).synchronize()
         ctx.close()
         self.h2_init = h2_init
         weights_out = {k_.split("/")[-1]: v for k_, v in wts.items()}
         weights_out['p_t'] = weights_out['p_r']
         if self.store_states:
+            if reference_stack_order:
+                sO, sI = reference_stacks(sO, sI)
             weights_out['store_O'], weights_out['store_I'] = sO, sI
             return sO, weights_out, {}
         return O, weights_out, {}
+
+
+def reference_stacks(states_O, states_I):
+    """The reference's own ``store_states`` stacks from the per-step O_t / I_t stacks [n, T, ...].
+
+    ``full(self, i0, O, I, store_O=None, store_I=None)`` (hgru_module.py:825) is called by
+    ``tf.while_loop`` with the loop variables ``[i0, O, I, store_I, store_O]`` (897-908) and returns
+    them in its own parameter order (857), so the two TensorArrays trade places every step: after
+    T steps the array returned as ``store_O`` (912-914) holds O_t where T-1-t is even and I_t
+    elsewhere, and ``store_I`` the complement (pinned symbolically, tests/test_hgru_structure.py).
+    Returns (O_ref, I_ref) with the reference's layout, for callers that relied on it."""
+    import torch
+    T = states_O.shape[1]
+    pick = torch.tensor([(T - 1 - t) % 2 == 0 for t in range(T)], device=states_O.device)
+    pick = pick.view((1, T) + (1,) * (states_O.dim() - 2))
+    return torch.where(pick, states_O, states_I), torch.where(pick, states_I, states_O)

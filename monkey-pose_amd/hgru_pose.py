@@ -68,6 +68,10 @@ class model:
         self._last = None          # (depth, h2_init) of the last forward
         self.states_O = None       # build(..., store_states=True): [N, T, 64, 64, 64] per-step states
         self.states_I = None
+        self.hidden_seed = 7       # hidden_init 'random' without h2_init: call c draws seed hidden_seed + c
+        self._calls = 0
+        self._rng_call = None
+        self._ref_order = False
 
     def __getitem__(self, name):
         return getattr(self, name)
@@ -159,21 +163,24 @@ class model:
     relu1 = property(lambda self: self._tap("relu1"))
 
     def build(self, depth, output_shape, batch_norm=None, train_mode=None, h2_init=None,
-              keep_intermediates=False, dtype=None, store_states=False):
+              keep_intermediates=False, dtype=None, store_states=False, reference_stack_order=False):
         """``hgru_pose.model.build`` (hgru_pose.py:47-105), inference only.
 
         depth     torch CUDA tensor [N, 128, 128, 1] fp32 (crop / 10000, train_cnn_networks_hgru.py:50)
         h2_init   optional [N, 64, 64, 64] initial hGRU output state for ``aux['hidden_init'] ==
-                  'random'`` (the default): the reference draws it at random per run
-                  (hgru_module.py:879-887), here it defaults to a seeded draw.  'zeros' / 'identity'
-                  (888-890, 876-878) need none.
+                  'random'`` (the default).  Without it the state is drawn on the device for every
+                  call, as the reference redraws it per run (hgru_module.py:879-887): call c of
+                  this model draws ``weights.synth_hidden((N, 64, 64, 64), seed=self.hidden_seed
+                  + c)`` bit for bit, no host RNG and no copy.  'zeros' / 'identity' (888-890,
+                  876-878) need none.
         dtype     None (keep ``compute_dtype``), 'fp32' (fp32-class, fastest path for the map:
                   ``compute_dtype = 'auto'``) or 'bf16' (bf16 spectral / gate GEMMs on the FFT path)
         store_states  also keep every hGRU timestep's states (the circuit's ``store_states``,
                   hgru_module.py:889-915) as ``self.states_O`` / ``self.states_I``, each
                   [N, T, 64, 64, 64]: O_t after the rho gain and I_t.  (With
                   ``aux['store_states']`` the reference itself would feed the 5-D stack into fc_1;
-                  that configuration is rejected.)
+                  that configuration is rejected.)  ``reference_stack_order=True`` gives the
+                  reference's own interleaved stacks instead (``hgru_module.reference_stacks``).
         """
         if dtype is not None:
             if dtype not in ('fp32', 'bf16'):
@@ -193,6 +200,7 @@ class model:
         self._hidden_init()   # validate the aux before any work
         self._ctx = self._context(self.output_shape, depth.device.index or 0,
                                   (int(depth.shape[1]), int(depth.shape[2])))
+        self._ref_order = bool(reference_stack_order)
         return self.forward(depth, h2_init, keep_intermediates, store_states)
 
     def _hidden_init(self) -> str:
@@ -211,12 +219,15 @@ class model:
         depth = depth.detach().float().contiguous()
         n, h, w, _ = depth.shape
         hi = self._hidden_init()
+        self._rng_call = None
         if hi == 'random':
             if h2_init is None:
-                h2_init = torch.from_numpy(W.synth_hidden((n, h // 2, w // 2, 64))).to(depth.device)
-            h2_init = h2_init.detach().float().contiguous()
-            if tuple(h2_init.shape) != (n, h // 2, w // 2, 64):
-                raise ValueError(f"h2_init must be [{n}, {h // 2}, {w // 2}, 64]")
+                self._rng_call = self._calls     # MP_HIDDEN_RANDOM: the library draws O0
+                self._calls += 1
+            else:
+                h2_init = h2_init.detach().float().contiguous()
+                if tuple(h2_init.shape) != (n, h // 2, w // 2, 64):
+                    raise ValueError(f"h2_init must be [{n}, {h // 2}, {w // 2}, 64]")
         elif h2_init is not None:
             raise ValueError(f"h2_init is only used with aux hidden_init='random' (got {hi!r})")
         self.h2_init = h2_init
@@ -232,6 +243,9 @@ class model:
         out = torch.empty((n, self.output_shape), dtype=torch.float32, device=dev)
         stream = _lib.current_stream(dev)
         hidden = _lib.MP_HIDDEN[self._hidden_init()]
+        call = getattr(self, "_rng_call", None)
+        if hidden == _lib.MP_HIDDEN_GIVEN and h2_init is None and call is not None:
+            hidden = _lib.MP_HIDDEN_RANDOM      # re-running a tap replays the same call's draw
         hh, ww = h // 2, w // 2
         taps = {}
         if keep:
@@ -243,13 +257,16 @@ class model:
             for k in _lib.STATE_NAMES:
                 taps[k] = torch.empty((n, T, hh, ww, 64), dtype=torch.float32, device=dev)
         if taps or hidden:
-            self._ctx.pose_fwd_taps(depth, h2_init, out, taps, stream, hidden)
+            self._ctx.pose_fwd_taps(depth, h2_init, out, taps, stream, hidden, self.hidden_seed, call or 0)
         else:
             self._ctx.pose_fwd(depth, h2_init, out, stream)
         if keep:
             self._taps = {k: taps[k] for k in _lib.TAP_NAMES}
         if store_states:
             self.states_O, self.states_I = taps["states_O"], taps["states_I"]
+            if self._ref_order:
+                from .hgru_module import reference_stacks
+                self.states_O, self.states_I = reference_stacks(self.states_O, self.states_I)
         self.out_put = out
         return out
 

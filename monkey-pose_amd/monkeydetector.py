@@ -28,6 +28,9 @@ _CROP_SIGS = {
     "mp_crop3d": (ctypes.c_int, [ctypes.POINTER(_Camera), ctypes.c_void_p, ctypes.c_int, ctypes.c_int64,
                                  ctypes.c_int64, ctypes.c_void_p, ctypes.c_int64, ctypes.c_void_p,
                                  ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
+    "mp_crop3d_ex": (ctypes.c_int, [ctypes.POINTER(_Camera), ctypes.c_void_p, ctypes.c_int, ctypes.c_int64,
+                                    ctypes.c_int64, ctypes.c_void_p, ctypes.c_int, ctypes.c_int64, ctypes.c_void_p,
+                                    ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
     "mp_crop3d_batch": (ctypes.c_int, [ctypes.POINTER(_Camera), ctypes.c_void_p, ctypes.c_int,
                                        ctypes.c_int64, ctypes.c_int64, ctypes.c_int64, ctypes.c_void_p,
                                        ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
@@ -99,9 +102,9 @@ class MonkeyDetector(object):
         return com
 
     def cropArea3D(self, dpt, com=None, dsize=(128, 128), docom=False):
-        """monkeydetector.py:261-334 -> (crop [dsize] float32 mm, M 3x3 numpy matrix, com)."""
-        if docom:
-            raise NotImplementedError("docom=True (second CoM refinement) is not on the inference path")
+        """monkeydetector.py:261-334 -> (crop [dsize] float32 mm, M 3x3 numpy matrix, com);
+        ``docom=True`` runs the second refinement (287-300): a CoM of the first crop, a second crop
+        around it, and the refined CoM returned."""
         if self.resizeMethod != self.RESIZE_CV2_NN:
             raise NotImplementedError("only RESIZE_CV2_NN (the reference default) is implemented")
         if len(dsize) != 2 or dsize[0] != dsize[1]:
@@ -113,9 +116,9 @@ class MonkeyDetector(object):
         info = np.zeros(8, np.int32)
         c = None if com is None else np.ascontiguousarray(np.asarray(com, np.float64).reshape(3))
         cam = self._cam()
-        _lib.check(_lib_crop().mp_crop3d(ctypes.byref(cam), _p(f), dt, f.shape[0], f.shape[1],
-                                         None if c is None else _p(c), dsize[0], _p(out), _p(M),
-                                         _p(com_out), _p(info)))
+        _lib.check(_lib_crop().mp_crop3d_ex(ctypes.byref(cam), _p(f), dt, f.shape[0], f.shape[1],
+                                            None if c is None else _p(c), 1 if docom else 0, dsize[0], _p(out),
+                                            _p(M), _p(com_out), _p(info)))
         self.last_crop_info = dict(bounds=tuple(int(v) for v in info[:4]), sz=(int(info[4]), int(info[5])),
                                    offset=(int(info[6]), int(info[7])))
         return out, np.asmatrix(M.reshape(3, 3)), com_out
@@ -193,16 +196,23 @@ class MonkeyDetector(object):
         return xstart, xend, ystart, yend, zstart, zend
 
     def xyztouvd(self, jnts_xyz):
-        """monkeydetector.py:85-112 (float32 output; z == 0 maps to the principal point)."""
+        """monkeydetector.py:85-112 / tf_monkeydetector.py:116-141 (float32 output; z == 0 maps to the
+        principal point).  The reference's scalar arithmetic under NumPy 1.x: ``x / z`` in the joints'
+        own dtype (float32 / float32 is a float32 division), then ``* fx`` and ``ux -`` in float64
+        (a float32 scalar with a Python float promotes), one rounding to float32 on the store."""
         j = np.asarray(jnts_xyz)
         one = j.ndim == 1
-        j = np.atleast_2d(j).astype(np.float64)
+        j = np.atleast_2d(j)
+        if j.dtype.kind != "f":
+            j = j.astype(np.float64)
         out = np.zeros((j.shape[0], 3), np.float32)
         z = j[:, 2]
         nz = z != 0.
         out[~nz, 0], out[~nz, 1] = self.ux, self.uy
-        out[nz, 0] = self.ux - j[nz, 0] / z[nz] * self.fx
-        out[nz, 1] = j[nz, 1] / z[nz] * self.fy + self.uy
+        qx = (j[nz, 0] / z[nz]).astype(np.float64)
+        qy = (j[nz, 1] / z[nz]).astype(np.float64)
+        out[nz, 0] = self.ux - qx * self.fx
+        out[nz, 1] = qy * self.fy + self.uy
         out[nz, 2] = -z[nz]
         return out[0] if one else out
 

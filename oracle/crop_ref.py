@@ -18,6 +18,12 @@ UNPINNED for these pieces):
 * NumPy float32 ``ndarray.sum()``: pairwise summation (blocks of 128, 8 partial sums) -- restated in
   ``np_pairwise_sum_f32`` and checked against numpy itself in the tests.
 Python 2 integer division in ``sz`` (monkeydetector.py:296-299) is floor division.
+
+The era's NumPy (<= 1.16, Python 2.7) casts scalars by value: a float32 array compared with a
+float64 scalar (getCrop's ``cropped < zstart`` / ``cropped > zend``, 209-210; calculateCoM's
+``dc < minDepth`` / ``dc > maxDepth``, 74-75) compares in float32 against f32(scalar) (``_lcmp``);
+a uint16 array compares in float64.  NumPy 2 (NEP 50) would compare in float64 throughout.
+Pinned by fixtures from the reference's own code, executed here (tests/golden/make_crop_fixtures.py).
 """
 from __future__ import annotations
 
@@ -32,8 +38,16 @@ CUBE = (800.0, 800.0, 1200.0)
 MIN_DEPTH, MAX_DEPTH = 200.0, 10000.0
 
 
+def _lscalar(arr: np.ndarray, s: float):
+    """the scalar as NumPy 1.x value-based casting sees it against ``arr`` (see the header)"""
+    if arr.dtype == np.float32 and -3.4e38 < s < 3.4e38:
+        return np.float32(s)
+    return np.float64(s)
+
+
 def np_pairwise_sum_f32(a: np.ndarray) -> np.float32:
-    """numpy's float32 pairwise summation over a contiguous array (loops_utils.h.src)."""
+    """numpy 1.x's float32 pairwise summation over a contiguous array (loops_utils.h.src): blocks of
+    <= 128 summed into 8 partial sums, halves split at multiples of 8."""
     flat = np.ascontiguousarray(a, dtype=np.float32).reshape(-1)
 
     def rec(lo, n):
@@ -43,11 +57,10 @@ def np_pairwise_sum_f32(a: np.ndarray) -> np.float32:
                 r = np.float32(r + flat[lo + i])
             return r
         if n <= 128:
-            r = [flat[lo + j] for j in range(8)]
+            r = flat[lo:lo + 8].copy()            # the 8 partial sums, one float32 add per element
             i = 8
             while i < n - (n % 8):
-                for j in range(8):
-                    r[j] = np.float32(r[j] + flat[lo + i + j])
+                r += flat[lo + i:lo + i + 8]
                 i += 8
             res = np.float32(np.float32(np.float32(r[0] + r[1]) + np.float32(r[2] + r[3])) +
                              np.float32(np.float32(r[4] + r[5]) + np.float32(r[6] + r[7])))
@@ -70,13 +83,14 @@ class MonkeyDetectorRef:
 
     def calculateCoM(self, dpt):
         dc = dpt.copy()
-        dc[dc < self.minDepth] = 0
-        dc[dc > self.maxDepth] = 0
+        dc[dc < _lscalar(dc, self.minDepth)] = 0
+        dc[dc > _lscalar(dc, self.maxDepth)] = 0
         cc = ndimage.center_of_mass(dc > 0)
         num = np.count_nonzero(dc)
         if num == 0:
             return np.array((0, 0, 0), np.float64)
-        com = np.array((cc[1] * num, cc[0] * num, dc.sum()), np.float64)
+        s = np_pairwise_sum_f32(dc) if dc.dtype == np.float32 else dc.sum()
+        com = np.array((cc[1] * num, cc[0] * num, s), np.float64)
         return com / num
 
     def comToBounds(self, com, size):
@@ -94,8 +108,8 @@ class MonkeyDetectorRef:
                                    (abs(xstart) - max(xstart, 0), abs(xend) - min(xend, dpt.shape[1]))),
                          mode='constant', constant_values=0)
         if thresh_z is True:
-            msk1 = np.bitwise_and(cropped < zstart, cropped != 0)
-            msk2 = np.bitwise_and(cropped > zend, cropped != 0)
+            msk1 = np.bitwise_and(cropped < _lscalar(cropped, zstart), cropped != 0)
+            msk2 = np.bitwise_and(cropped > _lscalar(cropped, zend), cropped != 0)
             cropped[msk1] = zstart
             cropped[msk2] = 0.
         return cropped
@@ -111,11 +125,21 @@ class MonkeyDetectorRef:
         ys = np.array([min(int(math.floor(y * ify)), sh - 1) for y in range(dh)], np.int64)
         return src[ys][:, xs]
 
-    def cropArea3D(self, dpt, com=None, dsize=(128, 128)):
+    def cropArea3D(self, dpt, com=None, dsize=(128, 128), docom=False):
         if com is None:
             com = self.calculateCoM(dpt)
         xstart, xend, ystart, yend, zstart, zend = self.comToBounds(com, self.cube)
         cropped = self.getCrop(dpt, xstart, xend, ystart, yend, zstart, zend)
+        if docom:                                           # monkeydetector.py:287-300
+            com = self.calculateCoM(cropped)
+            if np.allclose(com, 0.):
+                com[2] = cropped[cropped.shape[0] // 2, cropped.shape[1] // 2]
+                if np.isclose(com[2], 0):
+                    com[2] = 300.
+            com[0] += xstart
+            com[1] += ystart
+            xstart, xend, ystart, yend, zstart, zend = self.comToBounds(com, self.cube)
+            cropped = self.getCrop(dpt, xstart, xend, ystart, yend, zstart, zend)
         wb = (xend - xstart)
         hb = (yend - ystart)
         trans = np.eye(3)

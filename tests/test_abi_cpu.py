@@ -46,7 +46,7 @@ def test_ctypes_table_matches_header():
 def test_library_loads_and_reports():
     mp = pkg()
     lib = mp._lib.load()
-    assert lib.mp_version() == 1
+    assert lib.mp_version() == (0 << 16) | 2
     assert isinstance(lib.mp_last_error(), bytes)     # thread-local; earlier tests may have set it
     assert lib.mp_create(0, 99, ctypes.byref(ctypes.c_void_p())) < 0    # bad model kind
     assert b"model_kind" in lib.mp_last_error()
@@ -125,3 +125,19 @@ def test_plain_c_client_matches_python(tmp_path):
     m.compute_dtype = "fp32_fft"
     ref = m.build(torch.from_numpy(depth).cuda(), 69, h2_init=torch.from_numpy(o0).cuda()).cpu().numpy()
     assert np.array_equal(got, ref)
+
+
+def test_fwd_opts_struct_size_is_checked():
+    """mp_fwd_opts (ABI 0.2) carries struct_size; a caller whose struct is smaller than the 0.2
+    layout is rejected before anything is read past it (no GPU call: the check precedes the
+    context)."""
+    mp = pkg()
+    L = mp._lib
+    lib = L.load()
+    assert ctypes.sizeof(L.FwdOpts) == 56 and ctypes.sizeof(L.PoseTaps) == 7 * 8   # the header layouts
+    o = L.fwd_opts(L.MP_HIDDEN_RANDOM, 7, 0)
+    o.struct_size = 16
+    rc = lib.mp_hgru_pose_fwd_ex(None, None, 1, 128, 128, None, None, ctypes.byref(o), None)
+    assert rc == -1 and b"struct_size" in lib.mp_last_error()
+    rc = lib.mp_hgru_circuit_fwd_opts(None, None, None, 1, 64, 64, 64, 8, None, ctypes.byref(o), None)
+    assert rc == -1 and b"struct_size" in lib.mp_last_error()

@@ -94,8 +94,11 @@ def test_crop_errors():
     md, _ = _mds()
     with pytest.raises(Exception):
         md.cropArea3D(np.zeros((424, 512), np.float32))          # no valid pixel -> CoM depth 0
-    with pytest.raises(NotImplementedError):
-        md.cropArea3D(CR.synth_frame(1), com=(256, 212, 1000), docom=True)
+    # docom=True is implemented (monkeydetector.py:287-300; fixtures in test_crop_reference.py)
+    crop, _, com = md.cropArea3D(CR.synth_frame(1), com=(256, 212, 1000), docom=True)
+    exp, _, cr, _ = CR.MonkeyDetectorRef().cropArea3D(CR.synth_frame(1), com=np.array([256., 212, 1000]),
+                                                      docom=True)
+    assert np.array_equal(crop, exp) and np.array_equal(com, cr)
 
 
 def test_relative_absolute_round_trip():
