@@ -105,20 +105,29 @@ __device__ __forceinline__ uint32_t pack_bf2(float a, float b) {
 }
 
 
-// complex fp32: a plain struct, every complex operation two scalar VALU instructions (default).
-// FFT_PACKED=1 (A/B only): a 2-float vector, complex adds one v_pk_add_f32 and twiddle products two
-// v_pk_fma_f32 / v_pk_mul_f32 (the swapped halves folded into op_sel): -8 % fft_fwd, -6 % fft_inv,
-// bf16 forward +6.5 %, BUT the two-stream hGRU schedule then gave run-to-run different bits (up to
-// ~1e-4 on I_1 of the second slice's crops; more often the more op_sel-swap forms were packed),
-// while every FFT kernel alone, two slices of it side by side, and beside the spectral GEMM stayed
-// bit-identical (tools/fft_det.hip, tools/split_probe.py) -- root cause not found, so it stays off
+// complex fp32.  FFT_PACKED = 2 (default): a 2-float vector, so a complex add is one v_pk_add_f32 and a
+// twiddle product two v_pk_fma_f32 / v_pk_mul_f32, with the re/im half swap of swp() done by two
+// plain v_mov_b32 (inline asm, so the compiler cannot fold it into an op_sel operand select).
+// FFT_PACKED = 1 lets the compiler fold the swaps into op_sel on the packed FP32 instructions.  Its
+// results differed from the scalar build's, and under the two-stream hGRU schedule from run to run:
+// 13-19 of 256 crops differed between runs, up to 2.1e-5 (tools/pk_probe.sh,
+// profiles/r3a/pk_probe_det_fp32_pk0_pk1_pk2.log, where libmonkeypose.so was the scalar build).
+// Every op_sel-free build -- scalar (0) or packed with the swaps as moves (2), the only difference
+// from 1 -- is bit-identical to the scalar build and deterministic.  So the op_sel half-select reads
+// of v_pk_*_f32 are the cause: a timing-dependent read of the swapped VGPR half that ROCm 7.2's
+// hazard recognizer does not pad.  No other kernel of the library applies op_sel to a VGPR source of
+// a packed FP32 instruction (the f16x3 packing kernels only broadcast an SGPR half).  Guarded by
+// tests/test_gpu_parity.py::test_stream_split_is_bit_identical / test_batch_invariance_and_determinism.
+// Measured (same box, B = 256, fp32): fft_fwd 0.168 -> 0.157 ms, inv_a_fwd 0.339 -> 0.329, fft_inv
+// 0.130 -> 0.126, 10.56 -> 10.35-10.39 ms per forward, same bits; bf16 6.43-6.47 -> 6.23-6.28 ms.
+// 0: a plain struct, two scalar VALU instructions per complex op.
 #ifndef FFT_PACKED
-#define FFT_PACKED 0
+#define FFT_PACKED 2
 #endif
 #if FFT_PACKED
 typedef float cpx __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ cpx cfma(cpx a, cpx b, cpx c) { return __builtin_elementwise_fma(a, b, c); }
-#if FFT_PACKED == 2   // probe: the half swap as two plain moves the compiler cannot fold into op_sel
+#if FFT_PACKED == 2   // the half swap as two plain moves the compiler cannot fold into op_sel
 __device__ __forceinline__ cpx swp(cpx a) {
   float x, y;
   asm("v_mov_b32 %0, %2\n\tv_mov_b32 %1, %3" : "=&v"(x), "=&v"(y) : "v"(a.y), "v"(a.x));

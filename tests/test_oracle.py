@@ -156,3 +156,15 @@ def test_fp32_port_close_to_fp64():
     a = R.hgru_pose_forward(depth, wts, O0, 8, np.float32)
     b = golden_array("pose_c64_t8", "out")[:1]
     assert a.dtype == np.float32 and rel_inf(a, b) < 1e-4
+
+
+@pytest.mark.parametrize("case", ["pose_c64_t8", "pose_c128_t8"])
+def test_torch_cpu_baseline_matches_oracle(case):
+    """bench.py's timed CPU baseline (oracle/hgru_torch_cpu.py, torch-CPU fp32, BASELINE.md's
+    plan) computes the same forward as the float64 oracle: within the fp32 gate of the golden."""
+    from oracle import hgru_torch_cpu as TC
+    meta = golden_meta()[case]
+    wts, depth, O0 = MG.pose_inputs(meta["n"], meta["crop"], meta["timesteps"], meta["weight_seed"],
+                                    meta["crop_seed"], meta["o0_seed"])
+    out = TC.forward(depth, TC.prepare(wts, meta["timesteps"]), O0, meta["timesteps"])
+    assert rel_inf(out, golden_array(case, "out")) <= 1e-4

@@ -6,7 +6,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 mp = importlib.import_module("monkey-pose_amd")
 W = mp.weights
 dtype = sys.argv[1] if len(sys.argv) > 1 else "fp32_fft"
-n = 96
+n = int(os.environ.get("SPLIT_N", "96"))
+reps = int(os.environ.get("SPLIT_REPS", "3"))
 ctx = mp._lib.Context(mp._lib.MP_MODEL_HGRU_POSE, 0)
 for v in W.hgru_pose_vars(output_shape=69, timesteps=8, crop=128):
     ctx.set_weight(v.name, W.synth_value(v, 1234, 8))
@@ -16,14 +17,15 @@ depth = torch.from_numpy(W.synth_crops(n, seed=3, size=128)).to(dev)
 o0 = torch.from_numpy(W.synth_hidden((n, 64, 64, 64), seed=4)).to(dev)
 st = mp._lib.current_stream(dev)
 outs = {}
-for name, prof in [("split", False), ("split2", False), ("split3", False), ("prof", True), ("prof2", True)]:
+runs = [("split", False)] + [(f"split{r}", False) for r in range(2, reps + 1)] + [("prof", True), ("prof2", True)]
+for name, prof in runs:
     o = torch.empty((n, 69), device=dev)
     ctx.profile(prof)
     ctx.pose_fwd(depth, o0, o, st)
     ctx.profile(False)
     torch.cuda.synchronize()
     outs[name] = o.cpu()
-for a, b in [("split", "split2"), ("split", "split3"), ("prof", "prof2"), ("split", "prof")]:
+for a, b in [("split", f"split{r}") for r in range(2, reps + 1)] + [("prof", "prof2"), ("split", "prof")]:
     d = (outs[a] != outs[b]).any(dim=1).nonzero().flatten().tolist()
     m = (outs[a] - outs[b]).abs().max().item()
     print(f"{dtype} {a} vs {b}: {len(d)} crops differ (max |d| {m:.3e}) {d[:12]}")
