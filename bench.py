@@ -441,7 +441,7 @@ def cpu_baseline(depth, o0, out, wts, T, args):
     """BASELINE.md's CPU-baseline plan: the torch-CPU fp32 restatement of the forward
     (oracle/hgru_torch_cpu.py, checked against the float64 oracle in tests/test_oracle.py) on every
     CPU the process may use, timed on a bounded sample of the same crops (batches of 8 until ~12 s
-    have passed, at most 64 crops).  Its outputs double as the parity check of the measured GPU
+    have passed, at most the whole batch).  Its outputs double as the parity check of the measured GPU
     path; the float64 numpy oracle checks the first 2 crops as well."""
     import torch
     from oracle import hgru_ref as R
@@ -449,7 +449,7 @@ def cpu_baseline(depth, o0, out, wts, T, args):
     threads, avail, quota = cpu_threads()
     torch.set_num_threads(threads)
     P = TC.prepare(wts, T)
-    bs, cap, budget = 8, min(64, depth.shape[0]), 12.0
+    bs, cap, budget = 8, depth.shape[0], 12.0
     d = depth[:cap].cpu().numpy()
     oo = o0[:cap].cpu().numpy()
     TC.forward(d[:2], P, oo[:2], T)                       # warm-up (oneDNN primitive creation)

@@ -274,6 +274,14 @@ int mp_crop3d_dev(const mp_camera* cam, const float* frames, int64_t n, int64_t 
                   const float* com_norm, const double* com_scale, int64_t dsize, float* patches, double* Ms,
                   double* coms_out, int32_t* status, void* stream);
 
+/* mp_crop3d_dev with flags (since 0.2): MP_CROP_DOCOM runs cropArea3D's docom refinement per frame on
+ * the device (one block per frame: calculateCoM of the first crop with numpy's float32 pairwise
+ * sum order, the allclose / isclose fallbacks, the second crop); coms_out then holds the refined
+ * CoMs.  Bit-exact with mp_crop3d_ex(..., MP_CROP_DOCOM, ...). */
+int mp_crop3d_dev_ex(const mp_camera* cam, const float* frames, int64_t n, int64_t h, int64_t w, float frame_scale,
+                     const float* com_norm, const double* com_scale, int flags, int64_t dsize, float* patches,
+                     double* Ms, double* coms_out, int32_t* status, void* stream);
+
 /* read a model property: "output_shape", "timesteps", "ssf", "finalized", "workspace_bytes",
  * "weight_bytes"; graph contexts also "graph_kernels" (kernel launches per forward),
  * "graph_streams" (streams the schedule uses), "graph_captured" (1 once a hipGraph was built, MP_GRAPH_EXEC=1),

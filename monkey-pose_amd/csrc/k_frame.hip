@@ -61,15 +61,22 @@ __global__ __launch_bounds__(256) void crop3d_kernel(mp_camera cam, const float*
                                                      float frame_scale, const float* __restrict__ com_norm,
                                                      double cs0, double cs1, double cs2, int dsz,
                                                      float* __restrict__ patches, double* __restrict__ Ms,
-                                                     double* __restrict__ coms_out, int32_t* __restrict__ status) {
+                                                     double* __restrict__ coms_out, int32_t* __restrict__ status,
+                                                     int refined) {
   __shared__ mpgeom::CropGeom g;
   __shared__ int st;
   const int f = blockIdx.y;
   if (threadIdx.x == 0) {
-    // tr_res[im] * [image_orig_size[0], image_orig_size[1], image_max_depth] (float32 * float64)
+    // tr_res[im] * [image_orig_size[0], image_orig_size[1], image_max_depth] (float32 * float64), or
+    // the docom-refined CoM crop_refine_kernel left in coms_out (its status: the first crop failed)
     double com[3] = {(double)com_norm[3 * f] * cs0, (double)com_norm[3 * f + 1] * cs1,
                      (double)com_norm[3 * f + 2] * cs2};
-    st = mpgeom::crop_geometry(cam, com, H, W, dsz, &g);
+    if (refined) {
+      com[0] = coms_out[3 * f];
+      com[1] = coms_out[3 * f + 1];
+      com[2] = coms_out[3 * f + 2];
+    }
+    st = (refined && status[f] != mpgeom::CROP_OK) ? status[f] : mpgeom::crop_geometry(cam, com, H, W, dsz, &g);
     if (blockIdx.x == 0) {
       status[f] = st;
       coms_out[3 * f] = com[0];
@@ -115,12 +122,188 @@ __global__ __launch_bounds__(256) void crop3d_kernel(mp_camera cam, const float*
   }
 }
 
+// cropArea3D's docom refinement (monkeydetector.py:287-300) on the device, one block per frame:
+// calculateCoM of the first (padded, thresholded) crop -- integer mask sums (exact) and the crop's
+// float32 sum in numpy 1.x's pairwise order (pairwise_sum_FLOAT: halves split at multiples of 8,
+// blocks of <= 128 summed into 8 partial sums) -- then the allclose / isclose fallbacks and the
+// shift back to frame coordinates.  The refined CoM goes to coms_out, which crop3d_kernel then uses.
+// The pairwise tree's top D levels are complete (every node there holds >= 145 > 128 elements when
+// n / 2^D >= 160, since a split loses at most 15 from the smaller half over D levels), so thread t
+// sums the subtree on its D-bit path sequentially in numpy's order and the 2^D results are combined
+// pairwise level by level, which is exactly numpy's recursion.
+constexpr int REF_T = 256;
+// getCrop's output (monkeydetector.py:177-213) at flat index i of the padded crop
+__device__ float crop_getcrop_value(const mpgeom::CropGeom& g, const float* fr, int W, float frame_scale, int64_t i) {
+  const int64_t y = i / g.cols, x = i - y * g.cols;
+  const int64_t sy = y - g.pt, sx = x - g.pl;
+  float v = 0.f;   // getCrop: the zero padding, else the z-thresholded frame pixel
+  if (sy >= 0 && sy < g.r1 - g.r0 && sx >= 0 && sx < g.c1 - g.c0) {
+    const float d = fr[(g.r0 + sy) * W + (g.c0 + sx)] * frame_scale;
+    if (mpgeom::f32_lt(d, g.zstart) && d != 0.f)
+      v = (float)g.zstart;
+    else if (mpgeom::f32_gt(d, g.zend) && d != 0.f)
+      v = 0.f;
+    else
+      v = d;
+  }
+  return v;
+}
+
+// calculateCoM's dc of that crop: dc[dc < minDepth] = 0; dc[dc > maxDepth] = 0 (float32 compares)
+__device__ float crop_dc_value(const mpgeom::CropGeom& g, const float* fr, int W, float frame_scale,
+                               const mp_camera& cam, int64_t i) {
+  const float v = crop_getcrop_value(g, fr, W, frame_scale, i);
+  return (mpgeom::f32_lt(v, cam.min_depth) || mpgeom::f32_gt(v, cam.max_depth)) ? 0.f : v;
+}
+
+// numpy's pairwise float32 sum of dc[lo, lo + n), iteratively (explicit stack of pending right halves)
+__device__ float pairwise_dc(const mpgeom::CropGeom& g, const float* fr, int W, float fs, const mp_camera& cam,
+                             int64_t lo, int64_t n) {
+  // post-order evaluation: a node's value = left + right, computed with a small value stack
+  int64_t st_lo[40], st_n[40];
+  int st_state[40];
+  float vals[40];
+  int sp = 0, vp = 0;
+  st_lo[0] = lo; st_n[0] = n; st_state[0] = 0; sp = 1;
+  while (sp > 0) {
+    const int k = sp - 1;
+    const int64_t l = st_lo[k], m = st_n[k];
+    if (m <= 128) {
+      float r;
+      if (m < 8) {
+        r = 0.f;
+        for (int64_t i = 0; i < m; ++i) r += crop_dc_value(g, fr, W, fs, cam, l + i);
+      } else {
+        float a[8];
+        for (int j = 0; j < 8; ++j) a[j] = crop_dc_value(g, fr, W, fs, cam, l + j);
+        int64_t i = 8;
+        for (; i < m - (m % 8); i += 8)
+          for (int j = 0; j < 8; ++j) a[j] += crop_dc_value(g, fr, W, fs, cam, l + i + j);
+        r = ((a[0] + a[1]) + (a[2] + a[3])) + ((a[4] + a[5]) + (a[6] + a[7]));
+        for (; i < m; ++i) r += crop_dc_value(g, fr, W, fs, cam, l + i);
+      }
+      vals[vp++] = r;
+      --sp;
+      continue;
+    }
+    int64_t n2 = m / 2;
+    n2 -= n2 % 8;
+    if (st_state[k] == 0) {            // descend left
+      st_state[k] = 1;
+      st_lo[sp] = l; st_n[sp] = n2; st_state[sp] = 0; ++sp;
+    } else if (st_state[k] == 1) {     // then right
+      st_state[k] = 2;
+      st_lo[sp] = l + n2; st_n[sp] = m - n2; st_state[sp] = 0; ++sp;
+    } else {                           // both done: left + right
+      const float rgt = vals[--vp], lft = vals[--vp];
+      vals[vp++] = lft + rgt;
+      --sp;
+    }
+  }
+  return vals[0];
+}
+
+__global__ __launch_bounds__(REF_T) void crop_refine_kernel(mp_camera cam, const float* __restrict__ frames, int H,
+                                                            int W, float frame_scale, const float* __restrict__ com_norm,
+                                                            double cs0, double cs1, double cs2, int dsz,
+                                                            double* __restrict__ coms_out, int32_t* __restrict__ status) {
+#pragma clang fp contract(off)
+  __shared__ mpgeom::CropGeom g;
+  __shared__ int st;
+  __shared__ float part[REF_T];
+  __shared__ long long isum[4][REF_T];
+  __shared__ int D;
+  const int f = blockIdx.x, t = threadIdx.x;
+  const float* fr = frames + (size_t)f * H * W;
+  if (t == 0) {
+    double com[3] = {(double)com_norm[3 * f] * cs0, (double)com_norm[3 * f + 1] * cs1,
+                     (double)com_norm[3 * f + 2] * cs2};
+    st = mpgeom::crop_geometry(cam, com, H, W, dsz, &g);
+    const int64_t n = st == mpgeom::CROP_OK ? g.rows * g.cols : 0;
+    int d = 0;
+    while (d < 8 && (n >> (d + 1)) >= 160) ++d;
+    D = d;
+  }
+  __syncthreads();
+  if (st != mpgeom::CROP_OK) {   // the first crop already fails: crop3d_kernel reports it
+    if (t == 0) {
+      status[f] = st;
+      coms_out[3 * f] = coms_out[3 * f + 1] = coms_out[3 * f + 2] = 0.0;
+    }
+    return;
+  }
+  const int64_t n = g.rows * g.cols;
+  // integer sums of calculateCoM: positive count, row / column index sums, non-zero count
+  long long np = 0, sy = 0, sx = 0, nz = 0;
+  for (int64_t i = t; i < n; i += REF_T) {
+    const float v = crop_dc_value(g, fr, W, frame_scale, cam, i);
+    if (v > 0.f) {
+      ++np;
+      sy += i / g.cols;
+      sx += i % g.cols;
+    }
+    nz += v != 0.f;
+  }
+  isum[0][t] = np; isum[1][t] = sy; isum[2][t] = sx; isum[3][t] = nz;
+  // the float32 pairwise sum: thread t < 2^D sums the subtree on its path
+  const int nl = 1 << D;
+  if (t < nl) {
+    int64_t lo = 0, m = n;
+    for (int b = D - 1; b >= 0; --b) {
+      int64_t n2 = m / 2;
+      n2 -= n2 % 8;
+      if ((t >> b) & 1) { lo += n2; m -= n2; } else { m = n2; }
+    }
+    part[t] = pairwise_dc(g, fr, W, frame_scale, cam, lo, m);
+  }
+  __syncthreads();
+  for (int w = nl / 2; w >= 1; w /= 2) {   // combine the complete top levels in order
+    float v = 0.f;
+    if (t < w) v = part[2 * t] + part[2 * t + 1];
+    __syncthreads();
+    if (t < w) part[t] = v;
+    __syncthreads();
+  }
+  for (int w = REF_T / 2; w >= 1; w /= 2) {   // integer sums (exact: any order)
+    if (t < w)
+      for (int k = 0; k < 4; ++k) isum[k][t] += isum[k][t + w];
+    __syncthreads();
+  }
+  if (t == 0) {
+    double com[3];
+    const long long npos = isum[0][0], num = isum[3][0];
+    if (num == 0) {
+      com[0] = com[1] = com[2] = 0.0;
+    } else {
+      const double cc0 = (double)isum[1][0] / (double)npos, cc1 = (double)isum[2][0] / (double)npos;
+      const double s = (double)(0.f + part[0]);
+      com[0] = (cc1 * (double)num) / (double)num;
+      com[1] = (cc0 * (double)num) / (double)num;
+      com[2] = s / (double)num;
+    }
+    if (fabs(com[0]) <= 1e-8 && fabs(com[1]) <= 1e-8 && fabs(com[2]) <= 1e-8) {   // numpy.allclose(com, 0.)
+      const int64_t cy = g.rows / 2, cx = g.cols / 2;
+      com[2] = (double)crop_getcrop_value(g, fr, W, frame_scale, cy * g.cols + cx);   // cropped[h//2, w//2]
+      if (fabs(com[2]) <= 1e-8) com[2] = 300.;
+    }
+    com[0] += (double)g.xstart;
+    com[1] += (double)g.ystart;
+    coms_out[3 * f] = com[0];
+    coms_out[3 * f + 1] = com[1];
+    coms_out[3 * f + 2] = com[2];
+    status[f] = mpgeom::CROP_OK;
+  }
+}
+
 hipError_t launch_crop3d(const mp_camera& cam, const float* frames, int N, int H, int W, float frame_scale,
                          const float* com_norm, const double com_scale[3], int dsz, float* patches, double* Ms,
-                         double* coms_out, int32_t* status, hipStream_t st) {
+                         double* coms_out, int32_t* status, hipStream_t st, bool docom) {
   const int nb = (dsz * dsz + CROP_PIX_PER_BLOCK - 1) / CROP_PIX_PER_BLOCK;
+  if (docom)
+    hipLaunchKernelGGL(crop_refine_kernel, dim3(N), dim3(REF_T), 0, st, cam, frames, H, W, frame_scale, com_norm,
+                       com_scale[0], com_scale[1], com_scale[2], dsz, coms_out, status);
   hipLaunchKernelGGL(crop3d_kernel, dim3(nb, N), dim3(256), 0, st, cam, frames, H, W, frame_scale, com_norm,
-                     com_scale[0], com_scale[1], com_scale[2], dsz, patches, Ms, coms_out, status);
+                     com_scale[0], com_scale[1], com_scale[2], dsz, patches, Ms, coms_out, status, docom ? 1 : 0);
   return hipGetLastError();
 }
 

@@ -308,15 +308,24 @@ int mp_crop3d_batch(const mp_camera* cam, const void* frames, int depth_dtype, i
 int mp_crop3d_dev(const mp_camera* cam, const float* frames, int64_t n, int64_t h, int64_t w, float frame_scale,
                   const float* com_norm, const double* com_scale, int64_t dsize, float* patches, double* Ms,
                   double* coms_out, int32_t* status, void* stream) {
+  return mp_crop3d_dev_ex(cam, frames, n, h, w, frame_scale, com_norm, com_scale, 0, dsize, patches, Ms, coms_out,
+                          status, stream);
+}
+
+int mp_crop3d_dev_ex(const mp_camera* cam, const float* frames, int64_t n, int64_t h, int64_t w, float frame_scale,
+                     const float* com_norm, const double* com_scale, int flags, int64_t dsize, float* patches,
+                     double* Ms, double* coms_out, int32_t* status, void* stream) {
   return guard([&] {
     check_cam(cam);
+    if (flags & ~MP_CROP_DOCOM) fail(MP_ERR_ARG, "mp_crop3d_dev_ex: unknown flags");
     if (!frames || !com_norm || !com_scale || !patches || !Ms || !coms_out || !status)
       fail(MP_ERR_ARG, "mp_crop3d_dev: null pointer");
     if (n <= 0 || n > 65535 || h <= 0 || w <= 0 || h * w > ((int64_t)1 << 30) || dsize <= 0 || dsize > 4096)
       fail(MP_ERR_SHAPE, "mp_crop3d_dev: bad shape");
     if (!(cam->max_depth != 0.0)) fail(MP_ERR_ARG, "camera max_depth must be non-zero");
     hip_check(launch_crop3d(*cam, frames, (int)n, (int)h, (int)w, frame_scale, com_norm, com_scale, (int)dsize,
-                            patches, Ms, coms_out, status, static_cast<hipStream_t>(stream)),
+                            patches, Ms, coms_out, status, static_cast<hipStream_t>(stream),
+                            (flags & MP_CROP_DOCOM) != 0),
               "crop3d");
   });
 }

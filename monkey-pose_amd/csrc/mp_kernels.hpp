@@ -138,7 +138,7 @@ hipError_t launch_resize_bilinear(const float* x, int N, int H, int W, int C, fl
 hipError_t launch_hidden_uniform(float* out, int64_t n, uint64_t seed, double limit, hipStream_t st);
 hipError_t launch_crop3d(const mp_camera& cam, const float* frames, int N, int H, int W, float frame_scale,
                          const float* com_norm, const double com_scale[3], int dsz, float* patches, double* Ms,
-                         double* coms_out, int32_t* status, hipStream_t st);
+                         double* coms_out, int32_t* status, hipStream_t st, bool docom = false);
 hipError_t launch_fc_reduce(const float* part, int S, int M, int N, const float* bias, int relu,
                             const float* aff_s, const float* aff_t, float* out, int ldo, hipStream_t st);
 

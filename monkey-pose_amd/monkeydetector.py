@@ -39,6 +39,10 @@ _CROP_SIGS = {
                                      ctypes.c_int64, ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p,
                                      ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p,
                                      ctypes.c_void_p, ctypes.c_void_p]),
+    "mp_crop3d_dev_ex": (ctypes.c_int, [ctypes.POINTER(_Camera), ctypes.c_void_p, ctypes.c_int64, ctypes.c_int64,
+                                        ctypes.c_int64, ctypes.c_float, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_int, ctypes.c_int64, ctypes.c_void_p, ctypes.c_void_p,
+                                        ctypes.c_void_p, ctypes.c_void_p, ctypes.c_void_p]),
 }
 
 _CROP_MSG = {1: "CoM depth is zero or not finite (no valid pixel in range?)", 2: "empty crop",
@@ -140,7 +144,7 @@ class MonkeyDetector(object):
         return patches, Ms.reshape(n, 3, 3), com_out
 
     def crop_batch_device(self, frames, com_norm, com_scale=(424, 512, 10000.), frame_scale=10000.,
-                          dsize=128, check=True, stream=None):
+                          dsize=128, check=True, stream=None, docom=False):
         """``prepare_data_test`` (train_cnn_networks_hgru.py:61-74) on the GPU for a batch, with
         ``tr_res`` = the attention output still on the device (``mp_crop3d_dev``, one launch):
 
@@ -148,7 +152,8 @@ class MonkeyDetector(object):
         com_norm   CUDA [n, 3] fp32 attention output; com = com_norm * com_scale (float64)
         returns    (patches CUDA [n, dsize, dsize, 1] = crop / maxDepth, Ms CUDA [n, 3, 3] f64,
                     coms CUDA [n, 3] f64); with ``check`` the per-frame status is read back (one
-                    sync) and a failed frame raises like the host ``cropArea3D``."""
+                    sync) and a failed frame raises like the host ``cropArea3D``.  ``docom``: the
+                    second CoM refinement of ``cropArea3D(docom=True)`` per frame, on the device."""
         import torch
         if not (isinstance(frames, torch.Tensor) and frames.is_cuda and isinstance(com_norm, torch.Tensor)
                 and com_norm.is_cuda):
@@ -170,9 +175,9 @@ class MonkeyDetector(object):
         scale = (ctypes.c_double * 3)(*[float(v) for v in com_scale])   # host array (read at the call)
         st = _lib.current_stream(dev) if stream is None else stream
         cam = self._cam()
-        _lib.check(_lib_crop().mp_crop3d_dev(ctypes.byref(cam), ctypes.c_void_p(fr.data_ptr()), n, h, w,
-                                             float(frame_scale), ctypes.c_void_p(cn.data_ptr()),
-                                             ctypes.cast(scale, ctypes.c_void_p), int(dsize),
+        _lib.check(_lib_crop().mp_crop3d_dev_ex(ctypes.byref(cam), ctypes.c_void_p(fr.data_ptr()), n, h, w,
+                                                float(frame_scale), ctypes.c_void_p(cn.data_ptr()),
+                                                ctypes.cast(scale, ctypes.c_void_p), 1 if docom else 0, int(dsize),
                                              ctypes.c_void_p(patches.data_ptr()), ctypes.c_void_p(Ms.data_ptr()),
                                              ctypes.c_void_p(coms.data_ptr()), ctypes.c_void_p(status.data_ptr()),
                                              ctypes.c_void_p(st)))

@@ -179,3 +179,33 @@ def test_device_prepare_data_test_matches_reference(fx):
     assert np.array_equal(patches.cpu().numpy(), z["prep_patches"].astype(np.float32))
     assert np.array_equal(coms.cpu().numpy(), z["prep_coms"])
     assert np.allclose(Ms.cpu().numpy(), z["prep_Ms"], rtol=1e-12, atol=1e-9)
+
+
+@pytest.mark.gpu
+def test_device_docom_matches_host_docom(fx):
+    """cropArea3D(docom=True) on the device (mp_crop3d_dev_ex, MP_CROP_DOCOM) equals the host
+    refinement (itself bit-exact with the reference's code, test_native_crop_matches_reference_execution)
+    bit for bit: patches, refined CoMs, M.  Includes a frame whose first crop has no valid pixel (the
+    allclose -> centre-pixel -> 300 mm fallback)."""
+    import torch
+    z, _ = fx
+    P = pkg()
+    keys = ("f1", "f2", "f3", "tiebig")
+    frames = [z[f"frame_{k}"] for k in keys] + [np.zeros((424, 512), np.float32)]
+    fr = (np.stack(frames) / np.float32(10000.)).astype(np.float32)
+    rng = np.random.default_rng(5)
+    tr = np.stack([np.array([rng.uniform(0.2, 0.8), rng.uniform(0.2, 0.8), rng.uniform(0.08, 0.3)], np.float32)
+                   for _ in frames])
+    tr[3] = np.array([0.5, 0.5, 0.24], np.float32)
+    md = P.monkeydetector.MonkeyDetector(365.456, 365.456, 256, 212, [800, 800, 1200], 200, 10000)
+    patches, Ms, coms = md.crop_batch_device(torch.from_numpy(fr).cuda(), torch.from_numpy(tr).cuda(), docom=True)
+    torch.cuda.synchronize()
+    patches, Ms, coms = patches.cpu().numpy(), Ms.cpu().numpy(), coms.cpu().numpy()
+    scale = np.array([424., 512., 10000.])
+    for i in range(len(frames)):
+        com = tr[i].astype(np.float64) * scale
+        crop, M, c = md.cropArea3D(fr[i] * np.float32(10000.), com=com, docom=True)
+        assert np.array_equal(coms[i], c), i
+        assert np.array_equal(patches[i, :, :, 0], crop / np.float32(10000.)), i
+        assert np.allclose(Ms[i], np.asarray(M), rtol=1e-12, atol=1e-9), i
+    assert coms[4][2] == 300.0
