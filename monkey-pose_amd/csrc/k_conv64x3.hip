@@ -41,10 +41,11 @@ __device__ __forceinline__ f32x16 mfma16(f16x8 a, f16x8 b, f32x16 c) {
 // blocks per block (1: the block's n-half is blockIdx.x % 2; EPI_BB only).  Each accumulator's
 // MFMA sequence (chunks, taps, lo/hi order) is the same for every TH / NN, so the outputs are
 // bit-identical across the variants and a batch-size-dependent choice keeps batch invariance.
-template <int KS, int EPI, int NW, int SCHED, int NP = 3, int TH = TH3, int NN = 2>
+template <int KS, int EPI, int NW, int SCHED, int NP = 3, int TH = TH3, int NN = 2, int DB = 0>
 __global__ __launch_bounds__(NW * 64, 1) void conv64x3_kernel(ConvArgs p, const f16x8* __restrict__ wpk,
                                                               float unscale) {
   static_assert(NN == 2 || EPI == EPI_BB, "split output blocks only for the backbone epilogue");
+  static_assert(DB == 0 || SCHED == 1, "the double-buffered halo runs the prefetching tap loop");
   constexpr int R = KS / 2;
   constexpr int HY = TH + KS - 1, HX = TW + KS - 1;
   constexpr int KK = KS * KS;
@@ -52,7 +53,11 @@ __global__ __launch_bounds__(NW * 64, 1) void conv64x3_kernel(ConvArgs p, const 
   constexpr int MB = TH / NW;            // M-blocks (rows of 32 pixels) per wave
   static_assert(MB >= 1 && MB * NW == TH, "rows per tile must be a multiple of the wave count");
   constexpr int NT = NW * 64;
-  __shared__ f16x8 halo[HY * 4 * HX];
+  constexpr int HSZ = HY * 4 * HX;       // f16x8 cells of one halo chunk
+  // DB: two halo buffers; chunk Q+1's global loads are issued before chunk Q's tap loop and split /
+  // written into the other buffer after it, so the loads are in flight during the MFMAs
+  __shared__ f16x8 halo_all[(DB ? 2 : 1) * HSZ];
+  constexpr int NIT = (HY * HX * 2 + NT - 1) / NT;   // staging items per thread
 
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, col = lane & 31;
   const int H = p.H, W = p.W;
@@ -71,21 +76,33 @@ __global__ __launch_bounds__(NW * 64, 1) void conv64x3_kernel(ConvArgs p, const 
 #pragma unroll
     for (int m = 0; m < MB; ++m) acc[n][m] = f32x16{};
 
-  for (int Q = 0; Q < NQ16; ++Q) {
-    __syncthreads();
-    // ---- stage + split the 16-channel halo chunk (zero outside the image = SAME padding) ----
-    for (int it = tid; it < HY * HX * 2; it += NT) {
-      const int hh = it & 1;
-      const int pix = it >> 1;
+  // staging of one 16-channel chunk: item it = (pixel, half); raw fp32 loads, then split + LDS write
+  f32x4 pre[DB ? NIT : 1][2];
+  auto load_chunk = [&](int Q) {
+#pragma unroll
+    for (int k = 0; k < NIT; ++k) {
+      const int it = tid + k * NT;
+      const int hh = it & 1, pix = min(it >> 1, HY * HX - 1);
+      const int hy = pix / HX, hx = pix - hy * HX;
+      const int gy = min(max(y0 + hy - R, 0), H - 1), gx = min(max(x0 + hx - R, 0), W - 1);   // clamped
+      const f32x4* src = reinterpret_cast<const f32x4*>(p.src + c8_index(b, 2 * Q + hh, gy, gx, 0, H, W));
+      pre[k][0] = src[0];
+      pre[k][1] = src[1];
+    }
+  };
+  auto write_chunk = [&](f16x8* halo) {
+#pragma unroll
+    for (int k = 0; k < NIT; ++k) {
+      const int it = tid + k * NT;
+      if (it >= HY * HX * 2) break;
+      const int hh = it & 1, pix = it >> 1;
       const int hy = pix / HX, hx = pix - hy * HX;
       const int gy = y0 + hy - R, gx = x0 + hx - R;
       f16x8 vh = {}, vl = {};
       if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
-        const f32x4* src = reinterpret_cast<const f32x4*>(p.src + c8_index(b, 2 * Q + hh, gy, gx, 0, H, W));
-        const f32x4 a0 = src[0], a1 = src[1];
 #pragma unroll
         for (int j = 0; j < 8; ++j) {
-          const float v = (j < 4 ? a0[j] : a1[j - 4]) * p.ascale;
+          const float v = (j < 4 ? pre[k][0][j] : pre[k][1][j - 4]) * p.ascale;
           const _Float16 hi = (_Float16)v;
           vh[j] = hi;
           vl[j] = (_Float16)(v - (float)hi);
@@ -94,8 +111,42 @@ __global__ __launch_bounds__(NW * 64, 1) void conv64x3_kernel(ConvArgs p, const 
       halo[(hy * 4 + hh) * HX + hx] = vh;
       if constexpr (NP == 3) halo[(hy * 4 + 2 + hh) * HX + hx] = vl;
     }
-    __syncthreads();
+  };
+  if constexpr (DB) {
+    load_chunk(0);
+    write_chunk(halo_all);
+  }
 
+  for (int Q = 0; Q < NQ16; ++Q) {
+    f16x8* halo = halo_all + (DB ? (Q & 1) * HSZ : 0);
+    if constexpr (DB) {
+      __syncthreads();                        // chunk Q's halo written; chunk Q-1's reads done
+      if (Q + 1 < NQ16) load_chunk(Q + 1);    // in flight during chunk Q's taps
+    } else {
+      __syncthreads();
+      // ---- stage + split the 16-channel halo chunk (zero outside the image = SAME padding) ----
+      for (int it = tid; it < HY * HX * 2; it += NT) {
+        const int hh = it & 1;
+        const int pix = it >> 1;
+        const int hy = pix / HX, hx = pix - hy * HX;
+        const int gy = y0 + hy - R, gx = x0 + hx - R;
+        f16x8 vh = {}, vl = {};
+        if (gy >= 0 && gy < H && gx >= 0 && gx < W) {
+          const f32x4* src = reinterpret_cast<const f32x4*>(p.src + c8_index(b, 2 * Q + hh, gy, gx, 0, H, W));
+          const f32x4 a0 = src[0], a1 = src[1];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            const float v = (j < 4 ? a0[j] : a1[j - 4]) * p.ascale;
+            const _Float16 hi = (_Float16)v;
+            vh[j] = hi;
+            vl[j] = (_Float16)(v - (float)hi);
+          }
+        }
+        halo[(hy * 4 + hh) * HX + hx] = vh;
+        if constexpr (NP == 3) halo[(hy * 4 + 2 + hh) * HX + hx] = vl;
+      }
+      __syncthreads();
+    }
     const f16x8* wq = wpk + (size_t)Q * KK * 4 * 64 + lane;
     const f16x8* hb = halo + ((wv * MB) * 4 + h) * HX + col;
     if constexpr (SCHED == 0) {
@@ -168,6 +219,9 @@ __global__ __launch_bounds__(NW * 64, 1) void conv64x3_kernel(ConvArgs p, const 
         }
       }
     }
+    if constexpr (DB) {
+      if (Q + 1 < NQ16) write_chunk(halo_all + ((Q + 1) & 1) * HSZ);   // the other buffer
+    }
   }
 
   const int x = x0 + col;
@@ -205,11 +259,27 @@ __global__ void pack_conv64x3_kernel(const float* __restrict__ w, f16x8* out, in
   dst[64] = lv;
 }
 
+// MP_CONV_DB=0: the single-buffered halo (A/B); the double-buffered one is used for the backbone
+static bool conv_db() {
+  static const int on = [] {
+    const char* e = std::getenv("MP_CONV_DB");
+    return e ? std::atoi(e) : 1;
+  }();
+  return on;
+}
+
 template <int KS, int EPI, int NW, int SCHED, int NP = 3, int TH = TH3, int NN = 2>
 static hipError_t launch_x3_t(ConvArgs a, const void* wpk, float unscale, int B, hipStream_t st) {
   a.tiles_y = a.H / TH;
   const int nblk = B * a.tiles_x * a.tiles_y * (2 / NN);
-  hipLaunchKernelGGL((conv64x3_kernel<KS, EPI, NW, SCHED, NP, TH, NN>), dim3(nblk), dim3(NW * 64), 0, st, a,
+  if constexpr (EPI == EPI_BB && KS == 3 && SCHED == 1) {
+    if (conv_db()) {
+      hipLaunchKernelGGL((conv64x3_kernel<KS, EPI, NW, SCHED, NP, TH, NN, 1>), dim3(nblk), dim3(NW * 64), 0, st, a,
+                         static_cast<const f16x8*>(wpk), unscale);
+      return hipGetLastError();
+    }
+  }
+  hipLaunchKernelGGL((conv64x3_kernel<KS, EPI, NW, SCHED, NP, TH, NN, 0>), dim3(nblk), dim3(NW * 64), 0, st, a,
                      static_cast<const f16x8*>(wpk), unscale);
   return hipGetLastError();
 }

@@ -1,0 +1,587 @@
+// Fully-connected layers: split-K fp32 GEMM on v_mfma_f32_32x32x2_f32 + a reduce/epilogue kernel.
+//
+// Reference: hgru_pose.fc_layer (hgru_pose.py:156-163) = reshape [-1,in] -> tf.matmul(x, W[in,out])
+// -> bias_add; then relu (92) and inference BN (95-103, folded to an affine) for fc_1, plain
+// bias for fc_out (104).  The same kernels serve every fc_* of the dense / hier heads.
+//
+// D^T[n][m] = sum_k W[k][n] A[m][k]: W is the MFMA A operand, streamed once from HBM in a packed
+// fragment order ([k/8][n/32][lane] float4, one 16-byte load per lane per 8-deep k group); the
+// activations (the small M side) are staged in LDS [128 m][32 k + 4] (the +4 pad makes the
+// ds_read_b128 row reads conflict-free).  Partial sums per K slice go to a slab
+// part[split][M][Npad]; fc_reduce sums the slabs in fixed order (bit-reproducible), then applies
+// bias, relu and the per-feature affine.
+#include "mp_kernels.hpp"
+
+#include <algorithm>
+#include <cmath>
+#include <cstdlib>
+#include <vector>
+
+namespace mp {
+
+constexpr int FC_BM = 128, FC_BK = 32, FC_LDA = FC_BK + 4;
+
+__global__ void pack_fc_kernel(const float* __restrict__ W, f32x4* out, int K, int N, int K8, int N32) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  const size_t total = (size_t)K8 * N32 * 64;
+  if (i >= total) return;
+  const int lane = i % 64;
+  const int nb = (i / 64) % N32;
+  const size_t kb = i / ((size_t)64 * N32);
+  const int n = 32 * nb + (lane & 31);
+  const size_t k0 = 8 * kb + 4 * (lane >> 5);
+  f32x4 v;
+#pragma unroll
+  for (int s = 0; s < 4; ++s) v[s] = (k0 + s < (size_t)K && n < N) ? W[(k0 + s) * N + n] : 0.f;
+  out[i] = v;
+}
+
+// 1-D grid -> (m tile, n tile, K split), XCD-aware: workgroups are dispatched round-robin over the
+// 8 XCDs (separate L2s), so the Mt*Nt blocks of one K split are given ids 8 apart -- one XCD, back
+// to back -- and the split's activation rows and weight slab are fetched into that L2 once instead
+// of once per tile on different XCDs.  Blocks past the last split exit at once.
+struct FcTile {
+  int mt, nt, split;
+};
+__device__ __forceinline__ FcTile fc_tile(int Mt, int Nt) {
+  const int id = blockIdx.x, local = id >> 3, per = Mt * Nt;
+  const int r = local % per;
+  return {r / Nt, r % Nt, (local / per) * 8 + (id & 7)};
+}
+inline int fc_grid(int Mt, int Nt, int S) { return 8 * ((S + 7) / 8) * Mt * Nt; }
+
+__global__ __launch_bounds__(256) void fc_gemm_kernel(const float* __restrict__ A, int lda,
+                                                      const f32x4* __restrict__ Wpk,
+                                                      float* __restrict__ part, int M, int K,
+                                                      int N32, int kslice, int S) {
+  __shared__ float As[FC_BM * FC_LDA];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, col = lane & 31;
+  const FcTile tl = fc_tile((M + FC_BM - 1) / FC_BM, (N32 + 3) / 4);
+  if (tl.split >= S) return;
+  const int mt = tl.mt, ntile = tl.nt, split = tl.split;
+  const int K8 = (K + 7) / 8;
+  const int Npad = N32 * 32;
+  const int nb = ntile * 4 + wv;
+  const bool wave_on = nb < N32;   // wave-uniform
+  const int kbeg = split * kslice;
+  const int kend = min(K, kbeg + kslice);
+
+  f32x16 acc[4];
+#pragma unroll
+  for (int m = 0; m < 4; ++m) acc[m] = f32x16{};
+
+  for (int k0 = kbeg; k0 < kend; k0 += FC_BK) {
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int e = tid + i * 256;          // 0..1023 float4 slots: row = e / 8, k4 = e % 8
+      const int row = e >> 3, k4 = (e & 7) * 4;
+      const int gm = mt * FC_BM + row, gk = k0 + k4;
+      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      if (gm < M) {
+        if (gk + 3 < kend) {
+          v = *reinterpret_cast<const f32x4*>(A + (size_t)gm * lda + gk);
+        } else {
+#pragma unroll
+          for (int s = 0; s < 4; ++s) v[s] = (gk + s < kend) ? A[(size_t)gm * lda + gk + s] : 0.f;
+        }
+      }
+      *reinterpret_cast<f32x4*>(As + row * FC_LDA + k4) = v;
+    }
+    __syncthreads();
+    if (wave_on) {
+#pragma unroll
+      for (int g = 0; g < FC_BK / 8; ++g) {
+        const int kb = (k0 >> 3) + g;
+        if (kb >= K8) break;
+        const f32x4 wf = Wpk[((size_t)kb * N32 + nb) * 64 + lane];
+#pragma unroll
+        for (int m = 0; m < 4; ++m) {
+          const f32x4 a = *reinterpret_cast<const f32x4*>(As + (m * 32 + col) * FC_LDA + 8 * g + 4 * h);
+#pragma unroll
+          for (int s = 0; s < 4; ++s) acc[m] = mfma32(wf[s], a[s], acc[m]);
+        }
+      }
+    }
+  }
+  if (!wave_on) return;
+#pragma unroll
+  for (int m = 0; m < 4; ++m) {
+    const int gm = mt * FC_BM + m * 32 + col;
+    if (gm >= M) continue;
+    float* dst = part + ((size_t)split * M + gm) * Npad + 32 * nb + 4 * h;
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      *reinterpret_cast<f32x4*>(dst + 8 * g) =
+          f32x4{acc[m][4 * g], acc[m][4 * g + 1], acc[m][4 * g + 2], acc[m][4 * g + 3]};
+  }
+}
+
+__global__ void fc_reduce_kernel(const float* __restrict__ part, int S, int M, int N, int Npad,
+                                 const float* __restrict__ bias, int relu,
+                                 const float* __restrict__ aff_s, const float* __restrict__ aff_t,
+                                 float* out, int ldo) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (size_t)M * N) return;
+  const int m = i / N, n = i % N;
+  float v = 0.f;
+  for (int s = 0; s < S; ++s) v += part[((size_t)s * M + m) * Npad + n];
+  if (bias) v += bias[n];
+  if (relu) v = fmaxf(v, 0.f);
+  if (aff_s) v = v * aff_s[n] + aff_t[n];
+  out[(size_t)m * ldo + n] = v;
+}
+
+// ---------------------------------------------------------------------------------------------
+// fp32-accurate f16x3 variant (the hGRU pose head's fc_1 under MP_DTYPE_F32_SPLIT / _FFT): the
+// same split-K decomposition and slabs (so the same batch invariance), D^T = W^T A^T on
+// v_mfma_f32_32x32x16_f16 with both operands split into f16 hi + lo (three products per MAC).
+// W is packed [k/16][n/32][hi|lo][lane] f16x8 with a per-tensor power-of-two scale (max|W| at
+// 2^13..2^14, so the lo halves stay normal); activations are split unscaled when staged into LDS
+// (hi / lo planes [128 m][32 k] f16).
+typedef _Float16 f16x8 __attribute__((ext_vector_type(8)));
+typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+
+__device__ __forceinline__ f32x16 mfma16(f16x8 a, f16x8 b, f32x16 c) {
+  return __builtin_amdgcn_mfma_f32_32x32x16_f16(a, b, c, 0, 0, 0);
+}
+
+__global__ void pack_fc_x3_kernel(const float* __restrict__ W, f16x8* out, int K, int N, int N32, size_t total,
+                                  float wscale) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= total) return;
+  const int lane = i % 64;
+  const int nb = (i / 64) % N32;
+  const size_t k16 = i / ((size_t)64 * N32);
+  const int n = 32 * nb + (lane & 31);
+  const size_t k0 = 16 * k16 + 8 * (lane >> 5);
+  f16x8 hv, lv;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    const float v = (k0 + e < (size_t)K && n < N) ? W[(k0 + e) * N + n] * wscale : 0.f;
+    const _Float16 hh = (_Float16)v;
+    hv[e] = hh;
+    lv[e] = (_Float16)(v - (float)hh);
+  }
+  f16x8* dst = out + ((k16 * N32 + nb) * 2) * 64 + lane;
+  dst[0] = hv;
+  dst[64] = lv;
+}
+
+
+
+// K steps are software-pipelined one step ahead: the activation float4s and the weight fragments
+// of step k+1 are loaded into registers while step k's MFMAs run; loads are unconditional (row
+// index clamped, K a multiple of FC_BK), so all eight loads of a step are in flight together.
+// NP = 3: the fp32-accurate f16x3 product; NP = 1 (dtype bf16's fc_1): hi x hi only -- one MFMA per
+// MAC and only the hi weight planes are read (half the weight bytes), f16 operands (11-bit
+// mantissa, finer than bf16), fp32 accumulation
+// MB: 32-row m-blocks per block (4 = 128 rows; small batches take 1 or 2 so the MFMAs of empty rows
+// and their staging are not paid: fc_1 at batch 1 / 64)
+template <int NP, int MB, int BK = FC_BK>
+__global__ __launch_bounds__(256, 3) void fc_gemm_x3_kernel(const float* __restrict__ A, int lda,
+                                                         const f16x8* __restrict__ Wpk,
+                                                         float* __restrict__ part, int M, int K,
+                                                         int N32, int kslice, float unscale, int S) {
+  constexpr int BM = 32 * MB;
+  constexpr int LD = BK + 8;            // f16 pitch of the planes (+16 B: conflict-free b128 reads)
+  constexpr int RQ = BK / 4;            // float4s per activation row per K step
+  constexpr int NA = MB * BK / 32;      // activation float4s per thread per K step
+  __shared__ _Float16 Ah[BM * LD], Al[NP == 3 ? BM * LD : 1];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, col = lane & 31;
+  const FcTile tl = fc_tile((M + BM - 1) / BM, (N32 + 3) / 4);
+  if (tl.split >= S) return;
+  const int mt = tl.mt, ntile = tl.nt, split = tl.split;
+  const int K16 = (K + 15) / 16;
+  const int Npad = N32 * 32;
+  const int nb = ntile * 4 + wv;
+  const bool wave_on = nb < N32;   // wave-uniform
+  const int nbc = min(nb, N32 - 1);
+  const int kbeg = split * kslice;
+  const int kend = min(K, kbeg + kslice);
+
+  auto load_act = [&](int k0, f32x4 (&v)[NA]) {
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int e = tid + i * 256, row = e / RQ, k4 = (e % RQ) * 4;
+      const int gm = mt * BM + row;   // K % BK == 0 (launcher): every step is interior
+      v[i] = *reinterpret_cast<const f32x4*>(A + (size_t)min(gm, M - 1) * lda + k0 + k4);
+      if (gm >= M) v[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  };
+  auto load_w = [&](int k0, f16x8 (&w)[BK / 16][2]) {
+#pragma unroll
+    for (int g = 0; g < BK / 16; ++g) {
+      const int kb = min((k0 >> 4) + g, K16 - 1);
+      const f16x8* wp = Wpk + (((size_t)kb * N32 + nbc) * 2) * 64 + lane;
+      w[g][0] = wp[0];
+      if constexpr (NP == 3) w[g][1] = wp[64];
+    }
+  };
+
+  f32x16 acc[MB];
+#pragma unroll
+  for (int m = 0; m < MB; ++m) acc[m] = f32x16{};
+  f32x4 av[NA];
+  f16x8 wn[BK / 16][2];
+  if (kbeg < kend) {
+    load_act(kbeg, av);
+    load_w(kbeg, wn);
+  }
+  for (int k0 = kbeg; k0 < kend; k0 += BK) {
+    lds_barrier();   // the previous step's LDS reads are done
+#pragma unroll
+    for (int i = 0; i < NA; ++i) {
+      const int e = tid + i * 256, row = e / RQ, k4 = (e % RQ) * 4;
+      f16x4 hv, lv;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        hv[s] = (_Float16)av[i][s];
+        lv[s] = (_Float16)(av[i][s] - (float)hv[s]);
+      }
+      *reinterpret_cast<f16x4*>(Ah + row * LD + k4) = hv;   // one 8-byte LDS write per plane
+      if constexpr (NP == 3) *reinterpret_cast<f16x4*>(Al + row * LD + k4) = lv;
+    }
+    f16x8 wc[BK / 16][2];
+#pragma unroll
+    for (int g = 0; g < BK / 16; ++g) {
+      wc[g][0] = wn[g][0];
+      if constexpr (NP == 3) wc[g][1] = wn[g][1];
+    }
+    if (k0 + BK < kend) {   // prefetch the next step
+      load_act(k0 + BK, av);
+      load_w(k0 + BK, wn);
+    }
+    lds_barrier();
+    if (wave_on) {
+#pragma unroll
+      for (int g = 0; g < BK / 16; ++g) {
+        if ((k0 >> 4) + g >= K16) break;
+        const f16x8 wh = wc[g][0];
+        [[maybe_unused]] const f16x8 wl = wc[g][1];
+#pragma unroll
+        for (int m = 0; m < MB; ++m) {
+          const int o = (m * 32 + col) * LD + 16 * g + 8 * h;
+          const f16x8 ah = *reinterpret_cast<const f16x8*>(Ah + o);
+          if constexpr (NP == 3) {
+            const f16x8 al = *reinterpret_cast<const f16x8*>(Al + o);
+            acc[m] = mfma16(wl, ah, acc[m]);
+            acc[m] = mfma16(wh, al, acc[m]);
+          }
+          acc[m] = mfma16(wh, ah, acc[m]);
+        }
+      }
+    }
+  }
+  if (!wave_on) return;
+#pragma unroll
+  for (int m = 0; m < MB; ++m) {
+    const int gm = mt * BM + m * 32 + col;
+    if (gm >= M) continue;
+    float* dst = part + ((size_t)split * M + gm) * Npad + 32 * nb + 4 * h;
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      *reinterpret_cast<f32x4*>(dst + 8 * g) =
+          f32x4{acc[m][4 * g], acc[m][4 * g + 1], acc[m][4 * g + 2], acc[m][4 * g + 3]} * unscale;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// fc_1 on pre-split activations (the hGRU pose head, FFT dtypes): the last hGRU epilogue
+// (k_fft.hip spec_epi_b_kernel, mode 2) writes the BN'd NHWC activations as f16 hi / lo planes
+// Ah, Al [M][K] with exactly fc_gemm_x3_kernel's split (hi = (f16)a, lo = (f16)(a - hi)), so the K
+// loop here has no conversion work and no register staging: every K step's activation tile is
+// copied HBM -> LDS by global_load_lds_dwordx4 (1 KiB per wave-instruction, lane-linear in LDS),
+// double-buffered, one barrier per step, while the weights stream to registers one step ahead as
+// before.  The LDS image of a plane is [BM rows][BK k] f16 with the 16-byte chunks of each row
+// XOR-swizzled by row (the swizzle is applied to the global source address, since the DMA writes
+// LDS lane-linearly), so the 32 consecutive rows one ds_read_b128 fragment load touches hit
+// distinct banks.  MFMA order per output is fc_gemm_x3_kernel's: bit-identical results.
+#ifndef FC_P_MINB
+#define FC_P_MINB 3   // blocks per CU the pre-split kernel is register-budgeted for (one product)
+#endif
+#ifndef FC_P_BK3
+#define FC_P_BK3 32   // K step of the three-product kernel
+#endif
+#ifndef FC_P_MINB3
+#define FC_P_MINB3 3
+#endif
+#ifndef FC_P_NW3
+#define FC_P_NW3 4    // waves per block of the three-product kernel (each 32 output columns)
+#endif
+template <int BK>
+__device__ __forceinline__ int fcp_swz(int row) {   // 16-B chunk swizzle of a row (BK = 32: 4 chunks, 64: 8)
+  return BK == 32 ? (row >> 2) & 3 : (row >> 1) & 7;
+}
+
+template <int NP, int MB, int BK, int MINB, int NW = 4>
+__global__ __launch_bounds__(64 * NW, MINB) void fc_gemm_x3p_kernel(const _Float16* __restrict__ Ah,
+                                                               const _Float16* __restrict__ Al, int lda,
+                                                               const f16x8* __restrict__ Wpk,
+                                                               float* __restrict__ part, int M, int K, int N32,
+                                                               int kslice, float unscale, int S) {
+  constexpr int BM = 32 * MB;
+  constexpr int NPL = NP == 3 ? 2 : 1;         // activation planes staged (hi, lo)
+  constexpr int CH = BK / 8;                   // 16-B chunks per row
+  constexpr int PLANE = BM * BK;               // f16 per plane per stage
+  constexpr int STAGE = NPL * PLANE;
+  constexpr int RPI = 1024 / (BK * 2);         // rows per glds wave-instruction
+  constexpr int NI = NPL * BM / RPI;           // glds wave-instructions per stage
+  constexpr int NIW = (NI + NW - 1) / NW;      // per wave
+  __shared__ _Float16 lds[2 * STAGE];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, col = lane & 31;
+  const FcTile tl = fc_tile((M + BM - 1) / BM, (N32 + NW - 1) / NW);
+  if (tl.split >= S) return;
+  const int mt = tl.mt, ntile = tl.nt, split = tl.split;
+  const int K16 = (K + 15) / 16;
+  const int Npad = N32 * 32;
+  const int nb = ntile * NW + wv;
+  const bool wave_on = nb < N32;   // wave-uniform
+  const int nbc = min(nb, N32 - 1);
+  const int kbeg = split * kslice;
+  const int kend = min(K, kbeg + kslice);
+
+  // this lane's glds sources (k offset added per step) and the wave-uniform LDS destinations (a
+  // wave past the NI-th instruction repeats the last one: the same bytes to the same place)
+  const _Float16* src[NIW];
+  int dst[NIW];
+#pragma unroll
+  for (int j = 0; j < NIW; ++j) {
+    const int i = min(wv + NW * j, NI - 1);
+    const int pl = i / (BM / RPI), r0 = (i % (BM / RPI)) * RPI;
+    const int row = r0 + lane / CH, c = (lane % CH) ^ fcp_swz<BK>(row);
+    const int gm = min(mt * BM + row, M - 1);   // rows past M: valid addresses, outputs never stored
+    src[j] = (pl ? Al : Ah) + (size_t)gm * lda + 8 * c;
+    dst[j] = pl * PLANE + r0 * BK;
+  }
+  auto issue = [&](int k0, int stg) {
+#pragma unroll
+    for (int j = 0; j < NIW; ++j)
+      __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src[j] + k0),
+                                       (__attribute__((address_space(3))) void*)(lds + stg * STAGE + dst[j]), 16, 0, 0);
+  };
+  auto load_w = [&](int k0, f16x8 (&w)[BK / 16][2]) {
+#pragma unroll
+    for (int g = 0; g < BK / 16; ++g) {
+      const int kb = min((k0 >> 4) + g, K16 - 1);
+      const f16x8* wp = Wpk + (((size_t)kb * N32 + nbc) * 2) * 64 + lane;
+      w[g][0] = wp[0];
+      if constexpr (NP == 3) w[g][1] = wp[64];
+    }
+  };
+
+  f32x16 acc[MB];
+#pragma unroll
+  for (int m = 0; m < MB; ++m) acc[m] = f32x16{};
+  f16x8 wn[BK / 16][2];
+  if (kbeg < kend) {
+    issue(kbeg, 0);
+    load_w(kbeg, wn);
+  }
+  int stg = 0;
+  for (int k0 = kbeg; k0 < kend; k0 += BK, stg ^= 1) {
+    // this step's tile (DMA'd by every wave) and weights have landed; every wave is done reading
+    // the other stage (its previous step)
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    lds_barrier();
+    f16x8 wc[BK / 16][2];
+#pragma unroll
+    for (int g = 0; g < BK / 16; ++g) {
+      wc[g][0] = wn[g][0];
+      if constexpr (NP == 3) wc[g][1] = wn[g][1];
+    }
+    if (k0 + BK < kend) {
+      issue(k0 + BK, stg ^ 1);
+      load_w(k0 + BK, wn);
+    }
+    if (wave_on) {
+      const _Float16* tile = lds + stg * STAGE;
+#pragma unroll
+      for (int g = 0; g < BK / 16; ++g) {
+        const f16x8 wh = wc[g][0];
+        [[maybe_unused]] const f16x8 wl = wc[g][1];
+#pragma unroll
+        for (int m = 0; m < MB; ++m) {
+          const int row = m * 32 + col;
+          const int o = row * BK + 8 * ((2 * g + h) ^ fcp_swz<BK>(row));
+          const f16x8 ah = *reinterpret_cast<const f16x8*>(tile + o);
+          if constexpr (NP == 3) {
+            const f16x8 al = *reinterpret_cast<const f16x8*>(tile + PLANE + o);
+            acc[m] = mfma16(wl, ah, acc[m]);
+            acc[m] = mfma16(wh, al, acc[m]);
+          }
+          acc[m] = mfma16(wh, ah, acc[m]);
+        }
+      }
+    }
+  }
+  if (!wave_on) return;
+#pragma unroll
+  for (int m = 0; m < MB; ++m) {
+    const int gm = mt * BM + m * 32 + col;
+    if (gm >= M) continue;
+    float* dstp = part + ((size_t)split * M + gm) * Npad + 32 * nb + 4 * h;
+#pragma unroll
+    for (int g = 0; g < 4; ++g)
+      *reinterpret_cast<f32x4*>(dstp + 8 * g) =
+          f32x4{acc[m][4 * g], acc[m][4 * g + 1], acc[m][4 * g + 2], acc[m][4 * g + 3]} * unscale;
+  }
+}
+
+hipError_t launch_fc_gemm_x3p(const void* Ah, const void* Al, int lda, const void* Wpk, float unscale, float* part,
+                              int M, int K, int N, int S, int kslice, hipStream_t st, int nprod) {
+  const int BK = nprod == 1 ? 64 : FC_P_BK3;
+  if (K % BK || kslice % BK || lda % 8 || (nprod == 3 && !Al)) return hipErrorInvalidValue;
+  const int N32 = (N + 31) / 32;
+  const int mb = M <= 32 ? 1 : (M <= 64 ? 2 : 4);
+  const int nw = nprod == 3 ? FC_P_NW3 : 4;   // waves (32-column groups) per block
+  const int grid = fc_grid((M + 32 * mb - 1) / (32 * mb), (N32 + nw - 1) / nw, S);
+  const _Float16* h = static_cast<const _Float16*>(Ah);
+  const _Float16* l = static_cast<const _Float16*>(Al);
+  const f16x8* w = static_cast<const f16x8*>(Wpk);
+#define MP_FCP(NPV, MBV, BKV, MINBV)                                                                                   \
+  hipLaunchKernelGGL((fc_gemm_x3p_kernel<NPV, MBV, BKV, MINBV>), dim3(grid), dim3(256), 0, st, h, l, lda, w, part, M, K, \
+                     N32, kslice, unscale, S)
+#define MP_FCP3(MBV)                                                                                                   \
+  hipLaunchKernelGGL((fc_gemm_x3p_kernel<3, MBV, FC_P_BK3, FC_P_MINB3, FC_P_NW3>), dim3(grid), dim3(64 * FC_P_NW3), 0, \
+                     st, h, l, lda, w, part, M, K, N32, kslice, unscale, S)
+  if (nprod == 1) {
+    if (mb == 1) MP_FCP(1, 1, 64, FC_P_MINB);
+    else if (mb == 2) MP_FCP(1, 2, 64, FC_P_MINB);
+    else MP_FCP(1, 4, 64, FC_P_MINB);
+  } else {
+    if (mb == 1) MP_FCP3(1);
+    else if (mb == 2) MP_FCP3(2);
+    else MP_FCP3(4);
+  }
+#undef MP_FCP
+#undef MP_FCP3
+  return hipGetLastError();
+}
+
+__global__ void pad_cin_kernel(const float* __restrict__ w, float* __restrict__ out, int taps, int Cin, int cinp,
+                               int Cout) {
+  const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+  if (i >= (size_t)taps * cinp * Cout) return;
+  const int co = i % Cout;
+  const size_t r = i / Cout;
+  const int ci = r % cinp, t = r / cinp;
+  out[i] = ci < Cin ? w[((size_t)t * Cin + ci) * Cout + co] : 0.f;
+}
+
+hipError_t launch_pad_cin(const float* w, float* out, int taps, int Cin, int cinp, int Cout, hipStream_t st) {
+  const size_t total = (size_t)taps * cinp * Cout;
+  hipLaunchKernelGGL(pad_cin_kernel, dim3((total + 255) / 256), dim3(256), 0, st, w, out, taps, Cin, cinp, Cout);
+  return hipGetLastError();
+}
+
+size_t fc_x3_bytes(int K, int N) { return (size_t)(K + 15) / 16 * ((N + 31) / 32) * 2 * 64 * sizeof(f16x8); }
+
+hipError_t launch_pack_fc_x3(const float* W, void* out, int K, int N, float* unscale, hipStream_t st) {
+  // power-of-two weight scale from max|W|
+  float mx = 0.f;
+  hipError_t e = device_absmax(W, (size_t)K * N, &mx);
+  if (e != hipSuccess) return e;
+  int ex = 0;
+  if (mx > 0.f) std::frexp(mx, &ex);
+  const float wscale = std::ldexp(1.0f, 14 - ex);
+  *unscale = 1.0f / wscale;
+  const int N32 = (N + 31) / 32;
+  const size_t total = (size_t)(K + 15) / 16 * N32 * 64;
+  hipLaunchKernelGGL(pack_fc_x3_kernel, dim3((total + 255) / 256), dim3(256), 0, st, W, static_cast<f16x8*>(out),
+                     K, N, N32, total, wscale);
+  return hipGetLastError();
+}
+
+hipError_t launch_fc_gemm_x3(const float* A, int lda, const void* Wpk, float unscale, float* part, int M, int K,
+                             int N, int S, int kslice, hipStream_t st, int nprod) {
+  if (K % FC_BK || kslice % FC_BK || lda % 4) return hipErrorInvalidValue;
+  const int N32 = (N + 31) / 32;
+  const int mb = M <= 32 ? 1 : (M <= 64 ? 2 : 4);   // 32-row m-blocks per block
+  const int grid = fc_grid((M + 32 * mb - 1) / (32 * mb), (N32 + 3) / 4, S);
+  const f16x8* w = static_cast<const f16x8*>(Wpk);
+#define MP_FC_X3(NPV, MBV)                                                                                   \
+  hipLaunchKernelGGL((fc_gemm_x3_kernel<NPV, MBV>), dim3(grid), dim3(256), 0, st, A, lda, w, part, M, K, N32, \
+                     kslice, unscale, S)
+#define MP_FC_X3K(NPV, MBV, BKV)                                                                                   \
+  hipLaunchKernelGGL((fc_gemm_x3_kernel<NPV, MBV, BKV>), dim3(grid), dim3(256), 0, st, A, lda, w, part, M, K, N32, \
+                     kslice, unscale, S)
+  static const int bk64 = [] {
+    const char* e = std::getenv("MP_FC_BK64");
+    return e ? std::atoi(e) : 1;
+  }();
+  // one product (bf16): 64-deep K steps, half the barriers and LDS staging passes per MFMA --
+  // bf16 fc_1 0.320 -> 0.263 ms at batch 256, 0.161 -> 0.129 at 32, 0.153 -> 0.106 at 1
+  if (nprod == 1 && bk64 && K % 64 == 0 && kslice % 64 == 0) {
+    if (mb == 1) MP_FC_X3K(1, 1, 64);
+    else if (mb == 2) MP_FC_X3K(1, 2, 64);
+    else MP_FC_X3K(1, 4, 64);
+  } else if (nprod == 1) {
+    if (mb == 1) MP_FC_X3(1, 1);
+    else if (mb == 2) MP_FC_X3(1, 2);
+    else MP_FC_X3(1, 4);
+  } else {   // three products: 64-deep steps spill at 128 rows (160 B / lane, fc_1 0.46 -> 1.47 ms)
+    if (mb == 1) MP_FC_X3(3, 1);
+    else if (mb == 2) MP_FC_X3(3, 2);
+    else MP_FC_X3(3, 4);
+  }
+#undef MP_FC_X3
+#undef MP_FC_X3K
+  return hipGetLastError();
+}
+
+hipError_t launch_pack_fc(const float* W, f32x4* out, int K, int N, hipStream_t st) {
+  const int K8 = (K + 7) / 8, N32 = (N + 31) / 32;
+  const size_t total = (size_t)K8 * N32 * 64;
+  hipLaunchKernelGGL(pack_fc_kernel, dim3((total + 255) / 256), dim3(256), 0, st, W, out, K, N, K8, N32);
+  return hipGetLastError();
+}
+
+// K slices: a function of K only, so every output row is summed in the same order whatever the
+// batch size (results are bit-identical between a crop alone and inside a batch).  Large K
+// (fc_1: 262,144) in slices of ~4,096; small K in slices of 128 so a short GEMM still spreads
+// over enough blocks (fc_out, K = 1,024: 8 slices instead of 1).
+int fc_choose_splits(int M, int K, int N, int* kslice) {
+  (void)M;
+  // large K: slices of ~5.4k, i.e. 48 for fc_1 (K = 262,144): at batch 256 that is 2 x 8 x 48 = 768
+  // blocks = one full round of 3 blocks on each of the 256 CUs (64 slices left a 1/3-full second
+  // round); and at least 384 blocks per 128-row tile whatever N is (the dense head's fc_1_1 / fc_1_2,
+  // N = 512: 18 / 12 slices gave 192 / 128 blocks at batch 256 and 0.25 ms each).  A function of
+  // K and N only, so a crop's sums group the same way at every batch.  MP_FC_KSLICE (A/B only)
+  // fixes the slice length.
+  static const char* kenv = std::getenv("MP_FC_KSLICE");
+  static const int ksz = kenv ? std::max(32, std::atoi(kenv)) : 5440;
+  const int nt = ((N + 31) / 32 + 3) / 4;   // 128-column tiles
+  static const int smallk = [] {   // K per slice below 32k (A/B knob MP_FC_SMALLK)
+    const char* e = std::getenv("MP_FC_SMALLK");
+    return e ? std::max(32, std::atoi(e)) : 128;
+  }();
+  int S = K >= 32768 ? std::max(1, K / ksz) : std::min(64, (K + smallk - 1) / smallk);
+  if (K >= 32768 && !kenv) S = std::min(std::max(S, (384 + nt - 1) / nt), K / 512);
+  if (S < 1) S = 1;
+  int ks = (K + S - 1) / S;
+  const int q = K % 64 == 0 ? 64 : FC_BK;   // whole 64-deep steps where K allows (the one-product kernel)
+  ks = (ks + q - 1) / q * q;
+  S = (K + ks - 1) / ks;
+  *kslice = ks;
+  return S;
+}
+
+hipError_t launch_fc_gemm(const float* A, int lda, const f32x4* Wpk, float* part, int M, int K, int N,
+                          int S, int kslice, hipStream_t st) {
+  const int N32 = (N + 31) / 32;
+  const int grid = fc_grid((M + FC_BM - 1) / FC_BM, (N32 + 3) / 4, S);
+  hipLaunchKernelGGL(fc_gemm_kernel, dim3(grid), dim3(256), 0, st, A, lda, Wpk, part, M, K, N32, kslice, S);
+  return hipGetLastError();
+}
+
+hipError_t launch_fc_reduce(const float* part, int S, int M, int N, const float* bias, int relu,
+                            const float* aff_s, const float* aff_t, float* out, int ldo, hipStream_t st) {
+  const int Npad = (N + 31) / 32 * 32;
+  const size_t total = (size_t)M * N;
+  hipLaunchKernelGGL(fc_reduce_kernel, dim3((total + 255) / 256), dim3(256), 0, st, part, S, M, N, Npad,
+                     bias, relu, aff_s, aff_t, out, ldo);
+  return hipGetLastError();
+}
+
+}  // namespace mp
