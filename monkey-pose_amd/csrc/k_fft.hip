@@ -168,6 +168,12 @@ __device__ __forceinline__ cpx swp(cpx a) { return {a.y, a.x}; }
 #ifndef FFT_EPI_PIPE
 #define FFT_EPI_PIPE 1      // inv_a_fwd epilogue, bf16 maps: next chunk's X / O loads issued before this chunk's math
 #endif
+#ifndef FFT_EPI_PIPE32
+#define FFT_EPI_PIPE32 0    // the same pipelining with fp32 maps
+#endif
+#ifndef FFT_EPI_EARLY
+#define FFT_EPI_EARLY 1     // chunk 0's X / O loads issued before the inverse row phase (implies the pipelining)
+#endif
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void st16(uint4* p, uint4 v) {
@@ -632,6 +638,111 @@ __global__ __launch_bounds__(FNT, BF ? FFT_MINB_BF : FFT_MINB) void fft_fwd_kern
   FFT_STAMP_AT(5);
 }
 
+// fp32 forward FFT at three blocks per CU (FFT_FWD3): the transpose runs through a tile of TWO
+// channels (37 fx x 2 x 65 rows, 38.5 KB) in two rounds -- channel pair 0 (the p = 0 row threads'
+// outputs), then pair 1 -- so the block's LDS is the S staging buffer (43.8 KB) instead of the
+// 77 KB four-channel tile.  Every thread reads at most one column: round A's 74 readers are wave 2
+// and the even row threads 0..18 (their own row already written), round B's the odd row threads
+// and the even ones 20..38; all 148 then run the column FFT together.  Values and rounding are
+// those of fft_fwd_kernel (bit-identical S).
+constexpr int F3_TLD = 65;
+constexpr int F3_LDS = FX * STG_LD;      // dwords: the staging buffer (>= the 2-channel tile)
+static_assert(FX * 2 * F3_TLD * 2 <= F3_LDS, "the 2-channel tile fits in the staging buffer");
+__device__ __forceinline__ int f3_reader(int tid, int& fx, int& c) {   // round (0 A, 1 B, -1 none)
+  int j = -1, r = -1;
+  if (tid >= 128) { j = tid - 128; r = 0; }
+  else if (tid & 1) { j = tid >> 1; r = 1; }
+  else if (tid < 20) { j = 64 + (tid >> 1); r = 0; }
+  else if (tid < 40) { j = 64 + ((tid - 20) >> 1); r = 1; }
+  if (r < 0) return -1;
+  fx = j >> 1;
+  c = 2 * r + (j & 1);
+  return r;
+}
+__global__ __launch_bounds__(FNT, 3) void fft_fwd3_kernel(const float* __restrict__ src, void* __restrict__ S,
+                                                         int H, int W) {
+  __shared__ uint32_t lds3[F3_LDS];
+  cpx* T2 = reinterpret_cast<cpx*>(lds3);
+  const int b = fft_block_img(blockIdx.x), cq = fft_block_cq(blockIdx.x);
+  const int q = cq >> 1, e0 = 4 * (cq & 1);
+  const int tid = threadIdx.x;
+  int rfx = 0, rc = 0;
+  const int round = f3_reader(tid, rfx, rc);
+  cpx v[72];
+  const int y = tid >> 1, p = tid & 1;
+  if (tid < 128) {
+    const size_t row = c8_index(b, q, y < H ? y : 0, 0, e0, H, W);
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      const int x = 2 * k + p;
+      const bool in = y < H && x < W;
+      f32x4 u = *reinterpret_cast<const f32x4*>(src + row + 8 * min(x, W - 1));
+      if (!in) u = f32x4{0.f, 0.f, 0.f, 0.f};
+      const cpx lo = {u[0], u[1]}, hi = {u[2], u[3]};
+      const cpx mine = p ? hi : lo, send = p ? lo : hi;
+      const cpx recv = {__int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(send.x), 0xB1, 0xF, 0xF, false)),
+                        __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(send.y), 0xB1, 0xF, 0xF, false))};
+      v[2 * k] = p ? recv : mine;
+      v[2 * k + 1] = p ? mine : recv;
+    }
+#pragma unroll
+    for (int x = 64; x < 72; ++x) v[x] = {0.f, 0.f};
+    fft72<-1>(v);
+  }
+  // rounds: the row threads of pair `pr` write the half spectra of their two channels into T2
+  auto write_pair = [&](int pr) {
+    if (tid < 128 && p == pr) {
+#pragma unroll
+      for (int k = 0; k < FX; ++k) {
+        const cpx zk = v[k], zm = v[(72 - k) % 72];
+        const cpx A = cfma(zm, cpx{1.f, -1.f}, zk) * 0.5f;
+        const cpx B = cfma(swp(zk), cpx{1.f, -1.f}, swp(zm)) * 0.5f;
+        T2[(k * 2 + 0) * F3_TLD + y] = A;
+        T2[(k * 2 + 1) * F3_TLD + y] = B;
+      }
+    }
+  };
+  auto read_col = [&](int r) {
+    if (round == r) {
+#pragma unroll
+      for (int yy = 0; yy < 72; ++yy) v[yy] = yy < 64 ? T2[(rfx * 2 + (rc & 1)) * F3_TLD + yy] : cpx{0.f, 0.f};
+    }
+  };
+  write_pair(0);
+  lds_barrier();
+  read_col(0);
+  lds_barrier();
+  write_pair(1);
+  lds_barrier();
+  read_col(1);
+  if (round >= 0) fft72<-1>(v);
+  uint4* dst = reinterpret_cast<uint4*>(S) + ((size_t)b * 16 + cq) * NF * 2;
+#pragma unroll
+  for (int half = 0; half < 2; ++half) {
+    lds_barrier();   // T2 (half 0) / the previous half's staging is no longer read
+    if (round >= 0) {
+#pragma unroll
+      for (int j = 0; j < 36; ++j) {
+        const cpx z = v[36 * half + j];
+        const float re = z.x * SPEC_SCALE, im = z.y * SPEC_SCALE;
+        const _Float16 hr = (_Float16)re, hi = (_Float16)im;
+        const f16x2 hv = {hr, hi}, lv = {(_Float16)(re - (float)hr), (_Float16)(im - (float)hi)};
+        lds3[rfx * STG_LD + j * 8 + rc] = __builtin_bit_cast(uint32_t, hv);
+        lds3[rfx * STG_LD + j * 8 + 4 + rc] = __builtin_bit_cast(uint32_t, lv);
+      }
+    }
+    lds_barrier();
+    for (int i = tid; i < FX * 72; i += FNT) {
+      const int ffx = i / 72, w = i - ffx * 72;
+      st16(dst + (ffx * 72 + 36 * half) * 2 + w, *reinterpret_cast<const uint4*>(lds3 + ffx * STG_LD + w * 4));
+    }
+  }
+}
+
+#ifndef FFT_FWD3
+#define FFT_FWD3 1    // fp32 forward FFT at three blocks per CU (fft_fwd3_kernel); 0: fft_fwd_kernel
+#endif
+
 // inverse 2-D FFT of Y -> the spatial conv result P (C8)
 template <bool BF, bool BM>
 __global__ __launch_bounds__(FNT, BF ? FFT_MINB_BF : FFT_MINB) void fft_inv_kernel(const void* __restrict__ Y, float* __restrict__ P,
@@ -682,9 +793,25 @@ __global__ __launch_bounds__(FNT, BF ? FFT_MINB_BF : FFT_MINB) void fft_inv_a_fw
   const int q = cq >> 1, e0 = 4 * (cq & 1);
   const int tid = threadIdx.x;
   FFT_STAMP_AT(0);
+  // the A epilogue's X / O loads (see below); FFT_EPI_EARLY issues chunk 0's before the inverse row
+  // phase, so they are in flight during the row transforms
+  constexpr int EU = BM ? 8 : FFT_EPI_EU, ECH = EU * FNT, NECH = (64 * 64 + ECH - 1) / ECH;
+  constexpr bool PIPE = FFT_EPI_PIPE && (BM || FFT_EPI_PIPE32 || FFT_EPI_EARLY);
+  f32x4 xv[2][EU], ov[2][EU];
+  auto load_chunk = [&](int k, f32x4 (&xs)[EU], f32x4 (&os)[EU]) {
+#pragma unroll
+    for (int u = 0; u < EU; ++u) {
+      const int i = min(k * ECH + u * FNT + tid, 64 * 64 - 1);
+      const int yy = min(i >> 6, H - 1), x = min(i & 63, W - 1);
+      const size_t idx = c8_index(b, q, yy, x, e0, H, W);
+      xs[u] = map_ld4<BM>(p.X, idx);
+      os[u] = map_ld4<BM>(p.O, idx);
+    }
+  };
   inv_cols_to_T<BF>(Y, b, cq, tid, T);
   lds_barrier();
   FFT_STAMP_AT(1);
+  if constexpr (PIPE && FFT_EPI_EARLY) load_chunk(0, xv[0], ov[0]);
   const int y = tid >> 1, pp = tid & 1;
   const bool live = tid < 128 && y < H;
   {
@@ -708,20 +835,7 @@ __global__ __launch_bounds__(FNT, BF ? FFT_MINB_BF : FFT_MINB) void fft_inv_a_fw
     // maps (PIPE) the next chunk's loads are issued before this chunk's math: the phase is ~45k of
     // the block's ~100k cycles (tools/fft_stamps.hip); with fp32 maps the second register set
     // measured 2-4 % slower (inv_a_fwd 0.338 -> 0.351 ms), so there it stays one chunk at a time
-    constexpr int EU = BM ? 8 : FFT_EPI_EU, ECH = EU * FNT, NECH = (64 * 64 + ECH - 1) / ECH;
-    constexpr bool PIPE = FFT_EPI_PIPE && BM;
-    f32x4 xv[2][EU], ov[2][EU];
-    auto load_chunk = [&](int k, f32x4 (&xs)[EU], f32x4 (&os)[EU]) {
-#pragma unroll
-      for (int u = 0; u < EU; ++u) {
-        const int i = min(k * ECH + u * FNT + tid, 64 * 64 - 1);
-        const int yy = min(i >> 6, H - 1), x = min(i & 63, W - 1);
-        const size_t idx = c8_index(b, q, yy, x, e0, H, W);
-        xs[u] = map_ld4<BM>(p.X, idx);
-        os[u] = map_ld4<BM>(p.O, idx);
-      }
-    };
-    if constexpr (PIPE) load_chunk(0, xv[0], ov[0]);
+    if constexpr (PIPE && !FFT_EPI_EARLY) load_chunk(0, xv[0], ov[0]);
 #pragma unroll
     for (int k = 0; k < NECH; ++k) {
       const int cur = PIPE ? (k & 1) : 0;
@@ -1406,6 +1520,8 @@ hipError_t launch_fft_fwd(const float* act, void* S, int B, int H, int W, hipStr
     hipLaunchKernelGGL((fft_fwd_kernel<true, true>), dim3(B * 16), dim3(FNT), 0, st, act, S, H, W);
   else if (bf)
     hipLaunchKernelGGL((fft_fwd_kernel<true, false>), dim3(B * 16), dim3(FNT), 0, st, act, S, H, W);
+  else if (FFT_FWD3 && !fy_major<false>())
+    hipLaunchKernelGGL(fft_fwd3_kernel, dim3(B * 16), dim3(FNT), 0, st, act, S, H, W);
   else
     hipLaunchKernelGGL((fft_fwd_kernel<false, false>), dim3(B * 16), dim3(FNT), 0, st, act, S, H, W);
   return hipGetLastError();
