@@ -811,7 +811,10 @@ __global__ __launch_bounds__(FNT, BF ? FFT_MINB_BF : FFT_MINB) void fft_inv_a_fw
   inv_cols_to_T<BF>(Y, b, cq, tid, T);
   lds_barrier();
   FFT_STAMP_AT(1);
-  if constexpr (PIPE && FFT_EPI_EARLY) load_chunk(0, xv[0], ov[0]);
+  // (fp32 maps only: the bf16 kernels are held to 168 VGPRs for 3 blocks per CU, and the early set
+  // made their inv_a_fwd 0.178 -> 0.216 ms, profiles/r3g)
+  constexpr bool EARLY = FFT_EPI_EARLY && !BM;
+  if constexpr (PIPE && EARLY) load_chunk(0, xv[0], ov[0]);
   const int y = tid >> 1, pp = tid & 1;
   const bool live = tid < 128 && y < H;
   {
@@ -835,7 +838,7 @@ __global__ __launch_bounds__(FNT, BF ? FFT_MINB_BF : FFT_MINB) void fft_inv_a_fw
     // maps (PIPE) the next chunk's loads are issued before this chunk's math: the phase is ~45k of
     // the block's ~100k cycles (tools/fft_stamps.hip); with fp32 maps the second register set
     // measured 2-4 % slower (inv_a_fwd 0.338 -> 0.351 ms), so there it stays one chunk at a time
-    if constexpr (PIPE && !FFT_EPI_EARLY) load_chunk(0, xv[0], ov[0]);
+    if constexpr (PIPE && !EARLY) load_chunk(0, xv[0], ov[0]);
 #pragma unroll
     for (int k = 0; k < NECH; ++k) {
       const int cur = PIPE ? (k & 1) : 0;
