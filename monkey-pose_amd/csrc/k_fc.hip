@@ -15,6 +15,7 @@
 #include <algorithm>
 #include <cmath>
 #include <cstdlib>
+#include <utility>
 #include <vector>
 
 namespace mp {
@@ -314,12 +315,80 @@ __device__ __forceinline__ int fcp_swz(int row) {   // 16-B chunk swizzle of a r
   return BK == 32 ? (row >> 2) & 3 : (row >> 1) & 7;
 }
 
-template <int NP, int MB, int BK, int MINB, int NW = 4>
+#ifndef FC_P_NST
+#define FC_P_NST 3    // activation LDS stages / weight register slots: loads run NST - 1 K steps ahead
+#endif
+// The A fragments of one 16-deep k group: N = MB x planes ds_read_b128 at immediate offsets from the
+// lane's base, issued together and waited for in the SAME asm statement.  Written as plain loads,
+// LLVM's waitcnt pass cannot tell them from the LDS-DMA writes still in flight into the other
+// stages and puts an s_waitcnt vmcnt(0) before them: every later step's loads -- the weights and the
+// activation DMA issued one and two steps ahead -- were then waited for at each step, so nothing
+// overlapped the MFMAs.  Stage reuse is ordered by the explicit vmcnt + barrier of the K loop.
+#ifndef FC_P_ASMRD
+#define FC_P_ASMRD 1
+#endif
+template <int N, class F, int... I>
+__device__ __forceinline__ void fcp_unroll_(F&& f, std::integer_sequence<int, I...>) {
+  (f(std::integral_constant<int, I>{}), ...);
+}
+template <int N, class F>
+__device__ __forceinline__ void fcp_unroll(F&& f) {   // f(integral_constant<0>) ... f(<N - 1>)
+  fcp_unroll_<N>(f, std::make_integer_sequence<int, N>{});
+}
+// The weight fragments likewise load through asm (FC_P_ASMW): the compiler's own waits for them
+// merged to vmcnt(0) at the loop head (the slot registers are renamed around the unrolled loop), so
+// the loads are invisible to it and the K loop's explicit wait -- which names the slot's registers
+// as in/out operands, so no use of them can be scheduled above it -- is the only one.
+#ifndef FC_P_ASMW
+#define FC_P_ASMW 1
+#endif
+__device__ __forceinline__ void fcp_ldw2(f16x8& a, f16x8& b, const f16x8* p) {
+  asm volatile("global_load_dwordx4 %0, %2, off\n\tglobal_load_dwordx4 %1, %2, off offset:1024"
+               : "=&v"(a), "=&v"(b)
+               : "v"(p)
+               : "memory");
+}
+__device__ __forceinline__ void fcp_ldw1(f16x8& a, const f16x8* p) {
+  asm volatile("global_load_dwordx4 %0, %1, off" : "=&v"(a) : "v"(p) : "memory");
+}
+template <int CNT, int NP, int G>
+__device__ __forceinline__ void fcp_wait(f16x8 (&w)[G][2]) {
+  if constexpr (NP == 3) {
+    static_assert(G == 2, "three-product kernel: 32-deep K steps");
+    asm volatile("s_waitcnt vmcnt(%4)" : "+v"(w[0][0]), "+v"(w[0][1]), "+v"(w[1][0]), "+v"(w[1][1]) : "n"(CNT) : "memory");
+  } else {
+    static_assert(G == 4, "one-product kernel: 64-deep K steps");
+    asm volatile("s_waitcnt vmcnt(%4)" : "+v"(w[0][0]), "+v"(w[1][0]), "+v"(w[2][0]), "+v"(w[3][0]) : "n"(CNT) : "memory");
+  }
+}
+
+template <int O0, int O1, int O2, int O3>
+__device__ __forceinline__ void fcp_read4(f16x8 (&a)[4], uint32_t base) {
+  asm volatile("ds_read_b128 %0, %4 offset:%c5\n\tds_read_b128 %1, %4 offset:%c6\n\t"
+               "ds_read_b128 %2, %4 offset:%c7\n\tds_read_b128 %3, %4 offset:%c8\n\ts_waitcnt lgkmcnt(0)"
+               : "=&v"(a[0]), "=&v"(a[1]), "=&v"(a[2]), "=&v"(a[3])
+               : "v"(base), "n"(O0), "n"(O1), "n"(O2), "n"(O3)
+               : "memory");
+}
+template <int O0, int O1>
+__device__ __forceinline__ void fcp_read2(f16x8 (&a)[4], uint32_t base) {
+  asm volatile("ds_read_b128 %0, %2 offset:%c3\n\tds_read_b128 %1, %2 offset:%c4\n\ts_waitcnt lgkmcnt(0)"
+               : "=&v"(a[0]), "=&v"(a[1])
+               : "v"(base), "n"(O0), "n"(O1)
+               : "memory");
+}
+template <int O0>
+__device__ __forceinline__ void fcp_read1(f16x8 (&a)[4], uint32_t base) {
+  asm volatile("ds_read_b128 %0, %1 offset:%c2\n\ts_waitcnt lgkmcnt(0)" : "=&v"(a[0]) : "v"(base), "n"(O0) : "memory");
+}
+
+template <int NP, int MB, int BK, int MINB, int NW = 4, int NST = FC_P_NST>
 __global__ __launch_bounds__(64 * NW, MINB) void fc_gemm_x3p_kernel(const _Float16* __restrict__ Ah,
                                                                const _Float16* __restrict__ Al, int lda,
                                                                const f16x8* __restrict__ Wpk,
                                                                float* __restrict__ part, int M, int K, int N32,
                                                                int kslice, float unscale, int S) {
+  static_assert(NST >= 2 && NST <= 4, "stage count");
   constexpr int BM = 32 * MB;
   constexpr int NPL = NP == 3 ? 2 : 1;         // activation planes staged (hi, lo)
   constexpr int CH = BK / 8;                   // 16-B chunks per row
@@ -328,7 +397,11 @@ __global__ __launch_bounds__(64 * NW, MINB) void fc_gemm_x3p_kernel(const _Float
   constexpr int RPI = 1024 / (BK * 2);         // rows per glds wave-instruction
   constexpr int NI = NPL * BM / RPI;           // glds wave-instructions per stage
   constexpr int NIW = (NI + NW - 1) / NW;      // per wave
-  __shared__ _Float16 lds[2 * STAGE];
+  constexpr int GRP = NIW + (BK / 16) * NPL;   // vector-memory instructions one K step issues per lane
+  // asm weight loads for the 64- and 128-row tiles (B > 32: fc_1 0.477 -> 0.451 ms at B = 256); the
+  // 32-row tile keeps hipcc's loads (0.190 vs 0.197 ms at B = 1).  Same arithmetic either way.
+  constexpr bool ASMW = FC_P_ASMW && MB > 1;
+  __shared__ _Float16 lds[NST * STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, col = lane & 31;
   const FcTile tl = fc_tile((M + BM - 1) / BM, (N32 + NW - 1) / NW);
   if (tl.split >= S) return;
@@ -340,6 +413,7 @@ __global__ __launch_bounds__(64 * NW, MINB) void fc_gemm_x3p_kernel(const _Float
   const int nbc = min(nb, N32 - 1);
   const int kbeg = split * kslice;
   const int kend = min(K, kbeg + kslice);
+  const int nsteps = kend > kbeg ? (kend - kbeg) / BK : 0;   // K, kslice multiples of BK (launcher)
 
   // this lane's glds sources (k offset added per step) and the wave-uniform LDS destinations (a
   // wave past the NI-th instruction repeats the last one: the same bytes to the same place)
@@ -354,66 +428,112 @@ __global__ __launch_bounds__(64 * NW, MINB) void fc_gemm_x3p_kernel(const _Float
     src[j] = (pl ? Al : Ah) + (size_t)gm * lda + 8 * c;
     dst[j] = pl * PLANE + r0 * BK;
   }
-  auto issue = [&](int k0, int stg) {
+  // one K step's loads: the activation tile by LDS DMA into stage `stg`, the weight fragments into
+  // register slot `w` (issued in this order, GRP instructions)
+  auto issue = [&](int k0, int stg, f16x8 (&w)[BK / 16][2]) {
 #pragma unroll
     for (int j = 0; j < NIW; ++j)
       __builtin_amdgcn_global_load_lds((const __attribute__((address_space(1))) void*)(src[j] + k0),
                                        (__attribute__((address_space(3))) void*)(lds + stg * STAGE + dst[j]), 16, 0, 0);
-  };
-  auto load_w = [&](int k0, f16x8 (&w)[BK / 16][2]) {
 #pragma unroll
     for (int g = 0; g < BK / 16; ++g) {
       const int kb = min((k0 >> 4) + g, K16 - 1);
       const f16x8* wp = Wpk + (((size_t)kb * N32 + nbc) * 2) * 64 + lane;
-      w[g][0] = wp[0];
-      if constexpr (NP == 3) w[g][1] = wp[64];
+      if constexpr (ASMW) {
+        if constexpr (NP == 3) fcp_ldw2(w[g][0], w[g][1], wp);
+        else fcp_ldw1(w[g][0], wp);
+      } else {
+        w[g][0] = wp[0];
+        if constexpr (NP == 3) w[g][1] = wp[64];
+      }
     }
   };
 
+  // this lane's fragment address in a stage (bytes; plane, m and stage are immediate offsets): row
+  // col of each 32-row block (the swizzle depends on col only), chunk 2g + h
+  const uint32_t lds_base = (uint32_t)(size_t)(__attribute__((address_space(3))) _Float16*)lds;
+  uint32_t rd_off[BK / 16];
+#pragma unroll
+  for (int g = 0; g < BK / 16; ++g) rd_off[g] = (uint32_t)((col * BK + 8 * ((2 * g + h) ^ fcp_swz<BK>(col))) * 2);
   f32x16 acc[MB];
 #pragma unroll
   for (int m = 0; m < MB; ++m) acc[m] = f32x16{};
-  f16x8 wn[BK / 16][2];
-  if (kbeg < kend) {
-    issue(kbeg, 0);
-    load_w(kbeg, wn);
-  }
-  int stg = 0;
-  for (int k0 = kbeg; k0 < kend; k0 += BK, stg ^= 1) {
-    // this step's tile (DMA'd by every wave) and weights have landed; every wave is done reading
-    // the other stage (its previous step)
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    lds_barrier();
-    f16x8 wc[BK / 16][2];
+  // K step s: activation stage s % NST, weight slot s % NST; step s + NST - 1 is issued at step s,
+  // after the barrier that retires step s - 1 (the stage it overwrites)
+  // Every step issues a group, past the end too (the last step's addresses again, into a stage
+  // nobody reads any more): the number of groups in flight behind step s is then always NST - 2,
+  // and the compiler's own wait for the weight registers is exact (a conditional issue made it
+  // merge the two paths into vmcnt(0))
+  f16x8 wr[NST][BK / 16][2];
+  const int slast = max(nsteps - 1, 0);
+#pragma unroll
+  for (int d = 0; d < NST - 1; ++d) issue(kbeg + min(d, slast) * BK, d, wr[d]);
+  // step s (stage / slot u = s % NST): wait, barrier, issue step s + NST - 1, MFMAs
+  auto step = [&](auto U, int s) {
+    constexpr int u = decltype(U)::value;
+    // step s's tile and weights have landed; the NST - 2 later groups may stay in flight
+    if constexpr (ASMW) fcp_wait<(NST - 2) * GRP, NP>(wr[u]);   // ties slot u's registers to the wait
+    else asm volatile("s_waitcnt vmcnt(%0)" ::"n"((NST - 2) * GRP) : "memory");
+    lds_barrier();   // every wave's DMA share of stage u landed; every wave is done with step s - 1
+    issue(kbeg + min(s + NST - 1, slast) * BK, (u + NST - 1) % NST, wr[(u + NST - 1) % NST]);
+    // no wave_on branch: a wave past N computes column block nbc again and stores nothing (a
+    // branch here, like a conditional step, made the compiler's wait for the weight registers
+    // merge to vmcnt(0))
 #pragma unroll
     for (int g = 0; g < BK / 16; ++g) {
-      wc[g][0] = wn[g][0];
-      if constexpr (NP == 3) wc[g][1] = wn[g][1];
-    }
-    if (k0 + BK < kend) {
-      issue(k0 + BK, stg ^ 1);
-      load_w(k0 + BK, wn);
-    }
-    if (wave_on) {
-      const _Float16* tile = lds + stg * STAGE;
-#pragma unroll
-      for (int g = 0; g < BK / 16; ++g) {
-        const f16x8 wh = wc[g][0];
-        [[maybe_unused]] const f16x8 wl = wc[g][1];
-#pragma unroll
-        for (int m = 0; m < MB; ++m) {
-          const int row = m * 32 + col;
-          const int o = row * BK + 8 * ((2 * g + h) ^ fcp_swz<BK>(row));
-          const f16x8 ah = *reinterpret_cast<const f16x8*>(tile + o);
+      const f16x8 wh = wr[u][g][0];
+      [[maybe_unused]] const f16x8 wl = wr[u][g][1];
+      // m-blocks in pairs (one pair's hi / lo fragments live at a time: 16 VGPRs)
+      fcp_unroll<(MB + 1) / 2>([&](auto P) {
+        constexpr int m0 = 2 * decltype(P)::value, m1 = m0 + (MB > 1 ? 1 : 0);
+        constexpr int OS = u * STAGE * 2, OP = PLANE * 2, OM = 32 * BK * 2;
+        f16x8 a[4];   // ah(m0), ah(m1), al(m0), al(m1) (MB = 1: ah, al)
+        if constexpr (FC_P_ASMRD) {
+          const uint32_t base = lds_base + rd_off[g];
+          if constexpr (MB > 1 && NP == 3) fcp_read4<OS + m0 * OM, OS + m1 * OM, OS + OP + m0 * OM, OS + OP + m1 * OM>(a, base);
+          else if constexpr (MB > 1) fcp_read2<OS + m0 * OM, OS + m1 * OM>(a, base);
+          else if constexpr (NP == 3) { fcp_read2<OS, OS + OP>(a, base); a[2] = a[1]; }
+          else fcp_read1<OS>(a, base);
+        } else {
+          const _Float16* tile = lds + u * STAGE + rd_off[g] / 2;
+          a[0] = *reinterpret_cast<const f16x8*>(tile + m0 * 32 * BK);
+          a[1] = *reinterpret_cast<const f16x8*>(tile + m1 * 32 * BK);
           if constexpr (NP == 3) {
-            const f16x8 al = *reinterpret_cast<const f16x8*>(tile + PLANE + o);
+            a[2] = *reinterpret_cast<const f16x8*>(tile + PLANE + m0 * 32 * BK);
+            a[3] = *reinterpret_cast<const f16x8*>(tile + PLANE + m1 * 32 * BK);
+          }
+        }
+        fcp_unroll<(MB > 1 ? 2 : 1)>([&](auto Q) {
+          constexpr int q = decltype(Q)::value, m = m0 + q;
+          const f16x8 ah = a[q];
+          if constexpr (NP == 3) {
+            const f16x8 al = a[2 + q];
             acc[m] = mfma16(wl, ah, acc[m]);
             acc[m] = mfma16(wh, al, acc[m]);
           }
           acc[m] = mfma16(wh, ah, acc[m]);
-        }
-      }
+        });
+      });
     }
+  };
+  // whole rounds of NST steps (no conditional step inside the loop), then the remainder
+  const int nfull = nsteps / NST * NST;
+  for (int s0 = 0; s0 < nfull; s0 += NST) fcp_unroll<NST>([&](auto U) { step(U, s0 + decltype(U)::value); });
+  fcp_unroll<NST>([&](auto U) {
+    if (nfull + decltype(U)::value < nsteps) step(U, nfull + decltype(U)::value);
+  });
+  // the groups issued past the last step (weights and LDS DMA) land before the wave ends: a DMA
+  // still in flight at s_endpgm could write into LDS handed to the next workgroup.  Under
+  // FC_P_ASMW every weight slot is named in/out here, so the registers of the never-consumed
+  // groups stay allocated until their loads have landed (hipcc takes an asm load's destination
+  // as written at the statement: dead right away, it could hand the register to the epilogue)
+  if constexpr (ASMW) {
+    fcp_wait<0, NP>(wr[0]);
+    fcp_wait<0, NP>(wr[1]);
+    if constexpr (NST > 2) fcp_wait<0, NP>(wr[2]);
+    if constexpr (NST > 3) fcp_wait<0, NP>(wr[3]);
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
   }
   if (!wave_on) return;
 #pragma unroll

@@ -200,6 +200,7 @@ __global__ __launch_bounds__(256, NB == 4 ? 2 : 3) void igemm_x3_kernel(IgemmArg
     iky = tap / p.KS;
     ikx = tap - iky * p.KS;
   };
+  uint32_t okm = 0;   // bit i: slot i of the last load_act is inside the image and K
   auto load_act = [&](int k0, f32x4 (&v)[4]) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -208,9 +209,8 @@ __global__ __launch_bounds__(256, NB == 4 ? 2 : 3) void igemm_x3_kernel(IgemmArg
         const int iy = sy[i] + iky, ix = sx[i] + ikx;
         const bool ok = sok[i] && kk < p.K && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
         const int cy = min(max(iy, 0), p.H - 1), cx = min(max(ix, 0), p.W - 1);
-        const f32x4 t =
-            *reinterpret_cast<const f32x4*>(p.x + (((size_t)sn[i] * p.H + cy) * p.W + cx) * p.ldx + p.cix + ici);
-        v[i] = ok ? t : f32x4{0.f, 0.f, 0.f, 0.f};
+        v[i] = *reinterpret_cast<const f32x4*>(p.x + (((size_t)sn[i] * p.H + cy) * p.W + cx) * p.ldx + p.cix + ici);
+        okm = ok ? okm | (1u << i) : okm & ~(1u << i);   // applied at the LDS store
       } else {
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
@@ -223,6 +223,7 @@ __global__ __launch_bounds__(256, NB == 4 ? 2 : 3) void igemm_x3_kernel(IgemmArg
           const float t = p.x[(((size_t)sn[i] * p.H + cy) * p.W + cx) * p.ldx + p.cix + ci];
           v[i][s] = ok ? t : 0.f;
         }
+        okm |= 1u << i;
       }
     }
     if (vec) {   // the next K step: ci += 32, carrying into the tap (at most 32 / Cin carries)
@@ -264,10 +265,13 @@ __global__ __launch_bounds__(256, NB == 4 ? 2 : 3) void igemm_x3_kernel(IgemmArg
     for (int i = 0; i < 4; ++i) {   // one 8-byte store per plane and slot
       const int row = (tid >> 3) + 32 * i;
       f16x4 hv, lv;
+      // the padding / past-K mask of the load (a select at the load made hipcc wait for each load
+      // before issuing the next: the one-step prefetch was four serial HBM round trips)
+      const f32x4 a = ((okm >> i) & 1u) ? av[i] : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        hv[s] = (_Float16)av[i][s];
-        lv[s] = (_Float16)(av[i][s] - (float)hv[s]);
+        hv[s] = (_Float16)a[s];
+        lv[s] = (_Float16)(a[s] - (float)hv[s]);
       }
       *reinterpret_cast<f16x4*>(Ah + row * IGX_LD + k4) = hv;
       if constexpr (NP == 3) *reinterpret_cast<f16x4*>(Al + row * IGX_LD + k4) = lv;
@@ -280,10 +284,10 @@ __global__ __launch_bounds__(256, NB == 4 ? 2 : 3) void igemm_x3_kernel(IgemmArg
         wc[g][nb][0] = wn[g][nb][0];
         wc[g][nb][1] = wn[g][nb][1];
       }
-    if (k0 + IG_BK < p.K) {   // prefetch the next step
-      load_act(k0 + IG_BK, av);
-      load_w(k0 + IG_BK, wn);
-    }
+    // prefetch the next step, past the end too (masked, clamped addresses): a conditional prefetch
+    // made hipcc merge the two paths into vmcnt(0) waits
+    load_act(k0 + IG_BK, av);
+    load_w(k0 + IG_BK, wn);
     lds_barrier();
 #pragma unroll
     for (int g = 0; g < 2; ++g) {
@@ -407,6 +411,7 @@ __global__ __launch_bounds__(256, 3) void igemm_x3w_pm_kernel(IgemmArgs p, const
   };
   const int k4 = (tid & 7) * 4;
 
+  uint32_t okm = 0;   // bit i: slot i of the last load_act is inside the image and K
   auto load_act = [&](int k0, f32x4 (&v)[4]) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -417,9 +422,8 @@ __global__ __launch_bounds__(256, 3) void igemm_x3w_pm_kernel(IgemmArgs p, const
         const int iy = sy[i] + tap / p.KS, ix = sx[i] + tap % p.KS;
         const bool ok = sok[i] && kk < p.K && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
         const int cy = min(max(iy, 0), p.H - 1), cx = min(max(ix, 0), p.W - 1);
-        const f32x4 t =
-            *reinterpret_cast<const f32x4*>(p.x + (((size_t)sn[i] * p.H + cy) * p.W + cx) * p.ldx + p.cix + ci);
-        v[i] = ok ? t : f32x4{0.f, 0.f, 0.f, 0.f};
+        v[i] = *reinterpret_cast<const f32x4*>(p.x + (((size_t)sn[i] * p.H + cy) * p.W + cx) * p.ldx + p.cix + ci);
+        okm = ok ? okm | (1u << i) : okm & ~(1u << i);   // applied at the LDS store
       } else {
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
@@ -432,6 +436,7 @@ __global__ __launch_bounds__(256, 3) void igemm_x3w_pm_kernel(IgemmArgs p, const
           const float t = p.x[(((size_t)sn[i] * p.H + cy) * p.W + cx) * p.ldx + p.cix + ci];
           v[i][s] = ok ? t : 0.f;
         }
+        okm |= 1u << i;
       }
     }
   };
@@ -466,19 +471,23 @@ __global__ __launch_bounds__(256, 3) void igemm_x3w_pm_kernel(IgemmArgs p, const
     for (int i = 0; i < 4; ++i) {
       const int row = (tid >> 3) + 32 * i;
       f16x4 hv, lv;
+      // the padding / past-K mask of the load (a select at the load made hipcc wait for each load
+      // before issuing the next: the one-step prefetch was four serial HBM round trips)
+      const f32x4 a = ((okm >> i) & 1u) ? av[i] : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        hv[s] = (_Float16)av[i][s];
-        lv[s] = (_Float16)(av[i][s] - (float)hv[s]);
+        hv[s] = (_Float16)a[s];
+        lv[s] = (_Float16)(a[s] - (float)hv[s]);
       }
       *reinterpret_cast<f16x4*>(Ah + row * IGX_LD + k4) = hv;
       if constexpr (NP == 3) *reinterpret_cast<f16x4*>(Al + row * IGX_LD + k4) = lv;
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) Ws[tid + 256 * u] = wnx[u];
-    if (st + 1 < nsteps) {   // prefetch the next step
-      load_act(kof(st + 1), av);
-      load_w(kof(st + 1), wnx);
+    {   // the next step, past the end too (kof clamped, masked, clamped addresses)
+      const int kn = kof(min(st + 1, nsteps - 1));
+      load_act(kn, av);
+      load_w(kn, wnx);
     }
     lds_barrier();
     if (wave_on) {
@@ -645,6 +654,7 @@ __global__ __launch_bounds__(256, 3) void igemm_x3w_kernel(IgemmArgs p, const f1
     iky = tap / p.KS;
     ikx = tap - iky * p.KS;
   };
+  uint32_t okm = 0;   // bit i: slot i of the last load_act is inside the image and K
   auto load_act = [&](int k0, f32x4 (&v)[4]) {
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
@@ -653,9 +663,8 @@ __global__ __launch_bounds__(256, 3) void igemm_x3w_kernel(IgemmArgs p, const f1
         const int iy = sy[i] + iky, ix = sx[i] + ikx;
         const bool ok = sok[i] && kk < p.K && iy >= 0 && iy < p.H && ix >= 0 && ix < p.W;
         const int cy = min(max(iy, 0), p.H - 1), cx = min(max(ix, 0), p.W - 1);
-        const f32x4 t =
-            *reinterpret_cast<const f32x4*>(p.x + (((size_t)sn[i] * p.H + cy) * p.W + cx) * p.ldx + p.cix + ici);
-        v[i] = ok ? t : f32x4{0.f, 0.f, 0.f, 0.f};
+        v[i] = *reinterpret_cast<const f32x4*>(p.x + (((size_t)sn[i] * p.H + cy) * p.W + cx) * p.ldx + p.cix + ici);
+        okm = ok ? okm | (1u << i) : okm & ~(1u << i);   // applied at the LDS store
       } else {
 #pragma unroll
         for (int s = 0; s < 4; ++s) {
@@ -668,6 +677,7 @@ __global__ __launch_bounds__(256, 3) void igemm_x3w_kernel(IgemmArgs p, const f1
           const float t = p.x[(((size_t)sn[i] * p.H + cy) * p.W + cx) * p.ldx + p.cix + ci];
           v[i][s] = ok ? t : 0.f;
         }
+        okm |= 1u << i;
       }
     }
     if (vec) {   // the next K step: ci += 32, carrying into the tap (at most 32 / Cin carries)
@@ -715,20 +725,21 @@ __global__ __launch_bounds__(256, 3) void igemm_x3w_kernel(IgemmArgs p, const f1
     for (int i = 0; i < 4; ++i) {
       const int row = (tid >> 3) + 32 * i;
       f16x4 hv, lv;
+      // the padding / past-K mask of the load (a select at the load made hipcc wait for each load
+      // before issuing the next: the one-step prefetch was four serial HBM round trips)
+      const f32x4 a = ((okm >> i) & 1u) ? av[i] : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
       for (int s = 0; s < 4; ++s) {
-        hv[s] = (_Float16)av[i][s];
-        lv[s] = (_Float16)(av[i][s] - (float)hv[s]);
+        hv[s] = (_Float16)a[s];
+        lv[s] = (_Float16)(a[s] - (float)hv[s]);
       }
       *reinterpret_cast<f16x4*>(Ah + row * IGX_LD + k4) = hv;
       if constexpr (NP == 3) *reinterpret_cast<f16x4*>(Al + row * IGX_LD + k4) = lv;
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) Ws[tid + 256 * u] = wnx[u];
-    if (k0 + IG_BK < kb1) {   // prefetch the next step
-      load_act(k0 + IG_BK, av);
-      load_w(k0 + IG_BK, wnx);
-    }
+    load_act(k0 + IG_BK, av);   // the next step, past the end too (masked, clamped addresses)
+    load_w(k0 + IG_BK, wnx);
     lds_barrier();
     if (wave_on) {
 #pragma unroll

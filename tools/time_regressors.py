@@ -19,7 +19,10 @@ models = {
     "hier": (mp.train_hier_networks.hier_model_struct, (108, 39, 39, 39, 39, 36), 7.97),
     "dense_hier": (mp.train_dense_hier_networks.dense_hier_model_struct, (108, 39, 39, 39, 39, 36), 5.081),
 }
+only = os.environ.get("TR_MODELS")   # e.g. TR_MODELS=dense (comma-separated subset)
 for name, (cls, args, gf) in models.items():
+    if only and name not in only.split(","):
+        continue
     for dt in dtypes:
         m = cls()
         m.compute_dtype = dt
