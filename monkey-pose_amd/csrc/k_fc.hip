@@ -315,6 +315,12 @@ __device__ __forceinline__ int fcp_swz(int row) {   // 16-B chunk swizzle of a r
   return BK == 32 ? (row >> 2) & 3 : (row >> 1) & 7;
 }
 
+#ifndef FC_P_BIG
+#define FC_P_BIG 1    // the 256 x 256 tile (8 waves, one block per CU) for the three-product kernel above 128 rows
+#endif
+#ifndef FC_PB_PIPE
+#define FC_PB_PIPE 1  // 256-row tile: fragment reads one group ahead of the MFMAs
+#endif
 #ifndef FC_P_NST
 #define FC_P_NST 3    // activation LDS stages / weight register slots: loads run NST - 1 K steps ahead
 #endif
@@ -401,6 +407,8 @@ __global__ __launch_bounds__(64 * NW, MINB) void fc_gemm_x3p_kernel(const _Float
   // asm weight loads for the 64- and 128-row tiles (B > 32: fc_1 0.477 -> 0.451 ms at B = 256); the
   // 32-row tile keeps hipcc's loads (0.190 vs 0.197 ms at B = 1).  Same arithmetic either way.
   constexpr bool ASMW = FC_P_ASMW && MB > 1;
+  constexpr bool BIGOFF = NST * STAGE * 2 > 65536 - 32 * BK * 2 * MB;   // the 256-row tile's stages
+  static_assert(!BIGOFF || MB > 1, "big-offset reads pair m-blocks");
   __shared__ _Float16 lds[NST * STAGE];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, col = lane & 31;
   const FcTile tl = fc_tile((M + BM - 1) / BM, (N32 + NW - 1) / NW);
@@ -479,6 +487,43 @@ __global__ __launch_bounds__(64 * NW, MINB) void fc_gemm_x3p_kernel(const _Float
     // no wave_on branch: a wave past N computes column block nbc again and stores nothing (a
     // branch here, like a conditional step, made the compiler's wait for the weight registers
     // merge to vmcnt(0))
+    if constexpr (BIGOFF && FC_PB_PIPE && NP == 3) {
+      // 256-row tile: the (k group, m pair) fragment groups of the step in sequence, group i + 1's four
+      // ds_read_b128 issued before group i's MFMAs (two fragment sets), and the two m-blocks' MFMAs
+      // interleaved (each accumulator keeps its own product order: bit-identical)
+      constexpr int NPR = MB / 2, NGR = (BK / 16) * NPR;
+      constexpr int OS = u * STAGE * 2, OP = PLANE * 2, OM = 32 * BK * 2;
+      f16x8 fa[2][4];
+      auto rd = [&](auto I) {
+        constexpr int i = decltype(I)::value, g = i / NPR, m0 = 2 * (i % NPR), m1 = m0 + 1;
+        const uint32_t base = lds_base + rd_off[g] + (uint32_t)OS;
+        f16x8 (&a)[4] = fa[i & 1];
+        asm volatile("ds_read_b128 %0, %4 offset:%c5\n\tds_read_b128 %1, %4 offset:%c6\n\t"
+                     "ds_read_b128 %2, %4 offset:%c7\n\tds_read_b128 %3, %4 offset:%c8"
+                     : "=&v"(a[0]), "=&v"(a[1]), "=&v"(a[2]), "=&v"(a[3])
+                     : "v"(base), "n"(m0 * OM), "n"(m1 * OM), "n"(OP + m0 * OM), "n"(OP + m1 * OM)
+                     : "memory");
+      };
+      rd(std::integral_constant<int, 0>{});
+      fcp_unroll<NGR>([&](auto I) {
+        constexpr int i = decltype(I)::value, g = i / NPR, m0 = 2 * (i % NPR), m1 = m0 + 1;
+        f16x8 (&a)[4] = fa[i & 1];
+        if constexpr (i + 1 < NGR) {
+          rd(std::integral_constant<int, i + 1>{});
+          asm volatile("s_waitcnt lgkmcnt(4)" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]) :: "memory");
+        } else {
+          asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(a[0]), "+v"(a[1]), "+v"(a[2]), "+v"(a[3]) :: "memory");
+        }
+        const f16x8 wh = wr[u][g][0], wl = wr[u][g][1];
+        acc[m0] = mfma16(wl, a[0], acc[m0]);
+        acc[m1] = mfma16(wl, a[1], acc[m1]);
+        acc[m0] = mfma16(wh, a[2], acc[m0]);
+        acc[m1] = mfma16(wh, a[3], acc[m1]);
+        acc[m0] = mfma16(wh, a[0], acc[m0]);
+        acc[m1] = mfma16(wh, a[1], acc[m1]);
+      });
+      return;
+    }
 #pragma unroll
     for (int g = 0; g < BK / 16; ++g) {
       const f16x8 wh = wr[u][g][0];
@@ -488,7 +533,11 @@ __global__ __launch_bounds__(64 * NW, MINB) void fc_gemm_x3p_kernel(const _Float
         constexpr int m0 = 2 * decltype(P)::value, m1 = m0 + (MB > 1 ? 1 : 0);
         constexpr int OS = u * STAGE * 2, OP = PLANE * 2, OM = 32 * BK * 2;
         f16x8 a[4];   // ah(m0), ah(m1), al(m0), al(m1) (MB = 1: ah, al)
-        if constexpr (FC_P_ASMRD) {
+        if constexpr (FC_P_ASMRD && BIGOFF) {   // stage base in the address (ds_read offsets are 16-bit)
+          const uint32_t base = lds_base + rd_off[g] + (uint32_t)OS;
+          if constexpr (NP == 3) fcp_read4<m0 * OM, m1 * OM, OP + m0 * OM, OP + m1 * OM>(a, base);
+          else fcp_read2<m0 * OM, m1 * OM>(a, base);
+        } else if constexpr (FC_P_ASMRD) {
           const uint32_t base = lds_base + rd_off[g];
           if constexpr (MB > 1 && NP == 3) fcp_read4<OS + m0 * OM, OS + m1 * OM, OS + OP + m0 * OM, OS + OP + m1 * OM>(a, base);
           else if constexpr (MB > 1) fcp_read2<OS + m0 * OM, OS + m1 * OM>(a, base);
@@ -553,8 +602,13 @@ hipError_t launch_fc_gemm_x3p(const void* Ah, const void* Al, int lda, const voi
   const int BK = nprod == 1 ? 64 : FC_P_BK3;
   if (K % BK || kslice % BK || lda % 8 || (nprod == 3 && !Al)) return hipErrorInvalidValue;
   const int N32 = (N + 31) / 32;
-  const int mb = M <= 32 ? 1 : (M <= 64 ? 2 : 4);
-  const int nw = nprod == 3 ? FC_P_NW3 : 4;   // waves (32-column groups) per block
+  // three products above 128 rows: one 256 x 256 tile per block (8 waves of 256 rows x 32 columns,
+  // one block per CU).  Per 32-deep K step a CU then moves 32 KiB of activations (shared by the 8
+  // waves through LDS) and 32 KiB of weights for 48 MFMAs per wave, 21 B per cycle of MFMA time,
+  // where three 128 x 128 blocks per CU moved 43 B / cycle, ~2/3 of an XCD's L2 bandwidth per CU
+  const bool big = nprod == 3 && M > 128 && FC_P_BIG;
+  const int mb = M <= 32 ? 1 : (M <= 64 ? 2 : (big ? 8 : 4));
+  const int nw = big ? 8 : (nprod == 3 ? FC_P_NW3 : 4);   // waves (32-column groups) per block
   const int grid = fc_grid((M + 32 * mb - 1) / (32 * mb), (N32 + nw - 1) / nw, S);
   const _Float16* h = static_cast<const _Float16*>(Ah);
   const _Float16* l = static_cast<const _Float16*>(Al);
@@ -572,6 +626,9 @@ hipError_t launch_fc_gemm_x3p(const void* Ah, const void* Al, int lda, const voi
   } else {
     if (mb == 1) MP_FCP3(1);
     else if (mb == 2) MP_FCP3(2);
+    else if (mb == 8)
+      hipLaunchKernelGGL((fc_gemm_x3p_kernel<3, 8, FC_P_BK3, 1, 8>), dim3(grid), dim3(512), 0, st, h, l, lda, w, part,
+                         M, K, N32, kslice, unscale, S);
     else MP_FCP3(4);
   }
 #undef MP_FCP
@@ -678,6 +735,9 @@ int fc_choose_splits(int M, int K, int N, int* kslice) {
   }();
   int S = K >= 32768 ? std::max(1, K / ksz) : std::min(64, (K + smallk - 1) / smallk);
   if (K >= 32768 && !kenv) S = std::min(std::max(S, (384 + nt - 1) / nt), K / 512);
+  // N a multiple of 256 (fc_1: 1,024): the 256 x 256 tiles of launch_fc_gemm_x3p's 256-row kernel,
+  // 256 / (N / 256) K slices (64 for fc_1: one block on each of the 256 CUs at batch 256)
+  if (K >= 32768 && !kenv && FC_P_BIG && N % 256 == 0) S = std::min(std::max(1, 256 / (N / 256)), K / 512);
   if (S < 1) S = 1;
   int ks = (K + S - 1) / S;
   const int q = K % 64 == 0 ? 64 : FC_BK;   // whole 64-deep steps where K allows (the one-product kernel)

@@ -659,36 +659,17 @@ __device__ __forceinline__ int f3_reader(int tid, int& fx, int& c) {   // round 
   c = 2 * r + (j & 1);
   return r;
 }
-__global__ __launch_bounds__(FNT, 3) void fft_fwd3_kernel(const float* __restrict__ src, void* __restrict__ S,
-                                                         int H, int W) {
-  __shared__ uint32_t lds3[F3_LDS];
+// The forward half of the three-blocks-per-CU kernels, from the row FFT input on: the row threads
+// (tid < 128: y = tid >> 1, pair p = tid & 1) hold the packed row v (channels 2p, 2p+1 of row y,
+// zero padded); the forward row FFT, the two-round 2-channel transpose, the column FFT and the
+// LDS-staged S stores.  Called by every thread of the block (it contains barriers); lds3's space must
+// be free on entry (the caller's barrier).
+__device__ __forceinline__ void fwd3_tail(cpx (&v)[72], uint32_t* lds3, void* __restrict__ S, int b, int cq, int tid) {
   cpx* T2 = reinterpret_cast<cpx*>(lds3);
-  const int b = fft_block_img(blockIdx.x), cq = fft_block_cq(blockIdx.x);
-  const int q = cq >> 1, e0 = 4 * (cq & 1);
-  const int tid = threadIdx.x;
   int rfx = 0, rc = 0;
   const int round = f3_reader(tid, rfx, rc);
-  cpx v[72];
   const int y = tid >> 1, p = tid & 1;
-  if (tid < 128) {
-    const size_t row = c8_index(b, q, y < H ? y : 0, 0, e0, H, W);
-#pragma unroll
-    for (int k = 0; k < 32; ++k) {
-      const int x = 2 * k + p;
-      const bool in = y < H && x < W;
-      f32x4 u = *reinterpret_cast<const f32x4*>(src + row + 8 * min(x, W - 1));
-      if (!in) u = f32x4{0.f, 0.f, 0.f, 0.f};
-      const cpx lo = {u[0], u[1]}, hi = {u[2], u[3]};
-      const cpx mine = p ? hi : lo, send = p ? lo : hi;
-      const cpx recv = {__int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(send.x), 0xB1, 0xF, 0xF, false)),
-                        __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(send.y), 0xB1, 0xF, 0xF, false))};
-      v[2 * k] = p ? recv : mine;
-      v[2 * k + 1] = p ? mine : recv;
-    }
-#pragma unroll
-    for (int x = 64; x < 72; ++x) v[x] = {0.f, 0.f};
-    fft72<-1>(v);
-  }
+  if (tid < 128) fft72<-1>(v);
   // rounds: the row threads of pair `pr` write the half spectra of their two channels into T2
   auto write_pair = [&](int pr) {
     if (tid < 128 && p == pr) {
@@ -737,6 +718,34 @@ __global__ __launch_bounds__(FNT, 3) void fft_fwd3_kernel(const float* __restric
       st16(dst + (ffx * 72 + 36 * half) * 2 + w, *reinterpret_cast<const uint4*>(lds3 + ffx * STG_LD + w * 4));
     }
   }
+}
+__global__ __launch_bounds__(FNT, 3) void fft_fwd3_kernel(const float* __restrict__ src, void* __restrict__ S,
+                                                         int H, int W) {
+  __shared__ uint32_t lds3[F3_LDS];
+  const int b = fft_block_img(blockIdx.x), cq = fft_block_cq(blockIdx.x);
+  const int q = cq >> 1, e0 = 4 * (cq & 1);
+  const int tid = threadIdx.x;
+  cpx v[72];
+  const int y = tid >> 1, p = tid & 1;
+  if (tid < 128) {
+    const size_t row = c8_index(b, q, y < H ? y : 0, 0, e0, H, W);
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      const int x = 2 * k + p;
+      const bool in = y < H && x < W;
+      f32x4 u = *reinterpret_cast<const f32x4*>(src + row + 8 * min(x, W - 1));
+      if (!in) u = f32x4{0.f, 0.f, 0.f, 0.f};
+      const cpx lo = {u[0], u[1]}, hi = {u[2], u[3]};
+      const cpx mine = p ? hi : lo, send = p ? lo : hi;
+      const cpx recv = {__int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(send.x), 0xB1, 0xF, 0xF, false)),
+                        __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(send.y), 0xB1, 0xF, 0xF, false))};
+      v[2 * k] = p ? recv : mine;
+      v[2 * k + 1] = p ? mine : recv;
+    }
+#pragma unroll
+    for (int x = 64; x < 72; ++x) v[x] = {0.f, 0.f};
+  }
+  fwd3_tail(v, lds3, S, b, cq, tid);
 }
 
 #ifndef FFT_FWD3
@@ -888,6 +897,164 @@ __global__ __launch_bounds__(FNT, BF ? FFT_MINB_BF : FFT_MINB) void fft_inv_a_fw
   FFT_STAMP_AT(4);
   fwd_cols_to_S<BF>(T, S, b, cq, tid);
   FFT_STAMP_AT(5);
+}
+
+// ---------------------------------------------------------------------------------------------
+// fp32 inverse kernels at three blocks per CU (FFT_INV3).  The 77 KB four-channel tile of
+// inv_cols_to_T / inv_row_from_T is replaced by a 2-channel tile (64 rows x (2 x 37 + 1) complex,
+// 37.5 KB) filled in two rounds: round r carries channel pair r from the column threads to the row
+// threads of pair r, so every thread holds at most one 72-point vector (column, then row) and the
+// block's LDS is fft_fwd3_kernel's 43.8 KB staging buffer.  The inverse rows then stay in registers:
+// the row threads of a lane pair (y, p = 0 / 1) run the epilogue on their own two channels, trading
+// the other channel pair of each pixel with the partner lane (DPP) so that every map access is one
+// 16-byte load / store of a pixel's 4 channels, as the forward row loads of fft_fwd3_kernel.  No
+// parking of P or I in LDS; values and rounding are those of the two-block kernels (bit-identical).
+#ifndef FFT_INV3
+#define FFT_INV3 0
+#endif
+#ifndef I3_FENCE
+#define I3_FENCE 6   // row-tile reads per compiler fence (the old values of v stay live in the other lanes)
+#endif
+#ifndef I3_EFENCE
+#define I3_EFENCE 4  // epilogue pixel pairs per compiler fence
+#endif
+constexpr int I3_LD = 2 * FX + 1;   // complex pitch of a row y of the inverse tile (odd: conflict-free row reads)
+static_assert(64 * I3_LD * 2 <= F3_LDS, "the inverse 2-channel tile fits in the staging buffer");
+// the inverse column (fx, c = 2 r + cc) thread tid carries, and its round r (-1: none).  tid < 128:
+// lanes 4 fx .. 4 fx + 3 hold channels 0, 2, 1, 3 of fx (one 32-byte Y group per quad, as before)
+__device__ __forceinline__ int i3_col(int tid, int& fx, int& cc) {
+  int j, r;
+  if (tid < 128) { j = tid >> 1; r = tid & 1; }
+  else if (tid < 138) { j = 64 + (tid - 128); r = 1; }
+  else if (tid < 148) { j = 64 + (tid - 138); r = 0; }
+  else return -1;
+  fx = j >> 1;
+  cc = j & 1;
+  return r;
+}
+__device__ __forceinline__ cpx dpp_swap_pair(cpx a) {   // the partner lane's value (quad_perm [1,0,3,2])
+  return {__int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(a.x), 0xB1, 0xF, 0xF, false)),
+          __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(a.y), 0xB1, 0xF, 0xF, false))};
+}
+// Y -> the inverse rows in registers: for the row threads tid < 128 with y = tid >> 1 < H,
+// v[x] = (channel e0 + 2p, channel e0 + 2p + 1) of P at pixel (y, x), x < 64.  Called by every thread.
+__device__ __forceinline__ void inv3_front(const void* __restrict__ Y, int b, int cq, int tid, int H, cpx* T2,
+                                           cpx (&v)[72]) {
+  int fx = 0, cc = 0;
+  const int r = i3_col(tid, fx, cc);
+  if (r >= 0) {
+    const cpx* src = static_cast<const cpx*>(Y) + (((size_t)b * 16 + cq) * NF + spec_f<false>(fx, 0)) * 4 + 2 * r + cc;
+    constexpr int FS = spec_f<false>(0, 1) * 4;
+#pragma unroll
+    for (int fy = 0; fy < 72; ++fy) v[fy] = src[fy * FS];
+    fft72<1>(v);
+  }
+  const int y = tid >> 1, p = tid & 1;
+  const bool row = tid < 128 && y < H;
+  auto put = [&](int rr) {
+    if (r == rr) {
+#pragma unroll
+      for (int yy = 0; yy < 64; ++yy) T2[yy * I3_LD + cc * FX + fx] = v[yy];
+    }
+  };
+  auto get = [&](int rr) {   // inv_row_from_T on the 2-channel tile
+    if (row && p == rr) {
+      const int ta = y * I3_LD, tb = ta + FX;
+#pragma unroll
+      for (int k = 0; k < FX; ++k) {
+        const cpx A = T2[ta + k], B = T2[tb + k];
+        v[k] = cfma(swp(B), cpx{-1.f, 1.f}, A);
+        if (k > 0 && k < FX - 1) v[72 - k] = cfma(A, cpx{1.f, -1.f}, swp(B));
+        if (I3_FENCE && k % I3_FENCE == I3_FENCE - 1) asm volatile("" ::: "memory");   // bounds the hoisted reads
+      }
+    }
+  };
+  put(0);
+  lds_barrier();
+  get(0);
+  lds_barrier();
+  put(1);
+  lds_barrier();
+  get(1);
+  // the row FFT under a wave-uniform branch (rows y >= H transform stale values nobody reads): under
+  // the per-lane `row` the other lanes' column values had to stay live beside the transform (372 B /
+  // lane of scratch at 168 VGPRs; 12 B this way)
+  if (__builtin_amdgcn_readfirstlane(tid >> 6) < 2) fft72<1>(v);
+}
+
+// fft_inv_a_fwd_kernel at three blocks per CU (fp32 spectra and maps)
+__global__ __launch_bounds__(FNT, 3) void fft_inv_a_fwd3_kernel(const void* __restrict__ Y, ConvArgs pa,
+                                                               void* __restrict__ S) {
+  __shared__ uint32_t lds3[F3_LDS];
+  const int H = pa.H, W = pa.W;
+  const int b = fft_block_img(blockIdx.x), cq = fft_block_cq(blockIdx.x);
+  const int q = cq >> 1, e0 = 4 * (cq & 1);
+  const int tid = threadIdx.x;
+  cpx v[72];
+  inv3_front(Y, b, cq, tid, H, reinterpret_cast<cpx*>(lds3), v);
+  const int y = tid >> 1, p = tid & 1;
+  if (__builtin_amdgcn_readfirstlane(tid >> 6) < 2) {   // the row waves (wave-uniform, see inv3_front)
+    // the A epilogue (hgru_module.py:797-799) on this lane's channel pair: lane p loads all 4
+    // channels of pixel 2k + p and keeps pair p; the partner's pair of that pixel goes by DPP.
+    // Rows y >= H and columns x >= W become the forward transform's zero padding.
+    const int ch = 8 * q + e0 + 2 * p;
+    const cpx lat = {pa.vecs[V_LAT * 64 + ch], pa.vecs[V_LAT * 64 + ch + 1]};
+    const cpx be = {pa.vecs[V_BETA * 64 + ch], pa.vecs[V_BETA * 64 + ch + 1]};
+    const cpx nu = {pa.vecs[V_NU * 64 + ch], pa.vecs[V_NU * 64 + ch + 1]};
+    const bool yin = y < H;
+    const size_t row = c8_index(b, q, min(y, H - 1), 0, e0, H, W);
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      const int xo = 2 * k + p;
+      const size_t idx = row + 8 * min(xo, W - 1);   // unconditional (clamped) loads
+      const f32x4 xu = *reinterpret_cast<const f32x4*>(pa.X + idx);
+      const f32x4 ou = *reinterpret_cast<const f32x4*>(pa.O + idx);
+      const cpx xm = p ? cpx{xu[2], xu[3]} : cpx{xu[0], xu[1]}, xs = p ? cpx{xu[0], xu[1]} : cpx{xu[2], xu[3]};
+      const cpx om = p ? cpx{ou[2], ou[3]} : cpx{ou[0], ou[1]}, os = p ? cpx{ou[0], ou[1]} : cpx{ou[2], ou[3]};
+      const cpx xr = dpp_swap_pair(xs), orr = dpp_swap_pair(os);
+      cpx iv[2];
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {   // pixel 2k + e: own load (e == p) or the partner's
+        const cpx xe = e == p ? xm : xr, oe = e == p ? om : orr, pv = v[2 * k + e];
+        const float i0 = atanh_f(xe.x - (be.x * oe.x + nu.x) * (pv.x + lat.x));
+        const float i1 = atanh_f(xe.y - (be.y * oe.y + nu.y) * (pv.y + lat.y));
+        iv[e] = yin && 2 * k + e < W ? cpx{i0, i1} : cpx{0.f, 0.f};
+      }
+      v[2 * k] = iv[0];
+      v[2 * k + 1] = iv[1];
+      // pixel 2k + p's 4 channels: this lane's pair and the partner's pair of the same pixel
+      const cpx mine = p ? iv[1] : iv[0], other = dpp_swap_pair(p ? iv[0] : iv[1]);
+      const f32x4 o4 = p ? f32x4{other.x, other.y, mine.x, mine.y} : f32x4{mine.x, mine.y, other.x, other.y};
+      if (yin && xo < W) map_st4_stream<false>(pa.dst, idx, o4);
+      if (I3_EFENCE && k % I3_EFENCE == I3_EFENCE - 1) asm volatile("" ::: "memory");
+    }
+#pragma unroll
+    for (int x = 64; x < 72; ++x) v[x] = {0.f, 0.f};
+  }
+  lds_barrier();   // every inverse row has read the tile
+  fwd3_tail(v, lds3, S, b, cq, tid);
+}
+
+// fft_inv_kernel at three blocks per CU (fp32 spectra and maps): Y -> P (C8)
+__global__ __launch_bounds__(FNT, 3) void fft_inv3_kernel(const void* __restrict__ Y, float* __restrict__ P, int H,
+                                                         int W) {
+  __shared__ uint32_t lds3[F3_LDS];
+  const int b = fft_block_img(blockIdx.x), cq = fft_block_cq(blockIdx.x);
+  const int q = cq >> 1, e0 = 4 * (cq & 1);
+  const int tid = threadIdx.x;
+  cpx v[72];
+  inv3_front(Y, b, cq, tid, H, reinterpret_cast<cpx*>(lds3), v);
+  const int y = tid >> 1, p = tid & 1;
+  if (__builtin_amdgcn_readfirstlane(tid >> 6) < 2) {
+    const size_t row = c8_index(b, q, min(y, H - 1), 0, e0, H, W);
+#pragma unroll
+    for (int k = 0; k < 32; ++k) {
+      const int xo = 2 * k + p;
+      const cpx mine = p ? v[2 * k + 1] : v[2 * k], other = dpp_swap_pair(p ? v[2 * k] : v[2 * k + 1]);
+      const f32x4 o4 = p ? f32x4{other.x, other.y, mine.x, mine.y} : f32x4{mine.x, mine.y, other.x, other.y};
+      if (y < H && xo < W) map_st4_stream<false>(P, row + 8 * xo, o4);
+    }
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1535,6 +1702,8 @@ hipError_t launch_fft_inv_a_fwd(const void* Y, const ConvArgs& a, void* S, int B
     hipLaunchKernelGGL((fft_inv_a_fwd_kernel<true, true>), dim3(B * 16), dim3(FNT), 0, st, Y, a, S);
   else if (bf)
     hipLaunchKernelGGL((fft_inv_a_fwd_kernel<true, false>), dim3(B * 16), dim3(FNT), 0, st, Y, a, S);
+  else if (FFT_INV3 && !fy_major<false>())
+    hipLaunchKernelGGL(fft_inv_a_fwd3_kernel, dim3(B * 16), dim3(FNT), 0, st, Y, a, S);
   else
     hipLaunchKernelGGL((fft_inv_a_fwd_kernel<false, false>), dim3(B * 16), dim3(FNT), 0, st, Y, a, S);
   return hipGetLastError();
@@ -1557,6 +1726,8 @@ hipError_t launch_fft_inv(const void* Y, float* P, int B, int H, int W, hipStrea
     hipLaunchKernelGGL((fft_inv_kernel<true, true>), dim3(B * 16), dim3(FNT), 0, st, Y, P, H, W);
   else if (bf)
     hipLaunchKernelGGL((fft_inv_kernel<true, false>), dim3(B * 16), dim3(FNT), 0, st, Y, P, H, W);
+  else if (FFT_INV3 && !fy_major<false>())
+    hipLaunchKernelGGL(fft_inv3_kernel, dim3(B * 16), dim3(FNT), 0, st, Y, P, H, W);
   else
     hipLaunchKernelGGL((fft_inv_kernel<false, false>), dim3(B * 16), dim3(FNT), 0, st, Y, P, H, W);
   return hipGetLastError();
