@@ -256,6 +256,12 @@ __device__ __forceinline__ float rtanh(float x) {
   q = fmaf(x2, q, 4.89352518554385e-03f);
   return p * __builtin_amdgcn_rcpf(q);
 }
+// the A epilogue's tanh argument x - (beta o + nu) (p + lateral_bias) (hgru_module.py:797-799) with
+// both contractions written out: left to -ffp-contract, whether a product was fused into the
+// following add depended on the surrounding code, and the small-batch kernels rounded differently
+__device__ __forceinline__ float epi_a(float x, float o, float p, float be, float nu, float lat) {
+  return fmaf(-fmaf(be, o, nu), p + lat, x);
+}
 __device__ __forceinline__ float atanh_f(float x) {
   if constexpr (FFT_TANH == 1) return ftanh(x);
   else if constexpr (FFT_TANH == 2) return rtanh(x);
@@ -282,16 +288,19 @@ __device__ __forceinline__ void dft8(cpx (&x)[8]) {
   const cpx b0 = a0 + a2, b2 = a0 - a2, b1 = a1 + a3, b3 = a1 - a3;
   const cpx b4 = a4 + a6, b6 = a4 - a6, b5 = a5 + a7, b7 = a5 - a7;
   const cpx t6 = rotq<S>(b6);
-  const cpx t5 = cfma(swp(b5), cpx{(float)-S, (float)S}, b5) * H;    // b5 * W8^1 = H (b5 + rotq b5)
-  const cpx t7 = cfma(swp(b7), cpx{(float)-S, (float)S}, -b7) * H;   // b7 * W8^3 = H (rotq b7 - b7)
+  // b5 * W8^1 = H (b5 + rotq b5), b7 * W8^3 = H (rotq b7 - b7): the products by H fused into the
+  // butterflies explicitly (contraction left to the compiler was decided per call site: the same
+  // transform rounded differently in the batched and the small-batch kernels)
+  const cpx u5 = cfma(swp(b5), cpx{(float)-S, (float)S}, b5);
+  const cpx u7 = cfma(swp(b7), cpx{(float)-S, (float)S}, -b7);
   x[0] = b0 + b4;
   x[4] = b0 - b4;
   x[2] = b2 + t6;
   x[6] = b2 - t6;
-  x[1] = b1 + t5;
-  x[5] = b1 - t5;
-  x[3] = b3 + t7;
-  x[7] = b3 - t7;
+  x[1] = cfma(u5, cpx{H, H}, b1);
+  x[5] = cfma(u5, cpx{-H, -H}, b1);
+  x[3] = cfma(u7, cpx{H, H}, b3);
+  x[7] = cfma(u7, cpx{-H, -H}, b3);
 }
 
 template <int S>
@@ -299,10 +308,9 @@ __device__ __forceinline__ void dft3(cpx& z0, cpx& z1, cpx& z2) {
   constexpr float R3 = 0.86602540378443865f;
   const cpx t = z1 + z2, d = z1 - z2;
   const cpx m = z0 - scale(t, 0.5f);
-  const cpx s = swp(d) * cpx{-S * R3, S * R3};
   z0 = z0 + t;
-  z1 = m + s;
-  z2 = m - s;
+  z1 = cfma(swp(d), cpx{-S * R3, S * R3}, m);   // m + s, s = swp(d) (-S R3, S R3): fused explicitly
+  z2 = cfma(swp(d), cpx{S * R3, -S * R3}, m);   // m - s (see dft8)
 }
 
 // 9-point DFT as 3 x 3 (n = 3a + b, k = c + 3d)
@@ -871,7 +879,7 @@ __global__ __launch_bounds__(FNT, BF ? FFT_MINB_BF : FFT_MINB) void fft_inv_a_fw
 #ifdef FFT_PROBE_NOTANH   // timing probe: the A epilogue without tanhf
             iv[j] = xv[cur][u][j] - (be[j] * ov[cur][u][j] + nu[j]) * (pv[j] + lat[j]);
 #else
-            iv[j] = atanh_f(xv[cur][u][j] - (be[j] * ov[cur][u][j] + nu[j]) * (pv[j] + lat[j]));
+            iv[j] = atanh_f(epi_a(xv[cur][u][j], ov[cur][u][j], pv[j], be[j], nu[j], lat[j]));
 #endif
           }
           map_st4_stream<BM>(p.dst, c8_index(b, q, yy, x, e0, H, W), iv);
@@ -1016,8 +1024,8 @@ __global__ __launch_bounds__(FNT, 3) void fft_inv_a_fwd3_kernel(const void* __re
 #pragma unroll
       for (int e = 0; e < 2; ++e) {   // pixel 2k + e: own load (e == p) or the partner's
         const cpx xe = e == p ? xm : xr, oe = e == p ? om : orr, pv = v[2 * k + e];
-        const float i0 = atanh_f(xe.x - (be.x * oe.x + nu.x) * (pv.x + lat.x));
-        const float i1 = atanh_f(xe.y - (be.y * oe.y + nu.y) * (pv.y + lat.y));
+        const float i0 = atanh_f(epi_a(xe.x, oe.x, pv.x, be.x, nu.x, lat.x));
+        const float i1 = atanh_f(epi_a(xe.y, oe.y, pv.y, be.y, nu.y, lat.y));
         iv[e] = yin && 2 * k + e < W ? cpx{i0, i1} : cpx{0.f, 0.f};
       }
       v[2 * k] = iv[0];
@@ -1055,6 +1063,258 @@ __global__ __launch_bounds__(FNT, 3) void fft_inv3_kernel(const void* __restrict
       if (y < H && xo < W) map_st4_stream<false>(P, row + 8 * xo, o4);
     }
   }
+}
+
+// ---------------------------------------------------------------------------------------------
+// Small-batch (latency) forms of the three fp32 FFT kernels (FFT path, fp32 maps; B <= lfft_maxb()).
+// At batch 1 the batched kernels run 16 blocks, each a chain of per-thread 72-point transforms
+// (~7.4k cycles per row / column phase) and a 21-pixel-per-thread epilogue, so inv_a_fwd takes ~49k
+// cycles (tools/fft_stamps.hip, profiles/r3u).  Here every 72-point transform is spread over 9 lanes
+// exactly along fft72's prime-factor passes: lane n2 runs the 8-point DFT of inputs (9 n1 + 8 n2) % 72,
+// the 8 x 9 intermediates cross through LDS, lane k1 runs the 9-point DFT and holds outputs
+// (9 k1 + 64 k2) % 72.  A block is one (image, channel PAIR): 74 column / 64 row transforms x 9 lanes
+// (704 threads), 32 blocks per image.  Every value is produced by the same dft8 / dft9 / pair-separation
+// / epilogue operations on the same operands as in the batched kernels, so the results are
+// bit-identical to them (tests/test_gpu_parity.py::test_batch_invariance_and_determinism runs a crop
+// alone and inside a batch).
+constexpr int LF_NT = 704;             // 11 waves: 74 transforms x 9 lanes (666 used)
+constexpr int LF_T = 74;
+constexpr int LF_ZLD = 73;             // pitch (complex) of a row of the P / I rows and the forward row outputs
+constexpr int LF_BIG = NF * 2;         // complex: the pair's whole spectrum (Y in, or S staging out), 42.6 KB
+static_assert(LF_BIG >= 64 * I3_LD && LF_BIG >= 64 * LF_ZLD && LF_BIG >= LF_T * 72, "LDS plan");
+// block -> (image, channel pair): the four pairs of one C8 chunk (8 channels, 32 B per pixel) on one XCD
+__device__ __forceinline__ void lfft_block(int blk, int& b, int& cp) {
+  b = blk >> 5;
+  const int r = blk & 31;
+  cp = 4 * (r & 7) + (r >> 3);
+}
+// stage 1 of a 9-lane transform: lane j (< 9) = n2: in[n1] = x[(9 n1 + 8 n2) % 72] -> dft8 -> E
+template <int SG>
+__device__ __forceinline__ void lf_stage1(cpx (&in)[8], cpx* E, int t, int j) {
+  dft8<SG>(in);
+#pragma unroll
+  for (int k1 = 0; k1 < 8; ++k1) E[t * 72 + j * 8 + k1] = in[k1];
+}
+// stage 2: lane j (< 8) = k1: u[n2] = E[n2][k1] -> dft9 -> u[k2] = X[(9 k1 + 64 k2) % 72]
+template <int SG>
+__device__ __forceinline__ void lf_stage2(cpx (&u)[9], const cpx* E, int t, int j) {
+#pragma unroll
+  for (int n2 = 0; n2 < 9; ++n2) u[n2] = E[t * 72 + n2 * 8 + j];
+  dft9<SG>(u);
+}
+__device__ __forceinline__ int lf_in(int n1, int j) { return (9 * n1 + 8 * j) % 72; }
+__device__ __forceinline__ int lf_out(int j, int k2) { return (9 * j + 64 * k2) % 72; }
+
+// Y's channel pair (2 cp, 2 cp + 1) -> the P rows in R[y][x] (y, x < 64).  The spectrum is first
+// copied into LDS with one 16-byte load per frequency (both channels; the wave reads 64 consecutive
+// 32-byte groups), since the transforms' own access order scatters over the whole 85 KB run.
+// Big: LF_BIG complex of LDS (the Y copy, then the inverse tile).  Called by every thread.
+__device__ __forceinline__ void lf_inverse(const void* __restrict__ Y, int b, int cp, int tid, cpx* E, cpx* Big,
+                                           cpx* R) {
+  const int cq = cp >> 1, pp = cp & 1, t = tid / 9, j = tid - 9 * t;
+  const float4* ysrc = reinterpret_cast<const float4*>(Y) + ((size_t)b * 16 + cq) * NF * 2 + pp;
+  for (int f = tid; f < NF; f += LF_NT) {
+    const float4 v = ysrc[2 * f];
+    Big[2 * f] = cpx{v.x, v.y};
+    Big[2 * f + 1] = cpx{v.z, v.w};
+  }
+  lds_barrier();
+  cpx in[8], u[9];
+  // inverse column (fx, cc) = (t >> 1, t & 1) over fy (inv_cols_to_T)
+  if (t < LF_T && j < 9) {
+    const int fx = t >> 1, cc = t & 1;
+#pragma unroll
+    for (int n1 = 0; n1 < 8; ++n1) in[n1] = Big[2 * spec_f<false>(fx, lf_in(n1, j)) + cc];
+    lf_stage1<1>(in, E, t, j);
+  }
+  lds_barrier();   // stage 1 done: E complete, the Y copy no longer read
+  if (t < LF_T && j < 8) {
+    const int fx = t >> 1, cc = t & 1;
+    lf_stage2<1>(u, E, t, j);
+#pragma unroll
+    for (int k2 = 0; k2 < 9; ++k2) {
+      const int y = lf_out(j, k2);
+      if (y < 64) Big[y * I3_LD + cc * FX + fx] = u[k2];
+    }
+  }
+  lds_barrier();
+  // inverse row y = t: C[m] = A[m] + i B[m] from the Hermitian half spectra (inv_row_from_T)
+  if (t < 64 && j < 9) {
+#pragma unroll
+    for (int n1 = 0; n1 < 8; ++n1) {
+      const int m = lf_in(n1, j), k = m <= 36 ? m : 72 - m;
+      const cpx A = Big[t * I3_LD + k], B = Big[t * I3_LD + FX + k];
+      in[n1] = m <= 36 ? cfma(swp(B), cpx{-1.f, 1.f}, A) : cfma(A, cpx{1.f, -1.f}, swp(B));
+    }
+    lf_stage1<1>(in, E, t, j);
+  }
+  lds_barrier();
+  if (t < 64 && j < 8) {
+    lf_stage2<1>(u, E, t, j);
+#pragma unroll
+    for (int k2 = 0; k2 < 9; ++k2) {
+      const int x = lf_out(j, k2);
+      if (x < 64) R[t * LF_ZLD + x] = u[k2];
+    }
+  }
+  lds_barrier();
+}
+
+// the rows R[y][x] (x < 64; zero outside the map) -> S for the channel pair: forward rows, forward
+// columns, and the pair's S entries (hi / lo, 8 B each per frequency) staged in LDS and stored in
+// frequency order.  R must be complete on entry; Big's space is free (reused for the row outputs,
+// then the staging).  Called by every thread.
+__device__ __forceinline__ void lf_forward(const cpx* R, int b, int cp, int tid, cpx* E, cpx* Big,
+                                           void* __restrict__ S) {
+  const int cq = cp >> 1, pp = cp & 1, t = tid / 9, j = tid - 9 * t;
+  cpx in[8], u[9];
+  if (t < 64 && j < 9) {
+#pragma unroll
+    for (int n1 = 0; n1 < 8; ++n1) {
+      const int x = lf_in(n1, j);
+      in[n1] = x < 64 ? R[t * LF_ZLD + x] : cpx{0.f, 0.f};
+    }
+    lf_stage1<-1>(in, E, t, j);
+  }
+  lds_barrier();
+  if (t < 64 && j < 8) {
+    lf_stage2<-1>(u, E, t, j);
+#pragma unroll
+    for (int k2 = 0; k2 < 9; ++k2) Big[t * LF_ZLD + lf_out(j, k2)] = u[k2];
+  }
+  lds_barrier();
+  // forward column (fx, cc): the pair-separated half spectra of rows y (fwd_rows_to_T), then over y
+  if (t < LF_T && j < 9) {
+    const int fx = t >> 1, cc = t & 1;
+#pragma unroll
+    for (int n1 = 0; n1 < 8; ++n1) {
+      const int y = lf_in(n1, j);
+      cpx v = {0.f, 0.f};
+      if (y < 64) {
+        const cpx zk = Big[y * LF_ZLD + fx], zm = Big[y * LF_ZLD + (72 - fx) % 72];
+        v = cc == 0 ? cfma(zm, cpx{1.f, -1.f}, zk) * 0.5f : cfma(swp(zk), cpx{1.f, -1.f}, swp(zm)) * 0.5f;
+      }
+      in[n1] = v;
+    }
+    lf_stage1<-1>(in, E, t, j);
+  }
+  lds_barrier();   // the row outputs are no longer read: Big becomes the S staging [f][hi cc0, hi cc1, lo cc0, lo cc1]
+  uint32_t* stg = reinterpret_cast<uint32_t*>(Big);
+  if (t < LF_T && j < 8) {
+    const int fx = t >> 1, cc = t & 1;
+    lf_stage2<-1>(u, E, t, j);
+#pragma unroll
+    for (int k2 = 0; k2 < 9; ++k2) {
+      const cpx z = u[k2];
+      const float re = z.x * SPEC_SCALE, im = z.y * SPEC_SCALE;
+      const _Float16 hr = (_Float16)re, hi = (_Float16)im;
+      const f16x2 hv = {hr, hi}, lv = {(_Float16)(re - (float)hr), (_Float16)(im - (float)hi)};
+      const int f = spec_f<false>(fx, lf_out(j, k2));
+      stg[4 * f + cc] = __builtin_bit_cast(uint32_t, hv);
+      stg[4 * f + 2 + cc] = __builtin_bit_cast(uint32_t, lv);
+    }
+  }
+  lds_barrier();
+  // S group (b, cq, f): [hi c0..c3 | lo c0..c3], 4 B each; this pair's hi at 8 pp, lo at 16 + 8 pp
+  uint2* dst = reinterpret_cast<uint2*>(S) + ((size_t)b * 16 + cq) * NF * 4 + pp;
+  for (int f = tid; f < NF; f += LF_NT) {
+    const uint4 w = *reinterpret_cast<const uint4*>(stg + 4 * f);
+    dst[4 * f] = uint2{w.x, w.y};
+    dst[4 * f + 2] = uint2{w.z, w.w};
+  }
+}
+
+// pixels of the pixel-major passes: thread tid takes pixels tid + LF_NT i (i < LF_PX)
+constexpr int LF_PX = (64 * 64 + LF_NT - 1) / LF_NT;   // 6
+
+__global__ __launch_bounds__(LF_NT, 1) void lfft_inv_a_fwd_kernel(const void* __restrict__ Y, ConvArgs pa,
+                                                                 void* __restrict__ S) {
+  __shared__ cpx E[LF_T * 72];
+  __shared__ cpx Big[LF_BIG];
+  __shared__ cpx R[64 * LF_ZLD];   // the P rows, then the I rows
+  const int H = pa.H, W = pa.W;
+  int b, cp;
+  lfft_block(blockIdx.x, b, cp);
+  const int q = cp >> 2, ec = 2 * (cp & 3);   // C8 chunk and the pair's first channel in it
+  const int tid = threadIdx.x;
+  // the A epilogue's X / O of this thread's pixels, issued first (clamped addresses)
+  cpx xv[LF_PX], ov[LF_PX];
+#pragma unroll
+  for (int i = 0; i < LF_PX; ++i) {
+    const int px = min(tid + LF_NT * i, 64 * 64 - 1), y = min(px >> 6, H - 1), x = min(px & 63, W - 1);
+    const size_t idx = c8_index(b, q, y, x, ec, H, W);
+    xv[i] = map_ld2<false>(pa.X, idx);
+    ov[i] = map_ld2<false>(pa.O, idx);
+  }
+  lf_inverse(Y, b, cp, tid, E, Big, R);
+  // the A epilogue (hgru_module.py:797-799), pixel-major over the P rows; I back into R
+  const int ch = 8 * q + ec;
+  const cpx lat = {pa.vecs[V_LAT * 64 + ch], pa.vecs[V_LAT * 64 + ch + 1]};
+  const cpx be = {pa.vecs[V_BETA * 64 + ch], pa.vecs[V_BETA * 64 + ch + 1]};
+  const cpx nu = {pa.vecs[V_NU * 64 + ch], pa.vecs[V_NU * 64 + ch + 1]};
+#pragma unroll
+  for (int i = 0; i < LF_PX; ++i) {
+    const int px = tid + LF_NT * i;
+    if (px >= 64 * 64) break;
+    const int y = px >> 6, x = px & 63;
+    cpx iv = {0.f, 0.f};
+    if (y < H && x < W) {
+      const cpx pv = R[y * LF_ZLD + x];
+      iv = {atanh_f(epi_a(xv[i].x, ov[i].x, pv.x, be.x, nu.x, lat.x)),
+            atanh_f(epi_a(xv[i].y, ov[i].y, pv.y, be.y, nu.y, lat.y))};
+      *reinterpret_cast<float2*>(pa.dst + c8_index(b, q, y, x, ec, H, W)) = float2{iv.x, iv.y};
+    }
+    R[y * LF_ZLD + x] = iv;
+  }
+  lds_barrier();
+  lf_forward(R, b, cp, tid, E, Big, S);
+}
+
+__global__ __launch_bounds__(LF_NT, 1) void lfft_inv_kernel(const void* __restrict__ Y, float* __restrict__ P, int H,
+                                                           int W) {
+  __shared__ cpx E[LF_T * 72];
+  __shared__ cpx Big[LF_BIG];
+  __shared__ cpx R[64 * LF_ZLD];
+  int b, cp;
+  lfft_block(blockIdx.x, b, cp);
+  const int q = cp >> 2, ec = 2 * (cp & 3);
+  const int tid = threadIdx.x;
+  lf_inverse(Y, b, cp, tid, E, Big, R);
+  for (int px = tid; px < 64 * 64; px += LF_NT) {
+    const int y = px >> 6, x = px & 63;
+    if (y < H && x < W) {
+      const cpx v = R[y * LF_ZLD + x];
+      *reinterpret_cast<float2*>(P + c8_index(b, q, y, x, ec, H, W)) = float2{v.x, v.y};
+    }
+  }
+}
+
+__global__ __launch_bounds__(LF_NT, 1) void lfft_fwd_kernel(const float* __restrict__ src, void* __restrict__ S, int H,
+                                                           int W) {
+  __shared__ cpx E[LF_T * 72];
+  __shared__ cpx Big[LF_BIG];
+  __shared__ cpx R[64 * LF_ZLD];
+  int b, cp;
+  lfft_block(blockIdx.x, b, cp);
+  const int q = cp >> 2, ec = 2 * (cp & 3);
+  const int tid = threadIdx.x;
+  for (int px = tid; px < 64 * 64; px += LF_NT) {   // the pair's map rows, zero outside the map
+    const int y = px >> 6, x = px & 63;
+    R[y * LF_ZLD + x] = (y < H && x < W) ? map_ld2<false>(src, c8_index(b, q, y, x, ec, H, W)) : cpx{0.f, 0.f};
+  }
+  lds_barrier();
+  lf_forward(R, b, cp, tid, E, Big, S);
+}
+
+#ifndef LFFT_MAXB
+#define LFFT_MAXB 8   // largest batch for the latency kernels (profiles/r3y: B = 8 1.166 -> 1.126 ms, B = 16 1.354 -> 1.645); MP_LFFT_MAXB overrides, 0 = off
+#endif
+static int lfft_maxb() {
+  static const int v = [] {
+    const char* e = std::getenv("MP_LFFT_MAXB");
+    return e ? std::atoi(e) : LFFT_MAXB;
+  }();
+  return v;
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -1686,7 +1946,9 @@ hipError_t build_spec_weights(const float* w, int ks, void* Gx, float* unscale, 
 }
 
 hipError_t launch_fft_fwd(const float* act, void* S, int B, int H, int W, hipStream_t st, bool bf) {
-  if (bf && fft_bf16_maps())
+  if (!bf && !fy_major<false>() && B <= lfft_maxb())
+    hipLaunchKernelGGL(lfft_fwd_kernel, dim3(B * 32), dim3(LF_NT), 0, st, act, S, H, W);
+  else if (bf && fft_bf16_maps())
     hipLaunchKernelGGL((fft_fwd_kernel<true, true>), dim3(B * 16), dim3(FNT), 0, st, act, S, H, W);
   else if (bf)
     hipLaunchKernelGGL((fft_fwd_kernel<true, false>), dim3(B * 16), dim3(FNT), 0, st, act, S, H, W);
@@ -1698,7 +1960,9 @@ hipError_t launch_fft_fwd(const float* act, void* S, int B, int H, int W, hipStr
 }
 
 hipError_t launch_fft_inv_a_fwd(const void* Y, const ConvArgs& a, void* S, int B, hipStream_t st, bool bf) {
-  if (bf && fft_bf16_maps())
+  if (!bf && !fy_major<false>() && B <= lfft_maxb())
+    hipLaunchKernelGGL(lfft_inv_a_fwd_kernel, dim3(B * 32), dim3(LF_NT), 0, st, Y, a, S);
+  else if (bf && fft_bf16_maps())
     hipLaunchKernelGGL((fft_inv_a_fwd_kernel<true, true>), dim3(B * 16), dim3(FNT), 0, st, Y, a, S);
   else if (bf)
     hipLaunchKernelGGL((fft_inv_a_fwd_kernel<true, false>), dim3(B * 16), dim3(FNT), 0, st, Y, a, S);
@@ -1722,7 +1986,9 @@ hipError_t launch_spec_gemm(const void* S, const void* Gx, void* Y, int B, float
 }
 
 hipError_t launch_fft_inv(const void* Y, float* P, int B, int H, int W, hipStream_t st, bool bf) {
-  if (bf && fft_bf16_maps())
+  if (!bf && !fy_major<false>() && B <= lfft_maxb())
+    hipLaunchKernelGGL(lfft_inv_kernel, dim3(B * 32), dim3(LF_NT), 0, st, Y, P, H, W);
+  else if (bf && fft_bf16_maps())
     hipLaunchKernelGGL((fft_inv_kernel<true, true>), dim3(B * 16), dim3(FNT), 0, st, Y, P, H, W);
   else if (bf)
     hipLaunchKernelGGL((fft_inv_kernel<true, false>), dim3(B * 16), dim3(FNT), 0, st, Y, P, H, W);
