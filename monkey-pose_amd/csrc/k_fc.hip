@@ -125,8 +125,20 @@ __global__ void fc_reduce_kernel(const float* __restrict__ part, int S, int M, i
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= (size_t)M * N) return;
   const int m = i / N, n = i % N;
+  // the S partial slabs summed in slab order; their loads issued 16 at a time (a plain loop left
+  // one load's latency per slab exposed: 9.7 us for fc_1's 64 slabs at batch 1)
   float v = 0.f;
-  for (int s = 0; s < S; ++s) v += part[((size_t)s * M + m) * Npad + n];
+  const float* pp = part + (size_t)m * Npad + n;
+  const size_t ss = (size_t)M * Npad;
+  int s = 0;
+  for (; s + 16 <= S; s += 16) {
+    float t[16];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) t[u] = pp[(size_t)(s + u) * ss];
+#pragma unroll
+    for (int u = 0; u < 16; ++u) v += t[u];
+  }
+  for (; s < S; ++s) v += pp[(size_t)s * ss];
   if (bias) v += bias[n];
   if (relu) v = fmaxf(v, 0.f);
   if (aff_s) v = v * aff_s[n] + aff_t[n];

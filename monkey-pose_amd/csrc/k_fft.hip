@@ -1333,26 +1333,37 @@ static int lfft_maxb() {
 // [b][cq][f]; the weights stream from L2.  Blocks of one frequency quad are placed on one XCD so its
 // weights are fetched from HBM once.
 constexpr int SG_NI = 32;              // images per block
+#ifndef SPEC_SMALLB
+#define SPEC_SMALLB 8   // batches up to this run spec_gemm_kernel<0, 8> (8-image tiles); 0 = off
+#endif
+#ifndef SPEC_SMALL_MINB
+#define SPEC_SMALL_MINB 2   // blocks per CU of the 8-image kernel (3: 168 B / lane of scratch, 0.029 vs 0.019 ms at B = 1, profiles/r3z)
+#endif
 constexpr int NQUAD = NF / 4;          // 666 frequency quads
 constexpr int SG_SLD = 33;             // S tile pitch (16-B units) per (cq, part, f) row
 constexpr int SG_YLD = 16 * 4 * 2 + 1; // Y tile pitch (16-B units) per image
-template <int PROBE = 0>   // timing probes (tools/bench_fft.hip): 1 = no MFMA, 2 = no S / weight loads,
-                           // 3 = no weight loads, 4 = no S loads
-__global__ __launch_bounds__(256, 2) void spec_gemm_kernel(const uint4* __restrict__ S, const uint4* __restrict__ Gc,
+// NI: images per block -- 32, or 8 for batches <= SPEC_SMALLB (a quarter of the S tile's loads and
+// LDS; the MFMA columns of images past NI are zero, the per-output product order is the same)
+template <int PROBE = 0, int NI = SG_NI>   // timing probes (tools/bench_fft.hip): 1 = no MFMA, 2 = no S / weight loads,
+                                          // 3 = no weight loads, 4 = no S loads
+__global__ __launch_bounds__(256, NI == SG_NI ? 2 : SPEC_SMALL_MINB) void spec_gemm_kernel(const uint4* __restrict__ S, const uint4* __restrict__ Gc,
                                                            uint4* __restrict__ Y, int B, int ngrp, float unscale) {
-  __shared__ uint4 tile[16 * 2 * 4 * SG_SLD];   // 67,584 B
+  constexpr int SLD = NI + 1;               // S tile pitch (16-B units) per (cq, part, f) row
+  constexpr int NLD = NI * 16 * 8 / 256;    // 16-B S / Y pieces per thread
+  __shared__ uint4 tile[16 * 2 * 4 * SLD];   // 67,584 B (NI = 32)
+  static_assert(NI * SG_YLD <= 16 * 2 * 4 * SLD, "the Y tile fits in the S tile's space");
   // block -> (quad, image group): the ngrp groups of quad q run on XCD q % 8 (round-robin dispatch)
   const int q8 = blockIdx.x / (8 * ngrp), rem = blockIdx.x - q8 * 8 * ngrp;
   const int grp = rem >> 3, quad = q8 * 8 + (rem & 7);
   if (quad >= NQUAD) return;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, j = lane & 31;
-  const int img0 = grp * SG_NI;
+  const int img0 = grp * NI;
   // ---- S tile: 32 images x 16 cq lines of 128 B (4 f x [hi 16 B | lo 16 B]) ----
   // unconditional loads from clamped addresses: a per-lane "b < B ? load : 0" branch made the
   // compiler wait for each of the 16 loads before issuing the next
-  uint4 pre[16];
+  uint4 pre[NLD];
 #pragma unroll
-  for (int it = 0; it < 16; ++it) {
+  for (int it = 0; it < NLD; ++it) {
     const int idx = it * 256 + tid, line = idx >> 3, piece = idx & 7;
     const int bl = line >> 4, cq = line & 15;
     const int b = min(img0 + bl, B - 1);
@@ -1371,10 +1382,10 @@ __global__ __launch_bounds__(256, 2) void spec_gemm_kernel(const uint4* __restri
       wr[t][cb][1] = gw[(1 * 16 + 2 * t + h) * 64 + 32 * cb + j];
     }
 #pragma unroll
-  for (int it = 0; it < 16; ++it) {
+  for (int it = 0; it < NLD; ++it) {
     const int idx = it * 256 + tid, line = idx >> 3, piece = idx & 7;
     const int bl = line >> 4, cq = line & 15, f = piece >> 1, part = piece & 1;
-    tile[((cq * 2 + part) * 4 + f) * SG_SLD + bl] = img0 + bl < B ? pre[it] : uint4{0, 0, 0, 0};
+    tile[((cq * 2 + part) * 4 + f) * SLD + bl] = img0 + bl < B ? pre[it] : uint4{0, 0, 0, 0};
   }
   lds_barrier();
   f32x16 acc[4] = {};
@@ -1382,8 +1393,10 @@ __global__ __launch_bounds__(256, 2) void spec_gemm_kernel(const uint4* __restri
 #pragma unroll
   for (int t = 0; t < 8; ++t) {
     const int cq = 2 * t + h;
-    const f16x8 sh = __builtin_bit_cast(f16x8, tile[((cq * 2 + 0) * 4 + wv) * SG_SLD + j]);
-    const f16x8 sl = __builtin_bit_cast(f16x8, tile[((cq * 2 + 1) * 4 + wv) * SG_SLD + j]);
+    const int jj = NI == SG_NI ? j : min(j, NI - 1);   // columns past NI: zero operands (below)
+    f16x8 sh = __builtin_bit_cast(f16x8, tile[((cq * 2 + 0) * 4 + wv) * SLD + jj]);
+    f16x8 sl = __builtin_bit_cast(f16x8, tile[((cq * 2 + 1) * 4 + wv) * SLD + jj]);
+    if (NI != SG_NI && j >= NI) sh = sl = f16x8{};
 #pragma unroll
     for (int cb = 0; cb < 2; ++cb) {
       const uint4 gh = wr[t][cb][0], gl = wr[t][cb][1];
@@ -1406,21 +1419,23 @@ __global__ __launch_bounds__(256, 2) void spec_gemm_kernel(const uint4* __restri
   lds_barrier();   // every wave has read the S tile
   // ---- Y tile: lane (h, j), co block cb, row group g: channels 32cb + 8g + 4h + e, e < 4 ----
   f32x4* ytile = reinterpret_cast<f32x4*>(tile);
+  if (NI == SG_NI || j < NI) {
 #pragma unroll
-  for (int cb = 0; cb < 2; ++cb)
+    for (int cb = 0; cb < 2; ++cb)
 #pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int cqo = 8 * cb + 2 * g + h;
-      const f32x16& re = acc[cb];
-      const f32x16& im = acc[2 + cb];
-      const f32x4 lo = f32x4{re[4 * g], im[4 * g], re[4 * g + 1], im[4 * g + 1]} * unscale;
-      const f32x4 hi = f32x4{re[4 * g + 2], im[4 * g + 2], re[4 * g + 3], im[4 * g + 3]} * unscale;
-      ytile[j * SG_YLD + (cqo * 4 + wv) * 2] = lo;
-      ytile[j * SG_YLD + (cqo * 4 + wv) * 2 + 1] = hi;
-    }
+      for (int g = 0; g < 4; ++g) {
+        const int cqo = 8 * cb + 2 * g + h;
+        const f32x16& re = acc[cb];
+        const f32x16& im = acc[2 + cb];
+        const f32x4 lo = f32x4{re[4 * g], im[4 * g], re[4 * g + 1], im[4 * g + 1]} * unscale;
+        const f32x4 hi = f32x4{re[4 * g + 2], im[4 * g + 2], re[4 * g + 3], im[4 * g + 3]} * unscale;
+        ytile[j * SG_YLD + (cqo * 4 + wv) * 2] = lo;
+        ytile[j * SG_YLD + (cqo * 4 + wv) * 2 + 1] = hi;
+      }
+  }
   lds_barrier();
 #pragma unroll
-  for (int it = 0; it < 16; ++it) {
+  for (int it = 0; it < NLD; ++it) {
     const int idx = it * 256 + tid, line = idx >> 3, piece = idx & 7;
     const int bl = line >> 4, cqo = line & 15, b = img0 + bl;
     if (b < B) st16(Y + (((size_t)b * 16 + cqo) * NF + 4 * quad) * 2 + piece, tile[bl * SG_YLD + cqo * 8 + piece]);
@@ -1974,11 +1989,15 @@ hipError_t launch_fft_inv_a_fwd(const void* Y, const ConvArgs& a, void* S, int B
 }
 
 hipError_t launch_spec_gemm(const void* S, const void* Gx, void* Y, int B, float unscale, hipStream_t st, bool bf) {
-  const int ngrp = (B + SG_NI - 1) / SG_NI;
+  const bool small = !bf && B <= SPEC_SMALLB;
+  const int ngrp = small ? 1 : (B + SG_NI - 1) / SG_NI;
   const int nq8 = (NQUAD + 7) / 8;
   if (bf)
     hipLaunchKernelGGL(spec_gemm_bf_kernel, dim3(NQ16 * 16 * ngrp), dim3(256), 0, st, static_cast<const uint4*>(S),
                        static_cast<const uint4*>(Gx), static_cast<uint4*>(Y), B, ngrp);
+  else if (small)
+    hipLaunchKernelGGL((spec_gemm_kernel<0, 8>), dim3(nq8 * 8), dim3(256), 0, st, static_cast<const uint4*>(S),
+                       static_cast<const uint4*>(Gx), static_cast<uint4*>(Y), B, 1, unscale);
   else
     hipLaunchKernelGGL(spec_gemm_kernel<0>, dim3(nq8 * 8 * ngrp), dim3(256), 0, st, static_cast<const uint4*>(S),
                        static_cast<const uint4*>(Gx), static_cast<uint4*>(Y), B, ngrp, unscale);
