@@ -111,11 +111,11 @@ def fft_kernels(ctx, B, hw, steps, bf16=False):
 # per-kernel HBM bytes per launch from rocprofv3 PMC passes (FETCH_SIZE x2 on gfx950 + WRITE_SIZE,
 # MI355X_MICROARCH.md), collected with the full-batch single-stream launches of this workload by
 # tools/pmc_bytes.py and committed under profiles/ (bench cannot profile itself)
-PMC_TRAFFIC = {False: "profiles/r3h/pmc_traffic_fp32_b256.csv",
-               True: "profiles/r3h/pmc_traffic_bf16_b256.csv"}
+PMC_TRAFFIC = {False: "profiles/r3ze/pmc_traffic_fp32_b256.csv",
+               True: "profiles/r3ze/pmc_traffic_bf16_b256.csv"}
 PMC_KERNEL = {   # name: (fp32 path's kernel, bf16 path's kernel) as rocprofv3 names them
     "fft_fwd": ("fft_fwd3_kernel", "fft_fwd_kernel<true, true>"),
-    "spec_gemm": ("spec_gemm_kernel<0>", "spec_gemm_bf_kernel"),
+    "spec_gemm": ("spec_gemm_kernel<0, 32>", "spec_gemm_bf_kernel"),
     "inv_a_fwd": ("fft_inv_a_fwd_kernel<false, false>", "fft_inv_a_fwd_kernel<true, true>"),
     "fft_inv": ("fft_inv_kernel<false, false>", "fft_inv_kernel<true, true>"),
     "epi_b": ("spec_epi_b_kernel<false, false, false>", "spec_epi_b_kernel<true, true, false>")}
@@ -123,7 +123,7 @@ PMC_KERNEL = {   # name: (fp32 path's kernel, bf16 path's kernel) as rocprofv3 n
 
 # MFMA utilisation per kernel from the committed PMC pass (tools/pmc_mfma.sh / .py: SQ_VALU_MFMA_BUSY_CYCLES
 # over GRBM_GUI_ACTIVE x 1024 SIMDs, the gfx950 MfmaUtil), same one-stream B = 256 workload
-PMC_MFMA = "profiles/r2d/mfma_util_pose_fp32_b256.csv"
+PMC_MFMA = "profiles/r3ze/mfma_util_pose_fp32_b256.csv"
 MFMA_KERNELS = {"fc_gemm_x3p (fc_1 on split planes, k_fc.hip)": "fc_gemm_x3p_kernel", "conv64x3 (conv_2/3, k_conv64x3.hip)": "conv64x3_kernel",
                 "spec_gemm (k_fft.hip)": "spec_gemm_kernel", "spec_epi_b (gate GEMMs, k_fft.hip)": "spec_epi_b_kernel<false, false, false>",
                 "gate_init_x3 (k_fft.hip)": "gate_init_x3_kernel"}
@@ -398,16 +398,25 @@ def frame_chain(mp, dev, args):
     return res
 
 
-def e2e_latency(mp, ctx, dev, T, frames=40):
+def e2e_latency(mp, ctx, dev, T, wts, dtype, frames=40):
     """Config 5: one 424x512 float32 depth frame per call -> native host CoM crop -> H2D -> hGRU pose
-    forward at batch 1 -> D2H -> absolute joints; p50 / p99 wall latency."""
+    forward at batch 1 -> D2H -> absolute joints; p50 / p99 wall latency.  The headline figure runs
+    the product class for it (train_cnn_networks_hgru.StreamPosePipeline: the crop written into
+    pinned memory, async H2D / D2H on the forward's stream); the same loop with pageable
+    torch copies through the raw context is kept beside it."""
     import torch
     md = mp.monkeydetector.MonkeyDetector(365.456, 365.456, 256, 212, [800, 800, 1200], 200, 10000)
     W = mp.weights
     o0 = torch.from_numpy(W.synth_hidden((1, 64, 64, 64), seed=3)).to(dev)
+    fr = list(W.synth_frames(8, seed=14)[..., 0] * np.float32(10000.0))   # mm, as the crop sees it
+
+    def pct(lat):
+        lat = np.array(lat[5:]) * 1e3
+        return round(float(np.percentile(lat, 50)), 3), round(float(np.percentile(lat, 99)), 3), len(lat)
+
+    # pageable copies through the raw context (the round-2 measurement)
     out = torch.empty((1, 69), device=dev)
     stream = mp._lib.current_stream(dev)
-    fr = list(W.synth_frames(8, seed=14)[..., 0] * np.float32(10000.0))   # mm, as the crop sees it
     lat = []
     for i in range(frames):
         t0 = time.perf_counter()
@@ -417,10 +426,28 @@ def e2e_latency(mp, ctx, dev, T, frames=40):
         rel = out.cpu().numpy().reshape(23, 3) * 600.0
         md.getAbsoluteCoordinates(rel, com[0])
         lat.append(time.perf_counter() - t0)
-    lat = np.array(lat[5:]) * 1e3
-    return {"p50_ms": round(float(np.percentile(lat, 50)), 3), "p99_ms": round(float(np.percentile(lat, 99)), 3),
-            "frames": len(lat), "fps_capacity": round(1000.0 / float(np.percentile(lat, 50)), 1),
-            "path": "native host crop (mp_crop3d_batch) + H2D + hgru_pose fwd B=1 + D2H"}
+    p50_raw, p99_raw, _ = pct(lat)
+    # the pipeline class on a façade model with the same weights
+    pm = mp.hgru_pose.model()
+    pm.compute_dtype = {"f32_fft": "fp32_fft", "bf16": "bf16", "f32_split": "fp32_split", "f32": "fp32"}[dtype]
+    pm.load_weights(wts)
+    pm.build(torch.zeros((1, 128, 128, 1), device=dev), 69, h2_init=o0)
+    res = {}
+    for pinned in (False, True):
+        pipe = mp.train_cnn_networks_hgru.StreamPosePipeline(pm, md, h2_init=o0, pinned=pinned)
+        lat = []
+        for i in range(frames):
+            t0 = time.perf_counter()
+            pipe.run(fr[i % 8])
+            lat.append(time.perf_counter() - t0)
+        res[pinned] = pct(lat)
+    pm._ctx.close()
+    p50, p99, n = res[False]
+    return {"p50_ms": p50, "p99_ms": p99, "frames": n, "fps_capacity": round(1000.0 / p50, 1),
+            "path": "StreamPosePipeline: native host crop (mp_crop3d_batch) into a reused buffer + H2D + "
+                    "hgru_pose fwd B=1 (direct context call) + D2H + getAbsoluteCoordinates",
+            "pinned_async_copies": {"p50_ms": res[True][0], "p99_ms": res[True][1]},
+            "pageable_copies_raw_ctx": {"p50_ms": p50_raw, "p99_ms": p99_raw}}
 
 
 def cpu_threads():
@@ -643,7 +670,7 @@ def main():
         if not args.no_extras:
             head_rate = value
             try:
-                rec["extras"] = {"e2e_batch1_latency": e2e_latency(mp, ctx, dev, T)}
+                rec["extras"] = {"e2e_batch1_latency": e2e_latency(mp, ctx, dev, T, wts, args.dtype)}
             except Exception as e:  # noqa: BLE001
                 rec["extras"] = {"e2e_batch1_latency": {"error": repr(e)}}
             ctx.close()

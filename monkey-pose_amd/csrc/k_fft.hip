@@ -1077,7 +1077,7 @@ __global__ __launch_bounds__(FNT, 3) void fft_inv3_kernel(const void* __restrict
 // / epilogue operations on the same operands as in the batched kernels, so the results are
 // bit-identical to them (tests/test_gpu_parity.py::test_batch_invariance_and_determinism runs a crop
 // alone and inside a batch).
-constexpr int LF_NT = 704;             // 11 waves: 74 transforms x 9 lanes (666 used)
+constexpr int LF_NT = 704;             // 11 waves of 7 transforms x 9 lanes: 74 column / 64 row transforms
 constexpr int LF_T = 74;
 constexpr int LF_ZLD = 73;             // pitch (complex) of a row of the P / I rows and the forward row outputs
 constexpr int LF_BIG = NF * 2;         // complex: the pair's whole spectrum (Y in, or S staging out), 42.6 KB
@@ -1104,6 +1104,37 @@ __device__ __forceinline__ void lf_stage2(cpx (&u)[9], const cpx* E, int t, int 
 }
 __device__ __forceinline__ int lf_in(int n1, int j) { return (9 * n1 + 8 * j) % 72; }
 __device__ __forceinline__ int lf_out(int j, int k2) { return (9 * j + 64 * k2) % 72; }
+// the same index sets as lane tables built incrementally ((9 n1 + 8 j) steps by +9, (9 j + 64 k2) by
+// -8, mod 72): a conditional add instead of a division per element
+struct LfIdx {
+  int in[8], out[9];
+  __device__ __forceinline__ explicit LfIdx(int j) {
+    int a = 8 * j;   // j <= 8: a < 72
+#pragma unroll
+    for (int n1 = 0; n1 < 8; ++n1) {
+      in[n1] = a;
+      a += 9;
+      a -= a >= 72 ? 72 : 0;
+    }
+    int b = 9 * j;
+    b -= b >= 72 ? 72 : 0;
+#pragma unroll
+    for (int k2 = 0; k2 < 9; ++k2) {
+      out[k2] = b;
+      b -= 8;
+      b += b < 0 ? 72 : 0;
+    }
+  }
+};
+// thread -> (transform t, lane j): 7 transforms of 9 lanes per wave (lane 63 idle), so a transform's
+// exchange between its two passes stays inside one wave and needs no workgroup barrier
+__device__ __forceinline__ void lf_lane(int tid, int& t, int& j) {
+  const int ln = tid & 63, tw = ln / 9;
+  t = ln == 63 ? 1 << 20 : 7 * (tid >> 6) + tw;
+  j = ln - 9 * tw;
+}
+// the wave's own LDS writes of pass 1 have landed (DS instructions of a wave complete in order)
+__device__ __forceinline__ void lf_wave_sync() { asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory"); }
 
 // Y's channel pair (2 cp, 2 cp + 1) -> the P rows in R[y][x] (y, x < 64).  The spectrum is first
 // copied into LDS with one 16-byte load per frequency (both channels; the wave reads 64 consecutive
@@ -1111,53 +1142,59 @@ __device__ __forceinline__ int lf_out(int j, int k2) { return (9 * j + 64 * k2) 
 // Big: LF_BIG complex of LDS (the Y copy, then the inverse tile).  Called by every thread.
 __device__ __forceinline__ void lf_inverse(const void* __restrict__ Y, int b, int cp, int tid, cpx* E, cpx* Big,
                                            cpx* R) {
-  const int cq = cp >> 1, pp = cp & 1, t = tid / 9, j = tid - 9 * t;
+  const int cq = cp >> 1, pp = cp & 1;
+  int t, j;
+  lf_lane(tid, t, j);
+  const LfIdx ix(min(j, 8));
   const float4* ysrc = reinterpret_cast<const float4*>(Y) + ((size_t)b * 16 + cq) * NF * 2 + pp;
-  for (int f = tid; f < NF; f += LF_NT) {
+  for (int f = tid; f < NF; f += LF_NT) {   // the Y copy goes to R's space (free until the P rows)
     const float4 v = ysrc[2 * f];
-    Big[2 * f] = cpx{v.x, v.y};
-    Big[2 * f + 1] = cpx{v.z, v.w};
+    R[2 * f] = cpx{v.x, v.y};
+    R[2 * f + 1] = cpx{v.z, v.w};
   }
   lds_barrier();
+  FFT_STAMP_AT(1);
   cpx in[8], u[9];
   // inverse column (fx, cc) = (t >> 1, t & 1) over fy (inv_cols_to_T)
   if (t < LF_T && j < 9) {
     const int fx = t >> 1, cc = t & 1;
 #pragma unroll
-    for (int n1 = 0; n1 < 8; ++n1) in[n1] = Big[2 * spec_f<false>(fx, lf_in(n1, j)) + cc];
+    for (int n1 = 0; n1 < 8; ++n1) in[n1] = R[2 * spec_f<false>(fx, ix.in[n1]) + cc];
     lf_stage1<1>(in, E, t, j);
   }
-  lds_barrier();   // stage 1 done: E complete, the Y copy no longer read
+  lf_wave_sync();
   if (t < LF_T && j < 8) {
     const int fx = t >> 1, cc = t & 1;
     lf_stage2<1>(u, E, t, j);
 #pragma unroll
     for (int k2 = 0; k2 < 9; ++k2) {
-      const int y = lf_out(j, k2);
+      const int y = ix.out[k2];
       if (y < 64) Big[y * I3_LD + cc * FX + fx] = u[k2];
     }
   }
   lds_barrier();
+  FFT_STAMP_AT(2);
   // inverse row y = t: C[m] = A[m] + i B[m] from the Hermitian half spectra (inv_row_from_T)
   if (t < 64 && j < 9) {
 #pragma unroll
     for (int n1 = 0; n1 < 8; ++n1) {
-      const int m = lf_in(n1, j), k = m <= 36 ? m : 72 - m;
+      const int m = ix.in[n1], k = m <= 36 ? m : 72 - m;
       const cpx A = Big[t * I3_LD + k], B = Big[t * I3_LD + FX + k];
       in[n1] = m <= 36 ? cfma(swp(B), cpx{-1.f, 1.f}, A) : cfma(A, cpx{1.f, -1.f}, swp(B));
     }
     lf_stage1<1>(in, E, t, j);
   }
-  lds_barrier();
+  lf_wave_sync();
   if (t < 64 && j < 8) {
     lf_stage2<1>(u, E, t, j);
 #pragma unroll
     for (int k2 = 0; k2 < 9; ++k2) {
-      const int x = lf_out(j, k2);
+      const int x = ix.out[k2];
       if (x < 64) R[t * LF_ZLD + x] = u[k2];
     }
   }
   lds_barrier();
+  FFT_STAMP_AT(3);
 }
 
 // the rows R[y][x] (x < 64; zero outside the map) -> S for the channel pair: forward rows, forward
@@ -1166,29 +1203,33 @@ __device__ __forceinline__ void lf_inverse(const void* __restrict__ Y, int b, in
 // then the staging).  Called by every thread.
 __device__ __forceinline__ void lf_forward(const cpx* R, int b, int cp, int tid, cpx* E, cpx* Big,
                                            void* __restrict__ S) {
-  const int cq = cp >> 1, pp = cp & 1, t = tid / 9, j = tid - 9 * t;
+  const int cq = cp >> 1, pp = cp & 1;
+  int t, j;
+  lf_lane(tid, t, j);
+  const LfIdx ix(min(j, 8));
   cpx in[8], u[9];
   if (t < 64 && j < 9) {
 #pragma unroll
     for (int n1 = 0; n1 < 8; ++n1) {
-      const int x = lf_in(n1, j);
+      const int x = ix.in[n1];
       in[n1] = x < 64 ? R[t * LF_ZLD + x] : cpx{0.f, 0.f};
     }
     lf_stage1<-1>(in, E, t, j);
   }
-  lds_barrier();
+  lf_wave_sync();   // (R, read by pass 1, is not written here)
   if (t < 64 && j < 8) {
     lf_stage2<-1>(u, E, t, j);
 #pragma unroll
-    for (int k2 = 0; k2 < 9; ++k2) Big[t * LF_ZLD + lf_out(j, k2)] = u[k2];
+    for (int k2 = 0; k2 < 9; ++k2) Big[t * LF_ZLD + ix.out[k2]] = u[k2];
   }
   lds_barrier();
+  FFT_STAMP_AT(5);
   // forward column (fx, cc): the pair-separated half spectra of rows y (fwd_rows_to_T), then over y
   if (t < LF_T && j < 9) {
     const int fx = t >> 1, cc = t & 1;
 #pragma unroll
     for (int n1 = 0; n1 < 8; ++n1) {
-      const int y = lf_in(n1, j);
+      const int y = ix.in[n1];
       cpx v = {0.f, 0.f};
       if (y < 64) {
         const cpx zk = Big[y * LF_ZLD + fx], zm = Big[y * LF_ZLD + (72 - fx) % 72];
@@ -1198,8 +1239,10 @@ __device__ __forceinline__ void lf_forward(const cpx* R, int b, int cp, int tid,
     }
     lf_stage1<-1>(in, E, t, j);
   }
-  lds_barrier();   // the row outputs are no longer read: Big becomes the S staging [f][hi cc0, hi cc1, lo cc0, lo cc1]
-  uint32_t* stg = reinterpret_cast<uint32_t*>(Big);
+  lf_wave_sync();
+  // the S staging [f][hi cc0, hi cc1, lo cc0, lo cc1] in R's space (its rows were read before the
+  // last barrier)
+  uint32_t* stg = reinterpret_cast<uint32_t*>(const_cast<cpx*>(R));
   if (t < LF_T && j < 8) {
     const int fx = t >> 1, cc = t & 1;
     lf_stage2<-1>(u, E, t, j);
@@ -1209,12 +1252,13 @@ __device__ __forceinline__ void lf_forward(const cpx* R, int b, int cp, int tid,
       const float re = z.x * SPEC_SCALE, im = z.y * SPEC_SCALE;
       const _Float16 hr = (_Float16)re, hi = (_Float16)im;
       const f16x2 hv = {hr, hi}, lv = {(_Float16)(re - (float)hr), (_Float16)(im - (float)hi)};
-      const int f = spec_f<false>(fx, lf_out(j, k2));
+      const int f = spec_f<false>(fx, ix.out[k2]);
       stg[4 * f + cc] = __builtin_bit_cast(uint32_t, hv);
       stg[4 * f + 2 + cc] = __builtin_bit_cast(uint32_t, lv);
     }
   }
   lds_barrier();
+  FFT_STAMP_AT(6);
   // S group (b, cq, f): [hi c0..c3 | lo c0..c3], 4 B each; this pair's hi at 8 pp, lo at 16 + 8 pp
   uint2* dst = reinterpret_cast<uint2*>(S) + ((size_t)b * 16 + cq) * NF * 4 + pp;
   for (int f = tid; f < NF; f += LF_NT) {
@@ -1222,6 +1266,7 @@ __device__ __forceinline__ void lf_forward(const cpx* R, int b, int cp, int tid,
     dst[4 * f] = uint2{w.x, w.y};
     dst[4 * f + 2] = uint2{w.z, w.w};
   }
+  FFT_STAMP_AT(7);
 }
 
 // pixels of the pixel-major passes: thread tid takes pixels tid + LF_NT i (i < LF_PX)
@@ -1231,12 +1276,13 @@ __global__ __launch_bounds__(LF_NT, 1) void lfft_inv_a_fwd_kernel(const void* __
                                                                  void* __restrict__ S) {
   __shared__ cpx E[LF_T * 72];
   __shared__ cpx Big[LF_BIG];
-  __shared__ cpx R[64 * LF_ZLD];   // the P rows, then the I rows
+  __shared__ cpx R[LF_BIG];   // the Y copy, the P rows, the I rows, the S staging
   const int H = pa.H, W = pa.W;
   int b, cp;
   lfft_block(blockIdx.x, b, cp);
   const int q = cp >> 2, ec = 2 * (cp & 3);   // C8 chunk and the pair's first channel in it
   const int tid = threadIdx.x;
+  FFT_STAMP_AT(0);
   // the A epilogue's X / O of this thread's pixels, issued first (clamped addresses)
   cpx xv[LF_PX], ov[LF_PX];
 #pragma unroll
@@ -1267,6 +1313,7 @@ __global__ __launch_bounds__(LF_NT, 1) void lfft_inv_a_fwd_kernel(const void* __
     R[y * LF_ZLD + x] = iv;
   }
   lds_barrier();
+  FFT_STAMP_AT(4);
   lf_forward(R, b, cp, tid, E, Big, S);
 }
 
@@ -1274,7 +1321,7 @@ __global__ __launch_bounds__(LF_NT, 1) void lfft_inv_kernel(const void* __restri
                                                            int W) {
   __shared__ cpx E[LF_T * 72];
   __shared__ cpx Big[LF_BIG];
-  __shared__ cpx R[64 * LF_ZLD];
+  __shared__ cpx R[LF_BIG];
   int b, cp;
   lfft_block(blockIdx.x, b, cp);
   const int q = cp >> 2, ec = 2 * (cp & 3);
@@ -1293,7 +1340,7 @@ __global__ __launch_bounds__(LF_NT, 1) void lfft_fwd_kernel(const float* __restr
                                                            int W) {
   __shared__ cpx E[LF_T * 72];
   __shared__ cpx Big[LF_BIG];
-  __shared__ cpx R[64 * LF_ZLD];
+  __shared__ cpx R[LF_BIG];
   int b, cp;
   lfft_block(blockIdx.x, b, cp);
   const int q = cp >> 2, ec = 2 * (cp & 3);

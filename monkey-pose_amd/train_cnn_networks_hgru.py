@@ -118,3 +118,59 @@ class FramePosePipeline:
             frame_scale=float(cfg.image_max_depth), dsize=cfg.image_target_size[0], check=self.check_crops)
         out = self.pose.build(patches, cfg.num_classes, h2_init=h2_init)
         return out, coms, Ms
+
+
+class StreamPosePipeline:
+    """SURVEY config 5, one depth frame per call: the host CoM crop of ``MonkeyDetector`` (native
+    ``mp_crop3d_batch``) -> the hGRU pose forward at batch 1 -> absolute joints
+    (``getAbsoluteCoordinates``, monkeydetector.py:356-360).  The reference's frame loop
+    (train_cnn_networks_hgru.py:284-321 with the detector's ``cropArea3D`` in place of the attention
+    net) minus the per-call allocations: the crop is written straight into a pinned host buffer, one
+    asynchronous H2D and one asynchronous D2H (pinned) bracket the forward on the current stream, and
+    the call waits on that stream alone.
+
+    ``pose_model``: a built ``hgru_pose.model`` (weights loaded); ``h2_init``: an optional fixed
+    [1, dsize / 2, dsize / 2, 64] CUDA hidden state (else the model's own hidden init).
+    ``run(frame_mm)`` -> (joints_xyz [num_joints, 3] mm, joints_uvd [num_joints, 3], com_uvd [3])."""
+
+    def __init__(self, pose_model, md, h2_init=None, dsize: int = 128, num_joints: int = 23, device=None,
+                 pinned: bool = True):
+        import torch
+        self.pose, self.md, self.h2_init = pose_model, md, h2_init
+        self.dsize, self.num_joints = int(dsize), int(num_joints)
+        dev = torch.device(device) if device is not None else (
+            h2_init.device if h2_init is not None else torch.device("cuda", torch.cuda.current_device()))
+        self.pinned = bool(pinned)   # False: pageable staging, blocking copies (the copies' own waits)
+        self._x_host = torch.empty((1, self.dsize, self.dsize, 1), dtype=torch.float32)
+        if self.pinned:
+            self._x_host = self._x_host.pin_memory()
+        self._x_np = self._x_host.numpy()
+        self._x_dev = torch.empty((1, self.dsize, self.dsize, 1), dtype=torch.float32, device=dev)
+        self._y_host = torch.empty((1, self.num_joints * 3), dtype=torch.float32)
+        if self.pinned:
+            self._y_host = self._y_host.pin_memory()
+        self._y_dev = torch.empty((1, self.num_joints * 3), dtype=torch.float32, device=dev)
+        self._half_z = float(md.cube[2]) / 2.0
+        self._dev = dev
+        # with a given O0 the built context is called directly (no per-call façade work)
+        self._direct = h2_init is not None and getattr(pose_model, "_ctx", None) is not None
+        if self._direct:
+            self._h2 = h2_init.detach().float().contiguous()
+
+    def run(self, frame_mm, com=None, nthreads: int = 1):
+        import torch
+        ts = torch.cuda.current_stream(self._dev)   # the copies and the forward on the caller's stream
+        _, _, coms = self.md.crop_batch(np.asarray(frame_mm, np.float32)[None], None if com is None else [com],
+                                        dsize=self.dsize, nthreads=nthreads, out=self._x_np)
+        self._x_dev.copy_(self._x_host, non_blocking=self.pinned)
+        if self._direct:
+            self.pose._ctx.pose_fwd(self._x_dev, self._h2, self._y_dev, ts.cuda_stream)
+            out = self._y_dev
+        else:
+            out = self.pose.forward(self._x_dev, h2_init=self.h2_init)
+        self._y_host.copy_(out, non_blocking=self.pinned)
+        if self.pinned:
+            ts.synchronize()
+        rel = self._y_host.numpy().reshape(self.num_joints, 3) * np.float32(self._half_z)
+        xyz, uvd = self.md.getAbsoluteCoordinates(rel, coms[0])
+        return xyz, uvd, coms[0]
