@@ -330,6 +330,12 @@ __device__ __forceinline__ int fcp_swz(int row) {   // 16-B chunk swizzle of a r
 #ifndef FC_P_BIG
 #define FC_P_BIG 1    // the 256 x 256 tile (8 waves, one block per CU) for the three-product kernel above 128 rows
 #endif
+#ifndef FC_PB_NW
+#define FC_PB_NW 8    // waves per 256-row block: 8 (256 columns, one block per CU) or 4 (128 columns, two)
+#endif
+#ifndef FC_PB_NST
+#define FC_PB_NST 3   // its stages (32 KiB each)
+#endif
 #ifndef FC_PB_PIPE
 #define FC_PB_PIPE 1  // 256-row tile: fragment reads one group ahead of the MFMAs
 #endif
@@ -620,7 +626,7 @@ hipError_t launch_fc_gemm_x3p(const void* Ah, const void* Al, int lda, const voi
   // where three 128 x 128 blocks per CU moved 43 B / cycle, ~2/3 of an XCD's L2 bandwidth per CU
   const bool big = nprod == 3 && M > 128 && FC_P_BIG;
   const int mb = M <= 32 ? 1 : (M <= 64 ? 2 : (big ? 8 : 4));
-  const int nw = big ? 8 : (nprod == 3 ? FC_P_NW3 : 4);   // waves (32-column groups) per block
+  const int nw = big ? FC_PB_NW : (nprod == 3 ? FC_P_NW3 : 4);   // waves (32-column groups) per block
   const int grid = fc_grid((M + 32 * mb - 1) / (32 * mb), (N32 + nw - 1) / nw, S);
   const _Float16* h = static_cast<const _Float16*>(Ah);
   const _Float16* l = static_cast<const _Float16*>(Al);
@@ -639,7 +645,8 @@ hipError_t launch_fc_gemm_x3p(const void* Ah, const void* Al, int lda, const voi
     if (mb == 1) MP_FCP3(1);
     else if (mb == 2) MP_FCP3(2);
     else if (mb == 8)
-      hipLaunchKernelGGL((fc_gemm_x3p_kernel<3, 8, FC_P_BK3, 1, 8>), dim3(grid), dim3(512), 0, st, h, l, lda, w, part,
+      hipLaunchKernelGGL((fc_gemm_x3p_kernel<3, 8, FC_P_BK3, 8 / FC_PB_NW, FC_PB_NW, FC_PB_NST>), dim3(grid),
+                         dim3(64 * FC_PB_NW), 0, st, h, l, lda, w, part,
                          M, K, N32, kslice, unscale, S);
     else MP_FCP3(4);
   }
