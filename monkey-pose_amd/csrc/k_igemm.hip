@@ -991,11 +991,13 @@ __device__ __forceinline__ float dpp_xor1(float v) {   // lane ^ 1 (quad_perm [1
   return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0xB1, 0xF, 0xF, false));
 }
 // WR: the wave layout of igemm_x3h_kernel (wave rows; MBW 32-pixel blocks x NBW cout blocks per wave)
+// WR = 8: NARROW1 (Cout <= 32): four waves of 32 px x 32 couts -- the NARROW layout's second cout
+// block would be a clamped copy of the first (twice the MFMAs and weight loads for nothing)
 template <int WR>
 struct HaloLayout {
-  static constexpr int MBW = 4 / WR;                 // 32-pixel blocks per wave (the tile has 4)
-  static constexpr int NBW = WR == 1 ? 1 : 2;        // 32-cout blocks per wave
-  static constexpr int NT = (4 / WR) * NBW;          // 32-cout blocks per tile (WR = 4: 2, else 4)
+  static constexpr int MBW = WR == 8 ? 1 : 4 / WR;               // 32-pixel blocks per wave (the tile has 4)
+  static constexpr int NBW = (WR == 1 || WR == 8) ? 1 : 2;       // 32-cout blocks per wave
+  static constexpr int NT = WR == 8 ? 1 : (4 / WR) * NBW;        // 32-cout blocks per tile (WR = 4: 2, else 4)
 };
 
 template <int WR>
@@ -1231,7 +1233,7 @@ __global__ __launch_bounds__(256, 2) void igemm_x3h_kernel(IgemmArgs p, HaloGeom
       lds_barrier();
     }
   }
-  if constexpr (WR != 4) {
+  if constexpr (WR != 4 && WR != 8) {
     if (p.pool) {   // fused 2x2/2 max pool (uniform branch): the pooled map goes to the output view
       halo_pool_epilogue<WR>(p, acc, wave_on, unscale, m0, nb0, hs);
       return;
@@ -1351,7 +1353,10 @@ bool halo_geom(const IgemmArgs& a, HaloGeom& hg, size_t& lds) {
   hg.PH = hg.NI * hg.HH * hg.WW;
   const int ch = halo_ch(a);
   if (ch == 16 && a.Cout > 64) return false;   // 16-channel chunks exist for the NARROW layout only
-  lds = 2 * (size_t)hg.PH * (2 * ch + 8) * sizeof(_Float16);
+  // the second halo buffer only exists for the next chunk: one chunk, one buffer (Cin <= 16 / 32:
+  // half the LDS, so 4 instead of 3 NARROW / NARROW1 blocks fit a CU)
+  const int nchunk = (a.cinp ? a.cinp : a.Cin) / ch;
+  lds = (nchunk > 1 ? 2 : 1) * (size_t)hg.PH * (2 * ch + 8) * sizeof(_Float16);
   return ok && hg.PH * (ch / 4) <= 256 * HX_ITEMS && lds <= 80 * 1024;
 }
 
@@ -1483,7 +1488,15 @@ hipError_t launch_igemm_x3(const IgemmArgs& a, const void* wpk, float unscale, h
                               reinterpret_cast<const void*>(igemm_x3h_kernel<3, 3, 4, 16>),
                               reinterpret_cast<const void*>(igemm_x3h_kernel<5, 3, 4, 16>),
                               reinterpret_cast<const void*>(igemm_x3h_kernel<3, 1, 4, 16>),
-                              reinterpret_cast<const void*>(igemm_x3h_kernel<5, 1, 4, 16>)})
+                              reinterpret_cast<const void*>(igemm_x3h_kernel<5, 1, 4, 16>),
+                              reinterpret_cast<const void*>(igemm_x3h_kernel<3, 3, 8, 16>),
+                              reinterpret_cast<const void*>(igemm_x3h_kernel<3, 1, 8, 16>),
+                              reinterpret_cast<const void*>(igemm_x3h_kernel<5, 3, 8, 16>),
+                              reinterpret_cast<const void*>(igemm_x3h_kernel<5, 1, 8, 16>),
+                              reinterpret_cast<const void*>(igemm_x3h_kernel<3, 3, 8>),
+                              reinterpret_cast<const void*>(igemm_x3h_kernel<3, 1, 8>),
+                              reinterpret_cast<const void*>(igemm_x3h_kernel<5, 3, 8>),
+                              reinterpret_cast<const void*>(igemm_x3h_kernel<5, 1, 8>)})
           (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, 80 * 1024);
         return true;
       }();
@@ -1505,7 +1518,12 @@ hipError_t launch_igemm_x3(const IgemmArgs& a, const void* wpk, float unscale, h
   else if (one) MP_HALO(5, 1, WRV, CHV);         \
   else MP_HALO(5, 3, WRV, CHV)
 #define MP_HALO_WR(WRV) MP_HALO_WRC(WRV, 32)
-      if (N32 <= 2 && halo_ch(a) == 16) {   // Cout <= 64, 16-channel chunks
+      static const int narrow1 = env_flag("MP_IGEMM_HALO_NARROW1", 1);
+      if (narrow1 && N32 == 1 && !a.pool && halo_ch(a) == 16) {   // Cout <= 32 (NARROW1)
+        MP_HALO_WRC(8, 16);
+      } else if (narrow1 && N32 == 1 && !a.pool) {
+        MP_HALO_WR(8);
+      } else if (N32 <= 2 && halo_ch(a) == 16) {   // Cout <= 64, 16-channel chunks
         MP_HALO_WRC(4, 16);
       } else if (N32 <= 2) {   // Cout <= 64
         MP_HALO_WR(4);
