@@ -127,12 +127,20 @@ class MonkeyDetector(object):
                                    offset=(int(info[6]), int(info[7])))
         return out, np.asmatrix(M.reshape(3, 3)), com_out
 
-    def crop_batch(self, frames, coms=None, dsize=128, nthreads=None):
+    def crop_batch(self, frames, coms=None, dsize=128, nthreads=None, out=None):
         """Per-frame crop of ``prepare_data_test`` (train_cnn_networks_hgru.py:61-74) in one native
-        call: returns (patches [n, dsize, dsize, 1] = crop / maxDepth, Ms [n, 3, 3], coms [n, 3])."""
+        call: returns (patches [n, dsize, dsize, 1] = crop / maxDepth, Ms [n, 3, 3], coms [n, 3]).
+        ``out``: a C-contiguous float32 [n, dsize, dsize, 1] array the patches are written into (and
+        returned as ``patches``), e.g. a reused or pinned staging buffer."""
         fr, dt = self._frame(frames, ndim=3)
         n = fr.shape[0]
-        patches = np.empty((n, dsize, dsize, 1), np.float32)
+        if out is None:
+            patches = np.empty((n, dsize, dsize, 1), np.float32)
+        else:
+            if not (isinstance(out, np.ndarray) and out.dtype == np.float32 and out.flags.c_contiguous
+                    and out.shape == (n, dsize, dsize, 1)):
+                raise ValueError(f"out must be a C-contiguous float32 array of shape {(n, dsize, dsize, 1)}")
+            patches = out
         Ms = np.empty((n, 9), np.float64)
         com_out = np.empty((n, 3), np.float64)
         c = None if coms is None else np.ascontiguousarray(np.asarray(coms, np.float64).reshape(n, 3))

@@ -125,16 +125,17 @@ class StreamPosePipeline:
     ``mp_crop3d_batch``) -> the hGRU pose forward at batch 1 -> absolute joints
     (``getAbsoluteCoordinates``, monkeydetector.py:356-360).  The reference's frame loop
     (train_cnn_networks_hgru.py:284-321 with the detector's ``cropArea3D`` in place of the attention
-    net) minus the per-call allocations: the crop is written straight into a pinned host buffer, one
-    asynchronous H2D and one asynchronous D2H (pinned) bracket the forward on the current stream, and
-    the call waits on that stream alone.
+    net) minus the per-call allocations: the crop is written straight into a reused host buffer, one
+    H2D and one D2H bracket the forward on the current stream.  ``pinned=True`` stages through pinned
+    memory with asynchronous copies and waits on that stream alone; it measured no faster than the
+    default pageable blocking copies at batch 1 (1.103 vs 1.097 ms p50, DESIGN.md §3a'').
 
     ``pose_model``: a built ``hgru_pose.model`` (weights loaded); ``h2_init``: an optional fixed
     [1, dsize / 2, dsize / 2, 64] CUDA hidden state (else the model's own hidden init).
     ``run(frame_mm)`` -> (joints_xyz [num_joints, 3] mm, joints_uvd [num_joints, 3], com_uvd [3])."""
 
     def __init__(self, pose_model, md, h2_init=None, dsize: int = 128, num_joints: int = 23, device=None,
-                 pinned: bool = True):
+                 pinned: bool = False):
         import torch
         self.pose, self.md, self.h2_init = pose_model, md, h2_init
         self.dsize, self.num_joints = int(dsize), int(num_joints)

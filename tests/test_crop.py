@@ -88,6 +88,12 @@ def test_batch_matches_single_and_normalises():
         single, M, _ = md.cropArea3D(frames[i], com=coms[i])
         assert np.array_equal(patches[i, :, :, 0], single / np.float32(10000))   # train_cnn_networks_hgru.py:71
         assert np.array_equal(Ms[i], np.asarray(M))
+    # out=: the patches land in the caller's buffer (StreamPosePipeline's reused staging array)
+    buf = np.full((3, 128, 128, 1), np.nan, np.float32)
+    p2, Ms2, c2 = md.crop_batch(frames, coms, nthreads=2, out=buf)
+    assert p2 is buf and np.array_equal(buf, patches) and np.array_equal(Ms2, Ms) and np.array_equal(c2, c)
+    with pytest.raises(ValueError):
+        md.crop_batch(frames, coms, out=np.empty((3, 128, 128), np.float32))
 
 
 def test_crop_errors():
