@@ -965,6 +965,111 @@ __global__ __launch_bounds__(256, 2) void igemm_x3pw_kernel(IgemmArgs p, const f
   }
 }
 
+// The pointwise kernel for 5 or 6 cout blocks (161 .. 192 output channels; dense conv_6_1_1x1 fused
+// with conv_6_2_1x1_1: 184 -> 64 + 96, train_dense_networks.py:343-349).  igemm_x3pw_kernel covers
+// them with two 128-channel N tiles, so every pixel tile is loaded, split and staged twice and the
+// second tile runs one real cout block beside a clamped copy.  Here one block owns all NB cout
+// blocks of its 128 pixels: wave w runs pixel block w (32 px) x NB cout blocks, the K extent is
+// loaded once.  Per output the MFMA sequence (chunk, k16 group, lo*hi, hi*lo, hi*hi) is
+// igemm_x3pw_kernel's, so the result is bit for bit the same.
+template <int NP, int NCH, int NB>
+__global__ __launch_bounds__(256, 2) void igemm_x3pwn_kernel(IgemmArgs p, const f16x8* __restrict__ wpk, float unscale) {
+  __shared__ _Float16 Ah[IG_BM * IGX_LD], Al[IG_BM * IGX_LD];
+  __shared__ f16x8 Ws[2 * NB * 2 * 64];   // [k16 g][cout block nb][part][lane]
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, col = lane & 31;
+  const int M = p.N * p.Ho * p.Wo;
+  int mt_, nt_;
+  xcd_tile(p, false, mt_, nt_);
+  const int m0 = mt_ * IG_BM;
+  const int K16 = (p.K + 15) / 16;
+  const int k4 = (tid & 7) * 4;
+  f32x4 av[NCH][4];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int gm = m0 + (tid >> 3) + 32 * i, k = 32 * c + k4;
+      const f32x4 t =
+          *reinterpret_cast<const f32x4*>(p.x + (size_t)min(gm, M - 1) * p.ldx + p.cix + min(k, p.K - 4));
+      av[c][i] = (gm < M && k < p.K) ? t : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  auto load_w = [&](int k0, f16x8 (&w)[NB]) {
+#pragma unroll
+    for (int u = 0; u < NB; ++u) {
+      const int e = tid + 256 * u, l = e & 63, part = (e >> 6) & 1, q = e >> 7, g = q / NB, nb = q - g * NB;
+      const int kb = min((k0 >> 4) + g, K16 - 1);
+      if (NP == 3 || part == 0) w[u] = wpk[(((size_t)kb * NB + nb) * 2 + part) * 64 + l];
+    }
+  };
+  f32x16 acc[NB];
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) acc[nb] = f32x16{};
+  f16x8 wnx[NB];
+  load_w(0, wnx);
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int k0 = 32 * c;
+    lds_barrier();   // the previous chunk's LDS reads are done
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int row = (tid >> 3) + 32 * i;
+      f16x4 hv, lv;
+#pragma unroll
+      for (int s = 0; s < 4; ++s) {
+        hv[s] = (_Float16)av[c][i][s];
+        lv[s] = (_Float16)(av[c][i][s] - (float)hv[s]);
+      }
+      *reinterpret_cast<f16x4*>(Ah + row * IGX_LD + k4) = hv;
+      if constexpr (NP == 3) *reinterpret_cast<f16x4*>(Al + row * IGX_LD + k4) = lv;
+    }
+#pragma unroll
+    for (int u = 0; u < NB; ++u) Ws[tid + 256 * u] = wnx[u];
+    if (c + 1 < NCH) load_w(k0 + IG_BK, wnx);
+    lds_barrier();
+#pragma unroll
+    for (int g = 0; g < 2; ++g) {
+      if ((k0 >> 4) + g >= K16) break;   // block-uniform
+      const int o = (wv * 32 + col) * IGX_LD + 16 * g + 8 * h;
+      const f16x8 ah = *reinterpret_cast<const f16x8*>(Ah + o);
+      const f16x8 al = *reinterpret_cast<const f16x8*>(Al + o);
+#pragma unroll
+      for (int nb = 0; nb < NB; ++nb) {
+        const f16x8 wh = Ws[((g * NB + nb) * 2 + 0) * 64 + lane];
+        const f16x8 wl = Ws[((g * NB + nb) * 2 + 1) * 64 + lane];
+        if constexpr (NP == 3) {
+          acc[nb] = mfma16(wl, ah, acc[nb]);
+          acc[nb] = mfma16(wh, al, acc[nb]);
+        }
+        acc[nb] = mfma16(wh, ah, acc[nb]);
+      }
+    }
+  }
+  const int gm = m0 + wv * 32 + col;
+  if (gm >= M) return;
+  const bool vst = (p.ldo % 4 == 0) && (p.coff % 4 == 0) && (p.Cout % 4 == 0);
+  float* dst = p.out + (size_t)gm * p.ldo + p.coff;
+#pragma unroll
+  for (int nb = 0; nb < NB; ++nb) {
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int c = nb * 32 + 8 * g + 4 * h;
+      f32x4 o;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const float v = acc[nb][4 * g + j] * unscale + (c + j < p.Cout ? p.bias[c + j] : 0.f);
+        o[j] = p.relu ? fmaxf(v, 0.f) : v;
+      }
+      if (vst) {
+        if (c < p.Cout) *reinterpret_cast<f32x4*>(dst + c) = o;
+      } else {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (c + j < p.Cout) dst[c + j] = o[j];
+      }
+    }
+  }
+}
+
 // Halo-tiled f16x3 convolution (stride 1, odd KS, SAME, Cin % 32 == 0, Cout > 64): the im2col
 // kernels above gather, split and stage every input element once per tap (9x for 3x3); here a
 // block's 128 output pixels are whole rows (NI images x R rows x W cols, 128 % W == 0) and the
@@ -1444,6 +1549,35 @@ hipError_t launch_igemm_x3(const IgemmArgs& a, const void* wpk, float unscale, h
     const dim3 pgrid((M + IG_BM - 1) / IG_BM, (N32 + 3) / 4);   // 128-channel output tiles
     IgemmArgs pa = a;
     pa.xcd = xcd;
+    // 5 / 6 cout blocks: one block owns all of them (igemm_x3pwn_kernel; MP_IGEMM_PWN=0 for A/B)
+    // and 2 / 3 cout blocks, where the 2 x 2 wave grid idles or clamps waves (MP_IGEMM_PWN=1: 5 / 6 only;
+    // dense conv_4_1_1x1 0.195 -> 0.176 ms, conv_3_1_1x1 0.127 -> 0.114, profiles/r3zp)
+    static const int pwn = env_flag("MP_IGEMM_PWN", 2);
+    if ((pwn && (N32 == 5 || N32 == 6) && nch >= 4) || (pwn == 2 && (N32 == 2 || N32 == 3))) {
+      const dim3 ngrid((M + IG_BM - 1) / IG_BM, 1);
+#define MP_PWX(NPV, NCHV, NBV) hipLaunchKernelGGL((igemm_x3pwn_kernel<NPV, NCHV, NBV>), ngrid, dim3(256), 0, st, pa, w, unscale)
+#define MP_PWXB(NCHV, NBV) \
+  if (one) MP_PWX(1, NCHV, NBV); else MP_PWX(3, NCHV, NBV)
+#define MP_PWXN(NCHV)                  \
+  switch (N32) {                       \
+    case 2: MP_PWXB(NCHV, 2); break;   \
+    case 3: MP_PWXB(NCHV, 3); break;   \
+    case 5: MP_PWXB(NCHV, 5); break;   \
+    default: MP_PWXB(NCHV, 6); break;  \
+  }
+      switch (nch) {
+        case 1: MP_PWXN(1); break;
+        case 2: MP_PWXN(2); break;
+        case 3: MP_PWXN(3); break;
+        case 4: MP_PWXN(4); break;
+        case 5: MP_PWXN(5); break;
+        default: MP_PWXN(6); break;
+      }
+#undef MP_PWXB
+#undef MP_PWXN
+#undef MP_PWX
+      return hipGetLastError();
+    }
 #define MP_PW(NPV, NCHV) hipLaunchKernelGGL((igemm_x3pw_kernel<NPV, NCHV>), pgrid, dim3(256), 0, st, pa, w, unscale)
 #define MP_PWN(NCHV)     \
   if (one) MP_PW(1, NCHV); \

@@ -86,3 +86,35 @@ def test_switch_keeps_parity(env, kind, dtype, gate):
     err = json.loads(r.stdout.strip().splitlines()[-1])["err"]
     print(f"{env} {kind} {dtype}: rel_inf {err:.3e}")
     assert err <= gate, err
+
+
+_CHILD_BITS = r"""
+import hashlib, json, sys
+sys.path.insert(0, {tests!r})
+import numpy as np, torch
+from helpers import MG, pkg
+P = pkg()
+wts, depth = MG.regressor_inputs("dense", 12, 128, 5, 6)
+model = P.train_dense_networks.dense_model_struct()
+model.compute_dtype = {dtype!r}
+model.load_weights(wts)
+out = model.build(torch.from_numpy(depth).cuda(), 69, train_mode=False).cpu().numpy()
+print(json.dumps({{"sha": hashlib.sha256(np.ascontiguousarray(out).tobytes()).hexdigest()}}))
+"""
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dtype", ["fp32_split", "bf16"])
+def test_wide_pointwise_is_bit_identical(dtype):
+    """igemm_x3pwn_kernel (one block over all 5 / 6 cout blocks of a 1x1 conv, dense conv_6_1_1x1 +
+    conv_6_2_1x1_1) runs each output's MFMA sequence of igemm_x3pw_kernel: the dense output is the
+    same bytes with MP_IGEMM_PWN=0 (two 128-channel N tiles), with it on, and with MP_IGEMM_PWN=2 (also
+    the 2 / 3 cout-block 1x1s: dense conv_3_1_1x1, conv_4_1_1x1)."""
+    shas = []
+    for flag in ("0", "1", "2"):
+        code = _CHILD_BITS.format(tests=os.path.join(ROOT, "tests"), dtype=dtype)
+        r = subprocess.run([sys.executable, "-c", code], env={**os.environ, "MP_IGEMM_PWN": flag},
+                           capture_output=True, text=True, timeout=110)
+        assert r.returncode == 0, r.stderr[-2000:]
+        shas.append(json.loads(r.stdout.strip().splitlines()[-1])["sha"])
+    assert shas[0] == shas[1] == shas[2]
