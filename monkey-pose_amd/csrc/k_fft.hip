@@ -672,6 +672,10 @@ __device__ __forceinline__ int f3_reader(int tid, int& fx, int& c) {   // round 
 // zero padded); the forward row FFT, the two-round 2-channel transpose, the column FFT and the
 // LDS-staged S stores.  Called by every thread of the block (it contains barriers); lds3's space must
 // be free on entry (the caller's barrier).
+// NR: rounds of the S staging (2: 36 fy per round at pitch STG_LD, 43.8 KB; 3: 24 fy per round at
+// pitch STG3_LD, 29.6 KB, so the block's LDS is the 38.5 KB 2-channel tile and 4 blocks fit a CU)
+constexpr int STG3_LD = 200;   // 24 fy x 8 dwords + 8 pad
+template <int NR = 2>
 __device__ __forceinline__ void fwd3_tail(cpx (&v)[72], uint32_t* lds3, void* __restrict__ S, int b, int cq, int tid) {
   cpx* T2 = reinterpret_cast<cpx*>(lds3);
   int rfx = 0, rc = 0;
@@ -706,30 +710,35 @@ __device__ __forceinline__ void fwd3_tail(cpx (&v)[72], uint32_t* lds3, void* __
   read_col(1);
   if (round >= 0) fft72<-1>(v);
   uint4* dst = reinterpret_cast<uint4*>(S) + ((size_t)b * 16 + cq) * NF * 2;
+  constexpr int NY = 72 / NR, LD = NR == 2 ? STG_LD : STG3_LD, NW = 2 * NY;
 #pragma unroll
-  for (int half = 0; half < 2; ++half) {
-    lds_barrier();   // T2 (half 0) / the previous half's staging is no longer read
+  for (int half = 0; half < NR; ++half) {
+    lds_barrier();   // T2 (round 0) / the previous round's staging is no longer read
     if (round >= 0) {
 #pragma unroll
-      for (int j = 0; j < 36; ++j) {
-        const cpx z = v[36 * half + j];
+      for (int j = 0; j < NY; ++j) {
+        const cpx z = v[NY * half + j];
         const float re = z.x * SPEC_SCALE, im = z.y * SPEC_SCALE;
         const _Float16 hr = (_Float16)re, hi = (_Float16)im;
         const f16x2 hv = {hr, hi}, lv = {(_Float16)(re - (float)hr), (_Float16)(im - (float)hi)};
-        lds3[rfx * STG_LD + j * 8 + rc] = __builtin_bit_cast(uint32_t, hv);
-        lds3[rfx * STG_LD + j * 8 + 4 + rc] = __builtin_bit_cast(uint32_t, lv);
+        lds3[rfx * LD + j * 8 + rc] = __builtin_bit_cast(uint32_t, hv);
+        lds3[rfx * LD + j * 8 + 4 + rc] = __builtin_bit_cast(uint32_t, lv);
       }
     }
     lds_barrier();
-    for (int i = tid; i < FX * 72; i += FNT) {
-      const int ffx = i / 72, w = i - ffx * 72;
-      st16(dst + (ffx * 72 + 36 * half) * 2 + w, *reinterpret_cast<const uint4*>(lds3 + ffx * STG_LD + w * 4));
+    for (int i = tid; i < FX * NW; i += FNT) {
+      const int ffx = i / NW, w = i - ffx * NW;
+      st16(dst + (ffx * 72 + NY * half) * 2 + w, *reinterpret_cast<const uint4*>(lds3 + ffx * LD + w * 4));
     }
   }
 }
-__global__ __launch_bounds__(FNT, 3) void fft_fwd3_kernel(const float* __restrict__ src, void* __restrict__ S,
-                                                         int H, int W) {
-  __shared__ uint32_t lds3[F3_LDS];
+// NBLK = 4 (MP_FFT_FWD4): the S staging in three rounds, 38.5 KB of LDS, 4 blocks per CU
+constexpr int F4_LDS = FX * 2 * F3_TLD * 2;   // dwords: the 2-channel tile (>= FX * STG3_LD)
+static_assert(FX * STG3_LD <= F4_LDS, "the three-round staging fits in the 2-channel tile's space");
+template <int NBLK>
+__global__ __launch_bounds__(FNT, NBLK) void fft_fwd3_kernel(const float* __restrict__ src, void* __restrict__ S,
+                                                            int H, int W) {
+  __shared__ uint32_t lds3[NBLK == 4 ? F4_LDS : F3_LDS];
   const int b = fft_block_img(blockIdx.x), cq = fft_block_cq(blockIdx.x);
   const int q = cq >> 1, e0 = 4 * (cq & 1);
   const int tid = threadIdx.x;
@@ -753,7 +762,7 @@ __global__ __launch_bounds__(FNT, 3) void fft_fwd3_kernel(const float* __restric
 #pragma unroll
     for (int x = 64; x < 72; ++x) v[x] = {0.f, 0.f};
   }
-  fwd3_tail(v, lds3, S, b, cq, tid);
+  fwd3_tail<NBLK == 4 ? 3 : 2>(v, lds3, S, b, cq, tid);
 }
 
 #ifndef FFT_FWD3
@@ -2007,6 +2016,15 @@ hipError_t build_spec_weights(const float* w, int ks, void* Gx, float* unscale, 
   return e;
 }
 
+// MP_FFT_FWD4=1: the fp32 forward FFT at four blocks per CU (fft_fwd3_kernel<4>)
+static bool fft_fwd4() {
+  static const bool on = [] {
+    const char* e = std::getenv("MP_FFT_FWD4");
+    return e ? std::atoi(e) != 0 : false;
+  }();
+  return on;
+}
+
 hipError_t launch_fft_fwd(const float* act, void* S, int B, int H, int W, hipStream_t st, bool bf) {
   if (!bf && !fy_major<false>() && B <= lfft_maxb())
     hipLaunchKernelGGL(lfft_fwd_kernel, dim3(B * 32), dim3(LF_NT), 0, st, act, S, H, W);
@@ -2014,8 +2032,10 @@ hipError_t launch_fft_fwd(const float* act, void* S, int B, int H, int W, hipStr
     hipLaunchKernelGGL((fft_fwd_kernel<true, true>), dim3(B * 16), dim3(FNT), 0, st, act, S, H, W);
   else if (bf)
     hipLaunchKernelGGL((fft_fwd_kernel<true, false>), dim3(B * 16), dim3(FNT), 0, st, act, S, H, W);
+  else if (FFT_FWD3 && !fy_major<false>() && fft_fwd4())
+    hipLaunchKernelGGL(fft_fwd3_kernel<4>, dim3(B * 16), dim3(FNT), 0, st, act, S, H, W);
   else if (FFT_FWD3 && !fy_major<false>())
-    hipLaunchKernelGGL(fft_fwd3_kernel, dim3(B * 16), dim3(FNT), 0, st, act, S, H, W);
+    hipLaunchKernelGGL(fft_fwd3_kernel<3>, dim3(B * 16), dim3(FNT), 0, st, act, S, H, W);
   else
     hipLaunchKernelGGL((fft_fwd_kernel<false, false>), dim3(B * 16), dim3(FNT), 0, st, act, S, H, W);
   return hipGetLastError();

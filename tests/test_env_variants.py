@@ -94,27 +94,43 @@ sys.path.insert(0, {tests!r})
 import numpy as np, torch
 from helpers import MG, pkg
 P = pkg()
-wts, depth = MG.regressor_inputs("dense", 12, 128, 5, 6)
-model = P.train_dense_networks.dense_model_struct()
-model.compute_dtype = {dtype!r}
-model.load_weights(wts)
-out = model.build(torch.from_numpy(depth).cuda(), 69, train_mode=False).cpu().numpy()
+kind, dtype = {kind!r}, {dtype!r}
+if kind == "dense":
+    wts, depth = MG.regressor_inputs("dense", 12, 128, 5, 6)
+    model = P.train_dense_networks.dense_model_struct()
+    model.compute_dtype = dtype
+    model.load_weights(wts)
+    out = model.build(torch.from_numpy(depth).cuda(), 69, train_mode=False).cpu().numpy()
+else:   # 12 crops: above the small-batch FFT kernels' B <= 8
+    wts, depth, O0 = MG.pose_inputs(12, 64, 8, 5, 6, 7)
+    model = P.hgru_pose.model()
+    model.compute_dtype = dtype
+    model.load_weights(wts)
+    out = model.build(torch.from_numpy(depth).cuda(), 69, train_mode=False,
+                      h2_init=torch.from_numpy(O0).cuda()).cpu().numpy()
 print(json.dumps({{"sha": hashlib.sha256(np.ascontiguousarray(out).tobytes()).hexdigest()}}))
 """
 
+BITS_CASES = [
+    # igemm_x3pwn_kernel (one block over all 2 / 3 / 5 / 6 cout blocks of a 1x1 conv) runs each
+    # output's MFMA sequence of igemm_x3pw_kernel: MP_IGEMM_PWN = 0 / 1 / 2 give the same bytes
+    ("dense", "fp32_split", "MP_IGEMM_PWN", ("0", "1", "2")),
+    ("dense", "bf16", "MP_IGEMM_PWN", ("0", "1", "2")),
+    # the fp32 forward FFT at 4 blocks per CU only stages its S stores in three rounds, not two
+    ("pose", "fp32_fft", "MP_FFT_FWD4", ("0", "1")),
+]
+
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("dtype", ["fp32_split", "bf16"])
-def test_wide_pointwise_is_bit_identical(dtype):
-    """igemm_x3pwn_kernel (one block over all 5 / 6 cout blocks of a 1x1 conv, dense conv_6_1_1x1 +
-    conv_6_2_1x1_1) runs each output's MFMA sequence of igemm_x3pw_kernel: the dense output is the
-    same bytes with MP_IGEMM_PWN=0 (two 128-channel N tiles), with it on, and with MP_IGEMM_PWN=2 (also
-    the 2 / 3 cout-block 1x1s: dense conv_3_1_1x1, conv_4_1_1x1)."""
+@pytest.mark.parametrize("kind,dtype,var,values", BITS_CASES, ids=[f"{c[2]}-{c[0]}-{c[1]}" for c in BITS_CASES])
+def test_switch_is_bit_identical(kind, dtype, var, values):
+    """Switches whose forms compute every output with the same operations in the same order: the
+    model output is the same bytes under each setting (one child process per setting)."""
     shas = []
-    for flag in ("0", "1", "2"):
-        code = _CHILD_BITS.format(tests=os.path.join(ROOT, "tests"), dtype=dtype)
-        r = subprocess.run([sys.executable, "-c", code], env={**os.environ, "MP_IGEMM_PWN": flag},
+    for v in values:
+        code = _CHILD_BITS.format(tests=os.path.join(ROOT, "tests"), kind=kind, dtype=dtype)
+        r = subprocess.run([sys.executable, "-c", code], env={**os.environ, var: v},
                            capture_output=True, text=True, timeout=110)
         assert r.returncode == 0, r.stderr[-2000:]
         shas.append(json.loads(r.stdout.strip().splitlines()[-1])["sha"])
-    assert shas[0] == shas[1] == shas[2]
+    assert len(set(shas)) == 1, shas
