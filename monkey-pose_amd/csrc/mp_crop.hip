@@ -7,6 +7,7 @@
 #include <cmath>
 #include <cstring>
 #include <thread>
+#include <type_traits>
 #include <vector>
 
 #include "crop_geom.hpp"
@@ -18,6 +19,15 @@ namespace {
 
 // numpy 1.x float32 pairwise summation (numpy/core/src/umath/loops_utils.h.src), used by
 // calculateCoM's dc.sum() on a float32 frame (monkeydetector.py:78)
+// The leaf (8 <= n <= 128) keeps numpy's 8 accumulators in one 8-lane vector: r[j] += a[i + j] lane
+// by lane, then ((r0 + r1) + (r2 + r3)) + ((r4 + r5) + (r6 + r7)) -- the same additions in the same
+// order, without the scalar array the compiler did not vectorise.
+typedef float f32v8 __attribute__((ext_vector_type(8)));
+inline f32v8 load_v8(const float* p) {
+  f32v8 v;
+  std::memcpy(&v, p, sizeof(v));
+  return v;
+}
 float pairwise_sum_f32(const float* a, int64_t n) {
   if (n < 8) {
     float r = 0.f;
@@ -25,11 +35,9 @@ float pairwise_sum_f32(const float* a, int64_t n) {
     return r;
   }
   if (n <= 128) {
-    float r[8];
-    for (int j = 0; j < 8; ++j) r[j] = a[j];
+    f32v8 r = load_v8(a);
     int64_t i = 8;
-    for (; i < n - (n % 8); i += 8)
-      for (int j = 0; j < 8; ++j) r[j] += a[i + j];
+    for (; i < n - (n % 8); i += 8) r += load_v8(a + i);
     float res = ((r[0] + r[1]) + (r[2] + r[3])) + ((r[4] + r[5]) + (r[6] + r[7]));
     for (; i < n; ++i) res += a[i];
     return res;
@@ -78,6 +86,40 @@ struct Thresh<float> {
   bool out(float v) const { return v < lo || v > hi; }
 };
 
+// The float32 frame's threshold / mask-sum pass of center_of_mass below (w < 46000), as a plain
+// function so the host build carries AVX-512 / AVX2 clones of it beside the baseline x86-64 one,
+// picked at load time by the CPU (the device pass of hipcc does not take the attribute).
+#ifdef __HIP_DEVICE_COMPILE__
+#define MP_HOST_CLONES
+#else
+#define MP_HOST_CLONES __attribute__((target_clones("arch=x86-64-v4", "arch=x86-64-v3", "default")))
+#endif
+MP_HOST_CLONES void thresh_rows_f32(const float* dpt, float* dc, int64_t h, int64_t w, float lo, float hi,
+                                    int64_t acc[4]) {
+  int64_t sr = 0, sc = 0, npos = 0, num = 0;
+  for (int64_t y = 0; y < h; ++y) {
+    const float* src = dpt + y * w;
+    float* d = dc + y * w;
+    int32_t p32 = 0, x32 = 0, n32 = 0;
+    for (int32_t x = 0; x < (int32_t)w; ++x) {
+      const float v = (src[x] < lo || src[x] > hi) ? 0.f : src[x];
+      d[x] = v;
+      const int32_t pos = v > 0.f;
+      p32 += pos;
+      x32 += pos ? x : 0;
+      n32 += v != 0.f;
+    }
+    sr += y * p32;
+    sc += x32;
+    npos += p32;
+    num += n32;
+  }
+  acc[0] = sr;
+  acc[1] = sc;
+  acc[2] = npos;
+  acc[3] = num;
+}
+
 // numpy's calculateCoM (monkeydetector.py:66-84) in one pass: the thresholded frame dc goes to a
 // per-thread buffer reused across calls (no 0.9 MB allocation and page faults per frame), and the
 // mask sums are integer per row (the original's double sums of integers are exact, so this is
@@ -91,7 +133,19 @@ void center_of_mass(const mp_camera& cam, const T* dpt, int64_t h, int64_t w, do
   const Thresh<T> th(cam);
   const bool narrow = w < 46000;   // a row's sum of x fits int32
   int64_t sr = 0, sc = 0, num = 0, npos = 0;
-  for (int64_t y = 0; y < h; ++y) {
+  int64_t rows = h;
+  if constexpr (std::is_same<T, float>::value) {
+    if (narrow) {
+      int64_t acc[4];
+      thresh_rows_f32(dpt, dc, h, w, th.lo, th.hi, acc);
+      sr = acc[0];
+      sc = acc[1];
+      npos = acc[2];
+      num = acc[3];
+      rows = 0;   // the row loop below has nothing left to do
+    }
+  }
+  for (int64_t y = 0; y < rows; ++y) {
     const T* src = dpt + y * w;
     T* d = dc + y * w;
     int64_t rpos = 0, rx = 0, rnum = 0;
@@ -198,15 +252,41 @@ void crop_one(const mp_camera& cam, const T* dpt, int64_t h, int64_t w, const do
   for (int64_t i = 0; i < dsz * dsz; ++i) out[i] = (float)cam.max_depth;
   // the output columns inside the patch and their nearest-neighbour source columns, once per crop
   const int64_t x0 = std::max<int64_t>(0, -g.offx), x1 = std::min<int64_t>(g.szw, dsz - g.offx);
-  thread_local std::vector<int64_t> colmap;
-  colmap.resize((size_t)std::max<int64_t>(0, x1 - x0));
-  for (int64_t x = x0; x < x1; ++x) colmap[x - x0] = mpgeom::nn_col(g, x);
+  // per output column, the frame column its nearest-neighbour source pixel reads, or -1 where that
+  // pixel is the crop's zero padding; then per output row one frame row (or none) -- the per-pixel
+  // work is one gather and getCrop's two thresholds (crop_px, unchanged)
+  // float32 frames with both getCrop bounds in float32 range (always, for finite depths) compare
+  // against f32(zstart) / f32(zend) exactly as crop_px does
+  const bool fast = std::is_same<T, float>::value && mpgeom::legacy_in_f32(g.zstart) && mpgeom::legacy_in_f32(g.zend);
+  const float zs = (float)g.zstart, ze = (float)g.zend;
+  thread_local std::vector<int64_t> srccol;
+  srccol.resize((size_t)std::max<int64_t>(0, x1 - x0));
+  for (int64_t x = x0; x < x1; ++x) {
+    const int64_t sx = mpgeom::nn_col(g, x) - g.pl;
+    srccol[x - x0] = (sx >= 0 && sx < g.c1 - g.c0) ? g.c0 + sx : -1;
+  }
   for (int64_t y = 0; y < g.szh; ++y) {
     const int64_t oy = g.offy + y;
     if (oy < 0 || oy >= dsz) continue;
-    const int64_t sy = mpgeom::nn_row(g, y);
+    const int64_t sy = mpgeom::nn_row(g, y) - g.pt;
     float* orow = out + oy * dsz + (g.offx + x0);   // in-range base: output column offx + x0 >= 0
-    for (int64_t x = x0; x < x1; ++x) orow[x - x0] = (float)crop_at(g, dpt, w, sy, colmap[x - x0]);
+    if (sy < 0 || sy >= g.r1 - g.r0) {
+      for (int64_t x = x0; x < x1; ++x) orow[x - x0] = 0.f;
+      continue;
+    }
+    const T* src = dpt + (g.r0 + sy) * w;
+    if (fast) {   // crop_px with its float32 bounds hoisted
+      for (int64_t x = x0; x < x1; ++x) {
+        const int64_t c = srccol[x - x0];
+        const float v = c >= 0 ? (float)src[c] : 0.f;
+        orow[x - x0] = (v != 0.f && v < zs) ? zs : ((v != 0.f && v > ze) ? 0.f : v);
+      }
+    } else {
+      for (int64_t x = x0; x < x1; ++x) {
+        const int64_t c = srccol[x - x0];
+        orow[x - x0] = c >= 0 ? (float)crop_px(src[c], g) : 0.f;
+      }
+    }
   }
   mpgeom::crop_matrix(g, M);
   std::memcpy(com_out, com, sizeof(com));
