@@ -2055,16 +2055,26 @@ hipError_t launch_fft_inv_a_fwd(const void* Y, const ConvArgs& a, void* S, int B
   return hipGetLastError();
 }
 
+// MP_SPEC_SMALLB: the largest batch whose spectral GEMM runs on 8-image tiles (spec_gemm_kernel<0, 8>,
+// ceil(B / 8) image groups; bit-identical to the 32-image tiles); default SPEC_SMALLB
+static int spec_smallb() {
+  static const int v = [] {
+    const char* e = std::getenv("MP_SPEC_SMALLB");
+    return e ? std::atoi(e) : SPEC_SMALLB;
+  }();
+  return v;
+}
+
 hipError_t launch_spec_gemm(const void* S, const void* Gx, void* Y, int B, float unscale, hipStream_t st, bool bf) {
-  const bool small = !bf && B <= SPEC_SMALLB;
-  const int ngrp = small ? 1 : (B + SG_NI - 1) / SG_NI;
+  const bool small = !bf && B <= spec_smallb();
+  const int ngrp = small ? (B + 7) / 8 : (B + SG_NI - 1) / SG_NI;
   const int nq8 = (NQUAD + 7) / 8;
   if (bf)
     hipLaunchKernelGGL(spec_gemm_bf_kernel, dim3(NQ16 * 16 * ngrp), dim3(256), 0, st, static_cast<const uint4*>(S),
                        static_cast<const uint4*>(Gx), static_cast<uint4*>(Y), B, ngrp);
   else if (small)
-    hipLaunchKernelGGL((spec_gemm_kernel<0, 8>), dim3(nq8 * 8), dim3(256), 0, st, static_cast<const uint4*>(S),
-                       static_cast<const uint4*>(Gx), static_cast<uint4*>(Y), B, 1, unscale);
+    hipLaunchKernelGGL((spec_gemm_kernel<0, 8>), dim3(nq8 * 8 * ngrp), dim3(256), 0, st, static_cast<const uint4*>(S),
+                       static_cast<const uint4*>(Gx), static_cast<uint4*>(Y), B, ngrp, unscale);
   else
     hipLaunchKernelGGL(spec_gemm_kernel<0>, dim3(nq8 * 8 * ngrp), dim3(256), 0, st, static_cast<const uint4*>(S),
                        static_cast<const uint4*>(Gx), static_cast<uint4*>(Y), B, ngrp, unscale);

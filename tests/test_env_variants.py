@@ -118,6 +118,8 @@ BITS_CASES = [
     ("dense", "bf16", "MP_IGEMM_PWN", ("0", "1", "2")),
     # the fp32 forward FFT at 4 blocks per CU only stages its S stores in three rounds, not two
     ("pose", "fp32_fft", "MP_FFT_FWD4", ("0", "1")),
+    # the spectral GEMM on 8-image tiles (two groups at 12 crops) vs the 32-image tiles
+    ("pose", "fp32_fft", "MP_SPEC_SMALLB", ("8", "32")),
 ]
 
 
