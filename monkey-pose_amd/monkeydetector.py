@@ -266,6 +266,25 @@ class MonkeyDetector(object):
 
     def getAbsoluteCoordinates(self, rel_jnts_xyz, com_uvd):
         """monkeydetector.py:356-360 / tf_monkeydetector.py:387-391 (A19 post-step)."""
+        r = rel_jnts_xyz
+        c = np.asarray(com_uvd)
+        if (isinstance(r, np.ndarray) and r.dtype == np.float32 and r.ndim == 2 and r.shape[1] == 3
+                and c.shape == (3,) and c.dtype.kind == "f"):
+            # one joint set per frame (the config-5 loop): uvdtoxyz of the CoM as Python float64
+            # scalars (the same IEEE double operations numpy runs elementwise), one float32 rounding
+            # each, then xyztouvd's operations on whole columns when no joint has z == 0
+            u0, u1, u2 = float(c[0]), float(c[1]), float(c[2])
+            cxyz = np.array([(self.ux - u0) * u2 / (-self.fx), (u1 - self.uy) * u2 / (-self.fy), -u2], np.float32)
+            jnts_xyz = r + cxyz
+            z = jnts_xyz[:, 2]
+            if z.all():
+                q = (jnts_xyz[:, :2] / z[:, None]).astype(np.float64)
+                uvd = np.empty((r.shape[0], 3), np.float32)
+                uvd[:, 0] = self.ux - q[:, 0] * self.fx
+                uvd[:, 1] = q[:, 1] * self.fy + self.uy
+                uvd[:, 2] = -z
+                return jnts_xyz, uvd
+            return jnts_xyz, self.xyztouvd(jnts_xyz)
         jnts_xyz = rel_jnts_xyz + self.uvdtoxyz(com_uvd)
         return jnts_xyz, self.xyztouvd(jnts_xyz)
 

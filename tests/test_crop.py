@@ -123,3 +123,24 @@ def test_relative_absolute_round_trip():
     back_xyz, back_uvd = md.getAbsoluteCoordinates(rel_xyz, com_uvd)
     assert np.allclose(back_xyz, jnts_xyz, atol=1e-3)
     assert np.allclose(back_uvd, jnts_uvd, rtol=1e-5, atol=1e-3)
+
+
+def test_absolute_fast_path_is_the_general_path():
+    """getAbsoluteCoordinates' one-joint-set path (float32 [n, 3] joints, one CoM: the config-5 loop)
+    returns the bytes of the general uvdtoxyz / xyztouvd composition, for float64 and float32 CoMs
+    and with a joint at z == 0 (the principal-point branch)."""
+    md, _ = _mds()
+    rng = np.random.default_rng(3)
+    for com_dtype in (np.float64, np.float32):
+        for zero in (False, True):
+            rel = rng.uniform(-300, 300, (23, 3)).astype(np.float32)
+            com = np.array([rng.uniform(100, 400), rng.uniform(100, 300), rng.uniform(800, 2000)], com_dtype)
+            if zero:
+                rel[5, 2] = -np.float32(md.uvdtoxyz(com)[2])
+            a_xyz, a_uvd = md.getAbsoluteCoordinates(rel, com)
+            e_xyz = rel + md.uvdtoxyz(com)
+            e_uvd = md.xyztouvd(e_xyz)
+            assert a_xyz.dtype == e_xyz.dtype and np.array_equal(a_xyz, e_xyz)
+            assert a_uvd.dtype == e_uvd.dtype and np.array_equal(a_uvd, e_uvd)
+            if zero:
+                assert a_xyz[5, 2] == 0 and a_uvd[5, 0] == np.float32(md.ux)
