@@ -1552,8 +1552,11 @@ hipError_t launch_igemm_x3(const IgemmArgs& a, const void* wpk, float unscale, h
     // 5 / 6 cout blocks: one block owns all of them (igemm_x3pwn_kernel; MP_IGEMM_PWN=0 for A/B)
     // and 2 / 3 cout blocks, where the 2 x 2 wave grid idles or clamps waves (MP_IGEMM_PWN=1: 5 / 6 only;
     // dense conv_4_1_1x1 0.195 -> 0.176 ms, conv_3_1_1x1 0.127 -> 0.114, profiles/r3zp)
-    static const int pwn = env_flag("MP_IGEMM_PWN", 2);
-    if ((pwn && (N32 == 5 || N32 == 6) && nch >= 4) || (pwn == 2 && (N32 == 2 || N32 == 3))) {
+    static const int pwn = env_flag("MP_IGEMM_PWN", 3);
+    // and 4 cout blocks (dense conv_5_1_1x1 0.294 -> 0.254 ms, profiles/r3zw; MP_IGEMM_PWN=2: the 2 x 2
+    // wave grid there)
+    if ((pwn && (N32 == 5 || N32 == 6) && nch >= 4) || (pwn >= 2 && (N32 == 2 || N32 == 3)) ||
+        (pwn == 3 && N32 == 4)) {
       const dim3 ngrid((M + IG_BM - 1) / IG_BM, 1);
 #define MP_PWX(NPV, NCHV, NBV) hipLaunchKernelGGL((igemm_x3pwn_kernel<NPV, NCHV, NBV>), ngrid, dim3(256), 0, st, pa, w, unscale)
 #define MP_PWXB(NCHV, NBV) \
@@ -1562,6 +1565,7 @@ hipError_t launch_igemm_x3(const IgemmArgs& a, const void* wpk, float unscale, h
   switch (N32) {                       \
     case 2: MP_PWXB(NCHV, 2); break;   \
     case 3: MP_PWXB(NCHV, 3); break;   \
+    case 4: MP_PWXB(NCHV, 4); break;   \
     case 5: MP_PWXB(NCHV, 5); break;   \
     default: MP_PWXB(NCHV, 6); break;  \
   }

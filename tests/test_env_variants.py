@@ -114,8 +114,8 @@ print(json.dumps({{"sha": hashlib.sha256(np.ascontiguousarray(out).tobytes()).he
 BITS_CASES = [
     # igemm_x3pwn_kernel (one block over all 2 / 3 / 5 / 6 cout blocks of a 1x1 conv) runs each
     # output's MFMA sequence of igemm_x3pw_kernel: MP_IGEMM_PWN = 0 / 1 / 2 give the same bytes
-    ("dense", "fp32_split", "MP_IGEMM_PWN", ("0", "1", "2")),
-    ("dense", "bf16", "MP_IGEMM_PWN", ("0", "1", "2")),
+    ("dense", "fp32_split", "MP_IGEMM_PWN", ("0", "1", "2", "3")),
+    ("dense", "bf16", "MP_IGEMM_PWN", ("0", "1", "2", "3")),
     # the fp32 forward FFT at 4 blocks per CU only stages its S stores in three rounds, not two
     ("pose", "fp32_fft", "MP_FFT_FWD4", ("0", "1")),
     # the spectral GEMM on 8-image tiles (two groups at 12 crops) vs the 32-image tiles
