@@ -1549,12 +1549,12 @@ hipError_t launch_igemm_x3(const IgemmArgs& a, const void* wpk, float unscale, h
     const dim3 pgrid((M + IG_BM - 1) / IG_BM, (N32 + 3) / 4);   // 128-channel output tiles
     IgemmArgs pa = a;
     pa.xcd = xcd;
-    // 5 / 6 cout blocks: one block owns all of them (igemm_x3pwn_kernel; MP_IGEMM_PWN=0 for A/B)
-    // and 2 / 3 cout blocks, where the 2 x 2 wave grid idles or clamps waves (MP_IGEMM_PWN=1: 5 / 6 only;
-    // dense conv_4_1_1x1 0.195 -> 0.176 ms, conv_3_1_1x1 0.127 -> 0.114, profiles/r3zp)
+    // 2 .. 6 cout blocks: one block owns all of them (igemm_x3pwn_kernel).  MP_IGEMM_PWN for A/B:
+    // 0 = the 2 x 2 wave grid everywhere; 1 = one block at 5 / 6 only (dense conv_6_1_1x1 0.630 ->
+    // 0.420 ms); 2 = also 2 / 3, where the grid idles or clamps waves (conv_4_1_1x1 0.195 -> 0.176,
+    // conv_3_1_1x1 0.127 -> 0.114, profiles/r3zp); 3 (default) = also 4 (conv_5_1_1x1 0.294 -> 0.254,
+    // profiles/r3zw)
     static const int pwn = env_flag("MP_IGEMM_PWN", 3);
-    // and 4 cout blocks (dense conv_5_1_1x1 0.294 -> 0.254 ms, profiles/r3zw; MP_IGEMM_PWN=2: the 2 x 2
-    // wave grid there)
     if ((pwn && (N32 == 5 || N32 == 6) && nch >= 4) || (pwn >= 2 && (N32 == 2 || N32 == 3)) ||
         (pwn == 3 && N32 == 4)) {
       const dim3 ngrid((M + IG_BM - 1) / IG_BM, 1);
