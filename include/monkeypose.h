@@ -338,6 +338,20 @@ int mp_graph_set(mp_ctx* ctx, const mp_graph_op* ops, int n_ops, int in_channels
  * tensor i densely ([n, cout] for an fc output, [n, H, W, C] otherwise) */
 int mp_graph_fwd(mp_ctx* ctx, const float* x, int64_t n, int64_t h, int64_t w, float* const* outs, void* stream);
 
+/* ---- HBM streaming probe (diagnostic; bench.py's practical roof) ----------------------------
+ * The box's streaming HBM rates over `bytes`-sized buffers (>= 64 MiB; 2 GiB recommended):
+ * read-only, write-only and copy (read + write bytes / time), each the best over grids of 1024 -
+ * 8192 blocks of 256 threads, 1 / 4 / 8 16-byte accesses per thread in flight and default or
+ * non-temporal policy (the chosen form is reported).  The ceiling the HBM-bound FFT-path kernels
+ * are read against, next to the 8 TB/s spec figure.  Synchronous; not on any product path. */
+typedef struct {
+  double read_gbps, write_gbps, copy_gbps;
+  int32_t read_grid, read_unroll, read_nt;
+  int32_t write_grid, write_unroll, write_nt;
+  int32_t copy_grid, copy_unroll, copy_nt;
+} mp_hbm_rates;
+int mp_hbm_probe(int device, int64_t bytes, mp_hbm_rates* out);
+
 /* ---- TF1 checkpoint support (host only; monkey-pose_amd/tf_checkpoint.py) ----
  * CRC-32C (Castagnoli, reflected 0x82F63B78) of n bytes continuing from `init` (0 to start), as
  * tensor_bundle (BundleEntryProto.crc32c) and LevelDB-format table blocks store it before masking.

@@ -110,6 +110,7 @@ _SIGS = {
                                          ctypes.POINTER(ctypes.c_char_p), ctypes.POINTER(ctypes.c_void_p),
                                          ctypes.POINTER(ctypes.c_int64), ctypes.c_int]),
     "mp_crc32c": (ctypes.c_uint32, [ctypes.c_uint32, ctypes.c_void_p, ctypes.c_size_t]),
+    "mp_hbm_probe": (ctypes.c_int, [ctypes.c_int, ctypes.c_int64, ctypes.c_void_p]),
     "mp_info": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p, ctypes.POINTER(ctypes.c_int64)]),
     "mp_profile_enable": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_int]),
     "mp_profile_read": (ctypes.c_int, [ctypes.c_void_p, ctypes.c_char_p,
@@ -315,3 +316,22 @@ def resize_bilinear(x, size, stream: Optional[int] = None):
 def current_stream(device=None) -> int:
     import torch
     return int(torch.cuda.current_stream(device).cuda_stream)
+
+
+class HbmRates(ctypes.Structure):
+    """mp_hbm_rates (include/monkeypose.h)"""
+    _fields_ = [("read_gbps", ctypes.c_double), ("write_gbps", ctypes.c_double), ("copy_gbps", ctypes.c_double)] + \
+               [(f"{k}_{f}", ctypes.c_int32) for k in ("read", "write", "copy") for f in ("grid", "unroll", "nt")]
+
+
+def hbm_probe(device: int = 0, nbytes: int = 2 << 30) -> dict:
+    """The box's streaming HBM read / write / copy rates (GB/s) and the access form that reached
+    each (mp_hbm_probe; synchronous, allocates two nbytes buffers)."""
+    r = HbmRates()
+    check(load().mp_hbm_probe(int(device), int(nbytes), ctypes.byref(r)))
+    out = {}
+    for k in ("read", "write", "copy"):
+        out[f"{k}_GBps"] = round(getattr(r, f"{k}_gbps"), 1)
+        out[f"{k}_form"] = {"grid": getattr(r, f"{k}_grid"), "per_thread": getattr(r, f"{k}_unroll"),
+                            "nontemporal": bool(getattr(r, f"{k}_nt"))}
+    return out

@@ -98,6 +98,10 @@ __host__ __device__ inline int crop_geometry(const mp_camera& cam, const double 
 // promotes to float64 (the scalar's kind is higher), so those comparisons stay in double.
 // (NumPy 2's NEP 50 would compare in float64: a pixel equal to f32(zend) with zend < f32(zend) is
 // kept by the reference and would be zeroed.)
+// The bound is NumPy 1.x's literal 3.4e38 (min_scalar_type_num: `value > -3.4e38 && value < 3.4e38`
+// -> NPY_FLOAT), not FLT_MAX = 3.4028235e38: a scalar in [3.4e38, FLT_MAX] maps to NPY_DOUBLE there,
+// so the compare is in double, as here.  Non-finite scalars map to NPY_HALF (float32 compare); the
+// double compare below gives the same answer for +-inf and NaN.
 __host__ __device__ inline bool legacy_in_f32(double s) { return s > -3.4e38 && s < 3.4e38; }
 __host__ __device__ inline bool f32_lt(float v, double s) {
   return legacy_in_f32(s) ? v < (float)s : (double)v < s;

@@ -68,7 +68,10 @@ __global__ __launch_bounds__(256) void crop3d_kernel(mp_camera cam, const float*
   const int f = blockIdx.y;
   if (threadIdx.x == 0) {
     // tr_res[im] * [image_orig_size[0], image_orig_size[1], image_max_depth] (float32 * float64), or
-    // the docom-refined CoM crop_refine_kernel left in coms_out (its status: the first crop failed)
+    // the docom-refined CoM crop_refine_kernel left in coms_out with the final status in status[f]
+    // (the first crop's failure, or the refined crop's geometry status).  In the refined form every
+    // block only READS coms_out / status (crop_refine_kernel, the previous launch, wrote them), so
+    // no block's read races another block's write; unrefined, the other blocks never read them.
     double com[3] = {(double)com_norm[3 * f] * cs0, (double)com_norm[3 * f + 1] * cs1,
                      (double)com_norm[3 * f + 2] * cs2};
     if (refined) {
@@ -78,10 +81,12 @@ __global__ __launch_bounds__(256) void crop3d_kernel(mp_camera cam, const float*
     }
     st = (refined && status[f] != mpgeom::CROP_OK) ? status[f] : mpgeom::crop_geometry(cam, com, H, W, dsz, &g);
     if (blockIdx.x == 0) {
-      status[f] = st;
-      coms_out[3 * f] = com[0];
-      coms_out[3 * f + 1] = com[1];
-      coms_out[3 * f + 2] = com[2];
+      if (!refined) {
+        status[f] = st;
+        coms_out[3 * f] = com[0];
+        coms_out[3 * f + 1] = com[1];
+        coms_out[3 * f + 2] = com[2];
+      }
       double M[9];
       if (st == mpgeom::CROP_OK) {
         mpgeom::crop_matrix(g, M);
@@ -291,7 +296,9 @@ __global__ __launch_bounds__(REF_T) void crop_refine_kernel(mp_camera cam, const
     coms_out[3 * f] = com[0];
     coms_out[3 * f + 1] = com[1];
     coms_out[3 * f + 2] = com[2];
-    status[f] = mpgeom::CROP_OK;
+    // the second crop's geometry status, so that crop3d_kernel only reads these words
+    mpgeom::CropGeom g2;
+    status[f] = mpgeom::crop_geometry(cam, com, H, W, dsz, &g2);
   }
 }
 

@@ -236,6 +236,27 @@ class model:
         self.states_O = self.states_I = None
         return self._run(depth, h2_init, keep_intermediates, store_states)
 
+    @property
+    def last_hidden_call(self):
+        """The call index whose device draw of O0 the last forward used (None when it was given
+        ``h2_init`` or its aux hidden_init is not 'random')."""
+        return self._rng_call
+
+    def hidden_draw(self, call=None, batch=None, crop=(128, 128)):
+        """The O0 that call ``call`` (default: the last forward's, ``last_hidden_call``) of this model
+        drew on the device, recomputed on the host bit for bit: ``weights.synth_hidden((N, h/2, w/2,
+        64), seed=hidden_seed + call)`` as a float32 numpy array.  Passing it back as ``h2_init``
+        reproduces that call's output exactly."""
+        if call is None:
+            call = self._rng_call
+            if call is None:
+                raise ValueError("the last forward did not draw O0 on the device")
+        if batch is None:
+            if self._last is None:
+                raise ValueError("give batch= (no forward has run yet)")
+            batch, crop = self._last[0].shape[0], tuple(self._last[0].shape[1:3])
+        return W.synth_hidden((batch, crop[0] // 2, crop[1] // 2, 64), seed=self.hidden_seed + call)
+
     def _run(self, depth, h2_init, keep=False, store_states=False):
         import torch
         n, h, w, _ = depth.shape

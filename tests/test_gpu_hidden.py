@@ -43,6 +43,10 @@ def test_pose_default_hidden_is_a_fresh_device_draw(dtype):
     out = m.out_put.cpu().numpy()
     _ = m.conv3
     assert np.array_equal(m.out_put.cpu().numpy(), out)
+    # the call's O0, recomputed on the host, reproduces it as an explicit h2_init
+    assert m.last_hidden_call == 2
+    again = ref.build(x, 69, h2_init=_cuda(m.hidden_draw())).cpu().numpy()
+    assert np.array_equal(again, out)
 
 
 def test_circuit_default_hidden_is_a_fresh_device_draw():

@@ -275,11 +275,15 @@ def test_fft_precision_is_fp32_class():
     assert eb <= max(10 * ea, 1e-5)
 
 
-@pytest.mark.parametrize("n", [300, 1024])
+@pytest.mark.parametrize("n", [32, 64, 128, 300, 1024])
 def test_full_size_properties(n):
-    """Beyond the metric's batch (ragged 300 = 9 GEMM groups + 12, and 1024): every sampled crop is
-    bit-identical to its own batch-1 run (slices, streams and GEMM groups never mix crops), the
-    whole batch is finite, and the last crop matches the float64 oracle within the fp32 gate."""
+    """BASELINE config 2 (B = 64, train_cnn_networks_hgru.py:141-142) and the per-GPU batches of the
+    metric's strong-scaling reading (256 / N = 128, 64, 32), and beyond the metric's batch (ragged
+    300 = 9 GEMM groups + 12, and 1024).  The hGRU loop runs as batch slices on two streams from
+    64 crops on (mp_abi.hip run_circuit: 32 + 32 at B = 64, 64 + 64 at B = 128; one slice at 32).
+    Every sampled crop is bit-identical to its own batch-1 run (slices, streams and GEMM groups
+    never mix crops), the whole batch is finite, and the last crop of EACH slice matches the
+    float64 oracle within the fp32 gate."""
     from oracle import hgru_ref as R
     mp = pkg()
     W = mp.weights
@@ -297,9 +301,16 @@ def test_full_size_properties(n):
     torch.cuda.synchronize()
     assert bool(torch.isfinite(out).all())
     one = torch.empty((1, 69), device="cuda")
-    for i in (0, n // 2, n - 1):
+    # the two-slice split at these sizes: whole 32-crop GEMM groups, the first slice takes the
+    # larger half (mp_abi.hip run_circuit)
+    groups = (n + 31) // 32
+    first = min(n, ((groups + 1) // 2) * 32) if n >= 64 else n
+    for i in sorted({0, first - 1, first % n, n // 2, n - 1}):
         ctx.pose_fwd(depth[i:i + 1].contiguous(), o0[i:i + 1].contiguous(), one, st)
         torch.cuda.synchronize()
         assert torch.equal(one[0], out[i]), i
-    ref = R.hgru_pose_forward(depth_np[n - 1:], wts, o0_np[n - 1:], 8, np.float64)
-    assert rel_inf(out[n - 1:].cpu().numpy(), ref) <= FP32_REL_TOL
+    idx = sorted({first - 1, n - 1})
+    ref = R.hgru_pose_forward(depth_np[idx], wts, o0_np[idx], 8, np.float64)
+    err = rel_inf(out[idx].cpu().numpy(), ref)
+    print(f"n={n}: crops {idx} vs fp64 oracle rel_inf {err:.3e}")
+    assert err <= FP32_REL_TOL

@@ -22,6 +22,25 @@ def test_shard_ranges_cover_batch():
             assert max(sizes) - min(sizes) <= 1
 
 
+def test_fc_hi_plane_round_trip_keeps_scale_and_plane():
+    """fc_1's hi plane (the bf16 fc_1 reads only it) survives the w -> hi -> w' round trip with the
+    same power-of-two scale, including elements that round up to 2^14 (the scale's boundary)."""
+    par = pkg().parallel
+    rng = np.random.default_rng(3)
+    w = rng.standard_normal(4096).astype(np.float32)
+    m = float(np.abs(w).max())
+    e = int(np.frexp(np.float32(m))[1])
+    s = 2.0 ** (14 - e)
+    w[7] = np.float32((2 ** 14 - 1) / s)            # max element: s * w rounds up to 2^14 in f16
+    w[9] = -np.float32((2 ** 14 - 2) / s)           # another element rounding up in magnitude
+    h, e0, idx, vals = par.fc_hi_plane(w)
+    assert 7 in idx and 9 in idx
+    w2 = par.fc_from_hi_plane(torch.from_numpy(h), e0, torch.from_numpy(idx), torch.from_numpy(vals)).numpy()
+    h2, e2, _, _ = par.fc_hi_plane(w2)
+    assert e2 == e0 and np.array_equal(h.view(np.uint16), h2.view(np.uint16))
+    assert float(np.abs(w2).max()) == float(np.abs(w).max())
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
@@ -50,6 +69,22 @@ def _worker(rank, world, port, q):
     shard = torch.arange(s * 3, e * 3, dtype=torch.float32).view(-1, 3)
     full = par.gather_outputs(shard, gb, rank, world)
     ok = ok and torch.equal(full, torch.arange(gb * 3, dtype=torch.float32).view(gb, 3))
+    # dtype bf16: fc_1 travels as its f16 hi plane; the rebuilt blob packs to the same hi plane and
+    # scale on every rank, every other weight arrives bit for bit
+    ptab = W.hgru_pose_vars(output_shape=69, timesteps=3, crop=32)
+    pw = {v.name: W.synth_value(v, 1234, 3) for v in ptab}
+    info = {}
+    pflat, play, _ = par.broadcast_weights(ptab, pw if rank == 0 else None, torch.device("cpu"), rank, world,
+                                           dtype="bf16", info=info)
+    for nm, sh, o, n in play:
+        got = pflat[o:o + n].numpy().reshape(sh)
+        if nm == par.FC1_NAME:
+            h0, e0, _, _ = par.fc_hi_plane(pw[nm])
+            h1, e1, _, _ = par.fc_hi_plane(got)
+            ok = ok and e0 == e1 and np.array_equal(h0.view(np.uint16), h1.view(np.uint16))
+        else:
+            ok = ok and np.array_equal(got, pw[nm])
+    ok = ok and info["bytes"] < 0.55 * pflat.numel() * 4   # fc_1 is ~all of the bytes
     q.put((rank, bool(ok)))
     dist.destroy_process_group()
 
