@@ -105,49 +105,27 @@ __device__ __forceinline__ uint32_t pack_bf2(float a, float b) {
 }
 
 
-// complex fp32.  FFT_PACKED = 2 (default): a 2-float vector, so a complex add is one v_pk_add_f32 and a
-// twiddle product two v_pk_fma_f32 / v_pk_mul_f32, with the re/im half swap of swp() done by two
-// plain v_mov_b32 (inline asm, so the compiler cannot fold it into an op_sel operand select).
-// FFT_PACKED = 1 lets the compiler fold the swaps into op_sel on the packed FP32 instructions.  Its
-// results differed from the scalar build's, and under the two-stream hGRU schedule from run to run:
-// 13-19 of 256 crops differed between runs, up to 2.1e-5 (tools/pk_probe.sh,
-// profiles/r3a/pk_probe_det_fp32_pk0_pk1_pk2.log, where libmonkeypose.so was the scalar build).
-// Every op_sel-free build -- scalar (0) or packed with the swaps as moves (2), the only difference
-// from 1 -- is bit-identical to the scalar build and deterministic.  So the op_sel half-select reads
-// of v_pk_*_f32 are the cause: a timing-dependent read of the swapped VGPR half that ROCm 7.2's
-// hazard recognizer does not pad.  No other kernel of the library applies op_sel to a VGPR source of
-// a packed FP32 instruction (the f16x3 packing kernels only broadcast an SGPR half).  Guarded by
-// tests/test_gpu_parity.py::test_stream_split_is_bit_identical / test_batch_invariance_and_determinism.
-// Measured (same box, B = 256, fp32): fft_fwd 0.168 -> 0.157 ms, inv_a_fwd 0.339 -> 0.329, fft_inv
-// 0.130 -> 0.126, 10.56 -> 10.35-10.39 ms per forward, same bits; bf16 6.43-6.47 -> 6.23-6.28 ms.
-// 0: a plain struct, two scalar VALU instructions per complex op.
-#ifndef FFT_PACKED
-#define FFT_PACKED 2
-#endif
-#if FFT_PACKED
+// complex fp32: a 2-float vector, so a complex add is one v_pk_add_f32 and a twiddle product two
+// v_pk_fma_f32 / v_pk_mul_f32.  The re/im half swap of swp() is two plain v_mov_b32 in inline asm, so
+// the compiler cannot fold it into an op_sel half-select of a packed-FP32 source.  The folded form
+// (round 3's FFT_PACKED = 1: 7,902 such instructions in this file) gave results that differed from
+// the scalar build's and, under the two-stream hGRU schedule, from run to run (13-19 of 256 crops,
+// up to 2.1e-5, all in the batch's head / tail, where one slice runs alone:
+// profiles/r3a/pk_probe_det_fp32_pk0_pk1_pk2.log); this form is bit-identical to the scalar build
+// and deterministic.  The cause was not isolated: tools/pk_hazard.hip runs the exact folded
+// instruction (v_pk_fma_f32 v[a:a+1], v[a:a+1], s[k:k+1], v[a:a+1] op_sel:[1,0,0]
+// op_sel_hi:[0,1,1]) with and without destination overlap at 1-16 waves per SIMD and finds every
+// lane exact (profiles/r4a/pk_hazard.json), and the slice-boundary audit in DESIGN.md found no
+// cross-slice address.  Guarded by tests/test_gpu_parity.py::test_stream_split_is_bit_identical and
+// test_batch_invariance_and_determinism.  (Round 3, same box: this form against the scalar one,
+// fft_fwd 0.168 -> 0.157 ms, inv_a_fwd 0.339 -> 0.329, fft_inv 0.130 -> 0.126, same bits.)
 typedef float cpx __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ cpx cfma(cpx a, cpx b, cpx c) { return __builtin_elementwise_fma(a, b, c); }
-#if FFT_PACKED == 2   // the half swap as two plain moves the compiler cannot fold into op_sel
 __device__ __forceinline__ cpx swp(cpx a) {
   float x, y;
   asm("v_mov_b32 %0, %2\n\tv_mov_b32 %1, %3" : "=&v"(x), "=&v"(y) : "v"(a.y), "v"(a.x));
   return cpx{x, y};
 }
-#else
-__device__ __forceinline__ cpx swp(cpx a) { return a.yx; }
-#endif
-#else
-struct cpx {
-  float x, y;
-};
-__device__ __forceinline__ cpx operator+(cpx a, cpx b) { return {a.x + b.x, a.y + b.y}; }
-__device__ __forceinline__ cpx operator-(cpx a, cpx b) { return {a.x - b.x, a.y - b.y}; }
-__device__ __forceinline__ cpx operator-(cpx a) { return {-a.x, -a.y}; }
-__device__ __forceinline__ cpx operator*(cpx a, cpx b) { return {a.x * b.x, a.y * b.y}; }
-__device__ __forceinline__ cpx operator*(cpx a, float s) { return {a.x * s, a.y * s}; }
-__device__ __forceinline__ cpx cfma(cpx a, cpx b, cpx c) { return {fmaf(a.x, b.x, c.x), fmaf(a.y, b.y, c.y)}; }
-__device__ __forceinline__ cpx swp(cpx a) { return {a.y, a.x}; }
-#endif
 
 // streaming (non-temporal) access to the once-written, once-read spectra and P2 (A/B switches)
 #ifndef FFT_NT_STREAM
@@ -646,7 +624,7 @@ __global__ __launch_bounds__(FNT, BF ? FFT_MINB_BF : FFT_MINB) void fft_fwd_kern
   FFT_STAMP_AT(5);
 }
 
-// fp32 forward FFT at three blocks per CU (FFT_FWD3): the transpose runs through a tile of TWO
+// fp32 forward FFT at three blocks per CU (fft_fwd3_kernel): the transpose runs through a tile of TWO
 // channels (37 fx x 2 x 65 rows, 38.5 KB) in two rounds -- channel pair 0 (the p = 0 row threads'
 // outputs), then pair 1 -- so the block's LDS is the S staging buffer (43.8 KB) instead of the
 // 77 KB four-channel tile.  Every thread reads at most one column: round A's 74 readers are wave 2
@@ -672,10 +650,6 @@ __device__ __forceinline__ int f3_reader(int tid, int& fx, int& c) {   // round 
 // zero padded); the forward row FFT, the two-round 2-channel transpose, the column FFT and the
 // LDS-staged S stores.  Called by every thread of the block (it contains barriers); lds3's space must
 // be free on entry (the caller's barrier).
-// NR: rounds of the S staging (2: 36 fy per round at pitch STG_LD, 43.8 KB; 3: 24 fy per round at
-// pitch STG3_LD, 29.6 KB, so the block's LDS is the 38.5 KB 2-channel tile and 4 blocks fit a CU)
-constexpr int STG3_LD = 200;   // 24 fy x 8 dwords + 8 pad
-template <int NR = 2>
 __device__ __forceinline__ void fwd3_tail(cpx (&v)[72], uint32_t* lds3, void* __restrict__ S, int b, int cq, int tid) {
   cpx* T2 = reinterpret_cast<cpx*>(lds3);
   int rfx = 0, rc = 0;
@@ -710,7 +684,7 @@ __device__ __forceinline__ void fwd3_tail(cpx (&v)[72], uint32_t* lds3, void* __
   read_col(1);
   if (round >= 0) fft72<-1>(v);
   uint4* dst = reinterpret_cast<uint4*>(S) + ((size_t)b * 16 + cq) * NF * 2;
-  constexpr int NY = 72 / NR, LD = NR == 2 ? STG_LD : STG3_LD, NW = 2 * NY;
+  constexpr int NR = 2, NY = 72 / NR, LD = STG_LD, NW = 2 * NY;   // S staged in two fy halves
 #pragma unroll
   for (int half = 0; half < NR; ++half) {
     lds_barrier();   // T2 (round 0) / the previous round's staging is no longer read
@@ -732,13 +706,9 @@ __device__ __forceinline__ void fwd3_tail(cpx (&v)[72], uint32_t* lds3, void* __
     }
   }
 }
-// NBLK = 4 (MP_FFT_FWD4): the S staging in three rounds, 38.5 KB of LDS, 4 blocks per CU
-constexpr int F4_LDS = FX * 2 * F3_TLD * 2;   // dwords: the 2-channel tile (>= FX * STG3_LD)
-static_assert(FX * STG3_LD <= F4_LDS, "the three-round staging fits in the 2-channel tile's space");
-template <int NBLK>
-__global__ __launch_bounds__(FNT, NBLK) void fft_fwd3_kernel(const float* __restrict__ src, void* __restrict__ S,
+__global__ __launch_bounds__(FNT, 3) void fft_fwd3_kernel(const float* __restrict__ src, void* __restrict__ S,
                                                             int H, int W) {
-  __shared__ uint32_t lds3[NBLK == 4 ? F4_LDS : F3_LDS];
+  __shared__ uint32_t lds3[F3_LDS];
   const int b = fft_block_img(blockIdx.x), cq = fft_block_cq(blockIdx.x);
   const int q = cq >> 1, e0 = 4 * (cq & 1);
   const int tid = threadIdx.x;
@@ -762,12 +732,9 @@ __global__ __launch_bounds__(FNT, NBLK) void fft_fwd3_kernel(const float* __rest
 #pragma unroll
     for (int x = 64; x < 72; ++x) v[x] = {0.f, 0.f};
   }
-  fwd3_tail<NBLK == 4 ? 3 : 2>(v, lds3, S, b, cq, tid);
+  fwd3_tail(v, lds3, S, b, cq, tid);
 }
 
-#ifndef FFT_FWD3
-#define FFT_FWD3 1    // fp32 forward FFT at three blocks per CU (fft_fwd3_kernel); 0: fft_fwd_kernel
-#endif
 
 // inverse 2-D FFT of Y -> the spatial conv result P (C8)
 template <bool BF, bool BM>
@@ -916,163 +883,8 @@ __global__ __launch_bounds__(FNT, BF ? FFT_MINB_BF : FFT_MINB) void fft_inv_a_fw
   FFT_STAMP_AT(5);
 }
 
-// ---------------------------------------------------------------------------------------------
-// fp32 inverse kernels at three blocks per CU (FFT_INV3).  The 77 KB four-channel tile of
-// inv_cols_to_T / inv_row_from_T is replaced by a 2-channel tile (64 rows x (2 x 37 + 1) complex,
-// 37.5 KB) filled in two rounds: round r carries channel pair r from the column threads to the row
-// threads of pair r, so every thread holds at most one 72-point vector (column, then row) and the
-// block's LDS is fft_fwd3_kernel's 43.8 KB staging buffer.  The inverse rows then stay in registers:
-// the row threads of a lane pair (y, p = 0 / 1) run the epilogue on their own two channels, trading
-// the other channel pair of each pixel with the partner lane (DPP) so that every map access is one
-// 16-byte load / store of a pixel's 4 channels, as the forward row loads of fft_fwd3_kernel.  No
-// parking of P or I in LDS; values and rounding are those of the two-block kernels (bit-identical).
-#ifndef FFT_INV3
-#define FFT_INV3 0
-#endif
-#ifndef I3_FENCE
-#define I3_FENCE 6   // row-tile reads per compiler fence (the old values of v stay live in the other lanes)
-#endif
-#ifndef I3_EFENCE
-#define I3_EFENCE 4  // epilogue pixel pairs per compiler fence
-#endif
-constexpr int I3_LD = 2 * FX + 1;   // complex pitch of a row y of the inverse tile (odd: conflict-free row reads)
-static_assert(64 * I3_LD * 2 <= F3_LDS, "the inverse 2-channel tile fits in the staging buffer");
-// the inverse column (fx, c = 2 r + cc) thread tid carries, and its round r (-1: none).  tid < 128:
-// lanes 4 fx .. 4 fx + 3 hold channels 0, 2, 1, 3 of fx (one 32-byte Y group per quad, as before)
-__device__ __forceinline__ int i3_col(int tid, int& fx, int& cc) {
-  int j, r;
-  if (tid < 128) { j = tid >> 1; r = tid & 1; }
-  else if (tid < 138) { j = 64 + (tid - 128); r = 1; }
-  else if (tid < 148) { j = 64 + (tid - 138); r = 0; }
-  else return -1;
-  fx = j >> 1;
-  cc = j & 1;
-  return r;
-}
-__device__ __forceinline__ cpx dpp_swap_pair(cpx a) {   // the partner lane's value (quad_perm [1,0,3,2])
-  return {__int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(a.x), 0xB1, 0xF, 0xF, false)),
-          __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(a.y), 0xB1, 0xF, 0xF, false))};
-}
-// Y -> the inverse rows in registers: for the row threads tid < 128 with y = tid >> 1 < H,
-// v[x] = (channel e0 + 2p, channel e0 + 2p + 1) of P at pixel (y, x), x < 64.  Called by every thread.
-__device__ __forceinline__ void inv3_front(const void* __restrict__ Y, int b, int cq, int tid, int H, cpx* T2,
-                                           cpx (&v)[72]) {
-  int fx = 0, cc = 0;
-  const int r = i3_col(tid, fx, cc);
-  if (r >= 0) {
-    const cpx* src = static_cast<const cpx*>(Y) + (((size_t)b * 16 + cq) * NF + spec_f<false>(fx, 0)) * 4 + 2 * r + cc;
-    constexpr int FS = spec_f<false>(0, 1) * 4;
-#pragma unroll
-    for (int fy = 0; fy < 72; ++fy) v[fy] = src[fy * FS];
-    fft72<1>(v);
-  }
-  const int y = tid >> 1, p = tid & 1;
-  const bool row = tid < 128 && y < H;
-  auto put = [&](int rr) {
-    if (r == rr) {
-#pragma unroll
-      for (int yy = 0; yy < 64; ++yy) T2[yy * I3_LD + cc * FX + fx] = v[yy];
-    }
-  };
-  auto get = [&](int rr) {   // inv_row_from_T on the 2-channel tile
-    if (row && p == rr) {
-      const int ta = y * I3_LD, tb = ta + FX;
-#pragma unroll
-      for (int k = 0; k < FX; ++k) {
-        const cpx A = T2[ta + k], B = T2[tb + k];
-        v[k] = cfma(swp(B), cpx{-1.f, 1.f}, A);
-        if (k > 0 && k < FX - 1) v[72 - k] = cfma(A, cpx{1.f, -1.f}, swp(B));
-        if (I3_FENCE && k % I3_FENCE == I3_FENCE - 1) asm volatile("" ::: "memory");   // bounds the hoisted reads
-      }
-    }
-  };
-  put(0);
-  lds_barrier();
-  get(0);
-  lds_barrier();
-  put(1);
-  lds_barrier();
-  get(1);
-  // the row FFT under a wave-uniform branch (rows y >= H transform stale values nobody reads): under
-  // the per-lane `row` the other lanes' column values had to stay live beside the transform (372 B /
-  // lane of scratch at 168 VGPRs; 12 B this way)
-  if (__builtin_amdgcn_readfirstlane(tid >> 6) < 2) fft72<1>(v);
-}
-
-// fft_inv_a_fwd_kernel at three blocks per CU (fp32 spectra and maps)
-__global__ __launch_bounds__(FNT, 3) void fft_inv_a_fwd3_kernel(const void* __restrict__ Y, ConvArgs pa,
-                                                               void* __restrict__ S) {
-  __shared__ uint32_t lds3[F3_LDS];
-  const int H = pa.H, W = pa.W;
-  const int b = fft_block_img(blockIdx.x), cq = fft_block_cq(blockIdx.x);
-  const int q = cq >> 1, e0 = 4 * (cq & 1);
-  const int tid = threadIdx.x;
-  cpx v[72];
-  inv3_front(Y, b, cq, tid, H, reinterpret_cast<cpx*>(lds3), v);
-  const int y = tid >> 1, p = tid & 1;
-  if (__builtin_amdgcn_readfirstlane(tid >> 6) < 2) {   // the row waves (wave-uniform, see inv3_front)
-    // the A epilogue (hgru_module.py:797-799) on this lane's channel pair: lane p loads all 4
-    // channels of pixel 2k + p and keeps pair p; the partner's pair of that pixel goes by DPP.
-    // Rows y >= H and columns x >= W become the forward transform's zero padding.
-    const int ch = 8 * q + e0 + 2 * p;
-    const cpx lat = {pa.vecs[V_LAT * 64 + ch], pa.vecs[V_LAT * 64 + ch + 1]};
-    const cpx be = {pa.vecs[V_BETA * 64 + ch], pa.vecs[V_BETA * 64 + ch + 1]};
-    const cpx nu = {pa.vecs[V_NU * 64 + ch], pa.vecs[V_NU * 64 + ch + 1]};
-    const bool yin = y < H;
-    const size_t row = c8_index(b, q, min(y, H - 1), 0, e0, H, W);
-#pragma unroll
-    for (int k = 0; k < 32; ++k) {
-      const int xo = 2 * k + p;
-      const size_t idx = row + 8 * min(xo, W - 1);   // unconditional (clamped) loads
-      const f32x4 xu = *reinterpret_cast<const f32x4*>(pa.X + idx);
-      const f32x4 ou = *reinterpret_cast<const f32x4*>(pa.O + idx);
-      const cpx xm = p ? cpx{xu[2], xu[3]} : cpx{xu[0], xu[1]}, xs = p ? cpx{xu[0], xu[1]} : cpx{xu[2], xu[3]};
-      const cpx om = p ? cpx{ou[2], ou[3]} : cpx{ou[0], ou[1]}, os = p ? cpx{ou[0], ou[1]} : cpx{ou[2], ou[3]};
-      const cpx xr = dpp_swap_pair(xs), orr = dpp_swap_pair(os);
-      cpx iv[2];
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {   // pixel 2k + e: own load (e == p) or the partner's
-        const cpx xe = e == p ? xm : xr, oe = e == p ? om : orr, pv = v[2 * k + e];
-        const float i0 = atanh_f(epi_a(xe.x, oe.x, pv.x, be.x, nu.x, lat.x));
-        const float i1 = atanh_f(epi_a(xe.y, oe.y, pv.y, be.y, nu.y, lat.y));
-        iv[e] = yin && 2 * k + e < W ? cpx{i0, i1} : cpx{0.f, 0.f};
-      }
-      v[2 * k] = iv[0];
-      v[2 * k + 1] = iv[1];
-      // pixel 2k + p's 4 channels: this lane's pair and the partner's pair of the same pixel
-      const cpx mine = p ? iv[1] : iv[0], other = dpp_swap_pair(p ? iv[0] : iv[1]);
-      const f32x4 o4 = p ? f32x4{other.x, other.y, mine.x, mine.y} : f32x4{mine.x, mine.y, other.x, other.y};
-      if (yin && xo < W) map_st4_stream<false>(pa.dst, idx, o4);
-      if (I3_EFENCE && k % I3_EFENCE == I3_EFENCE - 1) asm volatile("" ::: "memory");
-    }
-#pragma unroll
-    for (int x = 64; x < 72; ++x) v[x] = {0.f, 0.f};
-  }
-  lds_barrier();   // every inverse row has read the tile
-  fwd3_tail(v, lds3, S, b, cq, tid);
-}
-
-// fft_inv_kernel at three blocks per CU (fp32 spectra and maps): Y -> P (C8)
-__global__ __launch_bounds__(FNT, 3) void fft_inv3_kernel(const void* __restrict__ Y, float* __restrict__ P, int H,
-                                                         int W) {
-  __shared__ uint32_t lds3[F3_LDS];
-  const int b = fft_block_img(blockIdx.x), cq = fft_block_cq(blockIdx.x);
-  const int q = cq >> 1, e0 = 4 * (cq & 1);
-  const int tid = threadIdx.x;
-  cpx v[72];
-  inv3_front(Y, b, cq, tid, H, reinterpret_cast<cpx*>(lds3), v);
-  const int y = tid >> 1, p = tid & 1;
-  if (__builtin_amdgcn_readfirstlane(tid >> 6) < 2) {
-    const size_t row = c8_index(b, q, min(y, H - 1), 0, e0, H, W);
-#pragma unroll
-    for (int k = 0; k < 32; ++k) {
-      const int xo = 2 * k + p;
-      const cpx mine = p ? v[2 * k + 1] : v[2 * k], other = dpp_swap_pair(p ? v[2 * k] : v[2 * k + 1]);
-      const f32x4 o4 = p ? f32x4{other.x, other.y, mine.x, mine.y} : f32x4{mine.x, mine.y, other.x, other.y};
-      if (y < H && xo < W) map_st4_stream<false>(P, row + 8 * xo, o4);
-    }
-  }
-}
+// pitch (complex) of a row y of a 2-channel inverse tile (odd: conflict-free row reads)
+constexpr int I3_LD = 2 * FX + 1;
 
 // ---------------------------------------------------------------------------------------------
 // Small-batch (latency) forms of the three fp32 FFT kernels (FFT path, fp32 maps; B <= lfft_maxb()).
@@ -2016,15 +1828,6 @@ hipError_t build_spec_weights(const float* w, int ks, void* Gx, float* unscale, 
   return e;
 }
 
-// MP_FFT_FWD4=1: the fp32 forward FFT at four blocks per CU (fft_fwd3_kernel<4>)
-static bool fft_fwd4() {
-  static const bool on = [] {
-    const char* e = std::getenv("MP_FFT_FWD4");
-    return e ? std::atoi(e) != 0 : false;
-  }();
-  return on;
-}
-
 hipError_t launch_fft_fwd(const float* act, void* S, int B, int H, int W, hipStream_t st, bool bf) {
   if (!bf && !fy_major<false>() && B <= lfft_maxb())
     hipLaunchKernelGGL(lfft_fwd_kernel, dim3(B * 32), dim3(LF_NT), 0, st, act, S, H, W);
@@ -2032,10 +1835,8 @@ hipError_t launch_fft_fwd(const float* act, void* S, int B, int H, int W, hipStr
     hipLaunchKernelGGL((fft_fwd_kernel<true, true>), dim3(B * 16), dim3(FNT), 0, st, act, S, H, W);
   else if (bf)
     hipLaunchKernelGGL((fft_fwd_kernel<true, false>), dim3(B * 16), dim3(FNT), 0, st, act, S, H, W);
-  else if (FFT_FWD3 && !fy_major<false>() && fft_fwd4())
-    hipLaunchKernelGGL(fft_fwd3_kernel<4>, dim3(B * 16), dim3(FNT), 0, st, act, S, H, W);
-  else if (FFT_FWD3 && !fy_major<false>())
-    hipLaunchKernelGGL(fft_fwd3_kernel<3>, dim3(B * 16), dim3(FNT), 0, st, act, S, H, W);
+  else if (!fy_major<false>())
+    hipLaunchKernelGGL(fft_fwd3_kernel, dim3(B * 16), dim3(FNT), 0, st, act, S, H, W);
   else
     hipLaunchKernelGGL((fft_fwd_kernel<false, false>), dim3(B * 16), dim3(FNT), 0, st, act, S, H, W);
   return hipGetLastError();
@@ -2048,8 +1849,6 @@ hipError_t launch_fft_inv_a_fwd(const void* Y, const ConvArgs& a, void* S, int B
     hipLaunchKernelGGL((fft_inv_a_fwd_kernel<true, true>), dim3(B * 16), dim3(FNT), 0, st, Y, a, S);
   else if (bf)
     hipLaunchKernelGGL((fft_inv_a_fwd_kernel<true, false>), dim3(B * 16), dim3(FNT), 0, st, Y, a, S);
-  else if (FFT_INV3 && !fy_major<false>())
-    hipLaunchKernelGGL(fft_inv_a_fwd3_kernel, dim3(B * 16), dim3(FNT), 0, st, Y, a, S);
   else
     hipLaunchKernelGGL((fft_inv_a_fwd_kernel<false, false>), dim3(B * 16), dim3(FNT), 0, st, Y, a, S);
   return hipGetLastError();
@@ -2088,8 +1887,6 @@ hipError_t launch_fft_inv(const void* Y, float* P, int B, int H, int W, hipStrea
     hipLaunchKernelGGL((fft_inv_kernel<true, true>), dim3(B * 16), dim3(FNT), 0, st, Y, P, H, W);
   else if (bf)
     hipLaunchKernelGGL((fft_inv_kernel<true, false>), dim3(B * 16), dim3(FNT), 0, st, Y, P, H, W);
-  else if (FFT_INV3 && !fy_major<false>())
-    hipLaunchKernelGGL(fft_inv3_kernel, dim3(B * 16), dim3(FNT), 0, st, Y, P, H, W);
   else
     hipLaunchKernelGGL((fft_inv_kernel<false, false>), dim3(B * 16), dim3(FNT), 0, st, Y, P, H, W);
   return hipGetLastError();

@@ -116,8 +116,6 @@ BITS_CASES = [
     # output's MFMA sequence of igemm_x3pw_kernel: MP_IGEMM_PWN = 0 / 1 / 2 give the same bytes
     ("dense", "fp32_split", "MP_IGEMM_PWN", ("0", "1", "2", "3")),
     ("dense", "bf16", "MP_IGEMM_PWN", ("0", "1", "2", "3")),
-    # the fp32 forward FFT at 4 blocks per CU only stages its S stores in three rounds, not two
-    ("pose", "fp32_fft", "MP_FFT_FWD4", ("0", "1")),
     # the spectral GEMM on 8-image tiles (two groups at 12 crops) vs the 32-image tiles
     ("pose", "fp32_fft", "MP_SPEC_SMALLB", ("8", "32")),
 ]
