@@ -115,7 +115,7 @@ __device__ __forceinline__ uint32_t pack_bf2(float a, float b) {
 // and deterministic.  The cause was not isolated: tools/pk_hazard.hip runs the exact folded
 // instruction (v_pk_fma_f32 v[a:a+1], v[a:a+1], s[k:k+1], v[a:a+1] op_sel:[1,0,0]
 // op_sel_hi:[0,1,1]) with and without destination overlap at 1-16 waves per SIMD and finds every
-// lane exact (profiles/r4a/pk_hazard.json), and the slice-boundary audit in DESIGN.md found no
+// lane exact (profiles/r4/pk_hazard.json), and the slice-boundary audit in DESIGN.md found no
 // cross-slice address.  Guarded by tests/test_gpu_parity.py::test_stream_split_is_bit_identical and
 // test_batch_invariance_and_determinism.  (Round 3, same box: this form against the scalar one,
 // fft_fwd 0.168 -> 0.157 ms, inv_a_fwd 0.339 -> 0.329, fft_inv 0.130 -> 0.126, same bits.)
