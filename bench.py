@@ -307,6 +307,23 @@ def extras(mp, dev, args):
         ctx.close()
     except Exception as e:  # noqa: BLE001
         out["dense_b256_abi"] = {"error": repr(e)}
+    try:   # cnn_model_struct: the regressor the reference's driver validates / tests with (169, 291, 363)
+        cm = mp.train_cnn_networks_hgru.cnn_model_struct()
+        g = cm.record(128, 128, 69)
+        cm.load_weights(W.synth_weights(cm._table(g), seed=81))
+        gf = mp._graph.flops_per_sample(g) / 1e9
+        rec = {"gflop_per_crop": round(gf, 3), "engine": "layer-graph runtime (mp_graph_fwd)"}
+        for dt in ("fp32_split", "bf16"):
+            cm.compute_dtype = dt
+            cm.build(depth, 69)
+            t = time_gpu(lambda: cm.forward(depth), 20, 3)
+            rec[dt] = {"crops_per_s": round(B / t, 2), "ms_per_batch": round(t * 1e3, 3),
+                       "tflops": round(gf * 1e9 * B / t / 1e12, 2)}
+        rec.update(rec["fp32_split"], dtype="fp32_split")
+        out["cnn_b256"] = rec
+        cm._ctx.close()
+    except Exception as e:  # noqa: BLE001
+        out["cnn_b256"] = {"error": repr(e)}
     try:   # dense-hierarchical hybrid on the layer-graph runtime (hipGraph replay)
         import os as _os
         DH = mp.train_dense_hier_networks

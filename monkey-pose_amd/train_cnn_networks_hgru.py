@@ -11,6 +11,10 @@
   crop (``mp_crop3d_batch``).
 * ``FramePosePipeline``: ``test_model``'s per-batch body (284-321) -- attention, device crop,
   hGRU pose regressor -- as one device-resident call.
+* ``cnn_model_struct().build(crops, num_classes)`` -> ``.out_put`` [N, num_classes]
+  (train_cnn_networks_hgru.py:626-760): the regressor the reference's driver builds for
+  validation (169), ``test_model`` (291) and ``eval_model_on_real_data`` (363) -- five conv +
+  max-pool stages and four FCs, recorded op for op and run on the native layer-graph runtime.
 
 Training (``train_model``: TFRecord queues, Adam, l2 losses) is outside the inference path.
 ``train_mode`` must be falsy: the reference's ``test_model`` builds the attention net with
@@ -26,7 +30,7 @@ import numpy as np
 
 from . import _lib
 from . import weights as W
-from ._regressor import RegressorBase
+from ._regressor import GraphRegressorBase, RegressorBase
 
 
 @dataclass
@@ -70,6 +74,43 @@ class attn_model_struct(RegressorBase):
         self._ctx.attn_fwd(depth, out, _lib.current_stream(depth.device))
         self.out_put = out
         return out
+
+
+class cnn_model_struct(GraphRegressorBase):
+    """``cnn_model_struct`` (train_cnn_networks_hgru.py:626-760), inference: conv_1 .. conv_5 (3x3,
+    conv_5 5x5; relu(conv2d SAME + b)) each with a 2x2 max pool, fc_1 .. fc_3 + relu, fc_4.  The
+    reference's driver builds it for the validation / test crops (169, 291, 363).  ``build``
+    records the reference's calls (``record``, op for op against the reference's AST in
+    tests/test_cnn_model.py) and runs them on the layer-graph runtime (the f16x3 halo / tap-skipping
+    convs fused with their max pools, split-K FCs)."""
+
+    OUTPUT_ATTRS = ("out_put",)
+
+    def record(self, h, w, output_shape):
+        """The graph of build (639-673)."""
+        g = self._new_graph(h, w)
+        c, put = self.conv_layer, self._set
+        prev = g.input                                                                       # 641
+        for i, (name, k, cin, cout) in enumerate(W.CNN_CONV_SPECS, 1):                       # 642-656
+            put(f"conv{i}", c(prev, cin, cout, name, filter_size=k))
+            prev = put(f"pool{i}", self.max_pool(getattr(self, f"conv{i}"), f"pool_{i}"))
+        flat = 1
+        for s in self.pool5.shape:
+            flat *= s
+        r1 = self._relu_fc("fc1", "relu1", self.pool5, flat, 1024, "fc_1")                     # 658-661
+        r2 = self._relu_fc("fc2", "relu2", r1, 1024, 1024, "fc_2")                            # 663-666
+        r3 = self._relu_fc("fc3", "relu3", r2, 1024, 1024, "fc_3")                            # 668-671
+        f4 = put("fc4", self.fc_layer(r3, 1024, int(output_shape), "fc_4"))                   # 672
+        put("out_put", g.identity(f4))                                                        # 673
+        return g
+
+    def build(self, depth, output_shape, batch_norm=None, train_mode=None):
+        """``depth`` CUDA [N, H, W, 1] fp32 crops (crop / 10000); sets and returns ``.out_put``
+        [N, output_shape] (joint-major, / (cube_z / 2), as hgru_pose)."""
+        return self._graph_build(depth, (output_shape,), batch_norm, train_mode)
+
+    def forward(self, depth):
+        return self._graph_forward(depth)
 
 
 def prepare_data_test(image_np, tr_res, md, config, dsize: Optional[int] = None):

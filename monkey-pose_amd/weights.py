@@ -189,6 +189,24 @@ def dense_vars(output_shape: int = 69, crop: int = 128) -> List[Var]:
     return v
 
 
+# cnn_model_struct.build (train_cnn_networks_hgru.py:639-673): the hGRU driver's validation / test
+# regressor -- five conv + 2x2 max-pool stages, then fc_1 .. fc_4
+CNN_CONV_SPECS = (("conv_1", 3, 1, 64), ("conv_2", 3, 64, 128), ("conv_3", 3, 128, 256),
+                  ("conv_4", 3, 256, 512), ("conv_5", 5, 512, 1024))
+
+
+def cnn_vars(output_shape: int = 69, crop: int = 128) -> List[Var]:
+    """All variables of ``cnn_model_struct.build`` in build order; fc_1's fan-in is the flattened
+    pool_5 (five 2x2 pools: (crop / 32)^2 x 1024, 16,384 at 128 x 128, 652)."""
+    v: List[Var] = []
+    for name, k, cin, cout in CNN_CONV_SPECS:
+        v += _conv_b(name, k, cin, cout)
+    q = -(-crop // 32)
+    v += _fc("cnn/fc_1", q * q * 1024, 1024) + _fc("cnn/fc_2", 1024, 1024) + _fc("cnn/fc_3", 1024, 1024)
+    v += _fc("cnn/fc_4", 1024, output_shape)
+    return v
+
+
 HIER_FINGERS = ("p", "r", "m", "i", "t")
 
 

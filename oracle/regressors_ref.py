@@ -180,6 +180,25 @@ def attn_forward(frames: np.ndarray, wts: Dict[str, np.ndarray], dtype=np.float6
     return out
 
 
+def cnn_forward(depth: np.ndarray, wts: Dict[str, np.ndarray], dtype=np.float64, keep=False):
+    """cnn_model_struct.build (train_cnn_networks_hgru.py:639-673), inference: conv_1 .. conv_5
+    (conv_layer = relu(conv2d SAME + b), 695-710; conv_5 is 5x5), each followed by a 2x2 max pool
+    SAME (690-693); fc_1 on the NHWC flatten of pool_5 (663, 712-719) + relu, fc_2 + relu, fc_3 +
+    relu, fc_4 = out_put (dropout only under train_mode == True)."""
+    x = depth.astype(dtype)
+    t = {}
+    for i, name in enumerate(("conv_1", "conv_2", "conv_3", "conv_4", "conv_5"), 1):   # 641-656
+        x = max_pool_same(_conv(wts, x, name))
+        t[f"pool{i}"] = x
+    for name in ("fc_1", "fc_2", "fc_3"):                                            # 658-671
+        x = np.maximum(_fc(wts, x, name), 0)
+        t[name] = x
+    out = _fc(wts, x, "fc_4")                                                         # 672-673
+    if keep:
+        return out, t
+    return out
+
+
 # dense_hier_model_struct (train_dense_hier_networks.py:338-2382)
 DH_LADDER = (12, 16, 24, 32, 48, 64, 96, 128, 164, 198, 230)
 

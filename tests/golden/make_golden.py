@@ -55,6 +55,7 @@ REGRESSOR_CASES = [
     ("dense_c128", "dense", 2, 128, 77, 43),
     ("hier_c128", "hier", 2, 128, 78, 44),
     ("dense_hier_c128", "dense_hier", 2, 128, 80, 45),
+    ("cnn_c128", "cnn", 2, 128, 81, 46),   # cnn_model_struct (train_cnn_networks_hgru.py:639-673)
 ]
 HIER_HEADS = (108, 39, 39, 39, 39, 36)     # train_hier_networks.py:263 with 36 joints
 
@@ -62,6 +63,8 @@ HIER_HEADS = (108, 39, 39, 39, 39, 36)     # train_hier_networks.py:263 with 36 
 def regressor_inputs(kind, n, crop, ws, cs):
     if kind == "dense_hier":
         table = importlib.import_module("monkey-pose_amd").train_dense_hier_networks.dense_hier_vars(HIER_HEADS, crop)
+    elif kind == "cnn":
+        table = W.cnn_vars(output_shape=69, crop=crop)
     else:
         table = (W.dense_vars(output_shape=69, crop=crop) if kind == "dense"
                  else W.hier_vars(output_shape=HIER_HEADS[0], part_shapes=HIER_HEADS[1:], crop=crop))
@@ -112,8 +115,8 @@ def main(which=None):
         if which and name not in which:
             continue
         wts, depth = regressor_inputs(kind, n, crop, ws, cs)
-        if kind == "dense":
-            out = RR.dense_forward(depth, wts)
+        if kind in ("dense", "cnn"):
+            out = (RR.dense_forward if kind == "dense" else RR.cnn_forward)(depth, wts)
             np.savez_compressed(os.path.join(HERE, f"{name}.npz"), out=out)
         else:
             out, parts = (RR.hier_forward if kind == "hier" else RR.dense_hier_forward)(depth, wts)

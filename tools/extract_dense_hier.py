@@ -18,11 +18,13 @@ import sys
 REF = "/root/reference/train_dense_hier_networks.py"
 REF_HIER = "/root/reference/train_hier_networks.py"   # hier_model_struct.build (338-530), same vocabulary
 REF_DENSE = "/root/reference/train_dense_networks.py"  # dense_model_struct.build (223-408)
+REF_CNN = "/root/reference/train_cnn_networks_hgru.py"   # cnn_model_struct.build (639-673): cls="cnn_model_struct"
 
 
-def _src_build(path=REF):
+def _src_build(path=REF, cls=None):
     lines = open(path).read().split("\n")
-    start = next(i for i, l in enumerate(lines) if l.strip().startswith("def build(self,depth,output_shape"))
+    first = 0 if cls is None else next(i for i, l in enumerate(lines) if l.startswith(f"class {cls}"))
+    start = next(i for i in range(first, len(lines)) if lines[i].strip().startswith("def build(self,depth,output_shape"))
     end = next(i for i in range(start + 1, len(lines)) if lines[i].strip().startswith("def "))
     body = "\n".join(l[4:] if l.startswith("    ") else l for l in lines[start:end])
     return ast.parse(body).body[0], start + 1
@@ -40,8 +42,8 @@ def _const(node):
     return ast.literal_eval(node)
 
 
-def extract(heads=(108, 39, 39, 39, 39, 36), path=REF):
-    fn, line0 = _src_build(path)
+def extract(heads=(108, 39, 39, 39, 39, 36), path=REF, cls=None):
+    fn, line0 = _src_build(path, cls)
     shapes = {"lr_input": (128, 128, 1)}
     alias = {}
     ops = []
