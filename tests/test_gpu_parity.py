@@ -314,3 +314,15 @@ def test_full_size_properties(n):
     err = rel_inf(out[idx].cpu().numpy(), ref)
     print(f"n={n}: crops {idx} vs fp64 oracle rel_inf {err:.3e}")
     assert err <= FP32_REL_TOL
+
+
+def test_hbm_probe_reports_plausible_rates():
+    """mp_hbm_probe (bench.py's practical roof): read / write / copy of 64 MiB buffers on this GPU,
+    each between 1 TB/s and the chip's ~10 TB/s ceiling, with the access form that reached it."""
+    r = pkg()._lib.hbm_probe(0, 64 << 20)
+    for k in ("read", "write", "copy"):
+        assert 1000.0 < r[f"{k}_GBps"] < 12000.0, r
+        f = r[f"{k}_form"]
+        assert f["grid"] in (1024, 2048, 4096, 8192) and f["per_thread"] in (1, 4, 8)
+    with pytest.raises(pkg()._lib.MonkeyPoseError):
+        pkg()._lib.hbm_probe(0, 1 << 20)   # below the 64 MiB floor
