@@ -324,8 +324,7 @@ def extras(mp, dev, args):
         cm._ctx.close()
     except Exception as e:  # noqa: BLE001
         out["cnn_b256"] = {"error": repr(e)}
-    try:   # dense-hierarchical hybrid on the layer-graph runtime (hipGraph replay)
-        import os as _os
+    try:   # dense-hierarchical hybrid on the layer-graph runtime
         DH = mp.train_dense_hier_networks
         model = DH.dense_hier_model_struct()
         g = model.record(128, 128, 108, 39, 39, 39, 39, 36)
@@ -335,13 +334,9 @@ def extras(mp, dev, args):
         rec = {"gflop_per_crop": round(gf, 3), "dtype": "fp32_split",
                "kernels": model._ctx.info("graph_kernels"), "streams": model._ctx.info("graph_streams"),
                "buffers": model._ctx.info("graph_buffers")}
-        for mode in ("1", "0"):   # hipGraph replay, then eager multi-stream launches (the default)
-            _os.environ["MP_GRAPH_EXEC"] = mode
-            t = time_gpu(lambda: model.forward(depth), 10, 2)
-            k = "hipgraph_replay" if mode == "1" else "eager_multistream"
-            rec[k] = {"crops_per_s": round(B / t, 2), "ms_per_batch": round(t * 1e3, 3),
-                      "tflops": round(gf * 1e9 * B / t / 1e12, 2)}
-        rec.update(rec["eager_multistream"])
+        t = time_gpu(lambda: model.forward(depth), 10, 2)   # eager multi-stream launches
+        rec.update({"crops_per_s": round(B / t, 2), "ms_per_batch": round(t * 1e3, 3),
+                    "tflops": round(gf * 1e9 * B / t / 1e12, 2)})
         d1 = depth[:1].contiguous()
         t1 = time_gpu(lambda: model.forward(d1), 20, 3)
         rec["b1_latency_ms"] = round(t1 * 1e3, 3)

@@ -284,8 +284,7 @@ int mp_crop3d_dev_ex(const mp_camera* cam, const float* frames, int64_t n, int64
 
 /* read a model property: "output_shape", "timesteps", "ssf", "finalized", "workspace_bytes",
  * "weight_bytes"; graph contexts also "graph_kernels" (kernel launches per forward),
- * "graph_streams" (streams the schedule uses), "graph_captured" (1 once a hipGraph was built, MP_GRAPH_EXEC=1),
- * "graph_buffers" (activation buffers after concat placement), "graph_fused_pools" (2x2 max pools
+ * "graph_streams" (streams the schedule uses), "graph_buffers" (activation buffers after concat placement), "graph_fused_pools" (2x2 max pools
  * computed inside their conv's kernel: MP_GRAPH_FUSE / MP_GRAPH_FUSE_POOL) -- as planned by the
  * last forward */
 int mp_info(mp_ctx* ctx, const char* key, int64_t* value);
@@ -305,8 +304,7 @@ int mp_profile_read(mp_ctx* ctx, const char* name, double* total_ms, int64_t* la
  *     range of one wide NHWC buffer per concat group, which its producers write in place;
  *   - relu / identity fold into their producer (conv_layer already applies relu; a relu after
  *     fc_layer becomes the FC epilogue);
- *   - kernels run as a dependency DAG over up to MP_GRAPH_STREAMS (env, default 8) HIP streams
- *     (MP_GRAPH_EXEC=1: built once per (n, h, w) into a hipGraph and replayed instead).
+ *   - kernels run as a dependency DAG over up to MP_GRAPH_STREAMS (env, default 8) HIP streams.
  * Replaces the graph-builder half of dense_hier_model_struct.build (train_dense_hier_networks.py:
  * 338-2382; helpers conv_layer 2431-2446, max_pool 2426-2429, avg_pool 2416-2419, max_pool_4
  * 2421-2424, fc_layer 2448-2455). */

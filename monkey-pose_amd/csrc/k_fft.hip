@@ -128,14 +128,8 @@ __device__ __forceinline__ cpx swp(cpx a) {
 }
 
 // streaming (non-temporal) access to the once-written, once-read spectra and P2 (A/B switches)
-#ifndef FFT_NT_STREAM
-#define FFT_NT_STREAM 0     // Y loads of the inverse column phase
-#endif
 #ifndef FFT_NT_ST
 #define FFT_NT_ST 1         // staged 16-B stores of S and Y (fft_fwd 0.198 -> 0.173 ms, spec_gemm -2 %)
-#endif
-#ifndef FFT_NT_MAP
-#define FFT_NT_MAP 0        // pixel-major stores of P2 and I
 #endif
 #ifndef FFT_EPI_EU
 #define FFT_EPI_EU 8        // inv_a_fwd epilogue, fp32 maps: pixels per thread per load chunk
@@ -145,9 +139,6 @@ __device__ __forceinline__ cpx swp(cpx a) {
 #endif
 #ifndef FFT_EPI_PIPE
 #define FFT_EPI_PIPE 1      // inv_a_fwd epilogue, bf16 maps: next chunk's X / O loads issued before this chunk's math
-#endif
-#ifndef FFT_EPI_PIPE32
-#define FFT_EPI_PIPE32 0    // the same pipelining with fp32 maps
 #endif
 #ifndef FFT_EPI_EARLY
 #define FFT_EPI_EARLY 1     // chunk 0's X / O loads issued before the inverse row phase (implies the pipelining)
@@ -184,20 +175,12 @@ __device__ __forceinline__ void map_st4(float* base, size_t idx, f32x4 v) {
   else
     *reinterpret_cast<f32x4*>(base + idx) = v;
 }
-// the same for maps read exactly once by the next kernel (P2, I): non-temporal under FFT_NT_ST
+// maps read exactly once by the next kernel (P2, I).  Plain stores: the non-temporal hint on them
+// made fft_inv 0.142 -> 0.229 ms (round 2, tools/exp_fft.hip), and on the inverse column phase's Y
+// loads +7-15 %; both forms were removed in round 4.
 template <bool BM>
 __device__ __forceinline__ void map_st4_stream(float* base, size_t idx, f32x4 v) {
-  if constexpr (FFT_NT_MAP) {
-    if constexpr (BM) {
-      typedef unsigned u32x2_t __attribute__((ext_vector_type(2)));
-      __builtin_nontemporal_store(u32x2_t{pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])},
-                                  reinterpret_cast<u32x2_t*>(reinterpret_cast<uint16_t*>(base) + idx));
-    } else {
-      __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(base + idx));
-    }
-  } else {
-    map_st4<BM>(base, idx, v);
-  }
+  map_st4<BM>(base, idx, v);
 }
 template <bool BM>
 __device__ __forceinline__ cpx map_ld2(const float* base, size_t idx) {
@@ -208,43 +191,18 @@ __device__ __forceinline__ cpx map_ld2(const float* base, size_t idx) {
     return cpx{t.x, t.y};
   }
 }
-// sigmoid / tanh on v_exp_f32 + v_rcp_f32 (absolute error ~1e-7).  The A epilogue keeps ocml's
-// tanhf: ftanh there measured no faster (inv_a_fwd is not VALU-bound) and raised the FFT path's
-// error 6.1e-7 -> 8.1e-7
+// sigmoid / tanh on v_exp_f32 + v_rcp_f32 (absolute error ~1e-7).  The A epilogue uses ftanh too
+// (ocml's tanhf branches per lane: a polynomial below |x| = 0.625, an exp form above, both run by a
+// mixed wave; an odd rational minimax was also tried and removed in round 4)
 __device__ __forceinline__ float fsigmoid(float x) { return __builtin_amdgcn_rcpf(1.f + __expf(-x)); }
 __device__ __forceinline__ float ftanh(float x) { return 1.f - 2.f * __builtin_amdgcn_rcpf(1.f + __expf(2.f * x)); }
-#ifndef FFT_TANH
-#define FFT_TANH 1
-#endif
-// tanh of the A epilogue.  0: ocml tanhf (a branch per lane: polynomial below |x| = 0.625, an
-// exp-based form above, both paths executed by a mixed wave); 1: ftanh; 2: odd rational minimax
-// (numerator degree 13, denominator 6, on |x| <= 7.9; one v_rcp_f32)
-__device__ __forceinline__ float rtanh(float x) {
-  const float c = __builtin_amdgcn_fmed3f(x, -7.90531110763549805f, 7.90531110763549805f);
-  const float x2 = c * c;
-  float p = fmaf(x2, -2.76076847742355e-16f, 2.00018790482477e-13f);
-  p = fmaf(x2, p, -8.60467152213735e-11f);
-  p = fmaf(x2, p, 5.12229709037114e-08f);
-  p = fmaf(x2, p, 1.48572235717979e-05f);
-  p = fmaf(x2, p, 6.37261928875436e-04f);
-  p = fmaf(x2, p, 4.89352455891786e-03f);
-  p *= c;
-  float q = fmaf(x2, 1.19825839466702e-06f, 1.18534705686654e-04f);
-  q = fmaf(x2, q, 2.26843463243900e-03f);
-  q = fmaf(x2, q, 4.89352518554385e-03f);
-  return p * __builtin_amdgcn_rcpf(q);
-}
 // the A epilogue's tanh argument x - (beta o + nu) (p + lateral_bias) (hgru_module.py:797-799) with
 // both contractions written out: left to -ffp-contract, whether a product was fused into the
 // following add depended on the surrounding code, and the small-batch kernels rounded differently
 __device__ __forceinline__ float epi_a(float x, float o, float p, float be, float nu, float lat) {
   return fmaf(-fmaf(be, o, nu), p + lat, x);
 }
-__device__ __forceinline__ float atanh_f(float x) {
-  if constexpr (FFT_TANH == 1) return ftanh(x);
-  else if constexpr (FFT_TANH == 2) return rtanh(x);
-  else return tanhf(x);
-}
+__device__ __forceinline__ float atanh_f(float x) { return ftanh(x); }   // the A epilogue's tanh
 __device__ __forceinline__ cpx scale(cpx a, float s) { return a * s; }
 // a * e^{S i 2 pi m / 72}  (S = -1 forward, +1 inverse)
 template <int S>
@@ -314,14 +272,10 @@ __device__ __forceinline__ void dft9(cpx (&x)[9]) {
 }
 
 // in-register 72-point DFT, X[k] = sum_n v[n] e^{S 2 pi i n k / 72} (unnormalised).
-// FFT_PFA (default): Good-Thomas prime-factor form of 72 = 8 x 9 (gcd 1): n = (9 n1 + 8 n2) mod 72,
+// Good-Thomas prime-factor form of 72 = 8 x 9 (gcd 1): n = (9 n1 + 8 n2) mod 72,
 // k = (9 k1 + 64 k2) mod 72 makes e^{2 pi i n k / 72} = e^{2 pi i n1 k1 / 8} e^{2 pi i n2 k2 / 9}, so
 // the 8-point and 9-point passes need no twiddles between them (56 complex products fewer per
-// transform; both index maps are register renamings).  0: Cooley-Tukey n = 9 n1 + n2, k = k1 + 8 k2
-// with a twiddle per (n2, k1).
-#ifndef FFT_PFA
-#define FFT_PFA 1
-#endif
+// transform than Cooley-Tukey n = 9 n1 + n2; both index maps are register renamings)
 template <int S>
 __device__ __forceinline__ void fft72(cpx (&v)[72]) {
 #ifdef FFT_PROBE_NOFFT   // timing probe (tools/fft_stamps.hip): data movement without the transforms
@@ -332,10 +286,10 @@ __device__ __forceinline__ void fft72(cpx (&v)[72]) {
   for (int n2 = 0; n2 < 9; ++n2) {
     cpx t[8];
 #pragma unroll
-    for (int n1 = 0; n1 < 8; ++n1) t[n1] = FFT_PFA ? v[(9 * n1 + 8 * n2) % 72] : v[9 * n1 + n2];
+    for (int n1 = 0; n1 < 8; ++n1) t[n1] = v[(9 * n1 + 8 * n2) % 72];
     dft8<S>(t);
 #pragma unroll
-    for (int k1 = 0; k1 < 8; ++k1) a[n2][k1] = (FFT_PFA || n2 * k1 == 0) ? t[k1] : twid<S>(t[k1], n2 * k1);
+    for (int k1 = 0; k1 < 8; ++k1) a[n2][k1] = t[k1];
   }
 #pragma unroll
   for (int k1 = 0; k1 < 8; ++k1) {
@@ -344,7 +298,7 @@ __device__ __forceinline__ void fft72(cpx (&v)[72]) {
     for (int n2 = 0; n2 < 9; ++n2) u[n2] = a[n2][k1];
     dft9<S>(u);
 #pragma unroll
-    for (int k2 = 0; k2 < 9; ++k2) v[FFT_PFA ? (9 * k1 + 64 * k2) % 72 : k1 + 8 * k2] = u[k2];
+    for (int k2 = 0; k2 < 9; ++k2) v[(9 * k1 + 64 * k2) % 72] = u[k2];
   }
 }
 
@@ -520,14 +474,7 @@ __device__ __forceinline__ void inv_cols_to_T(const void* __restrict__ Y, int b,
     } else {
       const cpx* src = static_cast<const cpx*>(Y) + off;
 #pragma unroll
-      for (int fy = 0; fy < 72; ++fy) {
-        if constexpr (FFT_NT_STREAM) {
-          const f32x2_t t = __builtin_nontemporal_load(reinterpret_cast<const f32x2_t*>(src + fy * FS));
-          v[fy] = {t[0], t[1]};
-        } else {
-          v[fy] = src[fy * FS];
-        }
-      }
+      for (int fy = 0; fy < 72; ++fy) v[fy] = src[fy * FS];
     }
     fft72<1>(v);
 #pragma unroll
@@ -789,7 +736,7 @@ __global__ __launch_bounds__(FNT, BF ? FFT_MINB_BF : FFT_MINB) void fft_inv_a_fw
   // the A epilogue's X / O loads (see below); FFT_EPI_EARLY issues chunk 0's before the inverse row
   // phase, so they are in flight during the row transforms
   constexpr int EU = BM ? 8 : FFT_EPI_EU, ECH = EU * FNT, NECH = (64 * 64 + ECH - 1) / ECH;
-  constexpr bool PIPE = FFT_EPI_PIPE && (BM || FFT_EPI_PIPE32 || FFT_EPI_EARLY);
+  constexpr bool PIPE = FFT_EPI_PIPE && (BM || FFT_EPI_EARLY);
   f32x4 xv[2][EU], ov[2][EU];
   auto load_chunk = [&](int k, f32x4 (&xs)[EU], f32x4 (&os)[EU]) {
 #pragma unroll

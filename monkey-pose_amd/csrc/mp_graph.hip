@@ -12,12 +12,10 @@
 //   4. schedule: the kernel ops as a dependency DAG over up to MP_GRAPH_STREAMS (default 8)
 //      streams: an op continues the stream whose last op it consumes, else takes the least
 //      recently used stream; cross-stream edges become events, pruned by vector clocks.
-//      MP_GRAPH_EXEC=1 instead builds the DAG once into a hipGraph (kernel nodes with edges from
-//      their producers) and replays it; measured slower on this ROCm for this graph (dense-hier
-//      B = 256: 25.8 ms replay vs 19.9 ms eager over 8 streams; B = 1: 15.1 vs 9.7 ms), so eager
-//      multi-stream is the default.
-// Activations: x is copied into a graph-owned input buffer and outputs copied out, so the captured
-// graph only ever sees its own pointers.
+//      (A hipGraph replay of the same DAG measured slower on this ROCm and was removed in round 4:
+//      DESIGN.md section 3c.)
+// Activations: x is copied into a graph-owned input buffer and outputs copied out, so the plan
+// only ever sees its own pointers.
 #include <algorithm>
 #include <map>
 #include <cstdio>
@@ -59,7 +57,6 @@ struct GraphState {
     int stream = 0;
     bool record = false;     // a later op on another stream waits for it
     std::vector<int> waits;  // kernel indices on other streams to wait for
-    std::vector<int> deps;   // every kernel whose output it reads (hipGraph edges)
     IgemmArgs ia{};
     // pool
     const float* px = nullptr;
@@ -90,19 +87,7 @@ struct GraphState {
   std::vector<hipEvent_t> kev;          // per kernel (those with record)
   std::vector<hipEvent_t> joins;        // per side stream
   hipEvent_t fork = nullptr;
-  hipGraph_t graph = nullptr;
-  hipGraphExec_t exec = nullptr;
-  bool captured = false;
-
-  void drop_exec() {
-    if (exec) (void)hipGraphExecDestroy(exec);
-    if (graph) (void)hipGraphDestroy(graph);
-    exec = nullptr;
-    graph = nullptr;
-    captured = false;
-  }
   ~GraphState() {
-    drop_exec();
     for (auto e : kev)
       if (e) (void)hipEventDestroy(e);
     for (auto e : joins) (void)hipEventDestroy(e);
@@ -211,7 +196,6 @@ const mp_ctx::PackedLayer& fused_1x1_pack(mp_ctx* c, G& g, const std::vector<int
 }
 
 void plan(mp_ctx* c, G& g, int64_t n, int64_t h, int64_t w) {
-  g.drop_exec();
   g.planned = false;
   g.kerns.clear();
   g.groups.clear();
@@ -610,7 +594,6 @@ void plan(mp_ctx* c, G& g, int64_t n, int64_t h, int64_t w) {
       }
     }
     k.stream = st;
-    k.deps = deps;
     for (auto it = deps.rbegin(); it != deps.rend(); ++it) {   // latest first: it covers earlier ones
       const int d = *it, ds = g.kerns[d]->stream;
       if (known[st][ds] >= d) continue;
@@ -723,73 +706,11 @@ void issue(mp_ctx* c, G& g, hipStream_t single_st = nullptr, bool single = false
   GDBG("issued");
 }
 
-// The hipGraph of a plan, built explicitly: each kernel op's launches are captured alone on one
-// stream and their kernel nodes copied into the plan's graph, with edges from the kernels that
-// produce its inputs (an fc's gemm -> reduce pair stays a chain).  (Capturing
-// the multi-stream schedule itself via cross-stream events faults inside hipStreamEndCapture on
-// this ROCm once three or more streams take part; an explicit DAG needs no streams at all, and the
-// runtime runs independent branches concurrently.)
-void build_exec(mp_ctx* c, G& g) {
-  hipGraph_t big = nullptr;
-  hip_check(hipGraphCreate(&big, 0), "hipGraphCreate");
-  std::vector<hipGraphNode_t> node(g.kerns.size(), nullptr);
-  try {
-    for (size_t ki = 0; ki < g.kerns.size(); ++ki) {
-      auto& k = *g.kerns[ki];
-      hipGraph_t sub = nullptr;
-      hip_check(hipStreamBeginCapture(g.streams[0], hipStreamCaptureModeThreadLocal), "hipStreamBeginCapture");
-      try {
-        launch_kern(c, g, k, g.streams[0]);
-      } catch (...) {
-        (void)hipStreamEndCapture(g.streams[0], &sub);
-        if (sub) (void)hipGraphDestroy(sub);
-        throw;
-      }
-      hip_check(hipStreamEndCapture(g.streams[0], &sub), "hipStreamEndCapture");
-      // flatten: copy the captured kernel node(s) into the big graph, chained in capture order
-      size_t nn = 0;
-      hip_check(hipGraphGetNodes(sub, nullptr, &nn), "hipGraphGetNodes");
-      std::vector<hipGraphNode_t> subn(nn);
-      hip_check(hipGraphGetNodes(sub, subn.data(), &nn), "hipGraphGetNodes");
-      std::vector<hipGraphNode_t> dn;
-      for (int d : k.deps) dn.push_back(node[d]);
-      hipError_t e = hipSuccess;
-      for (size_t j = 0; j < nn && e == hipSuccess; ++j) {
-        hipGraphNodeType ty;
-        e = hipGraphNodeGetType(subn[j], &ty);
-        if (e != hipSuccess) break;
-        if (ty != hipGraphNodeTypeKernel) {
-          e = hipErrorInvalidValue;
-          break;
-        }
-        hipKernelNodeParams kp{};
-        e = hipGraphKernelNodeGetParams(subn[j], &kp);
-        if (e != hipSuccess) break;
-        hipGraphNode_t nd = nullptr;
-        e = hipGraphAddKernelNode(&nd, big, dn.data(), dn.size(), &kp);
-        dn.assign(1, nd);
-        node[ki] = nd;
-      }
-      (void)hipGraphDestroy(sub);
-      hip_check(e, "hipGraphAddKernelNode");
-    }
-    GDBG("graph built: %zu nodes", node.size());
-    hip_check(hipGraphInstantiate(&g.exec, big, nullptr, nullptr, 0), "hipGraphInstantiate");
-    GDBG("instantiated");
-  } catch (...) {
-    (void)hipGraphDestroy(big);
-    throw;
-  }
-  g.graph = big;
-  g.captured = true;
-}
-
 }  // namespace
 
 void finalize_graph(mp_ctx* c) {
   if (!c->graph) fail(MP_ERR_STATE, "mp_graph_set must precede mp_finalize_weights");
   auto& g = *c->graph;
-  g.drop_exec();
   g.planned = false;
   g.kerns.clear();
   g.fused1x1.clear();   // packed from the previous weights
@@ -847,8 +768,6 @@ bool graph_info(mp_ctx* c, const std::string& k, int64_t* v) {
     *v = (int64_t)launches;
   else if (k == "graph_streams")
     *v = g.n_streams;
-  else if (k == "graph_captured")
-    *v = g.captured ? 1 : 0;
   else if (k == "graph_buffers")
     *v = (int64_t)g.groups.size();
   else if (k == "graph_fused_1x1") {   // 1x1 convs computed by a sibling's kernel
@@ -931,24 +850,19 @@ int mp_graph_fwd(mp_ctx* ctx, const float* x, int64_t n, int64_t h, int64_t w, f
     hip_check(hipMemcpyAsync(g.input.p, x, (size_t)n * h * w * g.in_channels * sizeof(float),
                              hipMemcpyDeviceToDevice, st),
               "graph input copy");
-    const bool use_graph = env_int("MP_GRAPH_EXEC", 0) != 0 && !ctx->prof;
-    if (ctx->prof) issue(ctx, g, st, true);
-    if (use_graph && !g.exec) build_exec(ctx, g);
-    if (!ctx->prof) {
-      if (use_graph) {
-        hip_check(hipGraphLaunch(g.exec, st), "hipGraphLaunch");
-      } else {
-        // eager: the graph's stream 0 joins the caller's stream on both ends
-        hipEvent_t a = ctx->ev();
-        hip_check(hipEventRecord(a, st), "hipEventRecord");
-        hip_check(hipStreamWaitEvent(g.streams[0], a, 0), "hipStreamWaitEvent");
-        issue(ctx, g);
-        hipEvent_t b = ctx->ev();
-        hip_check(hipEventRecord(b, g.streams[0]), "hipEventRecord");
-        hip_check(hipStreamWaitEvent(st, b, 0), "hipStreamWaitEvent");
-        ctx->pool.push_back(a);
-        ctx->pool.push_back(b);
-      }
+    if (ctx->prof) {
+      issue(ctx, g, st, true);
+    } else {
+      // eager: the graph's stream 0 joins the caller's stream on both ends
+      hipEvent_t a = ctx->ev();
+      hip_check(hipEventRecord(a, st), "hipEventRecord");
+      hip_check(hipStreamWaitEvent(g.streams[0], a, 0), "hipStreamWaitEvent");
+      issue(ctx, g);
+      hipEvent_t b = ctx->ev();
+      hip_check(hipEventRecord(b, g.streams[0]), "hipEventRecord");
+      hip_check(hipStreamWaitEvent(st, b, 0), "hipStreamWaitEvent");
+      ctx->pool.push_back(a);
+      ctx->pool.push_back(b);
     }
     GDBG("launched");
     for (size_t i = 0; i < g.outputs.size(); ++i) {

@@ -141,19 +141,15 @@ def test_dense_hier_gpu_matches_golden_and_oracle(dtype):
 
 
 @pytest.mark.gpu
-def test_graph_eager_equals_replay(monkeypatch):
-    """eager multi-stream (default) == one stream == hipGraph replay, bit for bit"""
+def test_graph_eager_equals_one_stream(monkeypatch):
+    """eager multi-stream (default) == one stream, bit for bit"""
     torch = pytest.importorskip("torch")
     m = golden_meta()["dense_hier_c128"]
     wts, depth = MG.regressor_inputs("dense_hier", 3, 128, m["weight_seed"], m["crop_seed"])
     model = _gpu_model("fp32_split", wts)
     x = torch.from_numpy(depth).cuda()
     ref = model.build(x, *HEADS).cpu().numpy()
-    monkeypatch.setenv("MP_GRAPH_EXEC", "1")
-    replay = model.forward(x).cpu().numpy()
-    assert model._ctx.info("graph_captured") == 1
-    assert np.array_equal(ref, replay)
-    monkeypatch.setenv("MP_GRAPH_EXEC", "0")
+    assert model._ctx.info("graph_streams") > 1
     monkeypatch.setenv("MP_GRAPH_STREAMS", "1")
     model2 = _gpu_model("fp32_split", wts)
     one = model2.build(x, *HEADS).cpu().numpy()

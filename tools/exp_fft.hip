@@ -147,7 +147,7 @@ int main(int argc, char** argv) {
   }
   {
     const float tg = time_ms([&] { CK(launch_spec_gemm(S, Gx, Y, B, unscale, 0, false)); }, 20);
-    printf("NT_ST %d NT_LD %d: spec_gemm %.4f ms\n", FFT_NT_ST, FFT_NT_STREAM, tg);
+    printf("NT_ST %d: spec_gemm %.4f ms\n", FFT_NT_ST, tg);
   }
   for (int extra : {0}) {
     const float tf = time_ms([&] {
@@ -159,7 +159,7 @@ int main(int argc, char** argv) {
     const float ta = time_ms([&] {
       hipLaunchKernelGGL((fft_inv_a_fwd_kernel<false, false>), dim3(B * 16), dim3(FNT), extra, 0, Y, a, S);
     }, 20);
-    printf("NT_ST %d NT_LD %d extra LDS %6d B: fft_fwd %.4f  fft_inv %.4f  inv_a_fwd %.4f ms\n", FFT_NT_ST, FFT_NT_STREAM, extra, tf, ti, ta);
+    printf("NT_ST %d extra LDS %6d B: fft_fwd %.4f  fft_inv %.4f  inv_a_fwd %.4f ms\n", FFT_NT_ST, extra, tf, ti, ta);
   }
   return 0;
 }

@@ -1,5 +1,5 @@
-"""A/B timing of the layer-graph runtime on dense_hier_model_struct: hipGraph replay vs eager
-multi-stream launches, stream counts, batch 256 and batch 1.  usage: python tools/time_graph.py"""
+"""A/B timing of the layer-graph runtime on dense_hier_model_struct: eager launches over 1 / 2 / 4 /
+8 streams, batch 256 and batch 1.  usage: python tools/time_graph.py  (STREAMS=1,8 for a subset)"""
 import importlib
 import json
 import os
@@ -34,15 +34,11 @@ def main():
             model = DH.dense_hier_model_struct()
             g = model.record(128, 128, 108, 39, 39, 39, 39, 36)
             model.load_weights(W.synth_weights(model._table(g), seed=8))
-            for mode in ("0", "1"):
-                if mode == "1" and streams != 4:
-                    continue   # the graph ignores the stream count
-                os.environ["MP_GRAPH_EXEC"] = mode
-                model.build(depth, 108, 39, 39, 39, 39, 36)
-                t = t_gpu(lambda: model.forward(depth), 10 if B > 1 else 30, 2)
-                k = f"B{B}_{'graph' if mode == '1' else 'eager'}_s{streams}"
-                res[k] = {"ms": round(t * 1e3, 3), "crops_per_s": round(B / t, 1)}
-                print(k, res[k], flush=True)
+            model.build(depth, 108, 39, 39, 39, 39, 36)
+            t = t_gpu(lambda: model.forward(depth), 10 if B > 1 else 30, 2)
+            k = f"B{B}_eager_s{streams}"
+            res[k] = {"ms": round(t * 1e3, 3), "crops_per_s": round(B / t, 1)}
+            print(k, res[k], flush=True)
             del model
     print(json.dumps(res))
 
