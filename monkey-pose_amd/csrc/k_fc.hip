@@ -366,8 +366,21 @@ __device__ __forceinline__ void fcp_unroll(F&& f) {   // f(integral_constant<0>)
 #ifndef FC_P_ASMW
 #define FC_P_ASMW 1
 #endif
+// FC_P_NTW: the three-product kernel's weight stream (every packed weight read once, by one CU)
+// loaded non-temporal, so it evicts less of the activation slices that the N tiles of a K slice
+// share through their XCD's L2: fp32 fc_1 at B = 256 0.369 -> 0.359-0.362 ms, PMC 1,645 -> 1,571 MB
+// (1.17x the algorithmic 1,342 instead of 1.22x; profiles/r4n).  The one-product (bf16) kernel keeps
+// the default policy: nt made it 0.19 -> 0.23 ms.
+#ifndef FC_P_NTW
+#define FC_P_NTW 1
+#endif
+#if FC_P_NTW
+#define FCP_WPOL " nt"
+#else
+#define FCP_WPOL ""
+#endif
 __device__ __forceinline__ void fcp_ldw2(f16x8& a, f16x8& b, const f16x8* p) {
-  asm volatile("global_load_dwordx4 %0, %2, off\n\tglobal_load_dwordx4 %1, %2, off offset:1024"
+  asm volatile("global_load_dwordx4 %0, %2, off" FCP_WPOL "\n\tglobal_load_dwordx4 %1, %2, off offset:1024" FCP_WPOL
                : "=&v"(a), "=&v"(b)
                : "v"(p)
                : "memory");
