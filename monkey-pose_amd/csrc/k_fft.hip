@@ -1151,8 +1151,14 @@ constexpr int SG_NI = 32;              // images per block
 #ifndef SPEC_SMALLB
 #define SPEC_SMALLB 8   // batches up to this run spec_gemm_kernel<0, 8> (8-image tiles); 0 = off
 #endif
+#ifndef SPEC_SMALL_HALF
+#define SPEC_SMALL_HALF 1   // 8-image kernel: the weights in two halves of 4 k-steps (64 VGPRs instead of 128)
+#endif
 #ifndef SPEC_SMALL_MINB
-#define SPEC_SMALL_MINB 2   // blocks per CU of the 8-image kernel (3: 168 B / lane of scratch, 0.029 vs 0.019 ms at B = 1, profiles/r3z)
+// blocks per CU of the 8-image kernel.  Whole-weight registers at 3 spilled (168 B / lane of
+// scratch, 0.029 vs 0.019 ms at B = 1, profiles/r3z); with SPEC_SMALL_HALF 3 fit, so the 666 blocks
+// run as one round of 768 slots instead of 1.3 rounds of 512
+#define SPEC_SMALL_MINB (SPEC_SMALL_HALF ? 3 : 2)
 #endif
 constexpr int NQUAD = NF / 4;          // 666 frequency quads
 constexpr int SG_SLD = 33;             // S tile pitch (16-B units) per (cq, part, f) row
@@ -1185,17 +1191,23 @@ __global__ __launch_bounds__(256, NI == SG_NI ? 2 : SPEC_SMALL_MINB) void spec_g
     pre[it] = S[(PROBE == 2 || PROBE == 4) ? (tid & 63) : (((size_t)b * 16 + cq) * NF + 4 * quad) * 2 + piece];
   }
   // ---- weights of frequency f = 4 quad + wv: one f16x8 per (t, h, part, co block), all 32 issued
-  // before the S tile is waited for, so their L2 latency overlaps the tile's HBM latency ----
+  // before the S tile is waited for, so their L2 latency overlaps the tile's HBM latency (the
+  // 8-image kernel under SPEC_SMALL_HALF: 16 per half, the second half issued after the first
+  // half's MFMAs; the per-output k-step order is unchanged) ----
+  constexpr int TW = (NI != SG_NI && SPEC_SMALL_HALF) ? 4 : 8;   // k-steps per weight batch
   const int f = 4 * quad + wv;
   const uint4* gw = Gc + ((PROBE == 2 || PROBE == 3) ? 0 : (size_t)f * 2 * 16 * 64);
-  uint4 wr[8][2][2];
+  uint4 wr[TW][2][2];
+  auto load_w = [&](int t0) {
 #pragma unroll
-  for (int t = 0; t < 8; ++t)
+    for (int t = 0; t < TW; ++t)
 #pragma unroll
-    for (int cb = 0; cb < 2; ++cb) {
-      wr[t][cb][0] = gw[(0 * 16 + 2 * t + h) * 64 + 32 * cb + j];
-      wr[t][cb][1] = gw[(1 * 16 + 2 * t + h) * 64 + 32 * cb + j];
-    }
+      for (int cb = 0; cb < 2; ++cb) {
+        wr[t][cb][0] = gw[(0 * 16 + 2 * (t0 + t) + h) * 64 + 32 * cb + j];
+        wr[t][cb][1] = gw[(1 * 16 + 2 * (t0 + t) + h) * 64 + 32 * cb + j];
+      }
+  };
+  load_w(0);
 #pragma unroll
   for (int it = 0; it < NLD; ++it) {
     const int idx = it * 256 + tid, line = idx >> 3, piece = idx & 7;
@@ -1206,28 +1218,33 @@ __global__ __launch_bounds__(256, NI == SG_NI ? 2 : SPEC_SMALL_MINB) void spec_g
   f32x16 acc[4] = {};
   const uint4 m = {0x80000000u, 0x80000000u, 0x80000000u, 0x80000000u};
 #pragma unroll
-  for (int t = 0; t < 8; ++t) {
-    const int cq = 2 * t + h;
-    const int jj = NI == SG_NI ? j : min(j, NI - 1);   // columns past NI: zero operands (below)
-    f16x8 sh = __builtin_bit_cast(f16x8, tile[((cq * 2 + 0) * 4 + wv) * SLD + jj]);
-    f16x8 sl = __builtin_bit_cast(f16x8, tile[((cq * 2 + 1) * 4 + wv) * SLD + jj]);
-    if (NI != SG_NI && j >= NI) sh = sl = f16x8{};
+  for (int t0 = 0; t0 < 8; t0 += TW) {
+    if (t0 > 0) load_w(t0);
 #pragma unroll
-    for (int cb = 0; cb < 2; ++cb) {
-      const uint4 gh = wr[t][cb][0], gl = wr[t][cb][1];
-      // ro = 0 rows: (gr, -gi) pairs; ro = 1 rows: (gi, gr) pairs
-      const f16x8 ah0 = __builtin_bit_cast(f16x8, gh ^ m), al0 = __builtin_bit_cast(f16x8, gl ^ m);
-      const f16x8 ah1 = __builtin_bit_cast(f16x8, (gh >> 16) | (gh << 16));
-      const f16x8 al1 = __builtin_bit_cast(f16x8, (gl >> 16) | (gl << 16));
-      if constexpr (PROBE == 1) {   // keep the operand loads alive, skip the matrix cores
-        acc[cb][0] += (float)(sh[0] + sl[0] + ah0[0] + al0[0] + ah1[1] + al1[1]);
-      } else {
-        acc[cb] = mfma16(al0, sh, acc[cb]);
-        acc[cb] = mfma16(ah0, sl, acc[cb]);
-        acc[cb] = mfma16(ah0, sh, acc[cb]);
-        acc[2 + cb] = mfma16(al1, sh, acc[2 + cb]);
-        acc[2 + cb] = mfma16(ah1, sl, acc[2 + cb]);
-        acc[2 + cb] = mfma16(ah1, sh, acc[2 + cb]);
+    for (int tt = 0; tt < TW; ++tt) {
+      const int t = t0 + tt;
+      const int cq = 2 * t + h;
+      const int jj = NI == SG_NI ? j : min(j, NI - 1);   // columns past NI: zero operands (below)
+      f16x8 sh = __builtin_bit_cast(f16x8, tile[((cq * 2 + 0) * 4 + wv) * SLD + jj]);
+      f16x8 sl = __builtin_bit_cast(f16x8, tile[((cq * 2 + 1) * 4 + wv) * SLD + jj]);
+      if (NI != SG_NI && j >= NI) sh = sl = f16x8{};
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        const uint4 gh = wr[tt][cb][0], gl = wr[tt][cb][1];
+        // ro = 0 rows: (gr, -gi) pairs; ro = 1 rows: (gi, gr) pairs
+        const f16x8 ah0 = __builtin_bit_cast(f16x8, gh ^ m), al0 = __builtin_bit_cast(f16x8, gl ^ m);
+        const f16x8 ah1 = __builtin_bit_cast(f16x8, (gh >> 16) | (gh << 16));
+        const f16x8 al1 = __builtin_bit_cast(f16x8, (gl >> 16) | (gl << 16));
+        if constexpr (PROBE == 1) {   // keep the operand loads alive, skip the matrix cores
+          acc[cb][0] += (float)(sh[0] + sl[0] + ah0[0] + al0[0] + ah1[1] + al1[1]);
+        } else {
+          acc[cb] = mfma16(al0, sh, acc[cb]);
+          acc[cb] = mfma16(ah0, sl, acc[cb]);
+          acc[cb] = mfma16(ah0, sh, acc[cb]);
+          acc[2 + cb] = mfma16(al1, sh, acc[2 + cb]);
+          acc[2 + cb] = mfma16(ah1, sl, acc[2 + cb]);
+          acc[2 + cb] = mfma16(ah1, sh, acc[2 + cb]);
+        }
       }
     }
   }
