@@ -1152,7 +1152,8 @@ constexpr int SG_NI = 32;              // images per block
 #define SPEC_SMALLB 8   // batches up to this run spec_gemm_kernel<0, 8> (8-image tiles); 0 = off
 #endif
 #ifndef SPEC_SMALL_HALF
-#define SPEC_SMALL_HALF 1   // 8-image kernel: the weights in two halves of 4 k-steps (64 VGPRs instead of 128)
+#define SPEC_SMALL_HALF 1   // 8-image kernel: the weights in two halves of 4 k-steps (64 VGPRs instead of 128):
+                            // 3 blocks per CU, B = 1 forward 0.925 -> 0.890-0.897 ms (profiles/r4s)
 #endif
 #ifndef SPEC_SMALL_MINB
 // blocks per CU of the 8-image kernel.  Whole-weight registers at 3 spilled (168 B / lane of
