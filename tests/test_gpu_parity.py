@@ -275,15 +275,17 @@ def test_fft_precision_is_fp32_class():
     assert eb <= max(10 * ea, 1e-5)
 
 
-@pytest.mark.parametrize("n", [32, 64, 128, 300, 1024])
-def test_full_size_properties(n):
+@pytest.mark.parametrize("n,dtype", [(32, "fp32_fft"), (64, "fp32_fft"), (128, "fp32_fft"), (300, "fp32_fft"),
+                                     (1024, "fp32_fft"), (256, "bf16")])
+def test_full_size_properties(n, dtype):
     """BASELINE config 2 (B = 64, train_cnn_networks_hgru.py:141-142) and the per-GPU batches of the
     metric's strong-scaling reading (256 / N = 128, 64, 32), and beyond the metric's batch (ragged
     300 = 9 GEMM groups + 12, and 1024).  The hGRU loop runs as batch slices on two streams from
     64 crops on (mp_abi.hip run_circuit: 32 + 32 at B = 64, 64 + 64 at B = 128; one slice at 32).
     Every sampled crop is bit-identical to its own batch-1 run (slices, streams and GEMM groups
     never mix crops), the whole batch is finite, and the last crop of EACH slice matches the
-    float64 oracle within the fp32 gate."""
+    float64 oracle within the fp32 gate.  bf16 at 256: BASELINE config 4's per-GPU batch (2,048
+    over 8 GPUs), against the oracle within the bf16 gate."""
     from oracle import hgru_ref as R
     mp = pkg()
     W = mp.weights
@@ -291,7 +293,7 @@ def test_full_size_properties(n):
     wts = {v.name: W.synth_value(v, 1234, 8) for v in W.hgru_pose_vars(output_shape=69, timesteps=8, crop=128)}
     for k, v in wts.items():
         ctx.set_weight(k, v)
-    ctx.finalize(mp._lib.MP_DTYPE_F32_FFT)
+    ctx.finalize(mp._lib.dtype_code(dtype))
     depth_np = W.synth_crops(n, seed=21, size=128)
     o0_np = W.synth_hidden((n, 64, 64, 64), seed=22)
     depth, o0 = _cuda(depth_np), _cuda(o0_np)
@@ -312,8 +314,8 @@ def test_full_size_properties(n):
     idx = sorted({first - 1, n - 1})
     ref = R.hgru_pose_forward(depth_np[idx], wts, o0_np[idx], 8, np.float64)
     err = rel_inf(out[idx].cpu().numpy(), ref)
-    print(f"n={n}: crops {idx} vs fp64 oracle rel_inf {err:.3e}")
-    assert err <= FP32_REL_TOL
+    print(f"n={n} {dtype}: crops {idx} vs fp64 oracle rel_inf {err:.3e}")
+    assert err <= (BF16_REL_TOL if dtype == "bf16" else FP32_REL_TOL)
 
 
 def test_hbm_probe_reports_plausible_rates():
