@@ -472,9 +472,15 @@ __device__ __forceinline__ void inv_cols_to_T(const void* __restrict__ Y, int b,
 #pragma unroll
       for (int fy = 0; fy < 72; ++fy) v[fy] = unpack_bf2(src[fy * FS]);
     } else {
+#ifdef FFT_PROBE_YCOAL   // timing probe (tools/bench_fft.hip): the block's Y run read wave-contiguously
+      const cpx* src = static_cast<const cpx*>(Y) + ((size_t)b * 16 + cq) * NF * 4 + tid;
+#pragma unroll
+      for (int fy = 0; fy < 72; ++fy) v[fy] = src[fy * FX * 4];
+#else
       const cpx* src = static_cast<const cpx*>(Y) + off;
 #pragma unroll
       for (int fy = 0; fy < 72; ++fy) v[fy] = src[fy * FS];
+#endif
     }
     fft72<1>(v);
 #pragma unroll
@@ -713,7 +719,11 @@ __global__ __launch_bounds__(FNT, BF ? FFT_MINB_BF : FFT_MINB) void fft_inv_kern
   for (int i = tid; i < H * W; i += FNT) {
     const int yy = i / W, x = i - yy * W;
     const cpx a = T.get((2 * yy) * RLD + x), c = T.get((2 * yy + 1) * RLD + x);
+#ifdef FFT_PROBE_PCOAL   // timing probe (tools/bench_fft.hip): the block's P quarter written contiguously
+    map_st4_stream<BM>(P, ((size_t)b * 16 + cq) * 4096 * 4 + 4 * i, f32x4{a.x, a.y, c.x, c.y});
+#else
     map_st4_stream<BM>(P, c8_index(b, q, yy, x, e0, H, W), f32x4{a.x, a.y, c.x, c.y});
+#endif
   }
   FFT_STAMP_AT(5);
 }
@@ -1162,6 +1172,7 @@ constexpr int SG_NI = 32;              // images per block
 #define SPEC_SMALL_MINB (SPEC_SMALL_HALF ? 3 : 2)
 #endif
 constexpr int NQUAD = NF / 4;          // 666 frequency quads
+constexpr int NQ8 = (NQUAD + 7) / 8;
 constexpr int SG_SLD = 33;             // S tile pitch (16-B units) per (cq, part, f) row
 constexpr int SG_YLD = 16 * 4 * 2 + 1; // Y tile pitch (16-B units) per image
 // NI: images per block -- 32, or 8 for batches <= SPEC_SMALLB (a quarter of the S tile's loads and
@@ -1169,14 +1180,27 @@ constexpr int SG_YLD = 16 * 4 * 2 + 1; // Y tile pitch (16-B units) per image
 template <int PROBE = 0, int NI = SG_NI>   // timing probes (tools/bench_fft.hip): 1 = no MFMA, 2 = no S / weight loads,
                                           // 3 = no weight loads, 4 = no S loads
 __global__ __launch_bounds__(256, NI == SG_NI ? 2 : SPEC_SMALL_MINB) void spec_gemm_kernel(const uint4* __restrict__ S, const uint4* __restrict__ Gc,
-                                                           uint4* __restrict__ Y, int B, int ngrp, float unscale) {
+                                                           uint4* __restrict__ Y, int B, int ngrp, float unscale,
+                                                           int gmaj) {
   constexpr int SLD = NI + 1;               // S tile pitch (16-B units) per (cq, part, f) row
   constexpr int NLD = NI * 16 * 8 / 256;    // 16-B S / Y pieces per thread
   __shared__ uint4 tile[16 * 2 * 4 * SLD];   // 67,584 B (NI = 32)
   static_assert(NI * SG_YLD <= 16 * 2 * 4 * SLD, "the Y tile fits in the S tile's space");
   // block -> (quad, image group): the ngrp groups of quad q run on XCD q % 8 (round-robin dispatch)
-  const int q8 = blockIdx.x / (8 * ngrp), rem = blockIdx.x - q8 * 8 * ngrp;
-  const int grp = rem >> 3, quad = q8 * 8 + (rem & 7);
+  // gmaj = G > 0: passes of G image groups, last groups first (quad q still on XCD q % 8, a pass's G
+  // groups of a quad one after the other), so the first blocks read the S lines the forward FFT wrote
+  // last and the last ones write the Y lines the inverse FFT reads first
+  int grp, quad;
+  if (gmaj) {
+    const int nb = NQ8 * 8, ps = blockIdx.x / (gmaj * nb), off = blockIdx.x - ps * gmaj * nb;
+    const int gp = min(gmaj, ngrp - ps * gmaj), q8 = off / (8 * gp), rem = off - q8 * 8 * gp;
+    grp = ngrp - 1 - (ps * gmaj + (rem >> 3));
+    quad = q8 * 8 + (rem & 7);
+  } else {
+    const int q8 = blockIdx.x / (8 * ngrp), rem = blockIdx.x - q8 * 8 * ngrp;
+    grp = rem >> 3;
+    quad = q8 * 8 + (rem & 7);
+  }
   if (quad >= NQUAD) return;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, j = lane & 31;
   const int img0 = grp * NI;
@@ -1285,11 +1309,23 @@ __global__ __launch_bounds__(256, NI == SG_NI ? 2 : SPEC_SMALL_MINB) void spec_g
 constexpr int NQ16 = (NQUAD + 15) / 16;
 constexpr int SGB_YLD = 16 * 4 + 1;    // Y tile pitch (16-B units) per image
 __global__ __launch_bounds__(256, 2) void spec_gemm_bf_kernel(const uint4* __restrict__ S, const uint4* __restrict__ Gb,
-                                                              uint4* __restrict__ Y, int B, int ngrp) {
+                                                              uint4* __restrict__ Y, int B, int ngrp, int gmaj) {
   __shared__ uint4 tile[16 * 4 * SG_SLD];   // 33,792 B (S tile [cq][f][b]; Y tile [b][cq][f])
   // block -> (quad, image group): XCD x = rem % 8 takes the quad pair (2x, 2x+1) of each 16
-  const int q16 = blockIdx.x / (16 * ngrp), rem = blockIdx.x - q16 * 16 * ngrp;
-  const int sq = rem >> 3, grp = sq >> 1, quad = q16 * 16 + 2 * (rem & 7) + (sq & 1);
+  // (gmaj: passes of image groups, last first, as in spec_gemm_kernel)
+  int grp, quad;
+  if (gmaj) {
+    const int nb = NQ16 * 16, ps = blockIdx.x / (gmaj * nb), off = blockIdx.x - ps * gmaj * nb;
+    const int gp = min(gmaj, ngrp - ps * gmaj), q16 = off / (16 * gp), rem = off - q16 * 16 * gp;
+    const int sq = rem >> 3;
+    grp = ngrp - 1 - (ps * gmaj + (sq >> 1));
+    quad = q16 * 16 + 2 * (rem & 7) + (sq & 1);
+  } else {
+    const int q16 = blockIdx.x / (16 * ngrp), rem = blockIdx.x - q16 * 16 * ngrp;
+    const int sq = rem >> 3;
+    grp = sq >> 1;
+    quad = q16 * 16 + 2 * (rem & 7) + (sq & 1);
+  }
   if (quad >= NQUAD) return;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, j = lane & 31;
   const int img0 = grp * SG_NI;
@@ -1488,10 +1524,14 @@ __device__ __forceinline__ void gate_any(const void* gpk, const f32x16 (&V)[2], 
 template <bool BF, bool BM, bool FINAL = false>
 __global__ __launch_bounds__(256) void spec_epi_b_kernel(ConvArgs p, const float* __restrict__ P,
                                                          const void* __restrict__ or_x3, float or_us,
-                                                         const void* __restrict__ ir_x3, float ir_us, int nseg) {
+                                                         const void* __restrict__ ir_x3, float ir_us, int nseg,
+                                                         int rev) {
   const int lane = threadIdx.x & 63, h = lane >> 5;
-  const int seg = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (seg >= nseg) return;
+  const int seg0 = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (seg0 >= nseg) return;
+  // rev: segments (images) in descending order, so the first blocks read the P2 lines fft_inv wrote
+  // last (still in the Infinity Cache) and the last ones write the Og lines the next fft_fwd reads first
+  const int seg = rev ? nseg - 1 - seg0 : seg0;
   const int H = p.H, W = p.W, xs = W / 32;
   const int x = (seg % xs) * 32 + (lane & 31);
   const int y = (seg / xs) % H, b = seg / xs / H;
@@ -1829,19 +1869,31 @@ static int spec_smallb() {
   return v;
 }
 
+// MP_SPEC_GMAJ = G (default 2): spectral-GEMM blocks in passes of G 32-image groups, last first
+// (spec_gemm_kernel gmaj; 0 = every quad's groups together, the weights fetched once per launch).
+// G = 2 with MP_EPI_REV: fp32 B = 256 10.43 -> 10.37 ms, bf16 6.23 -> 6.17 ms; G = 1 re-reads the
+// 87 MB of weights once per group and lost (10.93 ms; profiles/r4o)
+static int spec_gmaj() {
+  static const int v = [] {
+    const char* e = std::getenv("MP_SPEC_GMAJ");
+    return e ? std::atoi(e) : 2;
+  }();
+  return v;
+}
+
 hipError_t launch_spec_gemm(const void* S, const void* Gx, void* Y, int B, float unscale, hipStream_t st, bool bf) {
   const bool small = !bf && B <= spec_smallb();
   const int ngrp = small ? (B + 7) / 8 : (B + SG_NI - 1) / SG_NI;
-  const int nq8 = (NQUAD + 7) / 8;
+  const int gm = small ? 0 : spec_gmaj();
   if (bf)
     hipLaunchKernelGGL(spec_gemm_bf_kernel, dim3(NQ16 * 16 * ngrp), dim3(256), 0, st, static_cast<const uint4*>(S),
-                       static_cast<const uint4*>(Gx), static_cast<uint4*>(Y), B, ngrp);
+                       static_cast<const uint4*>(Gx), static_cast<uint4*>(Y), B, ngrp, gm);
   else if (small)
-    hipLaunchKernelGGL((spec_gemm_kernel<0, 8>), dim3(nq8 * 8 * ngrp), dim3(256), 0, st, static_cast<const uint4*>(S),
-                       static_cast<const uint4*>(Gx), static_cast<uint4*>(Y), B, ngrp, unscale);
+    hipLaunchKernelGGL((spec_gemm_kernel<0, 8>), dim3(NQ8 * 8 * ngrp), dim3(256), 0, st, static_cast<const uint4*>(S),
+                       static_cast<const uint4*>(Gx), static_cast<uint4*>(Y), B, ngrp, unscale, 0);
   else
-    hipLaunchKernelGGL(spec_gemm_kernel<0>, dim3(nq8 * 8 * ngrp), dim3(256), 0, st, static_cast<const uint4*>(S),
-                       static_cast<const uint4*>(Gx), static_cast<uint4*>(Y), B, ngrp, unscale);
+    hipLaunchKernelGGL(spec_gemm_kernel<0>, dim3(NQ8 * 8 * ngrp), dim3(256), 0, st, static_cast<const uint4*>(S),
+                       static_cast<const uint4*>(Gx), static_cast<uint4*>(Y), B, ngrp, unscale, gm);
   return hipGetLastError();
 }
 
@@ -1893,12 +1945,23 @@ hipError_t launch_gate_init_x3(const float* O0, float* O, float* Og, const void*
   return hipGetLastError();
 }
 
+// MP_EPI_REV (default 1): the B epilogue walks its images last to first, so its first blocks read the
+// P2 lines fft_inv wrote last and its last blocks write the Og lines the next fft_fwd reads first
+// (B = 256 fp32 10.43 -> 10.37 ms per forward, profiles/r4o; 0 restores ascending order)
+static int epi_rev() {
+  static const int v = [] {
+    const char* e = std::getenv("MP_EPI_REV");
+    return e ? std::atoi(e) : 1;
+  }();
+  return v;
+}
+
 hipError_t launch_spec_epi_b(const ConvArgs& a, const float* P, const void* or_x3, float or_us, const void* ir_x3,
                              float ir_us, int B, hipStream_t st, bool bf) {
   const int nseg = B * a.H * (a.W / 32);
 #define MP_EPIB(BFV, BMV, FV)                                                                                     \
   hipLaunchKernelGGL((spec_epi_b_kernel<BFV, BMV, FV>), dim3((nseg + 3) / 4), dim3(256), 0, st, a, P, or_x3, or_us, \
-                     ir_x3, ir_us, nseg)
+                     ir_x3, ir_us, nseg, epi_rev())
   const bool fin = a.mode != 0;
   if (bf && fft_bf16_maps()) {
     if (fin) MP_EPIB(true, true, true);

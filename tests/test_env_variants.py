@@ -101,8 +101,9 @@ if kind == "dense":
     model.compute_dtype = dtype
     model.load_weights(wts)
     out = model.build(torch.from_numpy(depth).cuda(), 69, train_mode=False).cpu().numpy()
-else:   # 12 crops: above the small-batch FFT kernels' B <= 8
-    wts, depth, O0 = MG.pose_inputs(12, 64, 8, 5, 6, 7)
+else:   # 12 crops: above the small-batch FFT kernels' B <= 8; pose80: three 32-image GEMM groups,
+        # two hGRU slices (64 + 16 crops)
+    wts, depth, O0 = MG.pose_inputs(80 if kind == "pose80" else 12, 64, 8, 5, 6, 7)
     model = P.hgru_pose.model()
     model.compute_dtype = dtype
     model.load_weights(wts)
@@ -118,6 +119,10 @@ BITS_CASES = [
     ("dense", "bf16", "MP_IGEMM_PWN", ("0", "1", "2", "3")),
     # the spectral GEMM on 8-image tiles (two groups at 12 crops) vs the 32-image tiles
     ("pose", "fp32_fft", "MP_SPEC_SMALLB", ("8", "32")),
+    # image order only: the B epilogue last image first, the spectral GEMM in passes of G groups
+    ("pose80", "fp32_fft", "MP_EPI_REV", ("0", "1")),
+    ("pose80", "fp32_fft", "MP_SPEC_GMAJ", ("0", "1", "2")),
+    ("pose80", "bf16", "MP_SPEC_GMAJ", ("0", "1", "2")),
 ]
 
 
