@@ -273,23 +273,24 @@ __global__ void nhwc_to_c8_kernel(const float* __restrict__ in, float* out, int 
 // dst_img: elements between consecutive images of the NHWC output (H*W*C when dense; larger when
 // writing one timestep of a [n, T, H, W, C] state stack)
 __global__ void c8_to_nhwc_kernel(const float* __restrict__ in, float* out, int B, int H, int W, bool bf,
-                                  size_t dst_img) {
+                                  size_t dst_img, bool c4) {
   const size_t total = (size_t)B * H * W * NQ;
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= total) return;
   const int q = i % NQ;
   const size_t pix = i / NQ;
   const int x = pix % W, y = (pix / W) % H, b = pix / ((size_t)W * H);
-  const size_t o = c8_index(b, q, y, x, 0, H, W);
+  // the chunk's two 4-channel halves (adjacent in C8, separate runs in C4)
+  const size_t o0 = c4 ? c4_index(b, q, y, x, 0, H, W) : c8_index(b, q, y, x, 0, H, W);
+  const size_t o1 = c4 ? c4_index(b, q, y, x, 4, H, W) : o0 + 4;
   f32x4* d = reinterpret_cast<f32x4*>(out + b * dst_img + ((size_t)y * W + x) * C + 8 * q);
   if (bf) {
-    const uint2* s = reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(in) + o);
-    d[0] = bf16x4_unpack(s[0]);
-    d[1] = bf16x4_unpack(s[1]);
+    const uint16_t* s = reinterpret_cast<const uint16_t*>(in);
+    d[0] = bf16x4_unpack(*reinterpret_cast<const uint2*>(s + o0));
+    d[1] = bf16x4_unpack(*reinterpret_cast<const uint2*>(s + o1));
   } else {
-    const f32x4* s = reinterpret_cast<const f32x4*>(in + o);
-    d[0] = s[0];
-    d[1] = s[1];
+    d[0] = *reinterpret_cast<const f32x4*>(in + o0);
+    d[1] = *reinterpret_cast<const f32x4*>(in + o1);
   }
 }
 
@@ -381,11 +382,11 @@ hipError_t launch_nhwc_to_c8(const float* in, float* out, int B, int H, int W, h
 }
 
 hipError_t launch_c8_to_nhwc(const float* in, float* out, int B, int H, int W, hipStream_t st, bool bf,
-                             size_t dst_img) {
+                             size_t dst_img, bool c4) {
   const size_t total = (size_t)B * H * W * NQ;
   if (dst_img == 0) dst_img = (size_t)H * W * C;
   hipLaunchKernelGGL(c8_to_nhwc_kernel, dim3((total + 255) / 256), dim3(256), 0, st, in, out, B, H, W, bf,
-                     dst_img);
+                     dst_img, c4);
   return hipGetLastError();
 }
 

@@ -8,8 +8,9 @@
 //
 //   fft_fwd   act (C8)          -> S[b][cq][f][4]    2-D real FFT per (image, 4-channel group)
 //   spec_gemm S, G              -> Y[b][cq][f][4]    per frequency: Y[b][co] = sum_ci S[b][ci] G[ci][co]
-//   fft_inv   Y                 -> P (C8)            2-D inverse (complex-to-real) FFT
-//   spec_epi  P (+ X, O, I ...) -> the fused hGRU epilogue of conv_epi.hpp, unchanged
+//   fft_inv   Y                 -> P (C4)            2-D inverse (complex-to-real) FFT
+//   inv_a_fwd Y, X, O           -> I (C4), S         inverse FFT + A epilogue + forward FFT of I
+//   epi_b     P, I, O           -> O', Og' (C8)      B epilogue with the 1x1 gates (all 64 channels)
 //
 // G[f][ci][co] = (1/N^2) sum_{ky,kx} w[ky][kx][ci][co] exp(-2 pi i (fy (R-ky) + fx (R-kx)) / N)
 // (cross-correlation written as a convolution with the flipped kernel, inverse-DFT scale folded in)
@@ -143,6 +144,23 @@ __device__ __forceinline__ cpx swp(cpx a) {
 #ifndef FFT_EPI_EARLY
 #define FFT_EPI_EARLY 1     // chunk 0's X / O loads issued before the inverse row phase (implies the pipelining)
 #endif
+// FFT_C4: the loop's P2 and I maps in the C4 layout (mp_common.hpp c4_index; bit 0: P2, bit 1: I), so
+// the inverse kernels (fft_inv, inv_a_fwd, their latency forms) write each block's 4-channel group as
+// one contiguous run instead of 16-B halves of 32-B C8 pixels; spec_epi_b and the state stacks read
+// them there.  Probes of the two writes made contiguous: fft_inv 0.134 -> 0.125 ms, inv_a_fwd 0.340 ->
+// 0.328 ms at B = 256.  Unswizzled C4 reads cost fp32 epi_b 0.259 -> 0.289 ms on one box; with the
+// odd group's row halves swapped (C4_SWZ) the same-box A/B against C8 is fp32 10.65 -> 10.46 ms, bf16
+// 6.20 -> 6.10, B = 64 3.34 -> 3.28 (profiles/r4o).  0 restores C8 maps.
+#ifndef FFT_C4
+#define FFT_C4 3
+#endif
+// (bit 0: P2, bit 1: I)
+__device__ __forceinline__ size_t pp_index(int b, int q, int y, int x, int e, int H, int W) {
+  return (FFT_C4 & 1) ? c4_index(b, q, y, x, e, H, W) : c8_index(b, q, y, x, e, H, W);
+}
+__device__ __forceinline__ size_t ii_index(int b, int q, int y, int x, int e, int H, int W) {
+  return (FFT_C4 & 2) ? c4_index(b, q, y, x, e, H, W) : c8_index(b, q, y, x, e, H, W);
+}
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ void st16(uint4* p, uint4 v) {
@@ -722,7 +740,7 @@ __global__ __launch_bounds__(FNT, BF ? FFT_MINB_BF : FFT_MINB) void fft_inv_kern
 #ifdef FFT_PROBE_PCOAL   // timing probe (tools/bench_fft.hip): the block's P quarter written contiguously
     map_st4_stream<BM>(P, ((size_t)b * 16 + cq) * 4096 * 4 + 4 * i, f32x4{a.x, a.y, c.x, c.y});
 #else
-    map_st4_stream<BM>(P, c8_index(b, q, yy, x, e0, H, W), f32x4{a.x, a.y, c.x, c.y});
+    map_st4_stream<BM>(P, pp_index(b, q, yy, x, e0, H, W), f32x4{a.x, a.y, c.x, c.y});
 #endif
   }
   FFT_STAMP_AT(5);
@@ -815,7 +833,11 @@ __global__ __launch_bounds__(FNT, BF ? FFT_MINB_BF : FFT_MINB) void fft_inv_a_fw
             iv[j] = atanh_f(epi_a(xv[cur][u][j], ov[cur][u][j], pv[j], be[j], nu[j], lat[j]));
 #endif
           }
-          map_st4_stream<BM>(p.dst, c8_index(b, q, yy, x, e0, H, W), iv);
+#ifdef FFT_PROBE_ICOAL   // timing probe (tools/bench_fft.hip): the block's I quarter written contiguously
+          map_st4_stream<BM>(p.dst, ((size_t)b * 16 + cq) * 4096 * 4 + 4 * i, iv);
+#else
+          map_st4_stream<BM>(p.dst, ii_index(b, q, yy, x, e0, H, W), iv);
+#endif
           T.set(ia, {iv[0], iv[1]});
           T.set(ic, {iv[2], iv[3]});
         } else {
@@ -1086,7 +1108,7 @@ __global__ __launch_bounds__(LF_NT, 1) void lfft_inv_a_fwd_kernel(const void* __
       const cpx pv = R[y * LF_ZLD + x];
       iv = {atanh_f(epi_a(xv[i].x, ov[i].x, pv.x, be.x, nu.x, lat.x)),
             atanh_f(epi_a(xv[i].y, ov[i].y, pv.y, be.y, nu.y, lat.y))};
-      *reinterpret_cast<float2*>(pa.dst + c8_index(b, q, y, x, ec, H, W)) = float2{iv.x, iv.y};
+      *reinterpret_cast<float2*>(pa.dst + ii_index(b, q, y, x, ec, H, W)) = float2{iv.x, iv.y};
     }
     R[y * LF_ZLD + x] = iv;
   }
@@ -1109,7 +1131,7 @@ __global__ __launch_bounds__(LF_NT, 1) void lfft_inv_kernel(const void* __restri
     const int y = px >> 6, x = px & 63;
     if (y < H && x < W) {
       const cpx v = R[y * LF_ZLD + x];
-      *reinterpret_cast<float2*>(P + c8_index(b, q, y, x, ec, H, W)) = float2{v.x, v.y};
+      *reinterpret_cast<float2*>(P + pp_index(b, q, y, x, ec, H, W)) = float2{v.x, v.y};
     }
   }
 }
@@ -1544,9 +1566,9 @@ __global__ __launch_bounds__(256) void spec_epi_b_kernel(ConvArgs p, const float
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const size_t idx = c8_index(b, 4 * n + g, y, x, 4 * h, H, W);
-      const f32x4 iv = map_ld4<BM>(p.I, idx);
+      const f32x4 iv = map_ld4<BM>(p.I, ii_index(b, 4 * n + g, y, x, 4 * h, H, W));
       if constexpr (BM) {
-        pvs[n][g] = map_ld4<BM>(P, idx);
+        pvs[n][g] = map_ld4<BM>(P, pp_index(b, 4 * n + g, y, x, 4 * h, H, W));
         ovs[n][g] = map_ld4<BM>(p.O, idx);
       }
 #pragma unroll
@@ -1559,7 +1581,7 @@ __global__ __launch_bounds__(256) void spec_epi_b_kernel(ConvArgs p, const float
     for (int g = 0; g < 4; ++g) {
       const int c = 32 * n + 8 * g + 4 * h;
       const size_t idx = c8_index(b, 4 * n + g, y, x, 4 * h, H, W);
-      const f32x4 pv = BM ? pvs[n][g] : map_ld4<BM>(P, idx);
+      const f32x4 pv = BM ? pvs[n][g] : map_ld4<BM>(P, pp_index(b, 4 * n + g, y, x, 4 * h, H, W));
       const f32x4 ov = BM ? ovs[n][g] : map_ld4<BM>(p.O, idx);
       const f32x4 lat = *reinterpret_cast<const f32x4*>(p.vecs + V_LAT * 64 + c);
       const f32x4 ga = *reinterpret_cast<const f32x4*>(p.vecs + V_GAMMA * 64 + c);
@@ -1748,29 +1770,8 @@ __global__ void pack_gate_bf_kernel(const float* __restrict__ g, uint4* __restri
   out[(n2 * 4 + s) * 64 + lane] = uint4{w[0], w[1], w[2], w[3]};
 }
 
-// the fused epilogue on the spatial result P: one wave per 32-pixel row segment, P loaded in the
-// v_mfma 32x32 accumulator layout conv_epilogue expects (cout 32n + 8g + 4h + j at lane col x)
-template <int EPI>
-__global__ __launch_bounds__(256) void spec_epi_kernel(ConvArgs p, const float* __restrict__ P, int nseg) {
-  const int lane = threadIdx.x & 63, h = lane >> 5;
-  const int seg = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (seg >= nseg) return;
-  const int xs = p.W / 32;
-  const int x = (seg % xs) * 32 + (lane & 31);
-  const int y = (seg / xs) % p.H, b = seg / xs / p.H;
-  f32x16 acc[2];
-#pragma unroll
-  for (int n = 0; n < 2; ++n)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const f32x4 v = *reinterpret_cast<const f32x4*>(P + c8_index(b, 4 * n + g, y, x, 4 * h, p.H, p.W));
-#pragma unroll
-      for (int j = 0; j < 4; ++j) acc[n][4 * g + j] = v[j];
-    }
-  conv_epilogue<EPI>(p, acc[0], acc[1], b, y, x, h, lane, 1.0f);
-}
-
 // ------------------------------------------------------------------------------------ launchers
+bool fft_c4_maps() { return (FFT_C4 & 2) != 0; }
 bool fft_bf16_maps() {
   static const bool v = [] {
     const char* e = std::getenv("MP_BF16_MAPS");
@@ -1974,17 +1975,6 @@ hipError_t launch_spec_epi_b(const ConvArgs& a, const float* P, const void* or_x
     else MP_EPIB(false, false, false);
   }
 #undef MP_EPIB
-  return hipGetLastError();
-}
-
-hipError_t launch_spec_epi(int epi, const ConvArgs& a, const float* P, int B, hipStream_t st) {
-  const int nseg = B * a.H * (a.W / 32);
-  if (epi == EPI_HGRU_A)
-    hipLaunchKernelGGL((spec_epi_kernel<EPI_HGRU_A>), dim3((nseg + 3) / 4), dim3(256), 0, st, a, P, nseg);
-  else if (epi == EPI_HGRU_B)
-    hipLaunchKernelGGL((spec_epi_kernel<EPI_HGRU_B>), dim3((nseg + 3) / 4), dim3(256), 0, st, a, P, nseg);
-  else
-    return hipErrorInvalidValue;
   return hipGetLastError();
 }
 

@@ -19,6 +19,17 @@ constexpr int NQ = C / 8;  // channel chunks in the C8 layout
 __device__ __forceinline__ size_t c8_index(int b, int q, int y, int x, int e, int H, int W) {
   return ((((size_t)b * NQ + q) * H + y) * W + x) * 8 + e;
 }
+// C4 [N][16 channel groups][H][W][4]: the FFT loop's P2 and I maps (k_fft.hip pi_index), written per
+// 4-channel group by the inverse FFT kernels as one contiguous run; channel 8 q + e of the C8 naming
+#ifndef C4_SWZ
+#define C4_SWZ 1
+#endif
+__device__ __forceinline__ size_t c4_index(int b, int q, int y, int x, int e, int H, int W) {
+  // C4_SWZ: the odd group's row halves swapped, so the two half-waves of a C8-pattern access (groups
+  // 2q and 2q + 1 at the same 32 pixels) read runs 512 B apart modulo 64 KiB
+  const int xs = (C4_SWZ && (e & 4)) ? (x ^ (W >> 1)) : x;
+  return ((((size_t)b * (2 * NQ) + 2 * q + (e >> 2)) * H + y) * W + xs) * 4 + (e & 3);
+}
 
 // bf16 C8 maps (MP_DTYPE_BF16's hGRU maps): 4 channels = 8 bytes, round to nearest even on store
 __device__ __forceinline__ uint2 bf16x4_pack(f32x4 v) {

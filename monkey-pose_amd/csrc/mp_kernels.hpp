@@ -44,8 +44,9 @@ hipError_t launch_conv1_pool_any(const float* in, const float* w, const float* b
                                  int B, int Hin, int Win, int Cout, hipStream_t st);
 // bf: the C8 side is a bf16 map
 hipError_t launch_nhwc_to_c8(const float* in, float* out, int B, int H, int W, hipStream_t st, bool bf = false);
+// c4: the source is a C4 map (mp_common.hpp c4_index: the FFT loop's I, fft_c4_maps())
 hipError_t launch_c8_to_nhwc(const float* in, float* out, int B, int H, int W, hipStream_t st, bool bf = false,
-                             size_t dst_img = 0);
+                             size_t dst_img = 0, bool c4 = false);
 hipError_t launch_pack_conv64(const float* w, f32x4* out, int ks, hipStream_t st);
 hipError_t launch_pack_gate(const float* g, f32x4* out, hipStream_t st);
 // k_conv64x3.hip (fp32-accurate split-f16 MFMA path)
@@ -60,6 +61,7 @@ hipError_t device_absmax(const float* x, size_t n, float* out);   // max |x| (sy
 // MP_DTYPE_BF16 keeps the hGRU state maps O, I, Og, P2 in bf16 (MP_BF16_MAPS=0: fp32, for A/B);
 // their element offsets are unchanged, so a map pointer offset by m elements is (bf16*)base + m
 bool fft_bf16_maps();
+bool fft_c4_maps();   // the FFT loop's I map is C4 (k_fft.hip FFT_C4)
 size_t fft_spec_bytes(int B);      // one spectrum buffer (S or Y) for B images
 size_t fft_weight_bytes();         // expanded split spectral weights
 // HWIO [ks][ks][64][64] -> packed split spectral weights (synchronous, finalize time)
@@ -70,7 +72,6 @@ hipError_t launch_spec_gemm(const void* S, const void* Gx, void* Y, int B, float
 hipError_t launch_fft_inv(const void* Y, float* P, int B, int H, int W, hipStream_t st, bool bf = false);
 // P1 = IFFT(Y); I = A-epilogue(P1) -> a.dst; S = FFT(I)   (the A half-step tail + B half-step head)
 hipError_t launch_fft_inv_a_fwd(const void* Y, const ConvArgs& a, void* S, int B, hipStream_t st, bool bf = false);
-hipError_t launch_spec_epi(int epi, const ConvArgs& a, const float* P, int B, hipStream_t st);
 // B epilogue with f16x3 gate GEMMs (FFT path); gate weights packed by pack_gate_x3 (synchronous)
 size_t gate_x3_bytes();
 hipError_t pack_gate_x3(const float* g, void* out, float* unscale, bool bf = false);
