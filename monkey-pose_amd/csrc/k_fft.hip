@@ -686,12 +686,18 @@ __global__ __launch_bounds__(FNT, 3) void fft_fwd3_kernel(const float* __restric
   cpx v[72];
   const int y = tid >> 1, p = tid & 1;
   if (tid < 128) {
+#ifdef FFT_PROBE_OGC4   // timing probe (tools/bench_fft.hip): the map read as a C4 group (16-B pixels)
+    const size_t row = ((size_t)(b * 16 + cq) * H + (y < H ? y : 0)) * W * 4;
+    constexpr int PXS = 4;
+#else
     const size_t row = c8_index(b, q, y < H ? y : 0, 0, e0, H, W);
+    constexpr int PXS = 8;
+#endif
 #pragma unroll
     for (int k = 0; k < 32; ++k) {
       const int x = 2 * k + p;
       const bool in = y < H && x < W;
-      f32x4 u = *reinterpret_cast<const f32x4*>(src + row + 8 * min(x, W - 1));
+      f32x4 u = *reinterpret_cast<const f32x4*>(src + row + PXS * min(x, W - 1));
       if (!in) u = f32x4{0.f, 0.f, 0.f, 0.f};
       const cpx lo = {u[0], u[1]}, hi = {u[2], u[3]};
       const cpx mine = p ? hi : lo, send = p ? lo : hi;
@@ -771,7 +777,11 @@ __global__ __launch_bounds__(FNT, BF ? FFT_MINB_BF : FFT_MINB) void fft_inv_a_fw
     for (int u = 0; u < EU; ++u) {
       const int i = min(k * ECH + u * FNT + tid, 64 * 64 - 1);
       const int yy = min(i >> 6, H - 1), x = min(i & 63, W - 1);
+#ifdef FFT_PROBE_XOC4   // timing probe (tools/bench_fft.hip): X / O read as C4 groups
+      const size_t idx = c4_index(b, q, yy, x, e0, H, W);
+#else
       const size_t idx = c8_index(b, q, yy, x, e0, H, W);
+#endif
       xs[u] = map_ld4<BM>(p.X, idx);
       os[u] = map_ld4<BM>(p.O, idx);
     }
@@ -1870,14 +1880,15 @@ static int spec_smallb() {
   return v;
 }
 
-// MP_SPEC_GMAJ = G (default 2): spectral-GEMM blocks in passes of G 32-image groups, last first
-// (spec_gemm_kernel gmaj; 0 = every quad's groups together, the weights fetched once per launch).
-// G = 2 with MP_EPI_REV: fp32 B = 256 10.43 -> 10.37 ms, bf16 6.23 -> 6.17 ms; G = 1 re-reads the
-// 87 MB of weights once per group and lost (10.93 ms; profiles/r4o)
+// MP_SPEC_GMAJ = G: spectral-GEMM blocks in passes of G 32-image groups, last pass first (spec_gemm_kernel
+// gmaj); 0 (default) = every quad's groups together, the weights fetched from HBM once per launch.
+// G = 2 beside MP_EPI_REV measured no faster than MP_EPI_REV alone (fp32 B = 256 10.34-10.39 vs
+// 10.37 ms) and raised the GEMM's PMC fetch to 1.30x its algorithmic bytes (the 87 MB of weights once
+// per pass); G = 1 lost (10.93 ms; profiles/r4o, profiles/r4z_gmaj2)
 static int spec_gmaj() {
   static const int v = [] {
     const char* e = std::getenv("MP_SPEC_GMAJ");
-    return e ? std::atoi(e) : 2;
+    return e ? std::atoi(e) : 0;
   }();
   return v;
 }
