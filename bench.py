@@ -113,8 +113,8 @@ def fft_kernels(ctx, B, hw, steps, bf16=False):
 # per-kernel HBM bytes per launch from rocprofv3 PMC passes (FETCH_SIZE x2 on gfx950 + WRITE_SIZE,
 # MI355X_MICROARCH.md), collected with the full-batch single-stream launches of this workload by
 # tools/pmc_bytes.py and committed under profiles/ (bench cannot profile itself)
-PMC_TRAFFIC = {False: "profiles/r4p/pmc_traffic_fp32_b256.csv",
-               True: "profiles/r4p/pmc_traffic_bf16_b256.csv"}
+PMC_TRAFFIC = {False: "profiles/r4z/pmc_traffic_fp32_b256.csv",
+               True: "profiles/r4z/pmc_traffic_bf16_b256.csv"}
 PMC_KERNEL = {   # name: (fp32 path's kernel, bf16 path's kernel) as rocprofv3 names them
     "fft_fwd": ("fft_fwd3_kernel", "fft_fwd_kernel<true, true>"),
     "spec_gemm": ("spec_gemm_kernel<0, 32>", "spec_gemm_bf_kernel"),
