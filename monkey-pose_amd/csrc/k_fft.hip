@@ -150,9 +150,13 @@ __device__ __forceinline__ cpx swp(cpx a) {
 // them there.  Probes of the two writes made contiguous: fft_inv 0.134 -> 0.125 ms, inv_a_fwd 0.340 ->
 // 0.328 ms at B = 256.  Unswizzled C4 reads cost fp32 epi_b 0.259 -> 0.289 ms on one box; with the
 // odd group's row halves swapped (C4_SWZ) the same-box A/B against C8 is fp32 10.65 -> 10.46 ms, bf16
-// 6.20 -> 6.10, B = 64 3.34 -> 3.28 (profiles/r4o).  0 restores C8 maps.
+// 6.20 -> 6.10, B = 64 3.34 -> 3.28 (profiles/r4o).  Bit 2 puts the state O there too (gate_init /
+// epi_b write it, inv_a_fwd's A epilogue and epi_b read it): fp32 10.21-10.27 -> 10.03-10.04 ms
+// (epi_b 0.279 -> 0.256, inv_a_fwd 0.314 -> 0.309), bf16 6.13-6.15 -> 6.11 (profiles/r4o/c4_state_ab.log).
+// Og (read by the forward FFT's row loads, where the C4 probe gained nothing) and X stay C8.
+// 0 restores C8 maps.
 #ifndef FFT_C4
-#define FFT_C4 3
+#define FFT_C4 7
 #endif
 // (bit 0: P2, bit 1: I)
 __device__ __forceinline__ size_t pp_index(int b, int q, int y, int x, int e, int H, int W) {
@@ -160,6 +164,10 @@ __device__ __forceinline__ size_t pp_index(int b, int q, int y, int x, int e, in
 }
 __device__ __forceinline__ size_t ii_index(int b, int q, int y, int x, int e, int H, int W) {
   return (FFT_C4 & 2) ? c4_index(b, q, y, x, e, H, W) : c8_index(b, q, y, x, e, H, W);
+}
+// bit 2: the state O (written by gate_init / epi_b, read by inv_a_fwd's A epilogue and epi_b)
+__device__ __forceinline__ size_t oo_index(int b, int q, int y, int x, int e, int H, int W) {
+  return (FFT_C4 & 4) ? c4_index(b, q, y, x, e, H, W) : c8_index(b, q, y, x, e, H, W);
 }
 typedef unsigned u32x4_t __attribute__((ext_vector_type(4)));
 typedef float f32x2_t __attribute__((ext_vector_type(2)));
@@ -783,7 +791,7 @@ __global__ __launch_bounds__(FNT, BF ? FFT_MINB_BF : FFT_MINB) void fft_inv_a_fw
       const size_t idx = c8_index(b, q, yy, x, e0, H, W);
 #endif
       xs[u] = map_ld4<BM>(p.X, idx);
-      os[u] = map_ld4<BM>(p.O, idx);
+      os[u] = map_ld4<BM>(p.O, (FFT_C4 & 4) ? oo_index(b, q, yy, x, e0, H, W) : idx);
     }
   };
   inv_cols_to_T<BF>(Y, b, cq, tid, T);
@@ -1100,7 +1108,7 @@ __global__ __launch_bounds__(LF_NT, 1) void lfft_inv_a_fwd_kernel(const void* __
     const int px = min(tid + LF_NT * i, 64 * 64 - 1), y = min(px >> 6, H - 1), x = min(px & 63, W - 1);
     const size_t idx = c8_index(b, q, y, x, ec, H, W);
     xv[i] = map_ld2<false>(pa.X, idx);
-    ov[i] = map_ld2<false>(pa.O, idx);
+    ov[i] = map_ld2<false>(pa.O, oo_index(b, q, y, x, ec, H, W));
   }
   lf_inverse(Y, b, cp, tid, E, Big, R);
   // the A epilogue (hgru_module.py:797-799), pixel-major over the P rows; I back into R
@@ -1575,11 +1583,10 @@ __global__ __launch_bounds__(256) void spec_epi_b_kernel(ConvArgs p, const float
   for (int n = 0; n < 2; ++n)
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
-      const size_t idx = c8_index(b, 4 * n + g, y, x, 4 * h, H, W);
       const f32x4 iv = map_ld4<BM>(p.I, ii_index(b, 4 * n + g, y, x, 4 * h, H, W));
       if constexpr (BM) {
         pvs[n][g] = map_ld4<BM>(P, pp_index(b, 4 * n + g, y, x, 4 * h, H, W));
-        ovs[n][g] = map_ld4<BM>(p.O, idx);
+        ovs[n][g] = map_ld4<BM>(p.O, oo_index(b, 4 * n + g, y, x, 4 * h, H, W));
       }
 #pragma unroll
       for (int j = 0; j < 4; ++j) Iv[n][4 * g + j] = iv[j];
@@ -1590,9 +1597,9 @@ __global__ __launch_bounds__(256) void spec_epi_b_kernel(ConvArgs p, const float
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       const int c = 32 * n + 8 * g + 4 * h;
-      const size_t idx = c8_index(b, 4 * n + g, y, x, 4 * h, H, W);
       const f32x4 pv = BM ? pvs[n][g] : map_ld4<BM>(P, pp_index(b, 4 * n + g, y, x, 4 * h, H, W));
-      const f32x4 ov = BM ? ovs[n][g] : map_ld4<BM>(p.O, idx);
+      const size_t odx = oo_index(b, 4 * n + g, y, x, 4 * h, H, W);
+      const f32x4 ov = BM ? ovs[n][g] : map_ld4<BM>(p.O, odx);
       const f32x4 lat = *reinterpret_cast<const f32x4*>(p.vecs + V_LAT * 64 + c);
       const f32x4 ga = *reinterpret_cast<const f32x4*>(p.vecs + V_GAMMA * 64 + c);
       const f32x4 ka = *reinterpret_cast<const f32x4*>(p.vecs + V_KAPPA * 64 + c);
@@ -1610,7 +1617,7 @@ __global__ __launch_bounds__(256) void spec_epi_b_kernel(ConvArgs p, const float
         o[j] = on;
         Iv[n][r] = on;
       }
-      map_st4<BM>(p.dst, idx, o);
+      map_st4<BM>(p.dst, odx, o);
     }
   f32x16 (&Ov)[2] = Iv;
   if constexpr (!FINAL) {
@@ -1741,7 +1748,7 @@ __global__ __launch_bounds__(256) void gate_init_x3_kernel(const float* __restri
         og[j] = o[j] * fsigmoid(Y[n][4 * g + j] + ib[j]);
       }
       const size_t idx = c8_index(b, 4 * n + g, y, x, 4 * h, H, W);
-      map_st4<BM>(O, idx, o);
+      map_st4<BM>(O, oo_index(b, 4 * n + g, y, x, 4 * h, H, W), o);
       map_st4<BM>(Og, idx, og);
     }
 }
@@ -1782,6 +1789,7 @@ __global__ void pack_gate_bf_kernel(const float* __restrict__ g, uint4* __restri
 
 // ------------------------------------------------------------------------------------ launchers
 bool fft_c4_maps() { return (FFT_C4 & 2) != 0; }
+bool fft_c4_state() { return (FFT_C4 & 4) != 0; }
 bool fft_bf16_maps() {
   static const bool v = [] {
     const char* e = std::getenv("MP_BF16_MAPS");

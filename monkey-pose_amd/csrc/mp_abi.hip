@@ -293,11 +293,11 @@ struct StateOut {
 // copy step t's O / I maps (C8, bf16 under MP_DTYPE_BF16 maps; ic4: I is the FFT loop's C4 map) of images
 // [b0, b0 + n) into the stacks
 void store_step(const StateOut* so, const float* Omap, const float* Imap, int b0, int n, int H, int W, int t,
-                bool bf, hipStream_t st, bool ic4 = false) {
+                bool bf, hipStream_t st, bool ic4 = false, bool oc4 = false) {
   if (!so) return;
   const size_t img = (size_t)H * W * 64, stride = img * so->T;
   const size_t off = (size_t)b0 * stride + (size_t)t * img;
-  if (so->O) hip_check(launch_c8_to_nhwc(Omap, so->O + off, n, H, W, st, bf, stride), "store_states O");
+  if (so->O) hip_check(launch_c8_to_nhwc(Omap, so->O + off, n, H, W, st, bf, stride, oc4), "store_states O");
   if (so->I) hip_check(launch_c8_to_nhwc(Imap, so->I + off, n, H, W, st, bf, stride, ic4), "store_states I");
 }
 
@@ -360,7 +360,7 @@ void fft_circuit_range(mp_ctx* c, int b0, int n, int H, int W, int T, float* fin
     hip_check(launch_spec_gemm(S, c->spec_g.p, Y, n, c->p_unscale, st, bf), "spec_gemm");
     hip_check(launch_fft_inv(Y, P, n, H, W, st, bf), "fft_inv");
     hip_check(launch_spec_epi_b(b, P, c->or_x3.p, c->or_us, c->ir_x3.p, c->ir_us, n, st, bf), "B epilogue");
-    store_step(so, b.O, b.I, b0, n, H, W, t, bm, st, fft_c4_maps());
+    store_step(so, b.O, b.I, b0, n, H, W, t, bm, st, fft_c4_maps(), fft_c4_state());
   }
 }
 
@@ -468,7 +468,8 @@ void run_circuit(mp_ctx* c, int64_t n, int H, int W, int T, const float* o0_nhwc
       ProfScope ps(c, st, "conv15_b");
       eCRF_conv(c, EPI_HGRU_B, b, (int)n, st);
     }
-    store_step(so, c->O.f(), c->I.f(), 0, (int)n, H, W, t, bf16_maps(c), st, is_fft(c->dtype) && fft_c4_maps());
+    store_step(so, c->O.f(), c->I.f(), 0, (int)n, H, W, t, bf16_maps(c), st, is_fft(c->dtype) && fft_c4_maps(),
+               is_fft(c->dtype) && fft_c4_state());
   }
 }
 

@@ -61,6 +61,7 @@ hipError_t device_absmax(const float* x, size_t n, float* out);   // max |x| (sy
 // MP_DTYPE_BF16 keeps the hGRU state maps O, I, Og, P2 in bf16 (MP_BF16_MAPS=0: fp32, for A/B);
 // their element offsets are unchanged, so a map pointer offset by m elements is (bf16*)base + m
 bool fft_bf16_maps();
+bool fft_c4_state();  // the FFT loop's O map is C4 (k_fft.hip FFT_C4 bit 2)
 bool fft_c4_maps();   // the FFT loop's I map is C4 (k_fft.hip FFT_C4)
 size_t fft_spec_bytes(int B);      // one spectrum buffer (S or Y) for B images
 size_t fft_weight_bytes();         // expanded split spectral weights
