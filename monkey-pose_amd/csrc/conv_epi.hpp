@@ -41,7 +41,7 @@ __device__ __forceinline__ void bb_epilogue_n(const ConvArgs& p, const f32x16& a
       const float v = fmaxf(acc[4 * g + j] + bb[j], 0.f);   // relu(conv + b)
       o[j] = v * ss[j] + tt[j];                             // folded BN
     }
-    const size_t idx = c8_index(b, 4 * n + g, y, x, 4 * h, p.H, p.W);
+    const size_t idx = p.dst_c4 ? c4_index(b, 4 * n + g, y, x, 4 * h, p.H, p.W) : c8_index(b, 4 * n + g, y, x, 4 * h, p.H, p.W);
     if (p.dst_bf16)
       *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(p.dst) + idx) = bf16x4_pack(o);
     else

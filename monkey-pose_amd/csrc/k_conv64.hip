@@ -250,7 +250,7 @@ hipError_t launch_conv1_pool_any(const float* in, const float* w, const float* b
 }
 
 // layout conversions (standalone ContextualCircuit API, debug taps)
-__global__ void nhwc_to_c8_kernel(const float* __restrict__ in, float* out, int B, int H, int W, bool bf) {
+__global__ void nhwc_to_c8_kernel(const float* __restrict__ in, float* out, int B, int H, int W, bool bf, bool c4) {
   const size_t total = (size_t)B * H * W * NQ;
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
   if (i >= total) return;
@@ -258,15 +258,15 @@ __global__ void nhwc_to_c8_kernel(const float* __restrict__ in, float* out, int 
   const size_t pix = i / NQ;
   const int x = pix % W, y = (pix / W) % H, b = pix / ((size_t)W * H);
   const f32x4* s = reinterpret_cast<const f32x4*>(in + pix * C + 8 * q);
-  const size_t o = c8_index(b, q, y, x, 0, H, W);
+  const size_t o0 = c4 ? c4_index(b, q, y, x, 0, H, W) : c8_index(b, q, y, x, 0, H, W);
+  const size_t o1 = c4 ? c4_index(b, q, y, x, 4, H, W) : o0 + 4;
   if (bf) {
-    uint2* d = reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(out) + o);
-    d[0] = bf16x4_pack(s[0]);
-    d[1] = bf16x4_pack(s[1]);
+    uint16_t* d = reinterpret_cast<uint16_t*>(out);
+    *reinterpret_cast<uint2*>(d + o0) = bf16x4_pack(s[0]);
+    *reinterpret_cast<uint2*>(d + o1) = bf16x4_pack(s[1]);
   } else {
-    f32x4* d = reinterpret_cast<f32x4*>(out + o);
-    d[0] = s[0];
-    d[1] = s[1];
+    *reinterpret_cast<f32x4*>(out + o0) = s[0];
+    *reinterpret_cast<f32x4*>(out + o1) = s[1];
   }
 }
 
@@ -375,9 +375,9 @@ hipError_t launch_conv1_pool_bn(const float* in, const float* w, const float* bi
   return hipGetLastError();
 }
 
-hipError_t launch_nhwc_to_c8(const float* in, float* out, int B, int H, int W, hipStream_t st, bool bf) {
+hipError_t launch_nhwc_to_c8(const float* in, float* out, int B, int H, int W, hipStream_t st, bool bf, bool c4) {
   const size_t total = (size_t)B * H * W * NQ;
-  hipLaunchKernelGGL(nhwc_to_c8_kernel, dim3((total + 255) / 256), dim3(256), 0, st, in, out, B, H, W, bf);
+  hipLaunchKernelGGL(nhwc_to_c8_kernel, dim3((total + 255) / 256), dim3(256), 0, st, in, out, B, H, W, bf, c4);
   return hipGetLastError();
 }
 

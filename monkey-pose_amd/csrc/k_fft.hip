@@ -153,10 +153,11 @@ __device__ __forceinline__ cpx swp(cpx a) {
 // 6.20 -> 6.10, B = 64 3.34 -> 3.28 (profiles/r4o).  Bit 2 puts the state O there too (gate_init /
 // epi_b write it, inv_a_fwd's A epilogue and epi_b read it): fp32 10.21-10.27 -> 10.03-10.04 ms
 // (epi_b 0.279 -> 0.256, inv_a_fwd 0.314 -> 0.309), bf16 6.13-6.15 -> 6.11 (profiles/r4o/c4_state_ab.log).
-// Og (read by the forward FFT's row loads, where the C4 probe gained nothing) and X stay C8.
-// 0 restores C8 maps.
+// Bit 3 the drive X (conv_3's backbone epilogue writes it, ConvArgs::dst_c4): fp32 9.95 -> 9.89 ms
+// (inv_a_fwd 0.307 -> 0.299), bf16 6.08-6.10 -> 6.05-6.06 (profiles/r4o/c4_drive_ab.log).  Og (read by
+// the forward FFT's row loads, where the C4 probe gained nothing) stays C8.  0 restores C8 maps.
 #ifndef FFT_C4
-#define FFT_C4 7
+#define FFT_C4 15
 #endif
 // (bit 0: P2, bit 1: I)
 __device__ __forceinline__ size_t pp_index(int b, int q, int y, int x, int e, int H, int W) {
@@ -164,6 +165,10 @@ __device__ __forceinline__ size_t pp_index(int b, int q, int y, int x, int e, in
 }
 __device__ __forceinline__ size_t ii_index(int b, int q, int y, int x, int e, int H, int W) {
   return (FFT_C4 & 2) ? c4_index(b, q, y, x, e, H, W) : c8_index(b, q, y, x, e, H, W);
+}
+// bit 3: the drive X (written by conv_3's backbone epilogue, ConvArgs::dst_c4; read by the A epilogue)
+__device__ __forceinline__ size_t xx_index(int b, int q, int y, int x, int e, int H, int W) {
+  return (FFT_C4 & 8) ? c4_index(b, q, y, x, e, H, W) : c8_index(b, q, y, x, e, H, W);
 }
 // bit 2: the state O (written by gate_init / epi_b, read by inv_a_fwd's A epilogue and epi_b)
 __device__ __forceinline__ size_t oo_index(int b, int q, int y, int x, int e, int H, int W) {
@@ -790,7 +795,7 @@ __global__ __launch_bounds__(FNT, BF ? FFT_MINB_BF : FFT_MINB) void fft_inv_a_fw
 #else
       const size_t idx = c8_index(b, q, yy, x, e0, H, W);
 #endif
-      xs[u] = map_ld4<BM>(p.X, idx);
+      xs[u] = map_ld4<BM>(p.X, (FFT_C4 & 8) ? xx_index(b, q, yy, x, e0, H, W) : idx);
       os[u] = map_ld4<BM>(p.O, (FFT_C4 & 4) ? oo_index(b, q, yy, x, e0, H, W) : idx);
     }
   };
@@ -1106,8 +1111,7 @@ __global__ __launch_bounds__(LF_NT, 1) void lfft_inv_a_fwd_kernel(const void* __
 #pragma unroll
   for (int i = 0; i < LF_PX; ++i) {
     const int px = min(tid + LF_NT * i, 64 * 64 - 1), y = min(px >> 6, H - 1), x = min(px & 63, W - 1);
-    const size_t idx = c8_index(b, q, y, x, ec, H, W);
-    xv[i] = map_ld2<false>(pa.X, idx);
+    xv[i] = map_ld2<false>(pa.X, xx_index(b, q, y, x, ec, H, W));
     ov[i] = map_ld2<false>(pa.O, oo_index(b, q, y, x, ec, H, W));
   }
   lf_inverse(Y, b, cp, tid, E, Big, R);
@@ -1790,6 +1794,7 @@ __global__ void pack_gate_bf_kernel(const float* __restrict__ g, uint4* __restri
 // ------------------------------------------------------------------------------------ launchers
 bool fft_c4_maps() { return (FFT_C4 & 2) != 0; }
 bool fft_c4_state() { return (FFT_C4 & 4) != 0; }
+bool fft_c4_drive() { return (FFT_C4 & 8) != 0; }
 bool fft_bf16_maps() {
   static const bool v = [] {
     const char* e = std::getenv("MP_BF16_MAPS");

@@ -229,6 +229,9 @@ void ensure_ws(mp_ctx* c, int64_t n, int64_t H, int64_t W) {
 // MP_DTYPE_BF16 keeps the FFT loop's maps (X, O, I, Og, P2) in bf16 (k_fft.hip map_ld4)
 bool bf16_maps(const mp_ctx* c) { return c->dtype == MP_DTYPE_BF16 && fft_bf16_maps(); }
 
+// the drive X of an FFT-path context is a C4 map (k_fft.hip FFT_C4 bit 3)
+bool x_c4(const mp_ctx* c) { return is_fft(c->dtype) && fft_c4_drive(); }
+
 // one association-field conv p_r * a.src with its fused hGRU epilogue, in the context's precision
 void eCRF_conv(mp_ctx* c, int epi, const ConvArgs& a, int n, hipStream_t st) {
   if (c->dtype == MP_DTYPE_F32_SPLIT)
@@ -496,7 +499,7 @@ const float* hidden_state(mp_ctx* c, int hidden_init, const float* o0, const flo
     case MP_HIDDEN_IDENTITY:
       if (x_nhwc) return x_nhwc;
       c->h0.alloc(bytes);
-      hip_check(launch_c8_to_nhwc(c->X.f(), c->h0.f(), (int)n, H, W, st, bf16_maps(c)), "hidden_init identity");
+      hip_check(launch_c8_to_nhwc(c->X.f(), c->h0.f(), (int)n, H, W, st, bf16_maps(c), 0, x_c4(c)), "hidden_init identity");
       return c->h0.f();
     default:
       fail(MP_ERR_ARG, "hidden_init must be MP_HIDDEN_GIVEN, _ZEROS, _IDENTITY or _RANDOM");
@@ -773,6 +776,7 @@ int pose_fwd(mp_ctx* ctx, const float* depth, int64_t n, int64_t h, int64_t w, c
       a.wpk = ctx->conv3_pk.v4();
       a.dst = ctx->X.f();
       a.dst_bf16 = bf16_maps(ctx) ? 1 : 0;
+      a.dst_c4 = x_c4(ctx) ? 1 : 0;
       a.bias = ctx->conv3_b.f();
       a.bn_s = ctx->bn2_s.f();
       a.bn_t = ctx->bn2_t.f();
@@ -782,7 +786,7 @@ int pose_fwd(mp_ctx* ctx, const float* depth, int64_t n, int64_t h, int64_t w, c
     }
     if (tp.pool1) hip_check(launch_c8_to_nhwc(ctx->bufA.f(), tp.pool1, N, H, W, st), "pool1 tap");
     if (tp.conv2) hip_check(launch_c8_to_nhwc(ctx->bufB.f(), tp.conv2, N, H, W, st), "conv2 tap");
-    if (tp.conv3) hip_check(launch_c8_to_nhwc(ctx->X.f(), tp.conv3, N, H, W, st, bf16_maps(ctx)), "conv3 tap");
+    if (tp.conv3) hip_check(launch_c8_to_nhwc(ctx->X.f(), tp.conv3, N, H, W, st, bf16_maps(ctx), 0, x_c4(ctx)), "conv3 tap");
     const float* h0 = hidden_state(ctx, fo.hidden_init, o0, nullptr, n, H, W, st, fo.rng_seed);
     StateOut so;
     so.O = fo.states_O;
@@ -901,7 +905,7 @@ int mp_hgru_circuit_fwd_opts(mp_ctx* ctx, const float* x, const float* o0, int64
     hip_check(hipSetDevice(ctx->device), "hipSetDevice");
     hipStream_t st = static_cast<hipStream_t>(stream);
     ensure_ws(ctx, n, h, w);
-    hip_check(launch_nhwc_to_c8(x, ctx->X.f(), (int)n, (int)h, (int)w, st, bf16_maps(ctx)), "nhwc_to_c8");
+    hip_check(launch_nhwc_to_c8(x, ctx->X.f(), (int)n, (int)h, (int)w, st, bf16_maps(ctx), x_c4(ctx)), "nhwc_to_c8");
     if (ctx->model == MP_MODEL_HGRU_POSE) {
       // the pose context's output affine is BN_3: use identity by running with a temporary copy
       fail(MP_ERR_UNSUPPORTED, "use an MP_MODEL_HGRU_CIRCUIT context for the standalone circuit");

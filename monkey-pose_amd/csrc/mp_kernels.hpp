@@ -30,6 +30,7 @@ struct ConvArgs {
   int H, W, tiles_x, tiles_y;
   float ascale;           // f16x3 kernel: activation split scale (0 = the hGRU default 2^10)
   int dst_bf16;           // BB: dst is a bf16 C8 map (MP_DTYPE_BF16's hGRU drive X)
+  int dst_c4;             // BB: dst is a C4 map (the FFT loop's drive X, k_fft.hip FFT_C4 bit 3)
 };
 
 // k_conv64.hip
@@ -43,7 +44,8 @@ hipError_t launch_conv1_pool_bn(const float* in, const float* w, const float* bi
 hipError_t launch_conv1_pool_any(const float* in, const float* w, const float* bias, float* out, int ldo, int coff,
                                  int B, int Hin, int Win, int Cout, hipStream_t st);
 // bf: the C8 side is a bf16 map
-hipError_t launch_nhwc_to_c8(const float* in, float* out, int B, int H, int W, hipStream_t st, bool bf = false);
+hipError_t launch_nhwc_to_c8(const float* in, float* out, int B, int H, int W, hipStream_t st, bool bf = false,
+                             bool c4 = false);
 // c4: the source is a C4 map (mp_common.hpp c4_index: the FFT loop's I, fft_c4_maps())
 hipError_t launch_c8_to_nhwc(const float* in, float* out, int B, int H, int W, hipStream_t st, bool bf = false,
                              size_t dst_img = 0, bool c4 = false);
@@ -61,6 +63,7 @@ hipError_t device_absmax(const float* x, size_t n, float* out);   // max |x| (sy
 // MP_DTYPE_BF16 keeps the hGRU state maps O, I, Og, P2 in bf16 (MP_BF16_MAPS=0: fp32, for A/B);
 // their element offsets are unchanged, so a map pointer offset by m elements is (bf16*)base + m
 bool fft_bf16_maps();
+bool fft_c4_drive();  // the FFT loop's X map is C4 (k_fft.hip FFT_C4 bit 3)
 bool fft_c4_state();  // the FFT loop's O map is C4 (k_fft.hip FFT_C4 bit 2)
 bool fft_c4_maps();   // the FFT loop's I map is C4 (k_fft.hip FFT_C4)
 size_t fft_spec_bytes(int B);      // one spectrum buffer (S or Y) for B images
