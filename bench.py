@@ -506,6 +506,21 @@ def cpu_baseline(depth, o0, out, wts, T, args):
     return res
 
 
+def launch_ranks(args) -> int:
+    """``python bench.py --gpus N`` (N > 1) outside a torch.distributed launcher: start the N ranks
+    as ``torch.distributed.run`` children (one process per GPU) and return their exit status.  Runs
+    before anything touches the GPU -- this process only waits; it never initialises HIP."""
+    import socket
+    import subprocess
+    with socket.socket() as s:   # a free rendezvous port on the loopback interface
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={args.gpus}",
+           "--master-addr=127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY=os.environ.get("HSA_ENABLE_IPC_MODE_LEGACY", "0"))
+    return subprocess.call(cmd, env=env)
+
+
 def main():
     args = parse()
     import torch
@@ -514,6 +529,10 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        # the driver's scaling curve reads n_gpus from this line: a launch whose world differs from
+        # --gpus (e.g. a launcher started with another --nproc-per-node) must not report either
+        raise SystemExit(f"bench.py: --gpus {args.gpus} but the launcher started {world} rank(s)")
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         # one rank per GPU; local % device_count only matters for --backend gloo rehearsals of the
@@ -526,6 +545,8 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local), timeout=tmo)
         else:
             dist.init_process_group(args.backend, timeout=tmo)
+        if dist.get_world_size() != args.gpus:
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but the process group has {dist.get_world_size()} ranks")
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
@@ -624,6 +645,11 @@ def main():
     kern = fft_kernels(ctx, B, px, prof_steps, args.dtype == "bf16") if fft else None
     hbm_meas = hbm_rates(dev) if fft else None   # after the timed region
     value = gb * args.steps / elapsed
+    dev_list = []
+    if world > 1:   # which device each rank ran on (RCCL needs one rank per GPU; gloo rehearsals may share)
+        dl = [None] * world
+        dist.all_gather_object(dl, dev.index)
+        dev_list = dl
     if strong:
         metric = (f"depth-crops/sec hGRU-8T fwd @global batch {gb} over {world} GPU (strong scaling, "
                   f"{crop}x{crop} crops)")
@@ -657,6 +683,9 @@ def main():
         "breakdown_ms_per_step": {"conv15": round((ms_a + ms_b) / prof_steps, 3),
                                   "fc1": round(ms_fc / max(1, nfc), 3),
                                   "backbone": round(ms_bb / max(1, nbb), 3)},
+        "ranks": dist.get_world_size() if world > 1 else 1,
+        "backend": (dist.get_backend() if world > 1 else "none (one process)"),
+        "devices": (dev_list if world > 1 else [dev.index]),
         "weight_bcast_ms": round(bcast_s * 1e3, 3),
         "weight_bcast_bytes": binfo.get("bytes"),
         "weight_bcast_form": binfo.get("form"),
@@ -698,6 +727,10 @@ def main():
 
 
 if __name__ == "__main__":
+    _a = parse()
+    if _a.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        # the driver's `python bench.py --gpus N`: one rank per GPU under torch.distributed.run
+        sys.exit(launch_ranks(_a))
     try:
         main()
     except BaseException as exc:   # noqa: BLE001

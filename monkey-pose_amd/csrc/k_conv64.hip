@@ -376,6 +376,7 @@ hipError_t launch_conv1_pool_bn(const float* in, const float* w, const float* bi
 }
 
 hipError_t launch_nhwc_to_c8(const float* in, float* out, int B, int H, int W, hipStream_t st, bool bf, bool c4) {
+  if (c4 && !c4_width_ok(W)) return hipErrorInvalidValue;   // the C4 swizzle needs a power-of-two width
   const size_t total = (size_t)B * H * W * NQ;
   hipLaunchKernelGGL(nhwc_to_c8_kernel, dim3((total + 255) / 256), dim3(256), 0, st, in, out, B, H, W, bf, c4);
   return hipGetLastError();
@@ -383,6 +384,7 @@ hipError_t launch_nhwc_to_c8(const float* in, float* out, int B, int H, int W, h
 
 hipError_t launch_c8_to_nhwc(const float* in, float* out, int B, int H, int W, hipStream_t st, bool bf,
                              size_t dst_img, bool c4) {
+  if (c4 && !c4_width_ok(W)) return hipErrorInvalidValue;
   const size_t total = (size_t)B * H * W * NQ;
   if (dst_img == 0) dst_img = (size_t)H * W * C;
   hipLaunchKernelGGL(c8_to_nhwc_kernel, dim3((total + 255) / 256), dim3(256), 0, st, in, out, B, H, W, bf,

@@ -1901,7 +1901,7 @@ static int spec_smallb() {
 static int spec_gmaj() {
   static const int v = [] {
     const char* e = std::getenv("MP_SPEC_GMAJ");
-    return e ? std::atoi(e) : 0;
+    return e ? std::max(0, std::atoi(e)) : 0;   // negative = off (a negative pass size would index past the buffers)
   }();
   return v;
 }

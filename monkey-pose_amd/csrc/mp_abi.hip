@@ -517,7 +517,9 @@ extern "C" {
 // 0.2: mp_pose_taps back to its 0.1 layout (the 0.1 header's seven pointers); the per-step states,
 // hidden_init and the device O0 draw moved to the size-checked mp_fwd_opts (mp_hgru_pose_fwd_ex,
 // mp_hgru_circuit_fwd_opts); mp_crop3d_ex (docom)
-int mp_version(void) { return (0 << 16) | 2; }
+// 0.3: mp_hbm_probe / mp_hbm_rates added; the "graph_captured" mp_info key removed (the hipGraph
+// replay path it reported was deleted in round 4)
+int mp_version(void) { return (0 << 16) | 3; }
 
 const char* mp_last_error(void) { return g_err.c_str(); }
 

@@ -19,11 +19,14 @@ constexpr int NQ = C / 8;  // channel chunks in the C8 layout
 __device__ __forceinline__ size_t c8_index(int b, int q, int y, int x, int e, int H, int W) {
   return ((((size_t)b * NQ + q) * H + y) * W + x) * 8 + e;
 }
-// C4 [N][16 channel groups][H][W][4]: the FFT loop's P2 and I maps (k_fft.hip pi_index), written per
-// 4-channel group by the inverse FFT kernels as one contiguous run; channel 8 q + e of the C8 naming
+// C4 [N][16 channel groups][H][W][4]: the FFT loop's P2, I, O and X maps (k_fft.hip pp_index, ii_index,
+// oo_index, xx_index), written per 4-channel group by the inverse FFT kernels as one contiguous run;
+// channel 8 q + e of the C8 naming.  W must be a power of two: the C4_SWZ swizzle x ^ (W / 2) maps
+// [0, W) onto itself only then (the FFT path's maps are 32 or 64 wide; launchers check c4_width_ok)
 #ifndef C4_SWZ
 #define C4_SWZ 1
 #endif
+__host__ __device__ constexpr bool c4_width_ok(int W) { return W > 0 && (W & (W - 1)) == 0; }
 __device__ __forceinline__ size_t c4_index(int b, int q, int y, int x, int e, int H, int W) {
   // C4_SWZ: the odd group's row halves swapped, so the two half-waves of a C8-pattern access (groups
   // 2q and 2q + 1 at the same 32 pixels) read runs 512 B apart modulo 64 KiB

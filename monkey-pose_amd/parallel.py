@@ -57,8 +57,11 @@ def fc_hi_plane(w: np.ndarray):
 
 def fc_from_hi_plane(hi, e: int, idx, vals):
     """Inverse of ``fc_hi_plane`` on either side (torch tensors): w' = hi / s with the exceptions
-    restored.  max|w'| = max|w|, so the library packs w' to the same scale and, since s * w' = hi
-    exactly, to the same hi plane; the lo plane differs, which the one-product fc_1 never reads."""
+    restored.  max|w'| has the same frexp exponent as max|w| (s * max|w| lies in [2^13, 2^14) and
+    its f16 rounding stays >= 2^13; a max rounding up past max|w| is sent as an exception), so the
+    library packs w' to the same scale and, since s * w' = hi exactly, to the same hi plane.
+    max|w'| itself may be smaller than max|w| when the max element rounds down.  The lo plane
+    differs, which the one-product fc_1 never reads."""
     import torch
     s = float(2.0 ** (14 - e))
     w = hi.to(torch.float32) / s
@@ -104,7 +107,9 @@ def broadcast_weights(table, weights: Dict[str, np.ndarray] | None, device, rank
         meta = torch.empty(2, dtype=torch.int64, device=device)
     nbytes = flat.numel() * 4
     secs = 0.0
-    if world > 1:
+    # any initialised group runs the collective, a one-rank one included (tests/test_gpu_bench_ranks.py
+    # drives RCCL through this exact code on one GPU); without a group there is nothing to send
+    if world > 1 or (dist.is_available() and dist.is_initialized()):
         if flat.is_cuda:
             torch.cuda.synchronize(device)
         dist.barrier(group=group)

@@ -46,7 +46,7 @@ def test_ctypes_table_matches_header():
 def test_library_loads_and_reports():
     mp = pkg()
     lib = mp._lib.load()
-    assert lib.mp_version() == (0 << 16) | 2
+    assert lib.mp_version() == (0 << 16) | 3
     assert isinstance(lib.mp_last_error(), bytes)     # thread-local; earlier tests may have set it
     assert lib.mp_create(0, 99, ctypes.byref(ctypes.c_void_p())) < 0    # bad model kind
     assert b"model_kind" in lib.mp_last_error()

@@ -41,6 +41,23 @@ def test_fc_hi_plane_round_trip_keeps_scale_and_plane():
     assert float(np.abs(w2).max()) == float(np.abs(w).max())
 
 
+def test_fc_hi_plane_round_trip_max_rounding_down():
+    """The max element rounds DOWN in f16: max|w'| < max|w|, but the frexp exponent -- hence the
+    pack scale and the hi plane -- is unchanged (the invariant fc_from_hi_plane relies on)."""
+    par = pkg().parallel
+    rng = np.random.default_rng(4)
+    w = (rng.standard_normal(4096) * 0.01).astype(np.float32)
+    e = 1
+    s = 2.0 ** (14 - e)
+    w[11] = np.float32((2 ** 13 + 3) / s)           # s * w = 8195: the f16 grid there is 8, -> 8192
+    h, e0, idx, vals = par.fc_hi_plane(w)
+    assert e0 == e and 11 not in idx
+    w2 = par.fc_from_hi_plane(torch.from_numpy(h), e0, torch.from_numpy(idx), torch.from_numpy(vals)).numpy()
+    assert float(np.abs(w2).max()) < float(np.abs(w).max())
+    h2, e2, _, _ = par.fc_hi_plane(w2)
+    assert e2 == e0 and np.array_equal(h.view(np.uint16), h2.view(np.uint16))
+
+
 def _free_port():
     s = socket.socket()
     s.bind(("127.0.0.1", 0))
