@@ -85,11 +85,18 @@ def fft_kernels(ctx, B, hw, steps, bf16=False):
     # the maps X, O, I, Og, P2 are bf16 under dtype bf16 (k_fft.hip map_ld4; MP_BF16_MAPS=0: fp32)
     sm = act // 2 if bf16 and os.environ.get("MP_BF16_MAPS", "1") != "0" else act
     algo = {   # name: (bytes, flops) per launch
+        # the six-launch loop (k_fft.hip; dtype bf16, or MP_FFT4=0)
         "fft_fwd": (sm + spec, 0.0),                   # Og in; S out
         "spec_gemm": (2 * spec + NF * ent * 1024, 8.0 * B * NF * 64 * 64),   # S in, Y out, weights
         "inv_a_fwd": (2 * spec + 3 * sm, 0.0),         # Y, X, O in; I, S out
         "fft_inv": (spec + sm, 0.0),                   # Y in; P out
         "epi_b": (5 * sm, 0.0),                        # P, I, O in; O', Og' out
+        # the four-step loop (k_fft4.hip, the fp32 default): Z is a spectrum-sized complex64 buffer
+        "col_gemm": (2 * spec + NF * ent * 1024, 8.0 * B * NF * 64 * 64),    # Z in, Z' out, weights
+        "row_a": (2 * spec + 3 * act, 0.0),            # Z', X, O in; I, Z out
+        "row_b": (2 * spec + 3 * act, 0.0),            # Z', I, O in; O', Z out
+        "row_final": (spec + 4 * act, 0.0),            # Z', I, O in; O', BN_3(O_T) NHWC out
+        "row_init": (2 * act + spec, 0.0),             # O0 in; O, Z out
     }
     out = {}
     # the fp32 path's spectral GEMM is f16x3 (three f16 MFMA products per fp32-accurate MAC): its
@@ -120,7 +127,9 @@ PMC_KERNEL = {   # name: (fp32 path's kernel, bf16 path's kernel) as rocprofv3 n
     "spec_gemm": ("spec_gemm_kernel<0, 32>", "spec_gemm_bf_kernel"),
     "inv_a_fwd": ("fft_inv_a_fwd_kernel<false, false>", "fft_inv_a_fwd_kernel<true, true>"),
     "fft_inv": ("fft_inv_kernel<false, false>", "fft_inv_kernel<true, true>"),
-    "epi_b": ("spec_epi_b_kernel<false, false, false>", "spec_epi_b_kernel<true, true, false>")}
+    "epi_b": ("spec_epi_b_kernel<false, false, false>", "spec_epi_b_kernel<true, true, false>"),
+    "col_gemm": ("col_gemm_kernel", None), "row_a": ("row_kernel<0>", None), "row_b": ("row_kernel<1>", None),
+    "row_final": ("row_kernel<2>", None), "row_init": ("row_kernel<3>", None)}
 
 
 # MFMA utilisation per kernel from the committed PMC pass (tools/pmc_mfma.sh / .py: SQ_VALU_MFMA_BUSY_CYCLES
@@ -155,6 +164,8 @@ def pmc_traffic(name, bf16, batch):
     if batch != 256 or not full or not os.path.exists(full):
         return None, "no PMC summary for this dtype / batch"
     tag = PMC_KERNEL[name][1 if bf16 else 0]
+    if tag is None:
+        return None, "no kernel of this name on this dtype"
     for r in csv.DictReader(open(full)):
         if tag in r["kernel"]:
             return round(float(r["traffic_MB"]) * 1e6), path
@@ -642,6 +653,7 @@ def main():
     achieved_tf = conv15_flop / (conv_launch_ms * 1e-3) / 1e12
 
     fft = args.dtype in ("f32_fft", "bf16")
+    fft_loop = ctx.info("fft_loop")
     kern = fft_kernels(ctx, B, px, prof_steps, args.dtype == "bf16") if fft else None
     hbm_meas = hbm_rates(dev) if fft else None   # after the timed region
     value = gb * args.steps / elapsed
@@ -677,7 +689,9 @@ def main():
                    "parallelism": (f"dp{world} (contiguous batch shards, one {'RCCL' if args.backend == 'nccl' else 'gloo'} "
                                    "weight broadcast before timing, no collective in the timed region)") if world > 1
                    else "dp1 (single GPU, no collective)",
-                   "hgru_streams": (int(os.environ.get("MP_STREAMS", "2")) if fft else 1)},
+                   "hgru_streams": (int(os.environ.get("MP_STREAMS", "2")) if fft else 1),
+                   "hgru_loop": {4: "four-step FFT loop (k_fft4.hip: 4 launches per timestep)",
+                                 6: "six-launch FFT loop (k_fft.hip)", 0: "direct conv"}[fft_loop]},
         "roofline": (fft_roofline(kern, args.dtype == "bf16", B, hbm_meas) if fft else
                      roofline(args.dtype, achieved_tf, conv_launch_ms, na + nb, conv15_flop)),
         "breakdown_ms_per_step": {"conv15": round((ms_a + ms_b) / prof_steps, 3),

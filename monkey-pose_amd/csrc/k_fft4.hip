@@ -1,0 +1,507 @@
+// Four-step FFT loop of the hGRU association-field convolution: the fp32 FFT path's default loop
+// (MP_DTYPE_F32_FFT; MP_FFT4=0 restores k_fft.hip's six-launch loop for A/B).
+//
+// The eCRF convolution (hgru_module.py:615-657 p_convolution / process_p: tf.nn.conv2d SAME, 15x15
+// taps, 64 -> 64 channels, twice per timestep) on a 64x64 map is a 72 x 72 circular convolution
+// (k_fft.hip's header: why that is exact).  Here the 72-point COLUMN transform is split in two
+// (y = 8 n1 + n2, fy = k1 + 9 k2; W_N = e^{-2 pi i / N}):
+//   X[k1 + 9 k2] = sum_{n2<8} W8^{n2 k2} W72^{n2 k1} sum_{n1<9} x[8 n1 + n2] W9^{n1 k1}
+// so that the kernels on either side of the spectral GEMM each hold everything their math needs:
+//   row kernel  (image b, row class n2): the 8 rows y = 8 n1 + n2 with ALL 64 channels -- the row
+//               transforms, the 9-point sums over n1, and every per-pixel channel mix (the 1x1 gates
+//               of hgru_module.py:696-711, 729-740), so the B half-step's epilogue runs between its
+//               inverse and the next step's forward transform without a map round trip;
+//   col kernel  (column fx, class k1, 32 images): the 8 frequencies fy = k1 + 9 k2 with all 64
+//               channels -- the twiddles W72^{n2 k1}, the 8-point sums over n2 and the per-frequency
+//               64 x 64 complex GEMM (f16x3, k_fft.hip spec_gemm_kernel's fragments).
+// One timestep is four launches (hgru_module.py:825-857):
+//   col: Z -> Z'   row_a: Z', X, O -> I, Z   col: Z -> Z'   row_b: Z', I, O -> O', Z
+// Z = [b][n2][fx][k1][64 channels] complex64 (1.36 MB per image, a spectrum's size) carries the
+// partial transforms between them IN PLACE: every block reads exactly the elements it writes.  Per
+// image and step: 8 spectra + 6 maps of traffic (17.2 MB) instead of the six-launch loop's 8 + 10
+// (22.1 MB): P2 and the gated state Og never reach HBM.  The numerics are the six-launch loop's (fp32
+// transforms, twiddles rounded once from double, the same f16x3 spectral GEMM and gate GEMMs, the same
+// epilogue expressions); only the transforms' association order differs (~1e-7 relative).
+#include "fft_dev.hpp"
+
+namespace mp {
+
+constexpr int Z_CLS = FX * 9;                        // 333 (fx, k1) column classes
+constexpr int RK_NT = 256;                           // row kernel: 4 waves, wave w = rows n1 = 2w, 2w + 1
+constexpr int RK_ITEMS = FX * 64;                    // (fx, channel) columns of the 9-point passes: 2368
+constexpr int RK_NIT = (RK_ITEMS + RK_NT - 1) / RK_NT;   // 10 per thread
+constexpr int RK_T = 8 * FX * 64;                    // T[n1][fx][c] complex: 151,552 B of LDS
+constexpr int RK_SP = 68;                            // staging pitch (floats) per pixel (16-B fragment reads)
+static_assert(128 * RK_SP * 4 <= 2 * FX * 64 * 8, "a wave's staging fits its two rows of T");
+
+// complex index of channel 0 of Z[b][n2][fx][k1]
+__device__ __forceinline__ size_t z_off(int b, int n2, int fx, int k1) {
+  return ((((size_t)b * 8 + n2) * FX + fx) * 9 + k1) * 64;
+}
+
+enum { ROW_A = 0, ROW_B = 1, ROW_FINAL = 2, ROW_INIT = 3 };
+
+// ---------------------------------------------------------------------------------------------
+// row kernel.  Block = (image b, row class n2), 256 threads; lane c of wave w owns channel c of rows
+// n1 = 2w (real part of its packed transforms) and 2w + 1 (imaginary part).
+//   Ia  (all threads) inverse 9-point sums over k1 of Z'[b][n2][fx][.][c] -> T[n1][fx][c]
+//   Ib  (lane c)      inverse row transform (Hermitian-extended, rows 2w / 2w+1 packed) -> P[x][c]
+//   II  (wave)        the half-step's epilogue on 32-pixel segments in the MFMA accumulator layout,
+//                     P staged through the wave's own rows of T ([pixel][68 floats])
+//   III (lane c)      forward row transform of the epilogue's output -> T[n1][fx][c]
+//   IIIb(all)         forward 9-point sums over n1 -> Z[b][n2][fx][k1][c]
+// ---------------------------------------------------------------------------------------------
+
+// Ia: thread i = (fx, c), c fastest: a wave reads 9 runs of 512 B per item, all items' loads issued
+// before the first transform
+__device__ __forceinline__ void rk_inv9(const cpx* __restrict__ Z, int b, int n2, int tid, cpx* T) {
+  cpx v[RK_NIT][9];
+#pragma unroll
+  for (int it = 0; it < RK_NIT; ++it) {
+    const int i = min(it * RK_NT + tid, RK_ITEMS - 1);
+    const cpx* src = Z + z_off(b, n2, i >> 6, 0) + (i & 63);
+#pragma unroll
+    for (int k1 = 0; k1 < 9; ++k1) v[it][k1] = src[k1 * 64];
+  }
+#pragma unroll
+  for (int it = 0; it < RK_NIT; ++it) {
+    const int i = it * RK_NT + tid;
+    if (i < RK_ITEMS) {
+      dft9<1>(v[it]);
+      const int fx = i >> 6, c = i & 63;
+#pragma unroll
+      for (int n1 = 0; n1 < 8; ++n1) T[(n1 * FX + fx) * 64 + c] = v[it][n1];   // n1 = 8: row 64 + n2, unused
+    }
+  }
+}
+
+// Ib: the half spectra A (row 2w) and B (row 2w + 1) of channel c packed as C = A + iB, extended
+// Hermitian, one inverse 72-point transform: v[x] = (P[row 2w][x][c], P[row 2w + 1][x][c])
+__device__ __forceinline__ void rk_inv_row(const cpx* T, int w, int c, cpx (&v)[72]) {
+  const int ta = (2 * w) * FX * 64 + c, tb = ta + FX * 64;
+#pragma unroll
+  for (int k = 0; k < FX; ++k) {
+    const cpx A = T[ta + k * 64], B = T[tb + k * 64];
+    v[k] = cfma(swp(B), cpx{-1.f, 1.f}, A);                                 // (A.x - B.y, A.y + B.x)
+    if (k > 0 && k < FX - 1) v[72 - k] = cfma(A, cpx{1.f, -1.f}, swp(B));   // (A.x + B.y, B.x - A.y)
+  }
+  fft72<1>(v);
+}
+
+// III: the staged rows (zero outside the map) -> forward 72-point transform of the packed pair ->
+// the two half spectra into the wave's rows of T.  The wave's staging IS those rows: every lane reads
+// its 128 staged values before any lane of the wave writes (one wave's LDS operations run in order).
+__device__ __forceinline__ void rk_fwd_row(cpx* T, const float* stg, int w, int c, bool la, bool lb, int W) {
+  cpx v[72];
+#pragma unroll
+  for (int x = 0; x < 72; ++x) {
+    const bool in = x < 64 && x < W;
+    v[x] = cpx{(in && la) ? stg[x * RK_SP + c] : 0.f, (in && lb) ? stg[(64 + x) * RK_SP + c] : 0.f};
+  }
+  fft72<-1>(v);
+  const int ta = (2 * w) * FX * 64 + c, tb = ta + FX * 64;
+#pragma unroll
+  for (int k = 0; k < FX; ++k) {   // Z = FFT(a + ib): A[k] = (Z[k] + conj Z[-k]) / 2, B[k] = (Z[k] - conj Z[-k]) / 2i
+    const cpx zk = v[k], zm = v[(72 - k) % 72];
+    T[ta + k * 64] = cfma(zm, cpx{1.f, -1.f}, zk) * 0.5f;
+    T[tb + k * 64] = cfma(swp(zk), cpx{1.f, -1.f}, swp(zm)) * 0.5f;
+  }
+}
+
+// IIIb: thread i = (fx, c): the 8 rows' half spectra (row 64 + n2 is zero padding) -> 9-point sums
+// over n1 -> Z[b][n2][fx][k1][c], a wave storing 9 runs of 512 B
+__device__ __forceinline__ void rk_fwd9(cpx* __restrict__ Z, int b, int n2, int tid, const cpx* T) {
+#pragma unroll 2
+  for (int it = 0; it < RK_NIT; ++it) {
+    const int i = it * RK_NT + tid;
+    if (i >= RK_ITEMS) break;
+    const int fx = i >> 6, c = i & 63;
+    cpx u[9];
+#pragma unroll
+    for (int n1 = 0; n1 < 8; ++n1) u[n1] = T[(n1 * FX + fx) * 64 + c];
+    u[8] = cpx{0.f, 0.f};
+    dft9<-1>(u);
+    cpx* dst = Z + z_off(b, n2, fx, 0) + c;
+#pragma unroll
+    for (int k1 = 0; k1 < 9; ++k1) dst[k1 * 64] = u[k1];
+  }
+}
+
+// II: the wave's four 32-pixel segments (s: row 2w + (s >> 1), columns 32 (s & 1) + j), lane (h, j),
+// register r of block n = channel 32 n + 8 (r >> 2) + 4 h + (r & 3) -- k_fft.hip spec_epi_b_kernel's
+// layout and expressions, P read from (and the epilogue's output written back to) the staging.
+template <int MODE>
+__device__ __forceinline__ void rk_epilogue(const ConvArgs& p, float* stg, int b, int n2, int w, int lane,
+                                            const void* __restrict__ or_x3, float or_us,
+                                            const void* __restrict__ ir_x3, float ir_us,
+                                            const float* __restrict__ O0) {
+  const int h = lane >> 5, j = lane & 31, H = p.H, W = p.W;
+#pragma unroll 1
+  for (int s = 0; s < 4; ++s) {
+    const int r = s >> 1, xs = 32 * (s & 1), y = 8 * (2 * w + r) + n2;
+    if (y >= H || xs >= W) continue;   // wave-uniform
+    const int x = xs + j, px = r * 64 + x;
+    float* sp = stg + px * RK_SP;
+    if constexpr (MODE == ROW_A) {
+      // hgru_module.py:797-799: I = tanh(X - (beta O + nu) (P1 + lateral_bias))
+      f32x4 xv[2][4], ov[2][4];
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          xv[n][g] = map_ld4<false>(p.X, xx_index(b, 4 * n + g, y, x, 4 * h, H, W));
+          ov[n][g] = map_ld4<false>(p.O, oo_index(b, 4 * n + g, y, x, 4 * h, H, W));
+        }
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int c = 32 * n + 8 * g + 4 * h;
+          const f32x4 pv = *reinterpret_cast<const f32x4*>(sp + c);
+          const f32x4 lat = *reinterpret_cast<const f32x4*>(p.vecs + V_LAT * 64 + c);
+          const f32x4 be = *reinterpret_cast<const f32x4*>(p.vecs + V_BETA * 64 + c);
+          const f32x4 nu = *reinterpret_cast<const f32x4*>(p.vecs + V_NU * 64 + c);
+          f32x4 iv;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) iv[e] = atanh_f(epi_a(xv[n][g][e], ov[n][g][e], pv[e], be[e], nu[e], lat[e]));
+          map_st4<false>(p.dst, ii_index(b, 4 * n + g, y, x, 4 * h, H, W), iv);
+          *reinterpret_cast<f32x4*>(sp + c) = iv;
+        }
+    } else if constexpr (MODE == ROW_INIT) {
+      // hgru_module.py:696-711 on O0 (NHWC): O = O0, Og = O0 * sigmoid(O0 . i_r + i_b)
+      f32x16 V[2], Y[2];
+      const float* src = O0 + (((size_t)b * H + y) * W + x) * C;
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 v = *reinterpret_cast<const f32x4*>(src + 32 * n + 8 * g + 4 * h);
+#pragma unroll
+          for (int e = 0; e < 4; ++e) V[n][4 * g + e] = v[e];
+        }
+      gate_x3(static_cast<const f16x8*>(ir_x3), V, Y, lane, ir_us);
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int c = 32 * n + 8 * g + 4 * h;
+          const f32x4 ib = *reinterpret_cast<const f32x4*>(p.vecs + V_IB * 64 + c);
+          f32x4 o, og;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            o[e] = V[n][4 * g + e];
+            og[e] = o[e] * fsigmoid(Y[n][4 * g + e] + ib[e]);
+          }
+          map_st4<false>(p.dst, oo_index(b, 4 * n + g, y, x, 4 * h, H, W), o);
+          *reinterpret_cast<f32x4*>(sp + c) = og;
+        }
+    } else {
+      // hgru_module.py:729-740, 806-849: g2 = sigmoid(I . o_r + o_b); e = gamma (P2 + lat);
+      // O' = (g2 O + (1 - g2) tanh(kappa (I + e) + omega (I e))) rho[t];  then Og' = O' sigmoid(O' . i_r + i_b)
+      f32x16 Iv[2], Y[2];
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const f32x4 iv = map_ld4<false>(p.I, ii_index(b, 4 * n + g, y, x, 4 * h, H, W));
+#pragma unroll
+          for (int e = 0; e < 4; ++e) Iv[n][4 * g + e] = iv[e];
+        }
+      gate_x3(static_cast<const f16x8*>(or_x3), Iv, Y, lane, or_us);
+#pragma unroll
+      for (int n = 0; n < 2; ++n)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int c = 32 * n + 8 * g + 4 * h;
+          const f32x4 pv = *reinterpret_cast<const f32x4*>(sp + c);
+          const size_t odx = oo_index(b, 4 * n + g, y, x, 4 * h, H, W);
+          const f32x4 ov = map_ld4<false>(p.O, odx);
+          const f32x4 lat = *reinterpret_cast<const f32x4*>(p.vecs + V_LAT * 64 + c);
+          const f32x4 ga = *reinterpret_cast<const f32x4*>(p.vecs + V_GAMMA * 64 + c);
+          const f32x4 ka = *reinterpret_cast<const f32x4*>(p.vecs + V_KAPPA * 64 + c);
+          const f32x4 om = *reinterpret_cast<const f32x4*>(p.vecs + V_OMEGA * 64 + c);
+          const f32x4 ob = *reinterpret_cast<const f32x4*>(p.vecs + V_OB * 64 + c);
+          f32x4 o;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) {
+            const int rr = 4 * g + e;
+            const float g2 = fsigmoid(Y[n][rr] + ob[e]);
+            const float iv = Iv[n][rr];
+            const float ee = ga[e] * (pv[e] + lat[e]);
+            const float S = ftanh(ka[e] * (iv + ee) + om[e] * (iv * ee));
+            const float on = (g2 * ov[e] + (1.f - g2) * S) * p.rho;
+            o[e] = on;
+            Iv[n][rr] = on;
+          }
+          map_st4<false>(p.dst, odx, o);
+        }
+      f32x16 (&Ov)[2] = Iv;
+      if constexpr (MODE == ROW_B) {
+        gate_x3(static_cast<const f16x8*>(ir_x3), Ov, Y, lane, ir_us);
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int c = 32 * n + 8 * g + 4 * h;
+            const f32x4 ib = *reinterpret_cast<const f32x4*>(p.vecs + V_IB * 64 + c);
+            f32x4 o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = Ov[n][4 * g + e] * fsigmoid(Y[n][4 * g + e] + ib[e]);
+            *reinterpret_cast<f32x4*>(sp + c) = o;
+          }
+      } else {
+        // ROW_FINAL: BN_3(O_T) (hgru_pose.py:82-90) as the NHWC fp32 map fc_1 flattens (mode 1) or as
+        // fc_1's f16 hi / lo planes (mode 2); the segment's 32 pixels x 64 channels are one contiguous
+        // 8 KiB run of the output, staged here and stored with contiguous lanes
+#pragma unroll
+        for (int n = 0; n < 2; ++n)
+#pragma unroll
+          for (int g = 0; g < 4; ++g) {
+            const int c = 32 * n + 8 * g + 4 * h;
+            const f32x4 ss = *reinterpret_cast<const f32x4*>(p.vecs + V_OUTS * 64 + c);
+            const f32x4 tt = *reinterpret_cast<const f32x4*>(p.vecs + V_OUTT * 64 + c);
+            f32x4 o;
+#pragma unroll
+            for (int e = 0; e < 4; ++e) o[e] = Ov[n][4 * g + e] * ss[e] + tt[e];
+            *reinterpret_cast<f32x4*>(sp + c) = o;
+          }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        const float* run = stg + (r * 64 + xs) * RK_SP;
+        const size_t e0 = (((size_t)b * H + y) * W + xs) * C;
+        if (p.mode != 2) {
+#pragma unroll
+          for (int k = 0; k < 8; ++k) {   // 8 x 1 KiB
+            const int q = k * 64 + lane, pp = q >> 4, c4 = (q & 15) * 4;
+            *reinterpret_cast<f32x4*>(p.dst2 + e0 + pp * C + c4) = *reinterpret_cast<const f32x4*>(run + pp * RK_SP + c4);
+          }
+        } else {   // fc_1's split planes, split exactly as fc_gemm_x3_kernel splits (k_fc.hip)
+#pragma unroll
+          for (int k = 0; k < 4; ++k) {
+            const int q = k * 64 + lane, pp = q >> 3, c8 = (q & 7) * 8;
+            const f32x4 a = *reinterpret_cast<const f32x4*>(run + pp * RK_SP + c8);
+            const f32x4 bq = *reinterpret_cast<const f32x4*>(run + pp * RK_SP + c8 + 4);
+            f16x8 hv, lv;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              const float v = e < 4 ? a[e] : bq[e - 4];
+              hv[e] = (_Float16)v;
+              lv[e] = (_Float16)(v - (float)hv[e]);
+            }
+            *reinterpret_cast<f16x8*>(reinterpret_cast<_Float16*>(p.dst2) + e0 + pp * C + c8) = hv;
+            if (p.dst3) *reinterpret_cast<f16x8*>(reinterpret_cast<_Float16*>(p.dst3) + e0 + pp * C + c8) = lv;
+          }
+        }
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      }
+    }
+  }
+}
+
+template <int MODE>
+__global__ __launch_bounds__(RK_NT, 1) void row_kernel(cpx* __restrict__ Z, ConvArgs p, const void* __restrict__ or_x3,
+                                                        float or_us, const void* __restrict__ ir_x3, float ir_us,
+                                                        const float* __restrict__ O0) {
+  __shared__ cpx T[RK_T];
+  const int b = blockIdx.x >> 3, n2 = blockIdx.x & 7;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  float* stg = reinterpret_cast<float*>(T + (2 * w) * FX * 64);   // the wave's own two rows of T
+  const int H = p.H, W = p.W;
+  const bool la = 8 * (2 * w) + n2 < H, lb = 8 * (2 * w + 1) + n2 < H;
+  if constexpr (MODE != ROW_INIT) {
+    rk_inv9(Z, b, n2, tid, T);
+    lds_barrier();
+    if (la || lb) {   // wave-uniform
+      cpx v[72];
+      rk_inv_row(T, w, lane, v);
+      // (in-wave order: the reads of T above precede these writes over the same rows)
+#pragma unroll
+      for (int x = 0; x < 64; ++x) {
+        if (x < W) {
+          stg[x * RK_SP + lane] = v[x].x;
+          stg[(64 + x) * RK_SP + lane] = v[x].y;
+        }
+      }
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  rk_epilogue<MODE>(p, stg, b, n2, w, lane, or_x3, or_us, ir_x3, ir_us, O0);
+  if constexpr (MODE == ROW_FINAL) return;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  rk_fwd_row(T, stg, w, lane, la, lb, W);
+  lds_barrier();
+  rk_fwd9(Z, b, n2, tid, T);
+}
+
+// ---------------------------------------------------------------------------------------------
+// column kernel (the spectral GEMM).  Block = (column class (fx, k1), 32 images), 512 threads; wave
+// k2 computes frequency fy = k1 + 9 k2:  Y[b][co] = sum_ci S[b][ci] G[ci][co]  (complex), as
+// k_fft.hip spec_gemm_kernel does for one frequency (f16x3 A/B fragments, the same k order).
+// Before it, thread (image, channel group) turns its 8 row-class partials Z[b][n2][fx][k1][4 ch]
+// into the 8 frequencies (twiddle, 8-point DFT, scale + f16 split into the S tile); after it, the
+// same thread takes the 8 frequencies back to row-class partials (8-point inverse DFT, twiddle) and
+// writes them over its inputs.  Blocks of one class run on one XCD (weights fetched once).
+// ---------------------------------------------------------------------------------------------
+constexpr int CG_NI = 32;
+constexpr int CG_SLD = CG_NI + 1;                    // S tile pitch (16-B units) per (cq, part, k2) row
+constexpr int CG_YLD = 16 * 8 * 2 + 1;               // Y tile pitch (16-B units) per image
+constexpr int CG_TILE = 16 * 2 * 8 * CG_SLD;         // 135,168 B
+static_assert(CG_NI * CG_YLD <= CG_TILE, "the Y tile fits the S tile's space");
+constexpr int CG_NC8 = (Z_CLS + 7) / 8;              // 42 groups of 8 classes (one per XCD)
+
+__global__ __launch_bounds__(512, 1) void col_gemm_kernel(cpx* __restrict__ Z, const uint4* __restrict__ Gc, int B,
+                                                          int ngrp, float unscale) {
+  __shared__ uint4 tile[CG_TILE];
+  const int c8 = blockIdx.x / (8 * ngrp), rem = blockIdx.x - c8 * 8 * ngrp;
+  const int grp = rem >> 3, cls = c8 * 8 + (rem & 7);
+  if (cls >= Z_CLS) return;
+  const int fx = cls / 9, k1 = cls - fx * 9;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, j = lane & 31;
+  const int img0 = grp * CG_NI;
+  const int bl = tid >> 4, cq = tid & 15;
+  const bool live = img0 + bl < B;
+  const int b = min(img0 + bl, B - 1);
+  // ---- the thread's 8 row-class partials (8 x 32 B; unconditional, clamped) ----
+  f32x4 zin[8][2];
+#pragma unroll
+  for (int n2 = 0; n2 < 8; ++n2) {
+    const f32x4* src = reinterpret_cast<const f32x4*>(Z + z_off(b, n2, fx, k1) + 4 * cq);
+    zin[n2][0] = src[0];
+    zin[n2][1] = src[1];
+  }
+  // ---- weights of frequency (fx, k1 + 9 wv): class-major pack, 32 KiB, issued before the tile wait ----
+  const uint4* gw = Gc + (size_t)(cls * 8 + wv) * 2 * 16 * 64;
+  uint4 wr[8][2][2];
+#pragma unroll
+  for (int t = 0; t < 8; ++t)
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      wr[t][cb][0] = gw[(0 * 16 + 2 * t + h) * 64 + 32 * cb + j];
+      wr[t][cb][1] = gw[(1 * 16 + 2 * t + h) * 64 + 32 * cb + j];
+    }
+  // ---- twiddle W72^{n2 k1}, 8-point DFT over n2 -> k2; scale and split into the S tile ----
+  {
+    cpx s[4][8];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+#pragma unroll
+      for (int n2 = 0; n2 < 8; ++n2) {
+        const f32x4 zz = zin[n2][e >> 1];
+        s[e][n2] = twid<-1>(cpx{zz[2 * (e & 1)], zz[2 * (e & 1) + 1]}, n2 * k1);
+      }
+      dft8<-1>(s[e]);
+    }
+#pragma unroll
+    for (int k2 = 0; k2 < 8; ++k2) {
+      f16x8 hv, lv;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        const float re = s[e][k2].x * SPEC_SCALE, im = s[e][k2].y * SPEC_SCALE;
+        const _Float16 hr = (_Float16)re, hm = (_Float16)im;
+        hv[2 * e] = hr;
+        hv[2 * e + 1] = hm;
+        lv[2 * e] = (_Float16)(re - (float)hr);
+        lv[2 * e + 1] = (_Float16)(im - (float)hm);
+      }
+      tile[((cq * 2 + 0) * 8 + k2) * CG_SLD + bl] = live ? __builtin_bit_cast(uint4, hv) : uint4{0, 0, 0, 0};
+      tile[((cq * 2 + 1) * 8 + k2) * CG_SLD + bl] = live ? __builtin_bit_cast(uint4, lv) : uint4{0, 0, 0, 0};
+    }
+  }
+  lds_barrier();
+  // ---- the 128 x 32 x 128 real product of frequency k2 = wv (spec_gemm_kernel's fragments) ----
+  f32x16 acc[4] = {};
+  const uint4 m = {0x80000000u, 0x80000000u, 0x80000000u, 0x80000000u};
+#pragma unroll
+  for (int t = 0; t < 8; ++t) {
+    const int cqq = 2 * t + h;
+    const f16x8 sh = __builtin_bit_cast(f16x8, tile[((cqq * 2 + 0) * 8 + wv) * CG_SLD + j]);
+    const f16x8 sl = __builtin_bit_cast(f16x8, tile[((cqq * 2 + 1) * 8 + wv) * CG_SLD + j]);
+#pragma unroll
+    for (int cb = 0; cb < 2; ++cb) {
+      const uint4 gh = wr[t][cb][0], gl = wr[t][cb][1];
+      const f16x8 ah0 = __builtin_bit_cast(f16x8, gh ^ m), al0 = __builtin_bit_cast(f16x8, gl ^ m);
+      const f16x8 ah1 = __builtin_bit_cast(f16x8, (gh >> 16) | (gh << 16));
+      const f16x8 al1 = __builtin_bit_cast(f16x8, (gl >> 16) | (gl << 16));
+      acc[cb] = mfma16(al0, sh, acc[cb]);
+      acc[cb] = mfma16(ah0, sl, acc[cb]);
+      acc[cb] = mfma16(ah0, sh, acc[cb]);
+      acc[2 + cb] = mfma16(al1, sh, acc[2 + cb]);
+      acc[2 + cb] = mfma16(ah1, sl, acc[2 + cb]);
+      acc[2 + cb] = mfma16(ah1, sh, acc[2 + cb]);
+    }
+  }
+  lds_barrier();   // every wave has read the S tile
+  // ---- Y tile [image][cq][k2] (lo: channels 0, 1 of the group; hi: 2, 3) ----
+  f32x4* ytile = reinterpret_cast<f32x4*>(tile);
+#pragma unroll
+  for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      const int cqo = 8 * cb + 2 * g + h;
+      const f32x16& re = acc[cb];
+      const f32x16& im = acc[2 + cb];
+      ytile[j * CG_YLD + (cqo * 8 + wv) * 2] = f32x4{re[4 * g], im[4 * g], re[4 * g + 1], im[4 * g + 1]} * unscale;
+      ytile[j * CG_YLD + (cqo * 8 + wv) * 2 + 1] =
+          f32x4{re[4 * g + 2], im[4 * g + 2], re[4 * g + 3], im[4 * g + 3]} * unscale;
+    }
+  lds_barrier();
+  // ---- 8-point inverse DFT over k2 -> n2, twiddle W72^{-n2 k1}, written over the inputs ----
+  cpx yv[4][8];
+#pragma unroll
+  for (int k2 = 0; k2 < 8; ++k2) {
+    const f32x4 lo = ytile[bl * CG_YLD + (cq * 8 + k2) * 2];
+    const f32x4 hi = ytile[bl * CG_YLD + (cq * 8 + k2) * 2 + 1];
+    yv[0][k2] = cpx{lo[0], lo[1]};
+    yv[1][k2] = cpx{lo[2], lo[3]};
+    yv[2][k2] = cpx{hi[0], hi[1]};
+    yv[3][k2] = cpx{hi[2], hi[3]};
+  }
+#pragma unroll
+  for (int e = 0; e < 4; ++e) {
+    dft8<1>(yv[e]);
+#pragma unroll
+    for (int n2 = 0; n2 < 8; ++n2) yv[e][n2] = twid<1>(yv[e][n2], n2 * k1);
+  }
+  if (live) {
+#pragma unroll
+    for (int n2 = 0; n2 < 8; ++n2) {
+      f32x4* dst = reinterpret_cast<f32x4*>(Z + z_off(b, n2, fx, k1) + 4 * cq);
+      dst[0] = f32x4{yv[0][n2].x, yv[0][n2].y, yv[1][n2].x, yv[1][n2].y};
+      dst[1] = f32x4{yv[2][n2].x, yv[2][n2].y, yv[3][n2].x, yv[3][n2].y};
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------ launchers
+bool fft4_enabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("MP_FFT4");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  return v;
+}
+
+hipError_t launch_col_gemm(void* Z, const void* Gc, int B, float unscale, hipStream_t st) {
+  if (B <= 0) return hipSuccess;
+  const int ngrp = (B + CG_NI - 1) / CG_NI;
+  hipLaunchKernelGGL(col_gemm_kernel, dim3(CG_NC8 * 8 * ngrp), dim3(512), 0, st, static_cast<cpx*>(Z),
+                     static_cast<const uint4*>(Gc), B, ngrp, unscale);
+  return hipGetLastError();
+}
+
+hipError_t launch_row(int mode, void* Z, const ConvArgs& a, const void* or_x3, float or_us, const void* ir_x3,
+                      float ir_us, const float* O0, int B, hipStream_t st) {
+  if (B <= 0) return hipSuccess;
+  if (a.H < 1 || a.H > 64 || (a.W != 32 && a.W != 64)) return hipErrorInvalidValue;
+  cpx* z = static_cast<cpx*>(Z);
+  const dim3 g(B * 8), t(RK_NT);
+  switch (mode) {
+    case ROW_A: hipLaunchKernelGGL(row_kernel<ROW_A>, g, t, 0, st, z, a, or_x3, or_us, ir_x3, ir_us, O0); break;
+    case ROW_B: hipLaunchKernelGGL(row_kernel<ROW_B>, g, t, 0, st, z, a, or_x3, or_us, ir_x3, ir_us, O0); break;
+    case ROW_FINAL: hipLaunchKernelGGL(row_kernel<ROW_FINAL>, g, t, 0, st, z, a, or_x3, or_us, ir_x3, ir_us, O0); break;
+    case ROW_INIT: hipLaunchKernelGGL(row_kernel<ROW_INIT>, g, t, 0, st, z, a, or_x3, or_us, ir_x3, ir_us, O0); break;
+    default: return hipErrorInvalidValue;
+  }
+  return hipGetLastError();
+}
+
+}  // namespace mp

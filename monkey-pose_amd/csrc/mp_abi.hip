@@ -102,7 +102,8 @@ void finalize_circuit(mp_ctx* c, const std::vector<float>* outs, const std::vect
   } else if (is_fft(c->dtype)) {
     const bool bf = c->dtype == MP_DTYPE_BF16;
     c->spec_g.alloc(fft_weight_bytes());
-    hip_check(build_spec_weights(it->second.dev->f(), c->ssf, c->spec_g.p, &c->p_unscale, bf), "p_r spectrum");
+    c->fft4 = c->dtype == MP_DTYPE_F32_FFT && fft4_enabled();
+    hip_check(build_spec_weights(it->second.dev->f(), c->ssf, c->spec_g.p, &c->p_unscale, bf, c->fft4), "p_r spectrum");
     c->or_x3.alloc(gate_x3_bytes());
     c->ir_x3.alloc(gate_x3_bytes());
     hip_check(pack_gate_x3(c->need("contextual_circuit/o_r", {1, 1, 64, 64}).dev->f(), c->or_x3.p, &c->or_us, bf),
@@ -367,6 +368,70 @@ void fft_circuit_range(mp_ctx* c, int b0, int n, int H, int W, int T, float* fin
   }
 }
 
+// the hGRU loop of images [b0, b0 + n) on stream st, four-step FFT path (k_fft4.hip): one row(INIT)
+// (hgru_module.py:696-711 on O0, and the forward transform of the gated state), then per timestep
+//   col -> row A (I = tanh(X - (beta O + nu) P1), hgru_module.py:797-799) -> col -> row B (O', the
+//   next gated state; the last step: O' and BN_3(O_T))
+// every launch in place on one spectrum-sized buffer Z
+void fft4_circuit_range(mp_ctx* c, int b0, int n, int H, int W, int T, const float* o0_nhwc, float* final_dst2,
+                        const StateOut* so, const SplitOut* sp, hipStream_t st) {
+  const size_t m = (size_t)b0 * 64 * H * W;
+  void* Z = static_cast<char*>(c->specS.p) + fft_spec_bytes(b0);
+  float* X = c->X.f() + m;
+  float* O = c->O.f() + m;
+  float* I = c->I.f() + m;
+  {
+    ConvArgs a0{};
+    a0.H = H;
+    a0.W = W;
+    a0.dst = O;
+    a0.vecs = c->vecs.f();
+    ProfScope pa(c, st, "conv15_a");
+    ProfScope ps(c, st, "row_init");
+    hip_check(launch_row(3, Z, a0, c->or_x3.p, c->or_us, c->ir_x3.p, c->ir_us, o0_nhwc + m, n, st), "row_init");
+  }
+  for (int t = 0; t < T; ++t) {
+    ConvArgs a{};
+    a.H = H;
+    a.W = W;
+    a.X = X;
+    a.O = O;
+    a.dst = I;
+    a.vecs = c->vecs.f();
+    ConvArgs b{};
+    b.H = H;
+    b.W = W;
+    b.I = I;
+    b.O = O;
+    b.dst = O;
+    b.vecs = c->vecs.f();
+    b.rho = c->rho[t];
+    b.mode = 0;
+    const bool last = t == T - 1;
+    if (last) final_out(b, final_dst2, sp, b0, H, W);
+    {
+      ProfScope pa(c, st, "conv15_a");
+      {
+        ProfScope ps(c, st, "col_gemm");
+        hip_check(launch_col_gemm(Z, c->spec_g.p, n, c->p_unscale, st), "col_gemm");
+      }
+      ProfScope ps(c, st, "row_a");
+      hip_check(launch_row(0, Z, a, c->or_x3.p, c->or_us, c->ir_x3.p, c->ir_us, nullptr, n, st), "row_a");
+    }
+    {
+      ProfScope pb(c, st, "conv15_b");
+      {
+        ProfScope ps(c, st, "col_gemm");
+        hip_check(launch_col_gemm(Z, c->spec_g.p, n, c->p_unscale, st), "col_gemm");
+      }
+      ProfScope ps(c, st, last ? "row_final" : "row_b");
+      hip_check(launch_row(last ? 2 : 1, Z, b, c->or_x3.p, c->or_us, c->ir_x3.p, c->ir_us, nullptr, n, st),
+                last ? "row_final" : "row_b");
+    }
+    store_step(so, O, I, b0, n, H, W, t, false, st, fft_c4_maps(), fft_c4_state());
+  }
+}
+
 // fc_1 on pre-split activation planes (MP_FC_PRESPLIT=0: the fp32 map + in-loop split, for A/B)
 bool fc_presplit() {
   static const bool v = [] {
@@ -399,8 +464,13 @@ void run_circuit(mp_ctx* c, int64_t n, int H, int W, int T, const float* o0_nhwc
   // FFT path, not profiling: batch slices are independent, so they run on separate streams and
   // their latency-bound kernels overlap (the per-kernel HIP-event profile keeps one stream)
   const int ns = std::min<int>(stream_count(), (int)(n / slice_min()));
+  if (c->fft4 && (c->prof || ns < 2)) {
+    fft4_circuit_range(c, 0, (int)n, H, W, T, o0_nhwc, final_dst2, so, sp, st);
+    return;
+  }
   if (is_fft(c->dtype) && !c->prof && ns >= 2) {
-    hip_check(launch_gate_init_x3(o0_nhwc, c->O.f(), c->Og.f(), c->ir_x3.p, c->ir_us, c->vecs.f(), (int)n, H, W,
+    if (!c->fft4)
+      hip_check(launch_gate_init_x3(o0_nhwc, c->O.f(), c->Og.f(), c->ir_x3.p, c->ir_us, c->vecs.f(), (int)n, H, W,
                                   st, c->dtype == MP_DTYPE_BF16),
               "gate_init");
     while ((int)c->sides.size() < ns - 1) {
@@ -422,7 +492,10 @@ void run_circuit(mp_ctx* c, int64_t n, int H, int W, int T, const float* o0_nhwc
       const int cnt = std::min<int>(g * gs, (int)n - b0);
       hipStream_t s = k == 0 ? st : c->sides[k - 1];
       if (k > 0) hip_check(hipStreamWaitEvent(s, c->ev_fork, 0), "hipStreamWaitEvent");
-      fft_circuit_range(c, b0, cnt, H, W, T, final_dst2, so, sp, s);
+      if (c->fft4)
+        fft4_circuit_range(c, b0, cnt, H, W, T, o0_nhwc, final_dst2, so, sp, s);
+      else
+        fft_circuit_range(c, b0, cnt, H, W, T, final_dst2, so, sp, s);
       b0 += cnt;
     }
     for (int k = 1; k < ns; ++k) {
@@ -936,6 +1009,8 @@ int mp_info(mp_ctx* ctx, const char* key, int64_t* value) {
       *value = ctx->finalized ? 1 : 0;
     else if (k == "fc1_in")
       *value = ctx->fc1_in;
+    else if (k == "fft_loop")   // 4: the four-step loop (k_fft4.hip), 6: the six-launch loop, 0: no FFT path
+      *value = is_fft(ctx->dtype) ? (ctx->fft4 ? 4 : 6) : 0;
     else if (k == "workspace_bytes")
       *value = (int64_t)(ctx->X.bytes + ctx->O.bytes + ctx->I.bytes + ctx->Og.bytes + ctx->bufA.bytes +
                          ctx->bufB.bytes + ctx->fcin.bytes + ctx->part.bytes + ctx->h1.bytes);

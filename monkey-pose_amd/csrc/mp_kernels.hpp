@@ -69,7 +69,8 @@ bool fft_c4_maps();   // the FFT loop's I map is C4 (k_fft.hip FFT_C4)
 size_t fft_spec_bytes(int B);      // one spectrum buffer (S or Y) for B images
 size_t fft_weight_bytes();         // expanded split spectral weights
 // HWIO [ks][ks][64][64] -> packed split spectral weights (synchronous, finalize time)
-hipError_t build_spec_weights(const float* w, int ks, void* Gx, float* unscale, bool bf = false);
+// cls_major: the four-step loop's class-major frequency order (k_fft4.hip)
+hipError_t build_spec_weights(const float* w, int ks, void* Gx, float* unscale, bool bf = false, bool cls_major = false);
 hipError_t launch_fft_fwd(const float* act, void* S, int B, int H, int W, hipStream_t st, bool bf = false);
 hipError_t launch_spec_gemm(const void* S, const void* Gx, void* Y, int B, float unscale, hipStream_t st,
                             bool bf = false);
@@ -83,6 +84,14 @@ hipError_t launch_gate_init_x3(const float* O0, float* O, float* Og, const void*
                                int B, int H, int W, hipStream_t st, bool bf = false);
 hipError_t launch_spec_epi_b(const ConvArgs& a, const float* P, const void* or_x3, float or_us, const void* ir_x3,
                              float ir_us, int B, hipStream_t st, bool bf = false);
+// k_fft4.hip: the fp32 FFT path's four-step loop (MP_FFT4, default on).  One spectrum-sized buffer Z
+// carries the partial transforms; per timestep col -> row(A) -> col -> row(B | FINAL), after one
+// row(INIT) per forward.  Row modes: 0 = A (a.X, a.O -> a.dst = I), 1 = B (a.I, a.O -> a.dst = O'),
+// 2 = the last B (O' and BN_3(O') to a.dst2 / a.dst3 per a.mode), 3 = INIT (O0 NHWC -> a.dst = O).
+bool fft4_enabled();
+hipError_t launch_col_gemm(void* Z, const void* Gc, int B, float unscale, hipStream_t st);
+hipError_t launch_row(int mode, void* Z, const ConvArgs& a, const void* or_x3, float or_us, const void* ir_x3,
+                      float ir_us, const float* O0, int B, hipStream_t st);
 // k_igemm.hip (dense / hierarchical regressors)
 struct IgemmArgs {
   const float* x;      // input view: pixel (n,y,x) channel ci at x[((n*H+y)*W+x)*ldx + cix + ci]

@@ -126,6 +126,7 @@ struct mp_ctx {
   DevBuf conv3_pk, conv3_b, bn2_s, bn2_t;
   DevBuf p_pk, ir_pk, or_pk, vecs;
   DevBuf spec_g;            // MP_DTYPE_F32_FFT: compact split spectral weights of p_r (k_fft.hip)
+  bool fft4 = false;        // the fp32 FFT path runs k_fft4.hip's four-step loop (class-major spec_g)
   DevBuf or_x3, ir_x3;      // MP_DTYPE_F32_FFT: o_r / i_r packed for the f16x3 gate GEMMs
   float or_us = 1.f, ir_us = 1.f;
   DevBuf fc1_pk, fc1_b, bn4_s, bn4_t, fco_pk, fco_b;
