@@ -130,169 +130,181 @@ __device__ __forceinline__ void rk_fwd9(cpx* __restrict__ Z, int b, int n2, int 
 // II: the wave's four 32-pixel segments (s: row 2w + (s >> 1), columns 32 (s & 1) + j), lane (h, j),
 // register r of block n = channel 32 n + 8 (r >> 2) + 4 h + (r & 3) -- k_fft.hip spec_epi_b_kernel's
 // layout and expressions, P read from (and the epilogue's output written back to) the staging.
+// The segment's map loads (A: X, O; B: I, O; INIT: O0) are issued one segment ahead, segment 0's at
+// the kernel's start: with one block per CU nothing else hides their latency.
+struct SegIn {
+  f32x4 a[2][4], o[2][4];
+};
+
+__device__ __forceinline__ bool seg_live(int s, int w, int n2, int H, int W) {
+  return 8 * (2 * w + (s >> 1)) + n2 < H && 32 * (s & 1) < W;
+}
+
 template <int MODE>
-__device__ __forceinline__ void rk_epilogue(const ConvArgs& p, float* stg, int b, int n2, int w, int lane,
-                                            const void* __restrict__ or_x3, float or_us,
-                                            const void* __restrict__ ir_x3, float ir_us,
-                                            const float* __restrict__ O0) {
+__device__ __forceinline__ void rk_load_seg(const ConvArgs& p, const float* __restrict__ O0, int b, int n2, int w,
+                                            int lane, int s, SegIn& L) {
+  const int H = p.H, W = p.W;
+  if (!seg_live(s, w, n2, H, W)) return;   // wave-uniform
+  const int h = lane >> 5, x = 32 * (s & 1) + (lane & 31), y = 8 * (2 * w + (s >> 1)) + n2;
+#pragma unroll
+  for (int n = 0; n < 2; ++n)
+#pragma unroll
+    for (int g = 0; g < 4; ++g) {
+      if constexpr (MODE == ROW_INIT) {
+        L.a[n][g] = *reinterpret_cast<const f32x4*>(O0 + (((size_t)b * H + y) * W + x) * C + 32 * n + 8 * g + 4 * h);
+      } else {
+        L.a[n][g] = MODE == ROW_A ? map_ld4<false>(p.X, xx_index(b, 4 * n + g, y, x, 4 * h, H, W))
+                                  : map_ld4<false>(p.I, ii_index(b, 4 * n + g, y, x, 4 * h, H, W));
+        L.o[n][g] = map_ld4<false>(p.O, oo_index(b, 4 * n + g, y, x, 4 * h, H, W));
+      }
+    }
+}
+
+template <int MODE>
+__device__ __forceinline__ void rk_segment(const ConvArgs& p, float* stg, int b, int n2, int w, int lane, int s,
+                                           const SegIn& L, const void* __restrict__ or_x3, float or_us,
+                                           const void* __restrict__ ir_x3, float ir_us) {
   const int h = lane >> 5, j = lane & 31, H = p.H, W = p.W;
-#pragma unroll 1
-  for (int s = 0; s < 4; ++s) {
-    const int r = s >> 1, xs = 32 * (s & 1), y = 8 * (2 * w + r) + n2;
-    if (y >= H || xs >= W) continue;   // wave-uniform
-    const int x = xs + j, px = r * 64 + x;
-    float* sp = stg + px * RK_SP;
-    if constexpr (MODE == ROW_A) {
-      // hgru_module.py:797-799: I = tanh(X - (beta O + nu) (P1 + lateral_bias))
-      f32x4 xv[2][4], ov[2][4];
+  if (!seg_live(s, w, n2, H, W)) return;   // wave-uniform
+  const int r = s >> 1, xs = 32 * (s & 1), y = 8 * (2 * w + r) + n2;
+  const int x = xs + j, px = r * 64 + x;
+  float* sp = stg + px * RK_SP;
+  if constexpr (MODE == ROW_A) {
+    // hgru_module.py:797-799: I = tanh(X - (beta O + nu) (P1 + lateral_bias))
 #pragma unroll
-      for (int n = 0; n < 2; ++n)
+    for (int n = 0; n < 2; ++n)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          xv[n][g] = map_ld4<false>(p.X, xx_index(b, 4 * n + g, y, x, 4 * h, H, W));
-          ov[n][g] = map_ld4<false>(p.O, oo_index(b, 4 * n + g, y, x, 4 * h, H, W));
+      for (int g = 0; g < 4; ++g) {
+        const int c = 32 * n + 8 * g + 4 * h;
+        const f32x4 pv = *reinterpret_cast<const f32x4*>(sp + c);
+        const f32x4 lat = *reinterpret_cast<const f32x4*>(p.vecs + V_LAT * 64 + c);
+        const f32x4 be = *reinterpret_cast<const f32x4*>(p.vecs + V_BETA * 64 + c);
+        const f32x4 nu = *reinterpret_cast<const f32x4*>(p.vecs + V_NU * 64 + c);
+        f32x4 iv;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) iv[e] = atanh_f(epi_a(L.a[n][g][e], L.o[n][g][e], pv[e], be[e], nu[e], lat[e]));
+        map_st4<false>(p.dst, ii_index(b, 4 * n + g, y, x, 4 * h, H, W), iv);
+        *reinterpret_cast<f32x4*>(sp + c) = iv;
+      }
+  } else if constexpr (MODE == ROW_INIT) {
+    // hgru_module.py:696-711 on O0 (NHWC): O = O0, Og = O0 * sigmoid(O0 . i_r + i_b)
+    f32x16 V[2], Y[2];
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int g = 0; g < 4; ++g)
+#pragma unroll
+        for (int e = 0; e < 4; ++e) V[n][4 * g + e] = L.a[n][g][e];
+    gate_x3(static_cast<const f16x8*>(ir_x3), V, Y, lane, ir_us);
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int c = 32 * n + 8 * g + 4 * h;
+        const f32x4 ib = *reinterpret_cast<const f32x4*>(p.vecs + V_IB * 64 + c);
+        f32x4 o, og;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          o[e] = V[n][4 * g + e];
+          og[e] = o[e] * fsigmoid(Y[n][4 * g + e] + ib[e]);
         }
+        map_st4<false>(p.dst, oo_index(b, 4 * n + g, y, x, 4 * h, H, W), o);
+        *reinterpret_cast<f32x4*>(sp + c) = og;
+      }
+  } else {
+    // hgru_module.py:729-740, 806-849: g2 = sigmoid(I . o_r + o_b); e = gamma (P2 + lat);
+    // O' = (g2 O + (1 - g2) tanh(kappa (I + e) + omega (I e))) rho[t];  then Og' = O' sigmoid(O' . i_r + i_b)
+    f32x16 Iv[2], Y[2];
 #pragma unroll
-      for (int n = 0; n < 2; ++n)
+    for (int n = 0; n < 2; ++n)
 #pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int c = 32 * n + 8 * g + 4 * h;
-          const f32x4 pv = *reinterpret_cast<const f32x4*>(sp + c);
-          const f32x4 lat = *reinterpret_cast<const f32x4*>(p.vecs + V_LAT * 64 + c);
-          const f32x4 be = *reinterpret_cast<const f32x4*>(p.vecs + V_BETA * 64 + c);
-          const f32x4 nu = *reinterpret_cast<const f32x4*>(p.vecs + V_NU * 64 + c);
-          f32x4 iv;
+      for (int g = 0; g < 4; ++g)
 #pragma unroll
-          for (int e = 0; e < 4; ++e) iv[e] = atanh_f(epi_a(xv[n][g][e], ov[n][g][e], pv[e], be[e], nu[e], lat[e]));
-          map_st4<false>(p.dst, ii_index(b, 4 * n + g, y, x, 4 * h, H, W), iv);
-          *reinterpret_cast<f32x4*>(sp + c) = iv;
+        for (int e = 0; e < 4; ++e) Iv[n][4 * g + e] = L.a[n][g][e];
+    gate_x3(static_cast<const f16x8*>(or_x3), Iv, Y, lane, or_us);
+#pragma unroll
+    for (int n = 0; n < 2; ++n)
+#pragma unroll
+      for (int g = 0; g < 4; ++g) {
+        const int c = 32 * n + 8 * g + 4 * h;
+        const f32x4 pv = *reinterpret_cast<const f32x4*>(sp + c);
+        const f32x4 ov = L.o[n][g];
+        const f32x4 lat = *reinterpret_cast<const f32x4*>(p.vecs + V_LAT * 64 + c);
+        const f32x4 ga = *reinterpret_cast<const f32x4*>(p.vecs + V_GAMMA * 64 + c);
+        const f32x4 ka = *reinterpret_cast<const f32x4*>(p.vecs + V_KAPPA * 64 + c);
+        const f32x4 om = *reinterpret_cast<const f32x4*>(p.vecs + V_OMEGA * 64 + c);
+        const f32x4 ob = *reinterpret_cast<const f32x4*>(p.vecs + V_OB * 64 + c);
+        f32x4 o;
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const int rr = 4 * g + e;
+          const float g2 = fsigmoid(Y[n][rr] + ob[e]);
+          const float iv = Iv[n][rr];
+          const float ee = ga[e] * (pv[e] + lat[e]);
+          const float S = ftanh(ka[e] * (iv + ee) + om[e] * (iv * ee));
+          const float on = (g2 * ov[e] + (1.f - g2) * S) * p.rho;
+          o[e] = on;
+          Iv[n][rr] = on;
         }
-    } else if constexpr (MODE == ROW_INIT) {
-      // hgru_module.py:696-711 on O0 (NHWC): O = O0, Og = O0 * sigmoid(O0 . i_r + i_b)
-      f32x16 V[2], Y[2];
-      const float* src = O0 + (((size_t)b * H + y) * W + x) * C;
-#pragma unroll
-      for (int n = 0; n < 2; ++n)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const f32x4 v = *reinterpret_cast<const f32x4*>(src + 32 * n + 8 * g + 4 * h);
-#pragma unroll
-          for (int e = 0; e < 4; ++e) V[n][4 * g + e] = v[e];
-        }
-      gate_x3(static_cast<const f16x8*>(ir_x3), V, Y, lane, ir_us);
+        map_st4<false>(p.dst, oo_index(b, 4 * n + g, y, x, 4 * h, H, W), o);
+      }
+    f32x16 (&Ov)[2] = Iv;
+    if constexpr (MODE == ROW_B) {
+      gate_x3(static_cast<const f16x8*>(ir_x3), Ov, Y, lane, ir_us);
 #pragma unroll
       for (int n = 0; n < 2; ++n)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int c = 32 * n + 8 * g + 4 * h;
           const f32x4 ib = *reinterpret_cast<const f32x4*>(p.vecs + V_IB * 64 + c);
-          f32x4 o, og;
+          f32x4 o;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            o[e] = V[n][4 * g + e];
-            og[e] = o[e] * fsigmoid(Y[n][4 * g + e] + ib[e]);
-          }
-          map_st4<false>(p.dst, oo_index(b, 4 * n + g, y, x, 4 * h, H, W), o);
-          *reinterpret_cast<f32x4*>(sp + c) = og;
+          for (int e = 0; e < 4; ++e) o[e] = Ov[n][4 * g + e] * fsigmoid(Y[n][4 * g + e] + ib[e]);
+          *reinterpret_cast<f32x4*>(sp + c) = o;
         }
     } else {
-      // hgru_module.py:729-740, 806-849: g2 = sigmoid(I . o_r + o_b); e = gamma (P2 + lat);
-      // O' = (g2 O + (1 - g2) tanh(kappa (I + e) + omega (I e))) rho[t];  then Og' = O' sigmoid(O' . i_r + i_b)
-      f32x16 Iv[2], Y[2];
-#pragma unroll
-      for (int n = 0; n < 2; ++n)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const f32x4 iv = map_ld4<false>(p.I, ii_index(b, 4 * n + g, y, x, 4 * h, H, W));
-#pragma unroll
-          for (int e = 0; e < 4; ++e) Iv[n][4 * g + e] = iv[e];
-        }
-      gate_x3(static_cast<const f16x8*>(or_x3), Iv, Y, lane, or_us);
+      // ROW_FINAL: BN_3(O_T) (hgru_pose.py:82-90) as the NHWC fp32 map fc_1 flattens (mode 1) or as
+      // fc_1's f16 hi / lo planes (mode 2); the segment's 32 pixels x 64 channels are one contiguous
+      // 8 KiB run of the output, staged here and stored with contiguous lanes
 #pragma unroll
       for (int n = 0; n < 2; ++n)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int c = 32 * n + 8 * g + 4 * h;
-          const f32x4 pv = *reinterpret_cast<const f32x4*>(sp + c);
-          const size_t odx = oo_index(b, 4 * n + g, y, x, 4 * h, H, W);
-          const f32x4 ov = map_ld4<false>(p.O, odx);
-          const f32x4 lat = *reinterpret_cast<const f32x4*>(p.vecs + V_LAT * 64 + c);
-          const f32x4 ga = *reinterpret_cast<const f32x4*>(p.vecs + V_GAMMA * 64 + c);
-          const f32x4 ka = *reinterpret_cast<const f32x4*>(p.vecs + V_KAPPA * 64 + c);
-          const f32x4 om = *reinterpret_cast<const f32x4*>(p.vecs + V_OMEGA * 64 + c);
-          const f32x4 ob = *reinterpret_cast<const f32x4*>(p.vecs + V_OB * 64 + c);
+          const f32x4 ss = *reinterpret_cast<const f32x4*>(p.vecs + V_OUTS * 64 + c);
+          const f32x4 tt = *reinterpret_cast<const f32x4*>(p.vecs + V_OUTT * 64 + c);
           f32x4 o;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) {
-            const int rr = 4 * g + e;
-            const float g2 = fsigmoid(Y[n][rr] + ob[e]);
-            const float iv = Iv[n][rr];
-            const float ee = ga[e] * (pv[e] + lat[e]);
-            const float S = ftanh(ka[e] * (iv + ee) + om[e] * (iv * ee));
-            const float on = (g2 * ov[e] + (1.f - g2) * S) * p.rho;
-            o[e] = on;
-            Iv[n][rr] = on;
-          }
-          map_st4<false>(p.dst, odx, o);
+          for (int e = 0; e < 4; ++e) o[e] = Ov[n][4 * g + e] * ss[e] + tt[e];
+          *reinterpret_cast<f32x4*>(sp + c) = o;
         }
-      f32x16 (&Ov)[2] = Iv;
-      if constexpr (MODE == ROW_B) {
-        gate_x3(static_cast<const f16x8*>(ir_x3), Ov, Y, lane, ir_us);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      const float* run = stg + (r * 64 + xs) * RK_SP;
+      const size_t e0 = (((size_t)b * H + y) * W + xs) * C;
+      if (p.mode != 2) {
 #pragma unroll
-        for (int n = 0; n < 2; ++n)
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const int c = 32 * n + 8 * g + 4 * h;
-            const f32x4 ib = *reinterpret_cast<const f32x4*>(p.vecs + V_IB * 64 + c);
-            f32x4 o;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) o[e] = Ov[n][4 * g + e] * fsigmoid(Y[n][4 * g + e] + ib[e]);
-            *reinterpret_cast<f32x4*>(sp + c) = o;
-          }
-      } else {
-        // ROW_FINAL: BN_3(O_T) (hgru_pose.py:82-90) as the NHWC fp32 map fc_1 flattens (mode 1) or as
-        // fc_1's f16 hi / lo planes (mode 2); the segment's 32 pixels x 64 channels are one contiguous
-        // 8 KiB run of the output, staged here and stored with contiguous lanes
-#pragma unroll
-        for (int n = 0; n < 2; ++n)
-#pragma unroll
-          for (int g = 0; g < 4; ++g) {
-            const int c = 32 * n + 8 * g + 4 * h;
-            const f32x4 ss = *reinterpret_cast<const f32x4*>(p.vecs + V_OUTS * 64 + c);
-            const f32x4 tt = *reinterpret_cast<const f32x4*>(p.vecs + V_OUTT * 64 + c);
-            f32x4 o;
-#pragma unroll
-            for (int e = 0; e < 4; ++e) o[e] = Ov[n][4 * g + e] * ss[e] + tt[e];
-            *reinterpret_cast<f32x4*>(sp + c) = o;
-          }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-        const float* run = stg + (r * 64 + xs) * RK_SP;
-        const size_t e0 = (((size_t)b * H + y) * W + xs) * C;
-        if (p.mode != 2) {
-#pragma unroll
-          for (int k = 0; k < 8; ++k) {   // 8 x 1 KiB
-            const int q = k * 64 + lane, pp = q >> 4, c4 = (q & 15) * 4;
-            *reinterpret_cast<f32x4*>(p.dst2 + e0 + pp * C + c4) = *reinterpret_cast<const f32x4*>(run + pp * RK_SP + c4);
-          }
-        } else {   // fc_1's split planes, split exactly as fc_gemm_x3_kernel splits (k_fc.hip)
-#pragma unroll
-          for (int k = 0; k < 4; ++k) {
-            const int q = k * 64 + lane, pp = q >> 3, c8 = (q & 7) * 8;
-            const f32x4 a = *reinterpret_cast<const f32x4*>(run + pp * RK_SP + c8);
-            const f32x4 bq = *reinterpret_cast<const f32x4*>(run + pp * RK_SP + c8 + 4);
-            f16x8 hv, lv;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              const float v = e < 4 ? a[e] : bq[e - 4];
-              hv[e] = (_Float16)v;
-              lv[e] = (_Float16)(v - (float)hv[e]);
-            }
-            *reinterpret_cast<f16x8*>(reinterpret_cast<_Float16*>(p.dst2) + e0 + pp * C + c8) = hv;
-            if (p.dst3) *reinterpret_cast<f16x8*>(reinterpret_cast<_Float16*>(p.dst3) + e0 + pp * C + c8) = lv;
-          }
+        for (int k = 0; k < 8; ++k) {   // 8 x 1 KiB
+          const int q = k * 64 + lane, pp = q >> 4, c4 = (q & 15) * 4;
+          *reinterpret_cast<f32x4*>(p.dst2 + e0 + pp * C + c4) = *reinterpret_cast<const f32x4*>(run + pp * RK_SP + c4);
         }
-        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      } else {   // fc_1's split planes, split exactly as fc_gemm_x3_kernel splits (k_fc.hip)
+#pragma unroll
+        for (int k = 0; k < 4; ++k) {
+          const int q = k * 64 + lane, pp = q >> 3, c8 = (q & 7) * 8;
+          const f32x4 a = *reinterpret_cast<const f32x4*>(run + pp * RK_SP + c8);
+          const f32x4 bq = *reinterpret_cast<const f32x4*>(run + pp * RK_SP + c8 + 4);
+          f16x8 hv, lv;
+#pragma unroll
+          for (int e = 0; e < 8; ++e) {
+            const float v = e < 4 ? a[e] : bq[e - 4];
+            hv[e] = (_Float16)v;
+            lv[e] = (_Float16)(v - (float)hv[e]);
+          }
+          *reinterpret_cast<f16x8*>(reinterpret_cast<_Float16*>(p.dst2) + e0 + pp * C + c8) = hv;
+          if (p.dst3) *reinterpret_cast<f16x8*>(reinterpret_cast<_Float16*>(p.dst3) + e0 + pp * C + c8) = lv;
+        }
       }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     }
   }
 }
@@ -307,6 +319,8 @@ __global__ __launch_bounds__(RK_NT, 1) void row_kernel(cpx* __restrict__ Z, Conv
   float* stg = reinterpret_cast<float*>(T + (2 * w) * FX * 64);   // the wave's own two rows of T
   const int H = p.H, W = p.W;
   const bool la = 8 * (2 * w) + n2 < H, lb = 8 * (2 * w + 1) + n2 < H;
+  SegIn L0, L1;
+  rk_load_seg<MODE>(p, O0, b, n2, w, lane, 0, L0);
   if constexpr (MODE != ROW_INIT) {
     rk_inv9(Z, b, n2, tid, T);
     lds_barrier();
@@ -324,7 +338,11 @@ __global__ __launch_bounds__(RK_NT, 1) void row_kernel(cpx* __restrict__ Z, Conv
     }
   }
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  rk_epilogue<MODE>(p, stg, b, n2, w, lane, or_x3, or_us, ir_x3, ir_us, O0);
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    if (s + 1 < 4) rk_load_seg<MODE>(p, O0, b, n2, w, lane, s + 1, (s & 1) ? L0 : L1);
+    rk_segment<MODE>(p, stg, b, n2, w, lane, s, (s & 1) ? L1 : L0, or_x3, or_us, ir_x3, ir_us);
+  }
   if constexpr (MODE == ROW_FINAL) return;
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   rk_fwd_row(T, stg, w, lane, la, lb, W);
@@ -333,24 +351,31 @@ __global__ __launch_bounds__(RK_NT, 1) void row_kernel(cpx* __restrict__ Z, Conv
 }
 
 // ---------------------------------------------------------------------------------------------
-// column kernel (the spectral GEMM).  Block = (column class (fx, k1), 32 images), 512 threads; wave
-// k2 computes frequency fy = k1 + 9 k2:  Y[b][co] = sum_ci S[b][ci] G[ci][co]  (complex), as
-// k_fft.hip spec_gemm_kernel does for one frequency (f16x3 A/B fragments, the same k order).
-// Before it, thread (image, channel group) turns its 8 row-class partials Z[b][n2][fx][k1][4 ch]
-// into the 8 frequencies (twiddle, 8-point DFT, scale + f16 split into the S tile); after it, the
-// same thread takes the 8 frequencies back to row-class partials (8-point inverse DFT, twiddle) and
-// writes them over its inputs.  Blocks of one class run on one XCD (weights fetched once).
+// column kernel (the spectral GEMM).  Block = (column class (fx, k1), 16 images), 256 threads, two
+// blocks per CU (68 KB of LDS).  Thread (image, channel group) turns its 8 row-class partials
+// Z[b][n2][fx][k1][4 ch] into the class's 8 frequencies (twiddle, 8-point DFT, scale + f16 split
+// into the S tile); wave w then computes frequency fy = k1 + 9 k2 for k2 = w and k2 = w + 4:
+//   Y[b][co] = sum_ci S[b][ci] G[ci][co]  (complex)
+// as k_fft.hip spec_gemm_kernel does for one frequency (f16x3 A / B fragments, the same k order; the
+// 16 MFMA columns past the block's images are zero); the first frequency's Y goes into the S tile
+// half it no longer needs while the second is computed.  Finally the same thread takes the 8
+// frequencies back to row-class partials (8-point inverse DFT, twiddle) and writes them over its
+// inputs.  Blocks of one class run on one XCD (its 256 KiB of weights fetched from HBM once).
 // ---------------------------------------------------------------------------------------------
-constexpr int CG_NI = 32;
-constexpr int CG_SLD = CG_NI + 1;                    // S tile pitch (16-B units) per (cq, part, k2) row
-constexpr int CG_YLD = 16 * 8 * 2 + 1;               // Y tile pitch (16-B units) per image
-constexpr int CG_TILE = 16 * 2 * 8 * CG_SLD;         // 135,168 B
-static_assert(CG_NI * CG_YLD <= CG_TILE, "the Y tile fits the S tile's space");
+constexpr int CG_NI = 16;                            // images per block
+constexpr int CG_SLD = CG_NI + 1;                    // S tile pitch (16-B units) per (cq, part, k2 % 4) row
+constexpr int CG_HALF = 16 * 2 * 4 * CG_SLD;         // one frequency half of the S tile: 34,816 B
+constexpr int CG_YLD = 16 * 4 * 2 + 1;               // Y tile pitch (16-B units) per image, one half
+static_assert(CG_NI * CG_YLD <= CG_HALF, "a half's Y tile fits the S tile half it replaces");
 constexpr int CG_NC8 = (Z_CLS + 7) / 8;              // 42 groups of 8 classes (one per XCD)
 
-__global__ __launch_bounds__(512, 1) void col_gemm_kernel(cpx* __restrict__ Z, const uint4* __restrict__ Gc, int B,
+__device__ __forceinline__ int cg_s(int k2, int cq, int part, int bl) {   // S tile index (16-B units)
+  return (k2 >> 2) * CG_HALF + ((cq * 2 + part) * 4 + (k2 & 3)) * CG_SLD + bl;
+}
+
+__global__ __launch_bounds__(256, 2) void col_gemm_kernel(cpx* __restrict__ Z, const uint4* __restrict__ Gc, int B,
                                                           int ngrp, float unscale) {
-  __shared__ uint4 tile[CG_TILE];
+  __shared__ uint4 tile[2 * CG_HALF];   // 69,632 B
   const int c8 = blockIdx.x / (8 * ngrp), rem = blockIdx.x - c8 * 8 * ngrp;
   const int grp = rem >> 3, cls = c8 * 8 + (rem & 7);
   if (cls >= Z_CLS) return;
@@ -368,16 +393,20 @@ __global__ __launch_bounds__(512, 1) void col_gemm_kernel(cpx* __restrict__ Z, c
     zin[n2][0] = src[0];
     zin[n2][1] = src[1];
   }
-  // ---- weights of frequency (fx, k1 + 9 wv): class-major pack, 32 KiB, issued before the tile wait ----
-  const uint4* gw = Gc + (size_t)(cls * 8 + wv) * 2 * 16 * 64;
-  uint4 wr[8][2][2];
+  // ---- weights of one frequency (fx, k1 + 9 k2): class-major pack, 32 KiB, in two batches of 4
+  // k-steps (64 VGPRs each; the per-output k order is unchanged) ----
+  constexpr int TW = 4;
+  uint4 wr[TW][2][2];
+  auto load_w = [&](int k2, int t0) {
+    const uint4* gw = Gc + (size_t)(cls * 8 + k2) * 2 * 16 * 64;
 #pragma unroll
-  for (int t = 0; t < 8; ++t)
+    for (int t = 0; t < TW; ++t)
 #pragma unroll
-    for (int cb = 0; cb < 2; ++cb) {
-      wr[t][cb][0] = gw[(0 * 16 + 2 * t + h) * 64 + 32 * cb + j];
-      wr[t][cb][1] = gw[(1 * 16 + 2 * t + h) * 64 + 32 * cb + j];
-    }
+      for (int cb = 0; cb < 2; ++cb) {
+        wr[t][cb][0] = gw[(0 * 16 + 2 * (t0 + t) + h) * 64 + 32 * cb + j];
+        wr[t][cb][1] = gw[(1 * 16 + 2 * (t0 + t) + h) * 64 + 32 * cb + j];
+      }
+  };
   // ---- twiddle W72^{n2 k1}, 8-point DFT over n2 -> k2; scale and split into the S tile ----
   {
     cpx s[4][8];
@@ -402,54 +431,67 @@ __global__ __launch_bounds__(512, 1) void col_gemm_kernel(cpx* __restrict__ Z, c
         lv[2 * e] = (_Float16)(re - (float)hr);
         lv[2 * e + 1] = (_Float16)(im - (float)hm);
       }
-      tile[((cq * 2 + 0) * 8 + k2) * CG_SLD + bl] = live ? __builtin_bit_cast(uint4, hv) : uint4{0, 0, 0, 0};
-      tile[((cq * 2 + 1) * 8 + k2) * CG_SLD + bl] = live ? __builtin_bit_cast(uint4, lv) : uint4{0, 0, 0, 0};
+      tile[cg_s(k2, cq, 0, bl)] = live ? __builtin_bit_cast(uint4, hv) : uint4{0, 0, 0, 0};
+      tile[cg_s(k2, cq, 1, bl)] = live ? __builtin_bit_cast(uint4, lv) : uint4{0, 0, 0, 0};
     }
   }
+  load_w(wv, 0);   // after the partials are consumed (register budget), in flight across the tile barrier
   lds_barrier();
-  // ---- the 128 x 32 x 128 real product of frequency k2 = wv (spec_gemm_kernel's fragments) ----
-  f32x16 acc[4] = {};
   const uint4 m = {0x80000000u, 0x80000000u, 0x80000000u, 0x80000000u};
+  // MFMA columns j >= 16 duplicate images j - 16: the columns of an MFMA are independent, and those
+  // outputs are never written
+  const int jj = j & (CG_NI - 1);
 #pragma unroll
-  for (int t = 0; t < 8; ++t) {
-    const int cqq = 2 * t + h;
-    const f16x8 sh = __builtin_bit_cast(f16x8, tile[((cqq * 2 + 0) * 8 + wv) * CG_SLD + j]);
-    const f16x8 sl = __builtin_bit_cast(f16x8, tile[((cqq * 2 + 1) * 8 + wv) * CG_SLD + j]);
+  for (int half = 0; half < 2; ++half) {
+    const int k2 = wv + 4 * half;
+    if (half) load_w(k2, 0);
+    // ---- the 128 x 32 x 128 real product of frequency k2 (spec_gemm_kernel's fragments) ----
+    f32x16 acc[4] = {};
 #pragma unroll
-    for (int cb = 0; cb < 2; ++cb) {
-      const uint4 gh = wr[t][cb][0], gl = wr[t][cb][1];
-      const f16x8 ah0 = __builtin_bit_cast(f16x8, gh ^ m), al0 = __builtin_bit_cast(f16x8, gl ^ m);
-      const f16x8 ah1 = __builtin_bit_cast(f16x8, (gh >> 16) | (gh << 16));
-      const f16x8 al1 = __builtin_bit_cast(f16x8, (gl >> 16) | (gl << 16));
-      acc[cb] = mfma16(al0, sh, acc[cb]);
-      acc[cb] = mfma16(ah0, sl, acc[cb]);
-      acc[cb] = mfma16(ah0, sh, acc[cb]);
-      acc[2 + cb] = mfma16(al1, sh, acc[2 + cb]);
-      acc[2 + cb] = mfma16(ah1, sl, acc[2 + cb]);
-      acc[2 + cb] = mfma16(ah1, sh, acc[2 + cb]);
+    for (int t = 0; t < 8; ++t) {
+      if (t == TW) load_w(k2, TW);
+      const int cqq = 2 * t + h;
+      const f16x8 sh = __builtin_bit_cast(f16x8, tile[cg_s(k2, cqq, 0, jj)]);
+      const f16x8 sl = __builtin_bit_cast(f16x8, tile[cg_s(k2, cqq, 1, jj)]);
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb) {
+        const uint4 gh = wr[t % TW][cb][0], gl = wr[t % TW][cb][1];
+        const f16x8 ah0 = __builtin_bit_cast(f16x8, gh ^ m), al0 = __builtin_bit_cast(f16x8, gl ^ m);
+        const f16x8 ah1 = __builtin_bit_cast(f16x8, (gh >> 16) | (gh << 16));
+        const f16x8 al1 = __builtin_bit_cast(f16x8, (gl >> 16) | (gl << 16));
+        acc[cb] = mfma16(al0, sh, acc[cb]);
+        acc[cb] = mfma16(ah0, sl, acc[cb]);
+        acc[cb] = mfma16(ah0, sh, acc[cb]);
+        acc[2 + cb] = mfma16(al1, sh, acc[2 + cb]);
+        acc[2 + cb] = mfma16(ah1, sl, acc[2 + cb]);
+        acc[2 + cb] = mfma16(ah1, sh, acc[2 + cb]);
+      }
+    }
+    lds_barrier();   // every wave has read this half of the S tile
+    // ---- Y of the half: [image][cq][k2 % 4] over its S (lo: channels 0, 1 of the group; hi: 2, 3) ----
+    f32x4* ytile = reinterpret_cast<f32x4*>(tile + half * CG_HALF);
+    if (j < CG_NI) {
+#pragma unroll
+      for (int cb = 0; cb < 2; ++cb)
+#pragma unroll
+        for (int g = 0; g < 4; ++g) {
+          const int cqo = 8 * cb + 2 * g + h;
+          const f32x16& re = acc[cb];
+          const f32x16& im = acc[2 + cb];
+          ytile[j * CG_YLD + (cqo * 4 + wv) * 2] = f32x4{re[4 * g], im[4 * g], re[4 * g + 1], im[4 * g + 1]} * unscale;
+          ytile[j * CG_YLD + (cqo * 4 + wv) * 2 + 1] =
+              f32x4{re[4 * g + 2], im[4 * g + 2], re[4 * g + 3], im[4 * g + 3]} * unscale;
+        }
     }
   }
-  lds_barrier();   // every wave has read the S tile
-  // ---- Y tile [image][cq][k2] (lo: channels 0, 1 of the group; hi: 2, 3) ----
-  f32x4* ytile = reinterpret_cast<f32x4*>(tile);
-#pragma unroll
-  for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-    for (int g = 0; g < 4; ++g) {
-      const int cqo = 8 * cb + 2 * g + h;
-      const f32x16& re = acc[cb];
-      const f32x16& im = acc[2 + cb];
-      ytile[j * CG_YLD + (cqo * 8 + wv) * 2] = f32x4{re[4 * g], im[4 * g], re[4 * g + 1], im[4 * g + 1]} * unscale;
-      ytile[j * CG_YLD + (cqo * 8 + wv) * 2 + 1] =
-          f32x4{re[4 * g + 2], im[4 * g + 2], re[4 * g + 3], im[4 * g + 3]} * unscale;
-    }
   lds_barrier();
   // ---- 8-point inverse DFT over k2 -> n2, twiddle W72^{-n2 k1}, written over the inputs ----
   cpx yv[4][8];
 #pragma unroll
   for (int k2 = 0; k2 < 8; ++k2) {
-    const f32x4 lo = ytile[bl * CG_YLD + (cq * 8 + k2) * 2];
-    const f32x4 hi = ytile[bl * CG_YLD + (cq * 8 + k2) * 2 + 1];
+    const f32x4* yt = reinterpret_cast<const f32x4*>(tile + (k2 >> 2) * CG_HALF);
+    const f32x4 lo = yt[bl * CG_YLD + (cq * 4 + (k2 & 3)) * 2];
+    const f32x4 hi = yt[bl * CG_YLD + (cq * 4 + (k2 & 3)) * 2 + 1];
     yv[0][k2] = cpx{lo[0], lo[1]};
     yv[1][k2] = cpx{lo[2], lo[3]};
     yv[2][k2] = cpx{hi[0], hi[1]};
@@ -483,7 +525,7 @@ bool fft4_enabled() {
 hipError_t launch_col_gemm(void* Z, const void* Gc, int B, float unscale, hipStream_t st) {
   if (B <= 0) return hipSuccess;
   const int ngrp = (B + CG_NI - 1) / CG_NI;
-  hipLaunchKernelGGL(col_gemm_kernel, dim3(CG_NC8 * 8 * ngrp), dim3(512), 0, st, static_cast<cpx*>(Z),
+  hipLaunchKernelGGL(col_gemm_kernel, dim3(CG_NC8 * 8 * ngrp), dim3(256), 0, st, static_cast<cpx*>(Z),
                      static_cast<const uint4*>(Gc), B, ngrp, unscale);
   return hipGetLastError();
 }

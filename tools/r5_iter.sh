@@ -1,0 +1,12 @@
+#!/bin/bash
+# one iteration on the box: four-step loop check + timing + per-kernel profile, then the parity suite
+#   usage: bash tools/r5_iter.sh <tag> [pytest files...]
+set -o pipefail
+out=gpurun_out/$1
+shift
+mkdir -p "$out"
+timeout -k 10 300 python tools/fft4_check.py > "$out/fft4_check.log" 2>&1 || exit 1
+if [ $# -gt 0 ]; then
+  timeout -k 10 600 python -u -m pytest -x -v --timeout 120 --timeout-method thread "$@" > "$out/gpu_tests.log" 2>&1 || exit 1
+fi
+echo done > "$out/DONE"
