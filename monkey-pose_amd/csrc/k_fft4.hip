@@ -127,6 +127,19 @@ __device__ __forceinline__ void rk_fwd9(cpx* __restrict__ Z, int b, int n2, int 
   }
 }
 
+// a value the compiler cannot see through: index math re-derived from it in a later phase is not
+// CSE'd with an earlier phase's (which would hold 64-bit item addresses live across the whole kernel),
+// and loads through a pointer passed through it are not hoisted out of their loop
+__device__ __forceinline__ int opaque(int v) {
+  asm volatile("" : "+v"(v));
+  return v;
+}
+template <typename P>
+__device__ __forceinline__ P* opaque_ptr(P* p) {
+  asm volatile("" : "+s"(p));
+  return p;
+}
+
 // II: the wave's four 32-pixel segments (s: row 2w + (s >> 1), columns 32 (s & 1) + j), lane (h, j),
 // register r of block n = channel 32 n + 8 (r >> 2) + 4 h + (r & 3) -- k_fft.hip spec_epi_b_kernel's
 // layout and expressions, P read from (and the epilogue's output written back to) the staging.
@@ -140,12 +153,12 @@ __device__ __forceinline__ bool seg_live(int s, int w, int n2, int H, int W) {
   return 8 * (2 * w + (s >> 1)) + n2 < H && 32 * (s & 1) < W;
 }
 
+// the segment at map row y, columns xs .. xs + 31 (lane (h, j): pixel xs + j)
 template <int MODE>
-__device__ __forceinline__ void rk_load_seg(const ConvArgs& p, const float* __restrict__ O0, int b, int n2, int w,
-                                            int lane, int s, SegIn& L) {
+__device__ __forceinline__ void rk_load_seg(const ConvArgs& p, const float* __restrict__ O0, int b, int y, int xs,
+                                            int lane, SegIn& L) {
   const int H = p.H, W = p.W;
-  if (!seg_live(s, w, n2, H, W)) return;   // wave-uniform
-  const int h = lane >> 5, x = 32 * (s & 1) + (lane & 31), y = 8 * (2 * w + (s >> 1)) + n2;
+  const int h = lane >> 5, x = xs + (lane & 31);
 #pragma unroll
   for (int n = 0; n < 2; ++n)
 #pragma unroll
@@ -155,20 +168,26 @@ __device__ __forceinline__ void rk_load_seg(const ConvArgs& p, const float* __re
       } else {
         L.a[n][g] = MODE == ROW_A ? map_ld4<false>(p.X, xx_index(b, 4 * n + g, y, x, 4 * h, H, W))
                                   : map_ld4<false>(p.I, ii_index(b, 4 * n + g, y, x, 4 * h, H, W));
-        L.o[n][g] = map_ld4<false>(p.O, oo_index(b, 4 * n + g, y, x, 4 * h, H, W));
+        // B: O is loaded by rk_segment after the o_r gate (64 fewer live registers across it)
+        if constexpr (MODE == ROW_A) L.o[n][g] = map_ld4<false>(p.O, oo_index(b, 4 * n + g, y, x, 4 * h, H, W));
       }
     }
 }
 
-template <int MODE>
-__device__ __forceinline__ void rk_segment(const ConvArgs& p, float* stg, int b, int n2, int w, int lane, int s,
+// seg: the segment's 32 staged pixels (pitch RK_SP floats); the output goes back over the input
+// LEAN: a scheduling fence after every 4-channel group, so the compiler does not hoist all eight groups'
+// loads and address math at once (row2_kernel's two-blocks-per-CU register budget)
+template <int MODE, bool LEAN = false>
+__device__ __forceinline__ void rk_segment(const ConvArgs& p, float* seg, int b, int y, int xs, int lane,
                                            const SegIn& L, const void* __restrict__ or_x3, float or_us,
-                                           const void* __restrict__ ir_x3, float ir_us) {
+                                           const void* __restrict__ ir_x3, float ir_us, const float* vec) {
   const int h = lane >> 5, j = lane & 31, H = p.H, W = p.W;
-  if (!seg_live(s, w, n2, H, W)) return;   // wave-uniform
-  const int r = s >> 1, xs = 32 * (s & 1), y = 8 * (2 * w + r) + n2;
-  const int x = xs + j, px = r * 64 + x;
-  float* sp = stg + px * RK_SP;
+  const int x = xs + j;
+  float* sp = seg + j * RK_SP;
+  // LEAN: the gate weights are re-read per segment (L1 / L2 hits) instead of 128 registers held across
+  // the kernel
+  const void* orw = LEAN ? opaque_ptr(or_x3) : or_x3;
+  const void* irw = LEAN ? opaque_ptr(ir_x3) : ir_x3;
   if constexpr (MODE == ROW_A) {
     // hgru_module.py:797-799: I = tanh(X - (beta O + nu) (P1 + lateral_bias))
 #pragma unroll
@@ -177,14 +196,15 @@ __device__ __forceinline__ void rk_segment(const ConvArgs& p, float* stg, int b,
       for (int g = 0; g < 4; ++g) {
         const int c = 32 * n + 8 * g + 4 * h;
         const f32x4 pv = *reinterpret_cast<const f32x4*>(sp + c);
-        const f32x4 lat = *reinterpret_cast<const f32x4*>(p.vecs + V_LAT * 64 + c);
-        const f32x4 be = *reinterpret_cast<const f32x4*>(p.vecs + V_BETA * 64 + c);
-        const f32x4 nu = *reinterpret_cast<const f32x4*>(p.vecs + V_NU * 64 + c);
+        const f32x4 lat = *reinterpret_cast<const f32x4*>(vec + V_LAT * 64 + c);
+        const f32x4 be = *reinterpret_cast<const f32x4*>(vec + V_BETA * 64 + c);
+        const f32x4 nu = *reinterpret_cast<const f32x4*>(vec + V_NU * 64 + c);
         f32x4 iv;
 #pragma unroll
         for (int e = 0; e < 4; ++e) iv[e] = atanh_f(epi_a(L.a[n][g][e], L.o[n][g][e], pv[e], be[e], nu[e], lat[e]));
         map_st4<false>(p.dst, ii_index(b, 4 * n + g, y, x, 4 * h, H, W), iv);
         *reinterpret_cast<f32x4*>(sp + c) = iv;
+        if constexpr (LEAN) __builtin_amdgcn_sched_barrier(0);
       }
   } else if constexpr (MODE == ROW_INIT) {
     // hgru_module.py:696-711 on O0 (NHWC): O = O0, Og = O0 * sigmoid(O0 . i_r + i_b)
@@ -195,13 +215,13 @@ __device__ __forceinline__ void rk_segment(const ConvArgs& p, float* stg, int b,
       for (int g = 0; g < 4; ++g)
 #pragma unroll
         for (int e = 0; e < 4; ++e) V[n][4 * g + e] = L.a[n][g][e];
-    gate_x3(static_cast<const f16x8*>(ir_x3), V, Y, lane, ir_us);
+    gate_x3(static_cast<const f16x8*>(irw), V, Y, lane, ir_us);
 #pragma unroll
     for (int n = 0; n < 2; ++n)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int c = 32 * n + 8 * g + 4 * h;
-        const f32x4 ib = *reinterpret_cast<const f32x4*>(p.vecs + V_IB * 64 + c);
+        const f32x4 ib = *reinterpret_cast<const f32x4*>(vec + V_IB * 64 + c);
         f32x4 o, og;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -210,6 +230,7 @@ __device__ __forceinline__ void rk_segment(const ConvArgs& p, float* stg, int b,
         }
         map_st4<false>(p.dst, oo_index(b, 4 * n + g, y, x, 4 * h, H, W), o);
         *reinterpret_cast<f32x4*>(sp + c) = og;
+        if constexpr (LEAN) __builtin_amdgcn_sched_barrier(0);
       }
   } else {
     // hgru_module.py:729-740, 806-849: g2 = sigmoid(I . o_r + o_b); e = gamma (P2 + lat);
@@ -221,19 +242,19 @@ __device__ __forceinline__ void rk_segment(const ConvArgs& p, float* stg, int b,
       for (int g = 0; g < 4; ++g)
 #pragma unroll
         for (int e = 0; e < 4; ++e) Iv[n][4 * g + e] = L.a[n][g][e];
-    gate_x3(static_cast<const f16x8*>(or_x3), Iv, Y, lane, or_us);
+    gate_x3(static_cast<const f16x8*>(orw), Iv, Y, lane, or_us);
 #pragma unroll
     for (int n = 0; n < 2; ++n)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int c = 32 * n + 8 * g + 4 * h;
         const f32x4 pv = *reinterpret_cast<const f32x4*>(sp + c);
-        const f32x4 ov = L.o[n][g];
-        const f32x4 lat = *reinterpret_cast<const f32x4*>(p.vecs + V_LAT * 64 + c);
-        const f32x4 ga = *reinterpret_cast<const f32x4*>(p.vecs + V_GAMMA * 64 + c);
-        const f32x4 ka = *reinterpret_cast<const f32x4*>(p.vecs + V_KAPPA * 64 + c);
-        const f32x4 om = *reinterpret_cast<const f32x4*>(p.vecs + V_OMEGA * 64 + c);
-        const f32x4 ob = *reinterpret_cast<const f32x4*>(p.vecs + V_OB * 64 + c);
+        const f32x4 ov = map_ld4<false>(p.O, oo_index(b, 4 * n + g, y, x, 4 * h, H, W));
+        const f32x4 lat = *reinterpret_cast<const f32x4*>(vec + V_LAT * 64 + c);
+        const f32x4 ga = *reinterpret_cast<const f32x4*>(vec + V_GAMMA * 64 + c);
+        const f32x4 ka = *reinterpret_cast<const f32x4*>(vec + V_KAPPA * 64 + c);
+        const f32x4 om = *reinterpret_cast<const f32x4*>(vec + V_OMEGA * 64 + c);
+        const f32x4 ob = *reinterpret_cast<const f32x4*>(vec + V_OB * 64 + c);
         f32x4 o;
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -247,20 +268,22 @@ __device__ __forceinline__ void rk_segment(const ConvArgs& p, float* stg, int b,
           Iv[n][rr] = on;
         }
         map_st4<false>(p.dst, oo_index(b, 4 * n + g, y, x, 4 * h, H, W), o);
+        if constexpr (LEAN) __builtin_amdgcn_sched_barrier(0);
       }
     f32x16 (&Ov)[2] = Iv;
     if constexpr (MODE == ROW_B) {
-      gate_x3(static_cast<const f16x8*>(ir_x3), Ov, Y, lane, ir_us);
+      gate_x3(static_cast<const f16x8*>(irw), Ov, Y, lane, ir_us);
 #pragma unroll
       for (int n = 0; n < 2; ++n)
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int c = 32 * n + 8 * g + 4 * h;
-          const f32x4 ib = *reinterpret_cast<const f32x4*>(p.vecs + V_IB * 64 + c);
+          const f32x4 ib = *reinterpret_cast<const f32x4*>(vec + V_IB * 64 + c);
           f32x4 o;
 #pragma unroll
           for (int e = 0; e < 4; ++e) o[e] = Ov[n][4 * g + e] * fsigmoid(Y[n][4 * g + e] + ib[e]);
           *reinterpret_cast<f32x4*>(sp + c) = o;
+          if constexpr (LEAN) __builtin_amdgcn_sched_barrier(0);
         }
     } else {
       // ROW_FINAL: BN_3(O_T) (hgru_pose.py:82-90) as the NHWC fp32 map fc_1 flattens (mode 1) or as
@@ -271,15 +294,15 @@ __device__ __forceinline__ void rk_segment(const ConvArgs& p, float* stg, int b,
 #pragma unroll
         for (int g = 0; g < 4; ++g) {
           const int c = 32 * n + 8 * g + 4 * h;
-          const f32x4 ss = *reinterpret_cast<const f32x4*>(p.vecs + V_OUTS * 64 + c);
-          const f32x4 tt = *reinterpret_cast<const f32x4*>(p.vecs + V_OUTT * 64 + c);
+          const f32x4 ss = *reinterpret_cast<const f32x4*>(vec + V_OUTS * 64 + c);
+          const f32x4 tt = *reinterpret_cast<const f32x4*>(vec + V_OUTT * 64 + c);
           f32x4 o;
 #pragma unroll
           for (int e = 0; e < 4; ++e) o[e] = Ov[n][4 * g + e] * ss[e] + tt[e];
           *reinterpret_cast<f32x4*>(sp + c) = o;
         }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      const float* run = stg + (r * 64 + xs) * RK_SP;
+      const float* run = seg;
       const size_t e0 = (((size_t)b * H + y) * W + xs) * C;
       if (p.mode != 2) {
 #pragma unroll
@@ -320,7 +343,7 @@ __global__ __launch_bounds__(RK_NT, 1) void row_kernel(cpx* __restrict__ Z, Conv
   const int H = p.H, W = p.W;
   const bool la = 8 * (2 * w) + n2 < H, lb = 8 * (2 * w + 1) + n2 < H;
   SegIn L0, L1;
-  rk_load_seg<MODE>(p, O0, b, n2, w, lane, 0, L0);
+  if (seg_live(0, w, n2, H, W)) rk_load_seg<MODE>(p, O0, b, 8 * (2 * w) + n2, 0, lane, L0);
   if constexpr (MODE != ROW_INIT) {
     rk_inv9(Z, b, n2, tid, T);
     lds_barrier();
@@ -340,8 +363,11 @@ __global__ __launch_bounds__(RK_NT, 1) void row_kernel(cpx* __restrict__ Z, Conv
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
   for (int s = 0; s < 4; ++s) {
-    if (s + 1 < 4) rk_load_seg<MODE>(p, O0, b, n2, w, lane, s + 1, (s & 1) ? L0 : L1);
-    rk_segment<MODE>(p, stg, b, n2, w, lane, s, (s & 1) ? L1 : L0, or_x3, or_us, ir_x3, ir_us);
+    if (s + 1 < 4 && seg_live(s + 1, w, n2, H, W))
+      rk_load_seg<MODE>(p, O0, b, 8 * (2 * w + ((s + 1) >> 1)) + n2, 32 * ((s + 1) & 1), lane, (s & 1) ? L0 : L1);
+    if (seg_live(s, w, n2, H, W))
+      rk_segment<MODE>(p, stg + ((s >> 1) * 64 + 32 * (s & 1)) * RK_SP, b, 8 * (2 * w + (s >> 1)) + n2, 32 * (s & 1),
+                       lane, (s & 1) ? L1 : L0, or_x3, or_us, ir_x3, ir_us, p.vecs);
   }
   if constexpr (MODE == ROW_FINAL) return;
   asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -351,16 +377,283 @@ __global__ __launch_bounds__(RK_NT, 1) void row_kernel(cpx* __restrict__ Z, Conv
 }
 
 // ---------------------------------------------------------------------------------------------
+// one real row of 72 points per lane (row2_kernel): a 36-point complex transform of the even / odd
+// samples packed as z[m] = x[2m] + i x[2m+1] and the split by W72^k, half the registers of fft72 on a
+// packed pair of rows (72 instead of 144 values)
+// ---------------------------------------------------------------------------------------------
+template <int S>
+__device__ __forceinline__ void dft4(cpx (&x)[4]) {
+  const cpx a0 = x[0] + x[2], a1 = x[0] - x[2], a2 = x[1] + x[3], a3 = rotq<S>(x[1] - x[3]);
+  x[0] = a0 + a2;
+  x[2] = a0 - a2;
+  x[1] = a1 + a3;
+  x[3] = a1 - a3;
+}
+
+// 36-point DFT, X[k] = sum_n v[n] e^{S 2 pi i n k / 36}: Good-Thomas 36 = 4 x 9 (gcd 1),
+// n = (9 n1 + 4 n2) mod 36, k = (9 k1 + 28 k2) mod 36 -- no twiddles between the passes
+template <int S>
+__device__ __forceinline__ void fft36(cpx (&v)[36]) {
+  cpx a[9][4];
+#pragma unroll
+  for (int n2 = 0; n2 < 9; ++n2) {
+    cpx t[4];
+#pragma unroll
+    for (int n1 = 0; n1 < 4; ++n1) t[n1] = v[(9 * n1 + 4 * n2) % 36];
+    dft4<S>(t);
+#pragma unroll
+    for (int k1 = 0; k1 < 4; ++k1) a[n2][k1] = t[k1];
+  }
+#pragma unroll
+  for (int k1 = 0; k1 < 4; ++k1) {
+    cpx u[9];
+#pragma unroll
+    for (int n2 = 0; n2 < 9; ++n2) u[n2] = a[n2][k1];
+    dft9<S>(u);
+#pragma unroll
+    for (int k2 = 0; k2 < 9; ++k2) v[(9 * k1 + 28 * k2) % 36] = u[k2];
+  }
+}
+
+// forward real transform: x[0..63] (x[64..71] = 0) -> X[k] = sum_n x[n] W72^{nk}, k = 0..36
+__device__ __forceinline__ void rfft72_fwd(const float (&x)[64], cpx (&X)[FX]) {
+  cpx z[36];
+#pragma unroll
+  for (int m = 0; m < 36; ++m) z[m] = m < 32 ? cpx{x[2 * m], x[2 * m + 1]} : cpx{0.f, 0.f};
+  fft36<-1>(z);
+#pragma unroll
+  for (int k = 0; k < FX; ++k) {
+    // E[k] = (Z[k] + conj Z[36-k]) / 2, O[k] = (Z[k] - conj Z[36-k]) / 2i, X[k] = E[k] + W72^k O[k]
+    const cpx zk = z[k % 36], zm = z[(36 - k) % 36];
+    const cpx E = cfma(zm, cpx{1.f, -1.f}, zk) * 0.5f;               // (zk.x + zm.x, zk.y - zm.y) / 2
+    const cpx O = cfma(swp(zk), cpx{1.f, -1.f}, swp(zm)) * 0.5f;     // (zk.y + zm.y, zm.x - zk.x) / 2
+    X[k] = E + twid<-1>(O, k);
+  }
+}
+
+// inverse real transform: X[0..36] (Hermitian half spectrum) -> x[n] = sum_{k<72} X[k] W72^{-nk}, n < 64
+__device__ __forceinline__ void rfft72_inv(const cpx (&X)[FX], float (&x)[64]) {
+  cpx z[36];
+#pragma unroll
+  for (int k = 0; k < 36; ++k) {
+    // x[2m] = IDFT36(E), x[2m+1] = IDFT36(O): E[k] = X[k] + conj X[36-k], O[k] = (X[k] - conj X[36-k]) W72^{-k}
+    const cpx a = X[k], c = X[36 - k];
+    const cpx E = cfma(c, cpx{1.f, -1.f}, a);                         // (a.x + c.x, a.y - c.y)
+    const cpx O = twid<1>(cfma(c, cpx{-1.f, 1.f}, a), k);            // (a.x - c.x, a.y + c.y) W72^{-k}
+    z[k] = cfma(swp(O), cpx{-1.f, 1.f}, E);                           // E + i O
+  }
+  fft36<1>(z);
+#pragma unroll
+  for (int m = 0; m < 32; ++m) {
+    x[2 * m] = z[m].x;
+    x[2 * m + 1] = z[m].y;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// row kernel, two blocks per CU (row2_kernel, the default; MP_ROW2=0 restores row_kernel above).
+// The same block (image b, row class n2), phases and arithmetic, with half the LDS: T holds 4 of the
+// 8 rows (75,776 B), so the two transposes run in two rounds.  Wave w owns rows n1 = w (the real part
+// of its packed transforms) and w + 4 (the imaginary part):
+//   Ia  items (fx, c): the 9-point inverse sums; rows 0-3 to T, rows 4-7 held in registers
+//   Ib  lane c reads its row w half spectrum (round 1); rows 4-7 replace rows 0-3 in T; it reads
+//       row w + 4 (round 2); one inverse transform of the packed pair: v[x] = (P[w][x], P[w+4][x])
+//   II  four 32-pixel segments per wave (rows w, w + 4): P staged through the wave's own row slot of
+//       T, the epilogue's output read back into v
+//   III one forward transform of the packed pair; row w's half spectrum to T (round 1), the items
+//       take rows 0-3 into registers; row w + 4's (round 2); the items' 9-point sums -> Z
+// ---------------------------------------------------------------------------------------------
+constexpr int R2_T = 4 * FX * 64;   // complex entries: 75,776 B
+static_assert(32 * RK_SP * 4 <= FX * 64 * 8, "a segment's staging fits the wave's row slot");
+
+template <int MODE>
+__global__ __launch_bounds__(RK_NT, 2) void row2_kernel(cpx* __restrict__ Z, ConvArgs p, const void* __restrict__ or_x3,
+                                                         float or_us, const void* __restrict__ ir_x3, float ir_us,
+                                                         const float* __restrict__ O0) {
+  __shared__ cpx T[R2_T];
+  // the epilogues' per-channel vectors in LDS: read per segment there, instead of ~100-200 registers of
+  // loop-invariant global loads held across the whole kernel
+  __shared__ float vsh[V_COUNT * 64];
+  const int b = blockIdx.x >> 3, n2 = blockIdx.x & 7;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int i = tid; i < V_COUNT * 64; i += RK_NT) vsh[i] = p.vecs[i];
+  if constexpr (MODE == ROW_INIT) lds_barrier();   // (the other modes pass Ia's barriers first)
+  const int H = p.H, W = p.W;
+  const int ya = 8 * w + n2, yb = 8 * (w + 4) + n2;   // the wave's two rows
+  const bool la = ya < H, lb = yb < H;
+  cpx* slot = T + w * FX * 64;                         // the wave's row slot of T
+  float* stg = reinterpret_cast<float*>(slot);
+  // Register budget (two waves per SIMD): no 64-value row is held across a transform; the row that
+  // waits sits in the wave's slot as staging instead.
+  float P0[64], P1[64];                                // rows w and w + 4 of this lane's channel
+  if constexpr (MODE != ROW_INIT) {
+    // ---- Ia: 9-point inverse sums over k1 (two batches of items); rows 0-3 to T, rows 4-7 kept ----
+    cpx keep[RK_NIT][4];
+#pragma unroll
+    for (int half = 0; half < 2; ++half) {
+      constexpr int NB = RK_NIT / 2;
+      cpx u[NB][9];
+#pragma unroll
+      for (int q = 0; q < NB; ++q) {
+        const int i = min((half * NB + q) * RK_NT + tid, RK_ITEMS - 1);
+        const cpx* src = Z + z_off(b, n2, i >> 6, 0) + (i & 63);
+#pragma unroll
+        for (int k1 = 0; k1 < 9; ++k1) u[q][k1] = src[k1 * 64];
+      }
+#pragma unroll
+      for (int q = 0; q < NB; ++q) {
+        const int it = half * NB + q, i = it * RK_NT + tid;
+        dft9<1>(u[q]);
+        if (i < RK_ITEMS) {
+          const int fx = i >> 6, c = i & 63;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) T[(r * FX + fx) * 64 + c] = u[q][r];
+        }
+#pragma unroll
+        for (int r = 0; r < 4; ++r) keep[it][r] = u[q][4 + r];
+      }
+    }
+    lds_barrier();
+#ifdef R2_MARK
+    asm volatile("; P_IB" ::: "memory");
+#endif
+    // ---- Ib round 1: row w's half spectrum; rows 4-7 replace rows 0-3; row w's inverse transform ----
+    {
+      cpx A[FX];
+#pragma unroll
+      for (int k = 0; k < FX; ++k) A[k] = slot[k * 64 + lane];
+      lds_barrier();
+      const int tk = opaque(tid);
+#pragma unroll
+      for (int it = 0; it < RK_NIT; ++it) {
+        const int i = it * RK_NT + tk;
+        if (i < RK_ITEMS) {
+          const int fx = i >> 6, c = i & 63;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) T[(r * FX + fx) * 64 + c] = keep[it][r];
+        }
+      }
+      rfft72_inv(A, P0);
+    }
+    lds_barrier();
+    // ---- Ib round 2: row w + 4's half spectrum into registers, row w's P staged over it, inverse ----
+    {
+      cpx Bv[FX];
+#pragma unroll
+      for (int k = 0; k < FX; ++k) Bv[k] = slot[k * 64 + lane];
+      if (la) {
+#pragma unroll
+        for (int x = 0; x < 64; ++x)
+          if (x < W) stg[x * RK_SP + lane] = P0[x];   // (in-wave order: after the reads above)
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      rfft72_inv(Bv, P1);
+    }
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+#ifdef R2_MARK
+  asm volatile("; P_II" ::: "memory");
+#endif
+  // ---- II: row w (staged), then row w + 4; two 32-pixel segments per row ----
+#pragma unroll
+  for (int rr = 0; rr < 2; ++rr) {
+    const bool live = rr ? lb : la;
+    const int y = rr ? yb : ya;
+    if (rr == 1) {
+      if constexpr (MODE != ROW_FINAL) {
+        // row w's output back into registers (zero outside the map) before row w + 4 is staged
+#pragma unroll
+        for (int x = 0; x < 64; ++x) P0[x] = (la && x < W) ? stg[x * RK_SP + lane] : 0.f;
+      }
+      if constexpr (MODE != ROW_INIT) {
+        if (live) {
+#pragma unroll
+          for (int x = 0; x < 64; ++x)
+            if (x < W) stg[x * RK_SP + lane] = P1[x];
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    if (live) {
+#pragma unroll 1
+      for (int sg = 0; sg < 2; ++sg) {
+        const int xs = 32 * sg;
+        if (xs >= W) continue;   // wave-uniform
+        SegIn L;
+        rk_load_seg<MODE>(p, O0, b, y, xs, lane, L);
+        rk_segment<MODE, true>(p, stg + xs * RK_SP, b, y, xs, lane, L, or_x3, or_us, ir_x3, ir_us, vsh);
+      }
+    }
+  }
+  if constexpr (MODE == ROW_FINAL) return;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+#ifdef R2_MARK
+  asm volatile("; P_III" ::: "memory");
+#endif
+  // ---- III: row w's forward transform (row w + 4's output waits in the staging), then row w + 4's ----
+  cpx X1[FX];
+  {
+    cpx X0[FX];
+    rfft72_fwd(P0, X0);
+#pragma unroll
+    for (int x = 0; x < 64; ++x) P1[x] = (lb && x < W) ? stg[x * RK_SP + lane] : 0.f;
+#pragma unroll
+    for (int k = 0; k < FX; ++k) slot[k * 64 + lane] = X0[k];   // (in-wave order: after the reads above)
+    __builtin_amdgcn_sched_barrier(0);
+    rfft72_fwd(P1, X1);
+  }
+  lds_barrier();   // round 1: rows 0-3 in T
+  cpx got[RK_NIT][4];
+  const int tg = opaque(tid);
+#pragma unroll
+  for (int it = 0; it < RK_NIT; ++it) {
+    const int i = min(it * RK_NT + tg, RK_ITEMS - 1);
+#pragma unroll
+    for (int r = 0; r < 4; ++r) got[it][r] = T[(r * FX + (i >> 6)) * 64 + (i & 63)];
+  }
+  lds_barrier();
+#pragma unroll
+  for (int k = 0; k < FX; ++k) slot[k * 64 + lane] = X1[k];   // round 2: rows 4-7
+  lds_barrier();
+#ifdef R2_MARK
+  asm volatile("; P_IIIB" ::: "memory");
+#endif
+  // ---- IIIb: 9-point forward sums over n1 (row 64 + n2 is zero padding) -> Z ----
+  const int ts = opaque(tid);
+#pragma unroll
+  for (int it = 0; it < RK_NIT; ++it) {
+    const int i = it * RK_NT + ts;
+    if (i >= RK_ITEMS) break;
+    const int fx = i >> 6, c = i & 63;
+    cpx u[9];
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      u[r] = got[it][r];
+      u[4 + r] = T[(r * FX + fx) * 64 + c];
+    }
+    u[8] = cpx{0.f, 0.f};
+    dft9<-1>(u);
+    cpx* dst = Z + z_off(b, n2, fx, 0) + c;
+#pragma unroll
+    for (int k1 = 0; k1 < 9; ++k1) dst[k1 * 64] = u[k1];
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // column kernel (the spectral GEMM).  Block = (column class (fx, k1), 16 images), 256 threads, two
-// blocks per CU (68 KB of LDS).  Thread (image, channel group) turns its 8 row-class partials
-// Z[b][n2][fx][k1][4 ch] into the class's 8 frequencies (twiddle, 8-point DFT, scale + f16 split
-// into the S tile); wave w then computes frequency fy = k1 + 9 k2 for k2 = w and k2 = w + 4:
-//   Y[b][co] = sum_ci S[b][ci] G[ci][co]  (complex)
-// as k_fft.hip spec_gemm_kernel does for one frequency (f16x3 A / B fragments, the same k order; the
-// 16 MFMA columns past the block's images are zero); the first frequency's Y goes into the S tile
-// half it no longer needs while the second is computed.  Finally the same thread takes the 8
-// frequencies back to row-class partials (8-point inverse DFT, twiddle) and writes them over its
-// inputs.  Blocks of one class run on one XCD (its 256 KiB of weights fetched from HBM once).
+// blocks per CU (68 KB of LDS).  Thread (image, channel pair a) holds channels 2a, 2a + 1 and
+// 32 + 2a, 33 + 2a of its image (each wave instruction reads / writes contiguous 256-B runs of Z) and
+// turns their 8 row-class partials Z[b][n2][fx][k1][.] into the class's 8 frequencies (twiddle, 8-point
+// DFT, scale + f16 split into the S tile).  Wave w then computes frequency fy = k1 + 9 k2 for k2 = w and
+// w + 4:  Y[b][co] = sum_ci S[b][ci] G[ci][co]  (complex), as a real 128 x 16 x 128 product on
+// v_mfma_f32_16x16x32_f16 in the f16x3 split (k = 2 ci + re|im; rows n = 64 ro + co, the re / im rows'
+// A fragments derived from the compact weights by a sign flip / half swap as in k_fft.hip's
+// spec_gemm_kernel).  The first frequency's Y goes into the S tile half it no longer needs while the
+// second is computed.  Finally the same thread takes its channels' 8 frequencies back to row-class
+// partials (8-point inverse DFT, twiddle) and writes them over its inputs.  Blocks of one class run on
+// one XCD (its 256 KiB of weights fetched from HBM once).
 // ---------------------------------------------------------------------------------------------
 constexpr int CG_NI = 16;                            // images per block
 constexpr int CG_SLD = CG_NI + 1;                    // S tile pitch (16-B units) per (cq, part, k2 % 4) row
@@ -372,6 +665,9 @@ constexpr int CG_NC8 = (Z_CLS + 7) / 8;              // 42 groups of 8 classes (
 __device__ __forceinline__ int cg_s(int k2, int cq, int part, int bl) {   // S tile index (16-B units)
   return (k2 >> 2) * CG_HALF + ((cq * 2 + part) * 4 + (k2 & 3)) * CG_SLD + bl;
 }
+__device__ __forceinline__ f32x4 mfma16x16(f16x8 a, f16x8 b, f32x4 c) {
+  return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
+}
 
 __global__ __launch_bounds__(256, 2) void col_gemm_kernel(cpx* __restrict__ Z, const uint4* __restrict__ Gc, int B,
                                                           int ngrp, float unscale) {
@@ -380,33 +676,20 @@ __global__ __launch_bounds__(256, 2) void col_gemm_kernel(cpx* __restrict__ Z, c
   const int grp = rem >> 3, cls = c8 * 8 + (rem & 7);
   if (cls >= Z_CLS) return;
   const int fx = cls / 9, k1 = cls - fx * 9;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, j = lane & 31;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
   const int img0 = grp * CG_NI;
-  const int bl = tid >> 4, cq = tid & 15;
+  const int bl = tid >> 4, a = tid & 15;   // DFT role: image bl, channels 2a, 2a + 1, 32 + 2a, 33 + 2a
   const bool live = img0 + bl < B;
   const int b = min(img0 + bl, B - 1);
-  // ---- the thread's 8 row-class partials (8 x 32 B; unconditional, clamped) ----
+  const int cq0 = a >> 1, cq1 = 8 + (a >> 1), hf = a & 1;   // their channel groups, half of the group
+  // ---- the thread's 8 row-class partials (unconditional, clamped) ----
   f32x4 zin[8][2];
 #pragma unroll
   for (int n2 = 0; n2 < 8; ++n2) {
-    const f32x4* src = reinterpret_cast<const f32x4*>(Z + z_off(b, n2, fx, k1) + 4 * cq);
-    zin[n2][0] = src[0];
-    zin[n2][1] = src[1];
+    const f32x4* src = reinterpret_cast<const f32x4*>(Z + z_off(b, n2, fx, k1));
+    zin[n2][0] = src[a];
+    zin[n2][1] = src[a + 16];
   }
-  // ---- weights of one frequency (fx, k1 + 9 k2): class-major pack, 32 KiB, in two batches of 4
-  // k-steps (64 VGPRs each; the per-output k order is unchanged) ----
-  constexpr int TW = 4;
-  uint4 wr[TW][2][2];
-  auto load_w = [&](int k2, int t0) {
-    const uint4* gw = Gc + (size_t)(cls * 8 + k2) * 2 * 16 * 64;
-#pragma unroll
-    for (int t = 0; t < TW; ++t)
-#pragma unroll
-      for (int cb = 0; cb < 2; ++cb) {
-        wr[t][cb][0] = gw[(0 * 16 + 2 * (t0 + t) + h) * 64 + 32 * cb + j];
-        wr[t][cb][1] = gw[(1 * 16 + 2 * (t0 + t) + h) * 64 + 32 * cb + j];
-      }
-  };
   // ---- twiddle W72^{n2 k1}, 8-point DFT over n2 -> k2; scale and split into the S tile ----
   {
     cpx s[4][8];
@@ -419,69 +702,81 @@ __global__ __launch_bounds__(256, 2) void col_gemm_kernel(cpx* __restrict__ Z, c
       }
       dft8<-1>(s[e]);
     }
+    typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+    uint2* t2 = reinterpret_cast<uint2*>(tile);
 #pragma unroll
     for (int k2 = 0; k2 < 8; ++k2) {
-      f16x8 hv, lv;
 #pragma unroll
-      for (int e = 0; e < 4; ++e) {
-        const float re = s[e][k2].x * SPEC_SCALE, im = s[e][k2].y * SPEC_SCALE;
-        const _Float16 hr = (_Float16)re, hm = (_Float16)im;
-        hv[2 * e] = hr;
-        hv[2 * e + 1] = hm;
-        lv[2 * e] = (_Float16)(re - (float)hr);
-        lv[2 * e + 1] = (_Float16)(im - (float)hm);
+      for (int pr = 0; pr < 2; ++pr) {   // channel pair 0: (2a, 2a+1) of group cq0; 1: of group cq1
+        f16x4 hv, lv;
+#pragma unroll
+        for (int e = 0; e < 2; ++e) {
+          const cpx z = s[2 * pr + e][k2];
+          const float re = z.x * SPEC_SCALE, im = z.y * SPEC_SCALE;
+          const _Float16 hr = (_Float16)re, hm = (_Float16)im;
+          hv[2 * e] = hr;
+          hv[2 * e + 1] = hm;
+          lv[2 * e] = (_Float16)(re - (float)hr);
+          lv[2 * e + 1] = (_Float16)(im - (float)hm);
+        }
+        const int cq = pr ? cq1 : cq0;
+        t2[cg_s(k2, cq, 0, bl) * 2 + hf] = live ? __builtin_bit_cast(uint2, hv) : uint2{0, 0};
+        t2[cg_s(k2, cq, 1, bl) * 2 + hf] = live ? __builtin_bit_cast(uint2, lv) : uint2{0, 0};
       }
-      tile[cg_s(k2, cq, 0, bl)] = live ? __builtin_bit_cast(uint4, hv) : uint4{0, 0, 0, 0};
-      tile[cg_s(k2, cq, 1, bl)] = live ? __builtin_bit_cast(uint4, lv) : uint4{0, 0, 0, 0};
     }
   }
+  // ---- GEMM role: lane (kq = lane >> 4, jj = lane & 15); k-step t covers groups 4t .. 4t + 3 ----
+  const int kq = lane >> 4, jj = lane & 15;
+  constexpr int TW = 2;   // k-steps per weight batch (64 VGPRs)
+  uint4 wr[TW][4][2];
+  auto load_w = [&](int k2, int t0) {
+    const uint4* gw = Gc + (size_t)(cls * 8 + k2) * 2 * 16 * 64;
+#pragma unroll
+    for (int t = 0; t < TW; ++t)
+#pragma unroll
+      for (int mq = 0; mq < 4; ++mq) {
+        wr[t][mq][0] = gw[(0 * 16 + 4 * (t0 + t) + kq) * 64 + 16 * mq + jj];
+        wr[t][mq][1] = gw[(1 * 16 + 4 * (t0 + t) + kq) * 64 + 16 * mq + jj];
+      }
+  };
   load_w(wv, 0);   // after the partials are consumed (register budget), in flight across the tile barrier
   lds_barrier();
   const uint4 m = {0x80000000u, 0x80000000u, 0x80000000u, 0x80000000u};
-  // MFMA columns j >= 16 duplicate images j - 16: the columns of an MFMA are independent, and those
-  // outputs are never written
-  const int jj = j & (CG_NI - 1);
 #pragma unroll
   for (int half = 0; half < 2; ++half) {
     const int k2 = wv + 4 * half;
     if (half) load_w(k2, 0);
-    // ---- the 128 x 32 x 128 real product of frequency k2 (spec_gemm_kernel's fragments) ----
-    f32x16 acc[4] = {};
+    f32x4 acc[8] = {};   // [mq] rows co = 16 mq + .. (re), [4 + mq] the same co (im)
 #pragma unroll
-    for (int t = 0; t < 8; ++t) {
-      if (t == TW) load_w(k2, TW);
-      const int cqq = 2 * t + h;
-      const f16x8 sh = __builtin_bit_cast(f16x8, tile[cg_s(k2, cqq, 0, jj)]);
-      const f16x8 sl = __builtin_bit_cast(f16x8, tile[cg_s(k2, cqq, 1, jj)]);
+    for (int t = 0; t < 4; ++t) {
+      if (t > 0 && t % TW == 0) load_w(k2, t);
+      const f16x8 sh = __builtin_bit_cast(f16x8, tile[cg_s(k2, 4 * t + kq, 0, jj)]);
+      const f16x8 sl = __builtin_bit_cast(f16x8, tile[cg_s(k2, 4 * t + kq, 1, jj)]);
 #pragma unroll
-      for (int cb = 0; cb < 2; ++cb) {
-        const uint4 gh = wr[t % TW][cb][0], gl = wr[t % TW][cb][1];
+      for (int mq = 0; mq < 4; ++mq) {
+        const uint4 gh = wr[t % TW][mq][0], gl = wr[t % TW][mq][1];
+        // re rows: (gr, -gi) pairs; im rows: (gi, gr) pairs
         const f16x8 ah0 = __builtin_bit_cast(f16x8, gh ^ m), al0 = __builtin_bit_cast(f16x8, gl ^ m);
         const f16x8 ah1 = __builtin_bit_cast(f16x8, (gh >> 16) | (gh << 16));
         const f16x8 al1 = __builtin_bit_cast(f16x8, (gl >> 16) | (gl << 16));
-        acc[cb] = mfma16(al0, sh, acc[cb]);
-        acc[cb] = mfma16(ah0, sl, acc[cb]);
-        acc[cb] = mfma16(ah0, sh, acc[cb]);
-        acc[2 + cb] = mfma16(al1, sh, acc[2 + cb]);
-        acc[2 + cb] = mfma16(ah1, sl, acc[2 + cb]);
-        acc[2 + cb] = mfma16(ah1, sh, acc[2 + cb]);
+        acc[mq] = mfma16x16(al0, sh, acc[mq]);
+        acc[mq] = mfma16x16(ah0, sl, acc[mq]);
+        acc[mq] = mfma16x16(ah0, sh, acc[mq]);
+        acc[4 + mq] = mfma16x16(al1, sh, acc[4 + mq]);
+        acc[4 + mq] = mfma16x16(ah1, sl, acc[4 + mq]);
+        acc[4 + mq] = mfma16x16(ah1, sh, acc[4 + mq]);
       }
     }
     lds_barrier();   // every wave has read this half of the S tile
-    // ---- Y of the half: [image][cq][k2 % 4] over its S (lo: channels 0, 1 of the group; hi: 2, 3) ----
+    // ---- Y of the half, [image][cq][k2 % 4] over its S: lane (kq, jj) holds rows 4 kq + r of each
+    // 16-row block, i.e. channels 4 (4 mq + kq) + r -- group cqo = 4 mq + kq, all four channels ----
     f32x4* ytile = reinterpret_cast<f32x4*>(tile + half * CG_HALF);
-    if (j < CG_NI) {
 #pragma unroll
-      for (int cb = 0; cb < 2; ++cb)
-#pragma unroll
-        for (int g = 0; g < 4; ++g) {
-          const int cqo = 8 * cb + 2 * g + h;
-          const f32x16& re = acc[cb];
-          const f32x16& im = acc[2 + cb];
-          ytile[j * CG_YLD + (cqo * 4 + wv) * 2] = f32x4{re[4 * g], im[4 * g], re[4 * g + 1], im[4 * g + 1]} * unscale;
-          ytile[j * CG_YLD + (cqo * 4 + wv) * 2 + 1] =
-              f32x4{re[4 * g + 2], im[4 * g + 2], re[4 * g + 3], im[4 * g + 3]} * unscale;
-        }
+    for (int mq = 0; mq < 4; ++mq) {
+      const int cqo = 4 * mq + kq;
+      const f32x4 re = acc[mq], im = acc[4 + mq];
+      ytile[jj * CG_YLD + (cqo * 4 + wv) * 2] = f32x4{re[0], im[0], re[1], im[1]} * unscale;
+      ytile[jj * CG_YLD + (cqo * 4 + wv) * 2 + 1] = f32x4{re[2], im[2], re[3], im[3]} * unscale;
     }
   }
   lds_barrier();
@@ -490,12 +785,12 @@ __global__ __launch_bounds__(256, 2) void col_gemm_kernel(cpx* __restrict__ Z, c
 #pragma unroll
   for (int k2 = 0; k2 < 8; ++k2) {
     const f32x4* yt = reinterpret_cast<const f32x4*>(tile + (k2 >> 2) * CG_HALF);
-    const f32x4 lo = yt[bl * CG_YLD + (cq * 4 + (k2 & 3)) * 2];
-    const f32x4 hi = yt[bl * CG_YLD + (cq * 4 + (k2 & 3)) * 2 + 1];
-    yv[0][k2] = cpx{lo[0], lo[1]};
-    yv[1][k2] = cpx{lo[2], lo[3]};
-    yv[2][k2] = cpx{hi[0], hi[1]};
-    yv[3][k2] = cpx{hi[2], hi[3]};
+    const f32x4 p0 = yt[bl * CG_YLD + (cq0 * 4 + (k2 & 3)) * 2 + hf];
+    const f32x4 p1 = yt[bl * CG_YLD + (cq1 * 4 + (k2 & 3)) * 2 + hf];
+    yv[0][k2] = cpx{p0[0], p0[1]};
+    yv[1][k2] = cpx{p0[2], p0[3]};
+    yv[2][k2] = cpx{p1[0], p1[1]};
+    yv[3][k2] = cpx{p1[2], p1[3]};
   }
 #pragma unroll
   for (int e = 0; e < 4; ++e) {
@@ -506,9 +801,9 @@ __global__ __launch_bounds__(256, 2) void col_gemm_kernel(cpx* __restrict__ Z, c
   if (live) {
 #pragma unroll
     for (int n2 = 0; n2 < 8; ++n2) {
-      f32x4* dst = reinterpret_cast<f32x4*>(Z + z_off(b, n2, fx, k1) + 4 * cq);
-      dst[0] = f32x4{yv[0][n2].x, yv[0][n2].y, yv[1][n2].x, yv[1][n2].y};
-      dst[1] = f32x4{yv[2][n2].x, yv[2][n2].y, yv[3][n2].x, yv[3][n2].y};
+      f32x4* dst = reinterpret_cast<f32x4*>(Z + z_off(b, n2, fx, k1));
+      dst[a] = f32x4{yv[0][n2].x, yv[0][n2].y, yv[1][n2].x, yv[1][n2].y};
+      dst[a + 16] = f32x4{yv[2][n2].x, yv[2][n2].y, yv[3][n2].x, yv[3][n2].y};
     }
   }
 }
@@ -517,6 +812,15 @@ __global__ __launch_bounds__(256, 2) void col_gemm_kernel(cpx* __restrict__ Z, c
 bool fft4_enabled() {
   static const bool v = [] {
     const char* e = std::getenv("MP_FFT4");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  return v;
+}
+
+// MP_ROW2 (default 1): the two-blocks-per-CU row kernel; 0: row_kernel (one block per CU), for A/B
+static bool row2_enabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("MP_ROW2");
     return e ? std::atoi(e) != 0 : true;
   }();
   return v;
@@ -536,6 +840,16 @@ hipError_t launch_row(int mode, void* Z, const ConvArgs& a, const void* or_x3, f
   if (a.H < 1 || a.H > 64 || (a.W != 32 && a.W != 64)) return hipErrorInvalidValue;
   cpx* z = static_cast<cpx*>(Z);
   const dim3 g(B * 8), t(RK_NT);
+  if (row2_enabled()) {
+    switch (mode) {
+      case ROW_A: hipLaunchKernelGGL(row2_kernel<ROW_A>, g, t, 0, st, z, a, or_x3, or_us, ir_x3, ir_us, O0); break;
+      case ROW_B: hipLaunchKernelGGL(row2_kernel<ROW_B>, g, t, 0, st, z, a, or_x3, or_us, ir_x3, ir_us, O0); break;
+      case ROW_FINAL: hipLaunchKernelGGL(row2_kernel<ROW_FINAL>, g, t, 0, st, z, a, or_x3, or_us, ir_x3, ir_us, O0); break;
+      case ROW_INIT: hipLaunchKernelGGL(row2_kernel<ROW_INIT>, g, t, 0, st, z, a, or_x3, or_us, ir_x3, ir_us, O0); break;
+      default: return hipErrorInvalidValue;
+    }
+    return hipGetLastError();
+  }
   switch (mode) {
     case ROW_A: hipLaunchKernelGGL(row_kernel<ROW_A>, g, t, 0, st, z, a, or_x3, or_us, ir_x3, ir_us, O0); break;
     case ROW_B: hipLaunchKernelGGL(row_kernel<ROW_B>, g, t, 0, st, z, a, or_x3, or_us, ir_x3, ir_us, O0); break;
