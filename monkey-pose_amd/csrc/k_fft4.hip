@@ -154,7 +154,9 @@ __device__ __forceinline__ bool seg_live(int s, int w, int n2, int H, int W) {
 }
 
 // the segment at map row y, columns xs .. xs + 31 (lane (h, j): pixel xs + j)
-template <int MODE>
+// PREO: O is loaded here with the other map (B modes: 32 more live registers across the o_r gate,
+// against eight dependent loads after it)
+template <int MODE, bool PREO = true>
 __device__ __forceinline__ void rk_load_seg(const ConvArgs& p, const float* __restrict__ O0, int b, int y, int xs,
                                             int lane, SegIn& L) {
   const int H = p.H, W = p.W;
@@ -168,8 +170,7 @@ __device__ __forceinline__ void rk_load_seg(const ConvArgs& p, const float* __re
       } else {
         L.a[n][g] = MODE == ROW_A ? map_ld4<false>(p.X, xx_index(b, 4 * n + g, y, x, 4 * h, H, W))
                                   : map_ld4<false>(p.I, ii_index(b, 4 * n + g, y, x, 4 * h, H, W));
-        // B: O is loaded by rk_segment after the o_r gate (64 fewer live registers across it)
-        if constexpr (MODE == ROW_A) L.o[n][g] = map_ld4<false>(p.O, oo_index(b, 4 * n + g, y, x, 4 * h, H, W));
+        if constexpr (MODE == ROW_A || PREO) L.o[n][g] = map_ld4<false>(p.O, oo_index(b, 4 * n + g, y, x, 4 * h, H, W));
       }
     }
 }
@@ -177,7 +178,7 @@ __device__ __forceinline__ void rk_load_seg(const ConvArgs& p, const float* __re
 // seg: the segment's 32 staged pixels (pitch RK_SP floats); the output goes back over the input
 // LEAN: a scheduling fence after every 4-channel group, so the compiler does not hoist all eight groups'
 // loads and address math at once (row2_kernel's two-blocks-per-CU register budget)
-template <int MODE, bool LEAN = false>
+template <int MODE, bool LEAN = false, bool PREO = true>
 __device__ __forceinline__ void rk_segment(const ConvArgs& p, float* seg, int b, int y, int xs, int lane,
                                            const SegIn& L, const void* __restrict__ or_x3, float or_us,
                                            const void* __restrict__ ir_x3, float ir_us, const float* vec) {
@@ -249,7 +250,7 @@ __device__ __forceinline__ void rk_segment(const ConvArgs& p, float* seg, int b,
       for (int g = 0; g < 4; ++g) {
         const int c = 32 * n + 8 * g + 4 * h;
         const f32x4 pv = *reinterpret_cast<const f32x4*>(sp + c);
-        const f32x4 ov = map_ld4<false>(p.O, oo_index(b, 4 * n + g, y, x, 4 * h, H, W));
+        const f32x4 ov = PREO ? L.o[n][g] : map_ld4<false>(p.O, oo_index(b, 4 * n + g, y, x, 4 * h, H, W));
         const f32x4 lat = *reinterpret_cast<const f32x4*>(vec + V_LAT * 64 + c);
         const f32x4 ga = *reinterpret_cast<const f32x4*>(vec + V_GAMMA * 64 + c);
         const f32x4 ka = *reinterpret_cast<const f32x4*>(vec + V_KAPPA * 64 + c);
@@ -466,7 +467,7 @@ __device__ __forceinline__ void rfft72_inv(const cpx (&X)[FX], float (&x)[64]) {
 constexpr int R2_T = 4 * FX * 64;   // complex entries: 75,776 B
 static_assert(32 * RK_SP * 4 <= FX * 64 * 8, "a segment's staging fits the wave's row slot");
 
-template <int MODE>
+template <int MODE, bool PREO = true>
 __global__ __launch_bounds__(RK_NT, 2) void row2_kernel(cpx* __restrict__ Z, ConvArgs p, const void* __restrict__ or_x3,
                                                          float or_us, const void* __restrict__ ir_x3, float ir_us,
                                                          const float* __restrict__ O0) {
@@ -581,8 +582,8 @@ __global__ __launch_bounds__(RK_NT, 2) void row2_kernel(cpx* __restrict__ Z, Con
         const int xs = 32 * sg;
         if (xs >= W) continue;   // wave-uniform
         SegIn L;
-        rk_load_seg<MODE>(p, O0, b, y, xs, lane, L);
-        rk_segment<MODE, true>(p, stg + xs * RK_SP, b, y, xs, lane, L, or_x3, or_us, ir_x3, ir_us, vsh);
+        rk_load_seg<MODE, PREO>(p, O0, b, y, xs, lane, L);
+        rk_segment<MODE, true, PREO>(p, stg + xs * RK_SP, b, y, xs, lane, L, or_x3, or_us, ir_x3, ir_us, vsh);
       }
     }
   }
@@ -826,6 +827,15 @@ static bool row2_enabled() {
   return v;
 }
 
+// MP_ROW2_PREO (default 1): B epilogue segments load O with I, before the o_r gate; 0: after it
+static bool row2_preo() {
+  static const bool v = [] {
+    const char* e = std::getenv("MP_ROW2_PREO");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  return v;
+}
+
 hipError_t launch_col_gemm(void* Z, const void* Gc, int B, float unscale, hipStream_t st) {
   if (B <= 0) return hipSuccess;
   const int ngrp = (B + CG_NI - 1) / CG_NI;
@@ -841,10 +851,17 @@ hipError_t launch_row(int mode, void* Z, const ConvArgs& a, const void* or_x3, f
   cpx* z = static_cast<cpx*>(Z);
   const dim3 g(B * 8), t(RK_NT);
   if (row2_enabled()) {
+    const bool pre = row2_preo();
     switch (mode) {
       case ROW_A: hipLaunchKernelGGL(row2_kernel<ROW_A>, g, t, 0, st, z, a, or_x3, or_us, ir_x3, ir_us, O0); break;
-      case ROW_B: hipLaunchKernelGGL(row2_kernel<ROW_B>, g, t, 0, st, z, a, or_x3, or_us, ir_x3, ir_us, O0); break;
-      case ROW_FINAL: hipLaunchKernelGGL(row2_kernel<ROW_FINAL>, g, t, 0, st, z, a, or_x3, or_us, ir_x3, ir_us, O0); break;
+      case ROW_B:
+        if (pre) hipLaunchKernelGGL((row2_kernel<ROW_B, true>), g, t, 0, st, z, a, or_x3, or_us, ir_x3, ir_us, O0);
+        else hipLaunchKernelGGL((row2_kernel<ROW_B, false>), g, t, 0, st, z, a, or_x3, or_us, ir_x3, ir_us, O0);
+        break;
+      case ROW_FINAL:
+        if (pre) hipLaunchKernelGGL((row2_kernel<ROW_FINAL, true>), g, t, 0, st, z, a, or_x3, or_us, ir_x3, ir_us, O0);
+        else hipLaunchKernelGGL((row2_kernel<ROW_FINAL, false>), g, t, 0, st, z, a, or_x3, or_us, ir_x3, ir_us, O0);
+        break;
       case ROW_INIT: hipLaunchKernelGGL(row2_kernel<ROW_INIT>, g, t, 0, st, z, a, or_x3, or_us, ir_x3, ir_us, O0); break;
       default: return hipErrorInvalidValue;
     }
