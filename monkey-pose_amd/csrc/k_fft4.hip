@@ -809,6 +809,122 @@ __global__ __launch_bounds__(256, 2) void col_gemm_kernel(cpx* __restrict__ Z, c
   }
 }
 
+// column kernel, eight waves (col8_kernel; MP_COL8=1): the same block (class, 16 images) and
+// arithmetic with 512 threads, so the per-thread DFT / split work halves (thread = image x channel
+// pair, one contiguous 512-B run of Z per image and n2 per wave instruction pair) and each wave
+// computes ONE frequency (k2 = wave): no second GEMM pass behind a weight reload.  Two blocks per
+// CU (16 waves) leave 128 VGPRs per wave.
+__global__ __launch_bounds__(512, 2) void col8_kernel(cpx* __restrict__ Z, const uint4* __restrict__ Gc, int B,
+                                                      int ngrp, float unscale) {
+  __shared__ uint4 tile[2 * CG_HALF];   // 69,632 B
+  const int c8 = blockIdx.x / (8 * ngrp), rem = blockIdx.x - c8 * 8 * ngrp;
+  const int grp = rem >> 3, cls = c8 * 8 + (rem & 7);
+  if (cls >= Z_CLS) return;
+  const int fx = cls / 9, k1 = cls - fx * 9;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int img0 = grp * CG_NI;
+  const int bl = tid >> 5, a = tid & 31;   // DFT role: image bl, channels 2a, 2a + 1 (group a >> 1, half a & 1)
+  const bool live = img0 + bl < B;
+  const int b = min(img0 + bl, B - 1);
+  const int cq = a >> 1, hf = a & 1;
+  {
+    f32x4 zin[8];
+#pragma unroll
+    for (int n2 = 0; n2 < 8; ++n2) zin[n2] = reinterpret_cast<const f32x4*>(Z + z_off(b, n2, fx, k1))[a];
+    cpx s[2][8];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+#pragma unroll
+      for (int n2 = 0; n2 < 8; ++n2) s[e][n2] = twid<-1>(cpx{zin[n2][2 * e], zin[n2][2 * e + 1]}, n2 * k1);
+      dft8<-1>(s[e]);
+    }
+    typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+    uint2* t2 = reinterpret_cast<uint2*>(tile);
+#pragma unroll
+    for (int k2 = 0; k2 < 8; ++k2) {
+      f16x4 hv, lv;
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const float re = s[e][k2].x * SPEC_SCALE, im = s[e][k2].y * SPEC_SCALE;
+        const _Float16 hr = (_Float16)re, hm = (_Float16)im;
+        hv[2 * e] = hr;
+        hv[2 * e + 1] = hm;
+        lv[2 * e] = (_Float16)(re - (float)hr);
+        lv[2 * e + 1] = (_Float16)(im - (float)hm);
+      }
+      t2[cg_s(k2, cq, 0, bl) * 2 + hf] = live ? __builtin_bit_cast(uint2, hv) : uint2{0, 0};
+      t2[cg_s(k2, cq, 1, bl) * 2 + hf] = live ? __builtin_bit_cast(uint2, lv) : uint2{0, 0};
+    }
+  }
+  const int kq = lane >> 4, jj = lane & 15, k2 = wv;
+  constexpr int TW = 2;
+  uint4 wr[TW][4][2];
+  const uint4* gw = Gc + (size_t)(cls * 8 + k2) * 2 * 16 * 64;
+  auto load_w = [&](int t0) {
+#pragma unroll
+    for (int t = 0; t < TW; ++t)
+#pragma unroll
+      for (int mq = 0; mq < 4; ++mq) {
+        wr[t][mq][0] = gw[(0 * 16 + 4 * (t0 + t) + kq) * 64 + 16 * mq + jj];
+        wr[t][mq][1] = gw[(1 * 16 + 4 * (t0 + t) + kq) * 64 + 16 * mq + jj];
+      }
+  };
+  load_w(0);
+  lds_barrier();
+  const uint4 m = {0x80000000u, 0x80000000u, 0x80000000u, 0x80000000u};
+  f32x4 acc[8] = {};
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    if (t > 0 && t % TW == 0) load_w(t);
+    const f16x8 sh = __builtin_bit_cast(f16x8, tile[cg_s(k2, 4 * t + kq, 0, jj)]);
+    const f16x8 sl = __builtin_bit_cast(f16x8, tile[cg_s(k2, 4 * t + kq, 1, jj)]);
+#pragma unroll
+    for (int mq = 0; mq < 4; ++mq) {
+      const uint4 gh = wr[t % TW][mq][0], gl = wr[t % TW][mq][1];
+      const f16x8 ah0 = __builtin_bit_cast(f16x8, gh ^ m), al0 = __builtin_bit_cast(f16x8, gl ^ m);
+      const f16x8 ah1 = __builtin_bit_cast(f16x8, (gh >> 16) | (gh << 16));
+      const f16x8 al1 = __builtin_bit_cast(f16x8, (gl >> 16) | (gl << 16));
+      acc[mq] = mfma16x16(al0, sh, acc[mq]);
+      acc[mq] = mfma16x16(ah0, sl, acc[mq]);
+      acc[mq] = mfma16x16(ah0, sh, acc[mq]);
+      acc[4 + mq] = mfma16x16(al1, sh, acc[4 + mq]);
+      acc[4 + mq] = mfma16x16(ah1, sl, acc[4 + mq]);
+      acc[4 + mq] = mfma16x16(ah1, sh, acc[4 + mq]);
+    }
+  }
+  lds_barrier();   // every wave has read the S tile
+  // Y tile over the whole S tile: [image][cq][k2] (16-B units, pitch 16 * 8 * 2 + 1 per image)
+  constexpr int YLD = 16 * 8 * 2 + 1;
+  static_assert(CG_NI * YLD <= 2 * CG_HALF, "the Y tile fits the S tile's space");
+  f32x4* ytile = reinterpret_cast<f32x4*>(tile);
+#pragma unroll
+  for (int mq = 0; mq < 4; ++mq) {
+    const int cqo = 4 * mq + kq;
+    const f32x4 re = acc[mq], im = acc[4 + mq];
+    ytile[jj * YLD + (cqo * 8 + k2) * 2] = f32x4{re[0], im[0], re[1], im[1]} * unscale;
+    ytile[jj * YLD + (cqo * 8 + k2) * 2 + 1] = f32x4{re[2], im[2], re[3], im[3]} * unscale;
+  }
+  lds_barrier();
+  cpx yv[2][8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const f32x4 pv = ytile[bl * YLD + (cq * 8 + q) * 2 + hf];
+    yv[0][q] = cpx{pv[0], pv[1]};
+    yv[1][q] = cpx{pv[2], pv[3]};
+  }
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    dft8<1>(yv[e]);
+#pragma unroll
+    for (int n2 = 0; n2 < 8; ++n2) yv[e][n2] = twid<1>(yv[e][n2], n2 * k1);
+  }
+  if (live) {
+#pragma unroll
+    for (int n2 = 0; n2 < 8; ++n2)
+      reinterpret_cast<f32x4*>(Z + z_off(b, n2, fx, k1))[a] = f32x4{yv[0][n2].x, yv[0][n2].y, yv[1][n2].x, yv[1][n2].y};
+  }
+}
+
 // ------------------------------------------------------------------------------------ launchers
 bool fft4_enabled() {
   static const bool v = [] {
@@ -836,11 +952,24 @@ static bool row2_preo() {
   return v;
 }
 
+// MP_COL8 (default 1): the eight-wave column kernel; 0: the four-wave one (two frequencies per wave)
+static bool col8_enabled() {
+  static const bool v = [] {
+    const char* e = std::getenv("MP_COL8");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  return v;
+}
+
 hipError_t launch_col_gemm(void* Z, const void* Gc, int B, float unscale, hipStream_t st) {
   if (B <= 0) return hipSuccess;
   const int ngrp = (B + CG_NI - 1) / CG_NI;
-  hipLaunchKernelGGL(col_gemm_kernel, dim3(CG_NC8 * 8 * ngrp), dim3(256), 0, st, static_cast<cpx*>(Z),
-                     static_cast<const uint4*>(Gc), B, ngrp, unscale);
+  if (col8_enabled())
+    hipLaunchKernelGGL(col8_kernel, dim3(CG_NC8 * 8 * ngrp), dim3(512), 0, st, static_cast<cpx*>(Z),
+                       static_cast<const uint4*>(Gc), B, ngrp, unscale);
+  else
+    hipLaunchKernelGGL(col_gemm_kernel, dim3(CG_NC8 * 8 * ngrp), dim3(256), 0, st, static_cast<cpx*>(Z),
+                       static_cast<const uint4*>(Gc), B, ngrp, unscale);
   return hipGetLastError();
 }
 
