@@ -93,10 +93,10 @@ def fft_kernels(ctx, B, hw, steps, bf16=False):
         "epi_b": (5 * sm, 0.0),                        # P, I, O in; O', Og' out
         # the four-step loop (k_fft4.hip, the fp32 default): Z is a spectrum-sized complex64 buffer
         "col_gemm": (2 * spec + NF * ent * 1024, 8.0 * B * NF * 64 * 64),    # Z in, Z' out, weights
-        "row_a": (2 * spec + 3 * act, 0.0),            # Z', X, O in; I, Z out
-        "row_b": (2 * spec + 3 * act, 0.0),            # Z', I, O in; O', Z out
-        "row_final": (spec + 4 * act, 0.0),            # Z', I, O in; O', BN_3(O_T) NHWC out
-        "row_init": (2 * act + spec, 0.0),             # O0 in; O, Z out
+        "row_a": (2 * spec + 3 * sm, 0.0),             # Z', X, O in; I, Z out
+        "row_b": (2 * spec + 3 * sm, 0.0),             # Z', I, O in; O', Z out
+        "row_final": (spec + 3 * sm + act, 0.0),       # Z', I, O in; O', BN_3(O_T) NHWC (fp32) out
+        "row_init": (act + sm + spec, 0.0),            # O0 (NHWC fp32) in; O, Z out
     }
     out = {}
     # the fp32 path's spectral GEMM is f16x3 (three f16 MFMA products per fp32-accurate MAC): its

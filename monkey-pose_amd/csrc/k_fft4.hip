@@ -156,7 +156,7 @@ __device__ __forceinline__ bool seg_live(int s, int w, int n2, int H, int W) {
 // the segment at map row y, columns xs .. xs + 31 (lane (h, j): pixel xs + j)
 // PREO: O is loaded here with the other map (B modes: 32 more live registers across the o_r gate,
 // against eight dependent loads after it)
-template <int MODE, bool PREO = true>
+template <int MODE, bool PREO = true, bool BM = false>
 __device__ __forceinline__ void rk_load_seg(const ConvArgs& p, const float* __restrict__ O0, int b, int y, int xs,
                                             int lane, SegIn& L) {
   const int H = p.H, W = p.W;
@@ -168,9 +168,9 @@ __device__ __forceinline__ void rk_load_seg(const ConvArgs& p, const float* __re
       if constexpr (MODE == ROW_INIT) {
         L.a[n][g] = *reinterpret_cast<const f32x4*>(O0 + (((size_t)b * H + y) * W + x) * C + 32 * n + 8 * g + 4 * h);
       } else {
-        L.a[n][g] = MODE == ROW_A ? map_ld4<false>(p.X, xx_index(b, 4 * n + g, y, x, 4 * h, H, W))
-                                  : map_ld4<false>(p.I, ii_index(b, 4 * n + g, y, x, 4 * h, H, W));
-        if constexpr (MODE == ROW_A || PREO) L.o[n][g] = map_ld4<false>(p.O, oo_index(b, 4 * n + g, y, x, 4 * h, H, W));
+        L.a[n][g] = MODE == ROW_A ? map_ld4<BM>(p.X, xx_index(b, 4 * n + g, y, x, 4 * h, H, W))
+                                  : map_ld4<BM>(p.I, ii_index(b, 4 * n + g, y, x, 4 * h, H, W));
+        if constexpr (MODE == ROW_A || PREO) L.o[n][g] = map_ld4<BM>(p.O, oo_index(b, 4 * n + g, y, x, 4 * h, H, W));
       }
     }
 }
@@ -178,7 +178,7 @@ __device__ __forceinline__ void rk_load_seg(const ConvArgs& p, const float* __re
 // seg: the segment's 32 staged pixels (pitch RK_SP floats); the output goes back over the input
 // LEAN: a scheduling fence after every 4-channel group, so the compiler does not hoist all eight groups'
 // loads and address math at once (row2_kernel's two-blocks-per-CU register budget)
-template <int MODE, bool LEAN = false, bool PREO = true>
+template <int MODE, bool LEAN = false, bool PREO = true, bool BM = false>
 __device__ __forceinline__ void rk_segment(const ConvArgs& p, float* seg, int b, int y, int xs, int lane,
                                            const SegIn& L, const void* __restrict__ or_x3, float or_us,
                                            const void* __restrict__ ir_x3, float ir_us, const float* vec) {
@@ -203,7 +203,7 @@ __device__ __forceinline__ void rk_segment(const ConvArgs& p, float* seg, int b,
         f32x4 iv;
 #pragma unroll
         for (int e = 0; e < 4; ++e) iv[e] = atanh_f(epi_a(L.a[n][g][e], L.o[n][g][e], pv[e], be[e], nu[e], lat[e]));
-        map_st4<false>(p.dst, ii_index(b, 4 * n + g, y, x, 4 * h, H, W), iv);
+        map_st4<BM>(p.dst, ii_index(b, 4 * n + g, y, x, 4 * h, H, W), iv);
         *reinterpret_cast<f32x4*>(sp + c) = iv;
         if constexpr (LEAN) __builtin_amdgcn_sched_barrier(0);
       }
@@ -216,7 +216,7 @@ __device__ __forceinline__ void rk_segment(const ConvArgs& p, float* seg, int b,
       for (int g = 0; g < 4; ++g)
 #pragma unroll
         for (int e = 0; e < 4; ++e) V[n][4 * g + e] = L.a[n][g][e];
-    gate_x3(static_cast<const f16x8*>(irw), V, Y, lane, ir_us);
+    gate_any<BM>(irw, V, Y, lane, ir_us);
 #pragma unroll
     for (int n = 0; n < 2; ++n)
 #pragma unroll
@@ -229,7 +229,7 @@ __device__ __forceinline__ void rk_segment(const ConvArgs& p, float* seg, int b,
           o[e] = V[n][4 * g + e];
           og[e] = o[e] * fsigmoid(Y[n][4 * g + e] + ib[e]);
         }
-        map_st4<false>(p.dst, oo_index(b, 4 * n + g, y, x, 4 * h, H, W), o);
+        map_st4<BM>(p.dst, oo_index(b, 4 * n + g, y, x, 4 * h, H, W), o);
         *reinterpret_cast<f32x4*>(sp + c) = og;
         if constexpr (LEAN) __builtin_amdgcn_sched_barrier(0);
       }
@@ -243,14 +243,14 @@ __device__ __forceinline__ void rk_segment(const ConvArgs& p, float* seg, int b,
       for (int g = 0; g < 4; ++g)
 #pragma unroll
         for (int e = 0; e < 4; ++e) Iv[n][4 * g + e] = L.a[n][g][e];
-    gate_x3(static_cast<const f16x8*>(orw), Iv, Y, lane, or_us);
+    gate_any<BM>(orw, Iv, Y, lane, or_us);
 #pragma unroll
     for (int n = 0; n < 2; ++n)
 #pragma unroll
       for (int g = 0; g < 4; ++g) {
         const int c = 32 * n + 8 * g + 4 * h;
         const f32x4 pv = *reinterpret_cast<const f32x4*>(sp + c);
-        const f32x4 ov = PREO ? L.o[n][g] : map_ld4<false>(p.O, oo_index(b, 4 * n + g, y, x, 4 * h, H, W));
+        const f32x4 ov = PREO ? L.o[n][g] : map_ld4<BM>(p.O, oo_index(b, 4 * n + g, y, x, 4 * h, H, W));
         const f32x4 lat = *reinterpret_cast<const f32x4*>(vec + V_LAT * 64 + c);
         const f32x4 ga = *reinterpret_cast<const f32x4*>(vec + V_GAMMA * 64 + c);
         const f32x4 ka = *reinterpret_cast<const f32x4*>(vec + V_KAPPA * 64 + c);
@@ -268,12 +268,12 @@ __device__ __forceinline__ void rk_segment(const ConvArgs& p, float* seg, int b,
           o[e] = on;
           Iv[n][rr] = on;
         }
-        map_st4<false>(p.dst, oo_index(b, 4 * n + g, y, x, 4 * h, H, W), o);
+        map_st4<BM>(p.dst, oo_index(b, 4 * n + g, y, x, 4 * h, H, W), o);
         if constexpr (LEAN) __builtin_amdgcn_sched_barrier(0);
       }
     f32x16 (&Ov)[2] = Iv;
     if constexpr (MODE == ROW_B) {
-      gate_x3(static_cast<const f16x8*>(irw), Ov, Y, lane, ir_us);
+      gate_any<BM>(irw, Ov, Y, lane, ir_us);
 #pragma unroll
       for (int n = 0; n < 2; ++n)
 #pragma unroll
@@ -467,8 +467,23 @@ __device__ __forceinline__ void rfft72_inv(const cpx (&X)[FX], float (&x)[64]) {
 constexpr int R2_T = 4 * FX * 64;   // complex entries: 75,776 B
 static_assert(32 * RK_SP * 4 <= FX * 64 * 8, "a segment's staging fits the wave's row slot");
 
-template <int MODE, bool PREO = true>
-__global__ __launch_bounds__(RK_NT, 2) void row2_kernel(cpx* __restrict__ Z, ConvArgs p, const void* __restrict__ or_x3,
+// Z element access: complex64 (fp32 path) or one bf16 (re, im) pair (MP_DTYPE_BF16: round to nearest
+// even on store, exact on load), at the same complex index
+template <bool BF>
+__device__ __forceinline__ cpx z_ld(const void* Z, size_t i) {
+  if constexpr (BF) return unpack_bf2(static_cast<const uint32_t*>(Z)[i]);
+  else return static_cast<const cpx*>(Z)[i];
+}
+template <bool BF>
+__device__ __forceinline__ void z_st(void* Z, size_t i, cpx v) {
+  if constexpr (BF) static_cast<uint32_t*>(Z)[i] = pack_bf2(v.x, v.y);
+  else static_cast<cpx*>(Z)[i] = v;
+}
+
+// BF: MP_DTYPE_BF16 -- Z and the hGRU maps in bf16, the gates one bf16 product (gate_bf); transforms,
+// epilogue math and the NHWC output fp32
+template <int MODE, bool PREO = true, bool BF = false>
+__global__ __launch_bounds__(RK_NT, 2) void row2_kernel(void* __restrict__ Z, ConvArgs p, const void* __restrict__ or_x3,
                                                          float or_us, const void* __restrict__ ir_x3, float ir_us,
                                                          const float* __restrict__ O0) {
   __shared__ cpx T[R2_T];
@@ -497,9 +512,9 @@ __global__ __launch_bounds__(RK_NT, 2) void row2_kernel(cpx* __restrict__ Z, Con
 #pragma unroll
       for (int q = 0; q < NB; ++q) {
         const int i = min((half * NB + q) * RK_NT + tid, RK_ITEMS - 1);
-        const cpx* src = Z + z_off(b, n2, i >> 6, 0) + (i & 63);
+        const size_t src = z_off(b, n2, i >> 6, 0) + (i & 63);
 #pragma unroll
-        for (int k1 = 0; k1 < 9; ++k1) u[q][k1] = src[k1 * 64];
+        for (int k1 = 0; k1 < 9; ++k1) u[q][k1] = z_ld<BF>(Z, src + k1 * 64);
       }
 #pragma unroll
       for (int q = 0; q < NB; ++q) {
@@ -582,8 +597,8 @@ __global__ __launch_bounds__(RK_NT, 2) void row2_kernel(cpx* __restrict__ Z, Con
         const int xs = 32 * sg;
         if (xs >= W) continue;   // wave-uniform
         SegIn L;
-        rk_load_seg<MODE, PREO>(p, O0, b, y, xs, lane, L);
-        rk_segment<MODE, true, PREO>(p, stg + xs * RK_SP, b, y, xs, lane, L, or_x3, or_us, ir_x3, ir_us, vsh);
+        rk_load_seg<MODE, PREO, BF>(p, O0, b, y, xs, lane, L);
+        rk_segment<MODE, true, PREO, BF>(p, stg + xs * RK_SP, b, y, xs, lane, L, or_x3, or_us, ir_x3, ir_us, vsh);
       }
     }
   }
@@ -636,9 +651,9 @@ __global__ __launch_bounds__(RK_NT, 2) void row2_kernel(cpx* __restrict__ Z, Con
     }
     u[8] = cpx{0.f, 0.f};
     dft9<-1>(u);
-    cpx* dst = Z + z_off(b, n2, fx, 0) + c;
+    const size_t dst = z_off(b, n2, fx, 0) + c;
 #pragma unroll
-    for (int k1 = 0; k1 < 9; ++k1) dst[k1 * 64] = u[k1];
+    for (int k1 = 0; k1 < 9; ++k1) z_st<BF>(Z, dst + k1 * 64, u[k1]);
   }
 }
 
@@ -925,6 +940,96 @@ __global__ __launch_bounds__(512, 2) void col8_kernel(cpx* __restrict__ Z, const
   }
 }
 
+// column kernel, bf16 (MP_DTYPE_BF16): col8_kernel's blocking with bf16 Z partials (8-B reads of a
+// thread's two channels), a bf16 S tile (one (re, im) pair per channel, no lo plane: 34 KB), one
+// v_mfma_f32_16x16x32_bf16 product per (k-step, row block, re|im) against the class-major bf16
+// weights Gb[f][cq][co] (16 KiB per frequency), fp32 accumulation, DFTs and twiddles in fp32.
+constexpr int CB_HALF = 16 * 4 * CG_SLD;             // one frequency half of the bf16 S tile (16-B units)
+__global__ __launch_bounds__(512, 2) void col8_bf_kernel(void* __restrict__ Zv, const uint4* __restrict__ Gb, int B,
+                                                         int ngrp) {
+  __shared__ uint4 tile[2 * CG_HALF];   // the Y tile (fp32) needs the fp32 kernel's space
+  const int c8 = blockIdx.x / (8 * ngrp), rem = blockIdx.x - c8 * 8 * ngrp;
+  const int grp = rem >> 3, cls = c8 * 8 + (rem & 7);
+  if (cls >= Z_CLS) return;
+  const int fx = cls / 9, k1 = cls - fx * 9;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int img0 = grp * CG_NI;
+  const int bl = tid >> 5, a = tid & 31;
+  const bool live = img0 + bl < B;
+  const int b = min(img0 + bl, B - 1);
+  const int cq = a >> 1, hf = a & 1;
+  uint32_t* Z = static_cast<uint32_t*>(Zv);
+  auto sidx = [](int k2, int c, int img) { return (k2 >> 2) * CB_HALF + (c * 4 + (k2 & 3)) * CG_SLD + img; };
+  {
+    uint2 zin[8];
+#pragma unroll
+    for (int n2 = 0; n2 < 8; ++n2) zin[n2] = reinterpret_cast<const uint2*>(Z + z_off(b, n2, fx, k1))[a];
+    cpx s[2][8];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+#pragma unroll
+      for (int n2 = 0; n2 < 8; ++n2) s[e][n2] = twid<-1>(unpack_bf2(e ? zin[n2].y : zin[n2].x), n2 * k1);
+      dft8<-1>(s[e]);
+    }
+    uint2* t2 = reinterpret_cast<uint2*>(tile);
+#pragma unroll
+    for (int k2 = 0; k2 < 8; ++k2)
+      t2[sidx(k2, cq, bl) * 2 + hf] =
+          live ? uint2{pack_bf2(s[0][k2].x, s[0][k2].y), pack_bf2(s[1][k2].x, s[1][k2].y)} : uint2{0, 0};
+  }
+  const int kq = lane >> 4, jj = lane & 15, k2 = wv;
+  uint4 wr[4][4];
+  const uint4* gw = Gb + (size_t)(cls * 8 + k2) * 16 * 64;
+#pragma unroll
+  for (int t = 0; t < 4; ++t)
+#pragma unroll
+    for (int mq = 0; mq < 4; ++mq) wr[t][mq] = gw[(4 * t + kq) * 64 + 16 * mq + jj];
+  lds_barrier();
+  const uint4 m = {0x80000000u, 0x80000000u, 0x80000000u, 0x80000000u};
+  f32x4 acc[8] = {};
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    const bf16x8 sb = __builtin_bit_cast(bf16x8, tile[sidx(k2, 4 * t + kq, jj)]);
+#pragma unroll
+    for (int mq = 0; mq < 4; ++mq) {
+      const uint4 g = wr[t][mq];
+      acc[mq] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, g ^ m), sb, acc[mq], 0, 0, 0);
+      acc[4 + mq] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, (g >> 16) | (g << 16)), sb,
+                                                            acc[4 + mq], 0, 0, 0);
+    }
+  }
+  lds_barrier();
+  constexpr int YLD = 16 * 8 * 2 + 1;
+  f32x4* ytile = reinterpret_cast<f32x4*>(tile);
+#pragma unroll
+  for (int mq = 0; mq < 4; ++mq) {
+    const int cqo = 4 * mq + kq;
+    const f32x4 re = acc[mq], im = acc[4 + mq];
+    ytile[jj * YLD + (cqo * 8 + k2) * 2] = f32x4{re[0], im[0], re[1], im[1]};
+    ytile[jj * YLD + (cqo * 8 + k2) * 2 + 1] = f32x4{re[2], im[2], re[3], im[3]};
+  }
+  lds_barrier();
+  cpx yv[2][8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const f32x4 pv = ytile[bl * YLD + (cq * 8 + q) * 2 + hf];
+    yv[0][q] = cpx{pv[0], pv[1]};
+    yv[1][q] = cpx{pv[2], pv[3]};
+  }
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    dft8<1>(yv[e]);
+#pragma unroll
+    for (int n2 = 0; n2 < 8; ++n2) yv[e][n2] = twid<1>(yv[e][n2], n2 * k1);
+  }
+  if (live) {
+#pragma unroll
+    for (int n2 = 0; n2 < 8; ++n2)
+      reinterpret_cast<uint2*>(Z + z_off(b, n2, fx, k1))[a] =
+          uint2{pack_bf2(yv[0][n2].x, yv[0][n2].y), pack_bf2(yv[1][n2].x, yv[1][n2].y)};
+  }
+}
+
 // ------------------------------------------------------------------------------------ launchers
 bool fft4_enabled() {
   static const bool v = [] {
@@ -961,10 +1066,13 @@ static bool col8_enabled() {
   return v;
 }
 
-hipError_t launch_col_gemm(void* Z, const void* Gc, int B, float unscale, hipStream_t st) {
+hipError_t launch_col_gemm(void* Z, const void* Gc, int B, float unscale, hipStream_t st, bool bf) {
   if (B <= 0) return hipSuccess;
   const int ngrp = (B + CG_NI - 1) / CG_NI;
-  if (col8_enabled())
+  if (bf)
+    hipLaunchKernelGGL(col8_bf_kernel, dim3(CG_NC8 * 8 * ngrp), dim3(512), 0, st, Z, static_cast<const uint4*>(Gc), B,
+                       ngrp);
+  else if (col8_enabled())
     hipLaunchKernelGGL(col8_kernel, dim3(CG_NC8 * 8 * ngrp), dim3(512), 0, st, static_cast<cpx*>(Z),
                        static_cast<const uint4*>(Gc), B, ngrp, unscale);
   else
@@ -974,11 +1082,23 @@ hipError_t launch_col_gemm(void* Z, const void* Gc, int B, float unscale, hipStr
 }
 
 hipError_t launch_row(int mode, void* Z, const ConvArgs& a, const void* or_x3, float or_us, const void* ir_x3,
-                      float ir_us, const float* O0, int B, hipStream_t st) {
+                      float ir_us, const float* O0, int B, hipStream_t st, bool bf) {
   if (B <= 0) return hipSuccess;
   if (a.H < 1 || a.H > 64 || (a.W != 32 && a.W != 64)) return hipErrorInvalidValue;
   cpx* z = static_cast<cpx*>(Z);
   const dim3 g(B * 8), t(RK_NT);
+  if (bf) {
+#define MP_ROW2BF(M) hipLaunchKernelGGL((row2_kernel<M, true, true>), g, t, 0, st, Z, a, or_x3, or_us, ir_x3, ir_us, O0)
+    switch (mode) {
+      case ROW_A: MP_ROW2BF(ROW_A); break;
+      case ROW_B: MP_ROW2BF(ROW_B); break;
+      case ROW_FINAL: MP_ROW2BF(ROW_FINAL); break;
+      case ROW_INIT: MP_ROW2BF(ROW_INIT); break;
+      default: return hipErrorInvalidValue;
+    }
+#undef MP_ROW2BF
+    return hipGetLastError();
+  }
   if (row2_enabled()) {
     const bool pre = row2_preo();
     switch (mode) {

@@ -102,7 +102,7 @@ void finalize_circuit(mp_ctx* c, const std::vector<float>* outs, const std::vect
   } else if (is_fft(c->dtype)) {
     const bool bf = c->dtype == MP_DTYPE_BF16;
     c->spec_g.alloc(fft_weight_bytes());
-    c->fft4 = c->dtype == MP_DTYPE_F32_FFT && fft4_enabled();
+    c->fft4 = fft4_enabled() && (c->dtype == MP_DTYPE_F32_FFT || (bf && fft_bf16_maps()));
     hip_check(build_spec_weights(it->second.dev->f(), c->ssf, c->spec_g.p, &c->p_unscale, bf, c->fft4), "p_r spectrum");
     c->or_x3.alloc(gate_x3_bytes());
     c->ir_x3.alloc(gate_x3_bytes());
@@ -376,10 +376,12 @@ void fft_circuit_range(mp_ctx* c, int b0, int n, int H, int W, int T, float* fin
 void fft4_circuit_range(mp_ctx* c, int b0, int n, int H, int W, int T, const float* o0_nhwc, float* final_dst2,
                         const StateOut* so, const SplitOut* sp, hipStream_t st) {
   const size_t m = (size_t)b0 * 64 * H * W;
-  void* Z = static_cast<char*>(c->specS.p) + fft_spec_bytes(b0);
-  float* X = c->X.f() + m;
-  float* O = c->O.f() + m;
-  float* I = c->I.f() + m;
+  const bool bf = c->dtype == MP_DTYPE_BF16;   // bf16 Z (half a spectrum's bytes per image) and maps
+  void* Z = static_cast<char*>(c->specS.p) + fft_spec_bytes(b0) / (bf ? 2 : 1);
+  auto map = [&](DevBuf& buf) { return bf ? reinterpret_cast<float*>(reinterpret_cast<uint16_t*>(buf.p) + m) : buf.f() + m; };
+  float* X = map(c->X);
+  float* O = map(c->O);
+  float* I = map(c->I);
   {
     ConvArgs a0{};
     a0.H = H;
@@ -388,7 +390,7 @@ void fft4_circuit_range(mp_ctx* c, int b0, int n, int H, int W, int T, const flo
     a0.vecs = c->vecs.f();
     ProfScope pa(c, st, "conv15_a");
     ProfScope ps(c, st, "row_init");
-    hip_check(launch_row(3, Z, a0, c->or_x3.p, c->or_us, c->ir_x3.p, c->ir_us, o0_nhwc + m, n, st), "row_init");
+    hip_check(launch_row(3, Z, a0, c->or_x3.p, c->or_us, c->ir_x3.p, c->ir_us, o0_nhwc + m, n, st, bf), "row_init");
   }
   for (int t = 0; t < T; ++t) {
     ConvArgs a{};
@@ -413,22 +415,22 @@ void fft4_circuit_range(mp_ctx* c, int b0, int n, int H, int W, int T, const flo
       ProfScope pa(c, st, "conv15_a");
       {
         ProfScope ps(c, st, "col_gemm");
-        hip_check(launch_col_gemm(Z, c->spec_g.p, n, c->p_unscale, st), "col_gemm");
+        hip_check(launch_col_gemm(Z, c->spec_g.p, n, c->p_unscale, st, bf), "col_gemm");
       }
       ProfScope ps(c, st, "row_a");
-      hip_check(launch_row(0, Z, a, c->or_x3.p, c->or_us, c->ir_x3.p, c->ir_us, nullptr, n, st), "row_a");
+      hip_check(launch_row(0, Z, a, c->or_x3.p, c->or_us, c->ir_x3.p, c->ir_us, nullptr, n, st, bf), "row_a");
     }
     {
       ProfScope pb(c, st, "conv15_b");
       {
         ProfScope ps(c, st, "col_gemm");
-        hip_check(launch_col_gemm(Z, c->spec_g.p, n, c->p_unscale, st), "col_gemm");
+        hip_check(launch_col_gemm(Z, c->spec_g.p, n, c->p_unscale, st, bf), "col_gemm");
       }
       ProfScope ps(c, st, last ? "row_final" : "row_b");
-      hip_check(launch_row(last ? 2 : 1, Z, b, c->or_x3.p, c->or_us, c->ir_x3.p, c->ir_us, nullptr, n, st),
+      hip_check(launch_row(last ? 2 : 1, Z, b, c->or_x3.p, c->or_us, c->ir_x3.p, c->ir_us, nullptr, n, st, bf),
                 last ? "row_final" : "row_b");
     }
-    store_step(so, O, I, b0, n, H, W, t, false, st, fft_c4_maps(), fft_c4_state());
+    store_step(so, O, I, b0, n, H, W, t, bf, st, fft_c4_maps(), fft_c4_state());
   }
 }
 

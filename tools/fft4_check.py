@@ -20,6 +20,7 @@ p = argparse.ArgumentParser()
 p.add_argument("--batch", type=int, default=256)
 p.add_argument("--steps", type=int, default=20)
 p.add_argument("--child", default=None)
+p.add_argument("--dtype", default="f32_fft")
 a = p.parse_args()
 dev = torch.device("cuda:0")
 T = 8
@@ -27,7 +28,7 @@ wts = {v.name: W.synth_value(v, 1234, T) for v in W.hgru_pose_vars(output_shape=
 ctx = mp._lib.Context(mp._lib.MP_MODEL_HGRU_POSE, 0)
 for k, v in wts.items():
     ctx.set_weight(k, v)
-ctx.finalize(mp._lib.dtype_code("f32_fft"))
+ctx.finalize(mp._lib.dtype_code(a.dtype))
 st = mp._lib.current_stream(dev)
 NB = 37   # odd: a partial 32-image group and partial slices
 d = W.synth_crops(NB, seed=42, size=128)
@@ -39,7 +40,7 @@ got = out.cpu().numpy()
 if a.child:
     np.save(a.child, got)
     sys.exit(0)
-res = {"fft4": os.environ.get("MP_FFT4", "1")}
+res = {"fft4": os.environ.get("MP_FFT4", "1"), "dtype": a.dtype, "fft_loop": ctx.info("fft_loop")}
 one = torch.empty((1, 69), device=dev)
 ctx.pose_fwd(torch.from_numpy(d[5:6]).to(dev), torch.from_numpy(o0[5:6]).to(dev), one, st)
 torch.cuda.synchronize()
@@ -53,7 +54,7 @@ r64 = R.hgru_pose_forward(d[:2], wts, o0[:2], T, np.float64)
 res["rel_err_fp64_oracle"] = float(np.abs(got[:2] - r64).max() / np.abs(r64).max())
 env = dict(os.environ, MP_FFT4="0")
 tmp = "/tmp/fft4_old.npy"
-r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", tmp], env=env, capture_output=True,
+r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", tmp, "--dtype", a.dtype], env=env, capture_output=True,
                    text=True, timeout=300)
 if r.returncode == 0:
     old = np.load(tmp)
@@ -88,3 +89,19 @@ for name in ("row_init", "col_gemm", "row_a", "row_b", "row_final", "fft_fwd", "
     if n:
         prof[name] = {"avg_ms": round(ms / n, 4), "per_fwd_ms": round(ms / 3, 3), "launches_per_fwd": n / 3}
 print(json.dumps(prof), flush=True)
+small = {}
+for bs in (1, 8, 32, 64, 128):
+    d1 = depth[:bs].contiguous()
+    h1 = h0[:bs].contiguous()
+    o1 = torch.empty((bs, 69), device=dev)
+    for _ in range(3):
+        ctx.pose_fwd(d1, h1, o1, st)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    n = 20
+    for _ in range(n):
+        ctx.pose_fwd(d1, h1, o1, st)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / n
+    small[bs] = {"ms": round(dt * 1e3, 3), "crops_per_s": round(bs / dt, 1)}
+print(json.dumps({"small_batch": small}), flush=True)
