@@ -929,27 +929,14 @@ constexpr int SG_YLD = 16 * 4 * 2 + 1; // Y tile pitch (16-B units) per image
 template <int PROBE = 0, int NI = SG_NI>   // timing probes (tools/bench_fft.hip): 1 = no MFMA, 2 = no S / weight loads,
                                           // 3 = no weight loads, 4 = no S loads
 __global__ __launch_bounds__(256, NI == SG_NI ? 2 : SPEC_SMALL_MINB) void spec_gemm_kernel(const uint4* __restrict__ S, const uint4* __restrict__ Gc,
-                                                           uint4* __restrict__ Y, int B, int ngrp, float unscale,
-                                                           int gmaj) {
+                                                           uint4* __restrict__ Y, int B, int ngrp, float unscale) {
   constexpr int SLD = NI + 1;               // S tile pitch (16-B units) per (cq, part, f) row
   constexpr int NLD = NI * 16 * 8 / 256;    // 16-B S / Y pieces per thread
   __shared__ uint4 tile[16 * 2 * 4 * SLD];   // 67,584 B (NI = 32)
   static_assert(NI * SG_YLD <= 16 * 2 * 4 * SLD, "the Y tile fits in the S tile's space");
   // block -> (quad, image group): the ngrp groups of quad q run on XCD q % 8 (round-robin dispatch)
-  // gmaj = G > 0: passes of G image groups, last groups first (quad q still on XCD q % 8, a pass's G
-  // groups of a quad one after the other), so the first blocks read the S lines the forward FFT wrote
-  // last and the last ones write the Y lines the inverse FFT reads first
-  int grp, quad;
-  if (gmaj) {
-    const int nb = NQ8 * 8, ps = blockIdx.x / (gmaj * nb), off = blockIdx.x - ps * gmaj * nb;
-    const int gp = min(gmaj, ngrp - ps * gmaj), q8 = off / (8 * gp), rem = off - q8 * 8 * gp;
-    grp = ngrp - 1 - (ps * gmaj + (rem >> 3));
-    quad = q8 * 8 + (rem & 7);
-  } else {
-    const int q8 = blockIdx.x / (8 * ngrp), rem = blockIdx.x - q8 * 8 * ngrp;
-    grp = rem >> 3;
-    quad = q8 * 8 + (rem & 7);
-  }
+  const int q8 = blockIdx.x / (8 * ngrp), rem = blockIdx.x - q8 * 8 * ngrp;
+  const int grp = rem >> 3, quad = q8 * 8 + (rem & 7);
   if (quad >= NQUAD) return;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, j = lane & 31;
   const int img0 = grp * NI;
@@ -1058,23 +1045,12 @@ __global__ __launch_bounds__(256, NI == SG_NI ? 2 : SPEC_SMALL_MINB) void spec_g
 constexpr int NQ16 = (NQUAD + 15) / 16;
 constexpr int SGB_YLD = 16 * 4 + 1;    // Y tile pitch (16-B units) per image
 __global__ __launch_bounds__(256, 2) void spec_gemm_bf_kernel(const uint4* __restrict__ S, const uint4* __restrict__ Gb,
-                                                              uint4* __restrict__ Y, int B, int ngrp, int gmaj) {
+                                                              uint4* __restrict__ Y, int B, int ngrp) {
   __shared__ uint4 tile[16 * 4 * SG_SLD];   // 33,792 B (S tile [cq][f][b]; Y tile [b][cq][f])
   // block -> (quad, image group): XCD x = rem % 8 takes the quad pair (2x, 2x+1) of each 16
-  // (gmaj: passes of image groups, last first, as in spec_gemm_kernel)
-  int grp, quad;
-  if (gmaj) {
-    const int nb = NQ16 * 16, ps = blockIdx.x / (gmaj * nb), off = blockIdx.x - ps * gmaj * nb;
-    const int gp = min(gmaj, ngrp - ps * gmaj), q16 = off / (16 * gp), rem = off - q16 * 16 * gp;
-    const int sq = rem >> 3;
-    grp = ngrp - 1 - (ps * gmaj + (sq >> 1));
-    quad = q16 * 16 + 2 * (rem & 7) + (sq & 1);
-  } else {
-    const int q16 = blockIdx.x / (16 * ngrp), rem = blockIdx.x - q16 * 16 * ngrp;
-    const int sq = rem >> 3;
-    grp = sq >> 1;
-    quad = q16 * 16 + 2 * (rem & 7) + (sq & 1);
-  }
+  const int q16 = blockIdx.x / (16 * ngrp), rem = blockIdx.x - q16 * 16 * ngrp;
+  const int sq = rem >> 3;
+  const int grp = sq >> 1, quad = q16 * 16 + 2 * (rem & 7) + (sq & 1);
   if (quad >= NQUAD) return;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, j = lane & 31;
   const int img0 = grp * SG_NI;
@@ -1555,32 +1531,18 @@ static int spec_smallb() {
   return v;
 }
 
-// MP_SPEC_GMAJ = G: spectral-GEMM blocks in passes of G 32-image groups, last pass first (spec_gemm_kernel
-// gmaj); 0 (default) = every quad's groups together, the weights fetched from HBM once per launch.
-// G = 2 beside MP_EPI_REV measured no faster than MP_EPI_REV alone (fp32 B = 256 10.34-10.39 vs
-// 10.37 ms) and raised the GEMM's PMC fetch to 1.30x its algorithmic bytes (the 87 MB of weights once
-// per pass); G = 1 lost (10.93 ms; profiles/r4o, profiles/r4z_gmaj2)
-static int spec_gmaj() {
-  static const int v = [] {
-    const char* e = std::getenv("MP_SPEC_GMAJ");
-    return e ? std::max(0, std::atoi(e)) : 0;   // negative = off (a negative pass size would index past the buffers)
-  }();
-  return v;
-}
-
 hipError_t launch_spec_gemm(const void* S, const void* Gx, void* Y, int B, float unscale, hipStream_t st, bool bf) {
   const bool small = !bf && B <= spec_smallb();
   const int ngrp = small ? (B + 7) / 8 : (B + SG_NI - 1) / SG_NI;
-  const int gm = small ? 0 : spec_gmaj();
   if (bf)
     hipLaunchKernelGGL(spec_gemm_bf_kernel, dim3(NQ16 * 16 * ngrp), dim3(256), 0, st, static_cast<const uint4*>(S),
-                       static_cast<const uint4*>(Gx), static_cast<uint4*>(Y), B, ngrp, gm);
+                       static_cast<const uint4*>(Gx), static_cast<uint4*>(Y), B, ngrp);
   else if (small)
     hipLaunchKernelGGL((spec_gemm_kernel<0, 8>), dim3(NQ8 * 8 * ngrp), dim3(256), 0, st, static_cast<const uint4*>(S),
-                       static_cast<const uint4*>(Gx), static_cast<uint4*>(Y), B, ngrp, unscale, 0);
+                       static_cast<const uint4*>(Gx), static_cast<uint4*>(Y), B, ngrp, unscale);
   else
     hipLaunchKernelGGL(spec_gemm_kernel<0>, dim3(NQ8 * 8 * ngrp), dim3(256), 0, st, static_cast<const uint4*>(S),
-                       static_cast<const uint4*>(Gx), static_cast<uint4*>(Y), B, ngrp, unscale, gm);
+                       static_cast<const uint4*>(Gx), static_cast<uint4*>(Y), B, ngrp, unscale);
   return hipGetLastError();
 }
 

@@ -68,6 +68,10 @@ CASES = [
     ({"MP_GRAPH_FUSE_POOL": "0"}, "hier", "bf16", 5e-3),
     ({"MP_IGEMM_HALO_TALL": "0"}, "hier", "fp32_split", 1e-4),
     ({"MP_IGEMM_SMALL_SPLITK": "0"}, "dense_hier", "fp32_split", 1e-4),
+    # the six-launch FFT loop and the one-block-per-CU row kernel (A/B forms of the four-step loop)
+    ({"MP_FFT4": "0"}, "pose", "fp32_fft", 1e-4),
+    ({"MP_FFT4": "0"}, "pose", "bf16", 5e-3),
+    ({"MP_ROW2": "0"}, "pose", "fp32_fft", 1e-4),
     ({"MP_IGEMM_PW": "0", "MP_IGEMM_HALO_NARROW": "0"}, "dense", "fp32_split", 1e-4),
     ({"MP_IGEMM_PW": "0", "MP_IGEMM_HALO_NARROW": "0"}, "dense", "bf16", 5e-3),
     ({"MP_GRAPH_FUSE_1X1": "0"}, "dense", "fp32_split", 1e-4),
@@ -115,26 +119,29 @@ print(json.dumps({{"sha": hashlib.sha256(np.ascontiguousarray(out).tobytes()).he
 BITS_CASES = [
     # igemm_x3pwn_kernel (one block over all 2 / 3 / 5 / 6 cout blocks of a 1x1 conv) runs each
     # output's MFMA sequence of igemm_x3pw_kernel: MP_IGEMM_PWN = 0 / 1 / 2 give the same bytes
-    ("dense", "fp32_split", "MP_IGEMM_PWN", ("0", "1", "2", "3")),
-    ("dense", "bf16", "MP_IGEMM_PWN", ("0", "1", "2", "3")),
-    # the spectral GEMM on 8-image tiles (two groups at 12 crops) vs the 32-image tiles
-    ("pose", "fp32_fft", "MP_SPEC_SMALLB", ("8", "32")),
-    # image order only: the B epilogue last image first, the spectral GEMM in passes of G groups
-    ("pose80", "fp32_fft", "MP_EPI_REV", ("0", "1")),
-    ("pose80", "fp32_fft", "MP_SPEC_GMAJ", ("0", "1", "2")),
-    ("pose80", "bf16", "MP_SPEC_GMAJ", ("0", "1", "2")),
+    ("dense", "fp32_split", "MP_IGEMM_PWN", ("0", "1", "2", "3"), {}),
+    ("dense", "bf16", "MP_IGEMM_PWN", ("0", "1", "2", "3"), {}),
+    # six-launch loop (MP_FFT4=0): the spectral GEMM on 8-image tiles (two groups at 12 crops) vs the
+    # 32-image tiles; the B epilogue's image order
+    ("pose", "fp32_fft", "MP_SPEC_SMALLB", ("8", "32"), {"MP_FFT4": "0"}),
+    ("pose80", "fp32_fft", "MP_EPI_REV", ("0", "1"), {"MP_FFT4": "0"}),
+    # four-step loop: the four- and eight-wave column kernels run each output's MFMA and DFT sequence
+    # identically; the B epilogue's O loads before / after the o_r gate move nothing but timing
+    ("pose80", "fp32_fft", "MP_COL8", ("0", "1"), {}),
+    ("pose80", "fp32_fft", "MP_ROW2_PREO", ("0", "1"), {}),
+    ("pose80", "bf16", "MP_ROW2_PREO", ("0", "1"), {}),
 ]
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kind,dtype,var,values", BITS_CASES, ids=[f"{c[2]}-{c[0]}-{c[1]}" for c in BITS_CASES])
-def test_switch_is_bit_identical(kind, dtype, var, values):
+@pytest.mark.parametrize("kind,dtype,var,values,base", BITS_CASES, ids=[f"{c[2]}-{c[0]}-{c[1]}" for c in BITS_CASES])
+def test_switch_is_bit_identical(kind, dtype, var, values, base):
     """Switches whose forms compute every output with the same operations in the same order: the
     model output is the same bytes under each setting (one child process per setting)."""
     shas = []
     for v in values:
         code = _CHILD_BITS.format(tests=os.path.join(ROOT, "tests"), kind=kind, dtype=dtype)
-        r = subprocess.run([sys.executable, "-c", code], env={**os.environ, var: v},
+        r = subprocess.run([sys.executable, "-c", code], env={**os.environ, **base, var: v},
                            capture_output=True, text=True, timeout=110)
         assert r.returncode == 0, r.stderr[-2000:]
         shas.append(json.loads(r.stdout.strip().splitlines()[-1])["sha"])

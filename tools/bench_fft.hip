@@ -89,7 +89,7 @@ int main(int argc, char** argv) {
 #define PRB(K)                                                                                          \
   if (v == K)                                                                                         \
     hipLaunchKernelGGL(spec_gemm_kernel<K>, dim3(nq8 * 8 * ngrp), dim3(256), 0, 0, (const uint4*)S, \
-                       (const uint4*)Gx, (uint4*)Y, B, ngrp, unscale, 0);
+                       (const uint4*)Gx, (uint4*)Y, B, ngrp, unscale);
     PRB(1) PRB(2) PRB(3) PRB(4)
 #undef PRB
     return hipGetLastError();
