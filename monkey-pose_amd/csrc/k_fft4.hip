@@ -658,6 +658,106 @@ __global__ __launch_bounds__(RK_NT, 2) void row2_kernel(void* __restrict__ Z, Co
 }
 
 // ---------------------------------------------------------------------------------------------
+// row kernel, eight waves (row8_kernel; small batches, MP_ROW8_MAXB): row2_kernel's block, phases and
+// per-element arithmetic re-parallelised for a full chip at few images -- 512 threads, wave w owns
+// row n1 = w alone, the whole T (151.5 KB, one block per CU) so both transposes run in one round.
+// Every value is produced by the same dft9 / rfft72 / rk_segment code as in row2_kernel: the two are
+// bit-identical (tests/test_gpu_parity.py batch invariance across the switch).
+// ---------------------------------------------------------------------------------------------
+constexpr int R8_NT = 512;
+constexpr int R8_NIT = (RK_ITEMS + R8_NT - 1) / R8_NT;   // 5
+
+template <int MODE, bool BF = false>
+__global__ __launch_bounds__(R8_NT, 1) void row8_kernel(void* __restrict__ Z, ConvArgs p, const void* __restrict__ or_x3,
+                                                        float or_us, const void* __restrict__ ir_x3, float ir_us,
+                                                        const float* __restrict__ O0) {
+  __shared__ cpx T[RK_T];
+  __shared__ float vsh[V_COUNT * 64];
+  const int b = blockIdx.x >> 3, n2 = blockIdx.x & 7;
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  for (int i = tid; i < V_COUNT * 64; i += R8_NT) vsh[i] = p.vecs[i];
+  const int H = p.H, W = p.W;
+  const int y = 8 * w + n2;
+  const bool live = y < H;
+  cpx* slot = T + w * FX * 64;
+  float* stg = reinterpret_cast<float*>(slot);
+  float P[64];
+  if constexpr (MODE != ROW_INIT) {
+    {
+      cpx u[R8_NIT][9];
+#pragma unroll
+      for (int it = 0; it < R8_NIT; ++it) {
+        const int i = min(it * R8_NT + tid, RK_ITEMS - 1);
+        const size_t src = z_off(b, n2, i >> 6, 0) + (i & 63);
+#pragma unroll
+        for (int k1 = 0; k1 < 9; ++k1) u[it][k1] = z_ld<BF>(Z, src + k1 * 64);
+      }
+#pragma unroll
+      for (int it = 0; it < R8_NIT; ++it) {
+        const int i = it * R8_NT + tid;
+        dft9<1>(u[it]);
+        if (i < RK_ITEMS) {
+          const int fx = i >> 6, c = i & 63;
+#pragma unroll
+          for (int r = 0; r < 8; ++r) T[(r * FX + fx) * 64 + c] = u[it][r];
+        }
+      }
+    }
+    lds_barrier();
+    {
+      cpx A[FX];
+#pragma unroll
+      for (int k = 0; k < FX; ++k) A[k] = slot[k * 64 + lane];
+      rfft72_inv(A, P);
+    }
+    if (live) {
+#pragma unroll
+      for (int x = 0; x < 64; ++x)
+        if (x < W) stg[x * RK_SP + lane] = P[x];   // (in-wave order: after the reads above)
+    }
+  } else {
+    lds_barrier();   // vsh
+  }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  if (live) {
+#pragma unroll 1
+    for (int sg = 0; sg < 2; ++sg) {
+      const int xs = 32 * sg;
+      if (xs >= W) continue;   // wave-uniform
+      SegIn L;
+      rk_load_seg<MODE, true, BF>(p, O0, b, y, xs, lane, L);
+      rk_segment<MODE, true, true, BF>(p, stg + xs * RK_SP, b, y, xs, lane, L, or_x3, or_us, ir_x3, ir_us, vsh);
+    }
+  }
+  if constexpr (MODE == ROW_FINAL) return;
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int x = 0; x < 64; ++x) P[x] = (live && x < W) ? stg[x * RK_SP + lane] : 0.f;
+  {
+    cpx X[FX];
+    rfft72_fwd(P, X);
+#pragma unroll
+    for (int k = 0; k < FX; ++k) slot[k * 64 + lane] = X[k];   // (in-wave order: after the reads above)
+  }
+  lds_barrier();
+  const int ts = opaque(tid);
+#pragma unroll
+  for (int it = 0; it < R8_NIT; ++it) {
+    const int i = it * R8_NT + ts;
+    if (i >= RK_ITEMS) break;
+    const int fx = i >> 6, c = i & 63;
+    cpx u[9];
+#pragma unroll
+    for (int r = 0; r < 8; ++r) u[r] = T[(r * FX + fx) * 64 + c];
+    u[8] = cpx{0.f, 0.f};
+    dft9<-1>(u);
+    const size_t dst = z_off(b, n2, fx, 0) + c;
+#pragma unroll
+    for (int k1 = 0; k1 < 9; ++k1) z_st<BF>(Z, dst + k1 * 64, u[k1]);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // column kernel (the spectral GEMM).  Block = (column class (fx, k1), 16 images), 256 threads, two
 // blocks per CU (68 KB of LDS).  Thread (image, channel pair a) holds channels 2a, 2a + 1 and
 // 32 + 2a, 33 + 2a of its image (each wave instruction reads / writes contiguous 256-B runs of Z) and
@@ -1048,6 +1148,16 @@ static bool row2_enabled() {
   return v;
 }
 
+// MP_ROW8_MAXB (default 32): the largest launch batch on the eight-wave, one-block-per-CU row kernel
+// (a full chip at few images; bit-identical to row2_kernel, which fills two blocks per CU above it)
+static int row8_maxb() {
+  static const int v = [] {
+    const char* e = std::getenv("MP_ROW8_MAXB");
+    return e ? std::atoi(e) : 32;
+  }();
+  return v;
+}
+
 // MP_ROW2_PREO (default 1): B epilogue segments load O with I, before the o_r gate; 0: after it
 static bool row2_preo() {
   static const bool v = [] {
@@ -1087,6 +1197,25 @@ hipError_t launch_row(int mode, void* Z, const ConvArgs& a, const void* or_x3, f
   if (a.H < 1 || a.H > 64 || (a.W != 32 && a.W != 64)) return hipErrorInvalidValue;
   cpx* z = static_cast<cpx*>(Z);
   const dim3 g(B * 8), t(RK_NT);
+  if (B <= row8_maxb()) {
+#define MP_ROW8(M, BFV) hipLaunchKernelGGL((row8_kernel<M, BFV>), g, dim3(R8_NT), 0, st, Z, a, or_x3, or_us, ir_x3, ir_us, O0)
+#define MP_ROW8S(BFV)                          \
+  switch (mode) {                              \
+    case ROW_A: MP_ROW8(ROW_A, BFV); break;         \
+    case ROW_B: MP_ROW8(ROW_B, BFV); break;         \
+    case ROW_FINAL: MP_ROW8(ROW_FINAL, BFV); break; \
+    case ROW_INIT: MP_ROW8(ROW_INIT, BFV); break;   \
+    default: return hipErrorInvalidValue;      \
+  }
+    if (bf) {
+      MP_ROW8S(true)
+    } else {
+      MP_ROW8S(false)
+    }
+#undef MP_ROW8S
+#undef MP_ROW8
+    return hipGetLastError();
+  }
   if (bf) {
 #define MP_ROW2BF(M) hipLaunchKernelGGL((row2_kernel<M, true, true>), g, t, 0, st, Z, a, or_x3, or_us, ir_x3, ir_us, O0)
     switch (mode) {
