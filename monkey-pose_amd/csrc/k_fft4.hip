@@ -1148,12 +1148,15 @@ static bool row2_enabled() {
   return v;
 }
 
-// MP_ROW8_MAXB (default 32): the largest launch batch on the eight-wave, one-block-per-CU row kernel
-// (a full chip at few images; bit-identical to row2_kernel, which fills two blocks per CU above it)
+// MP_ROW8_MAXB (default: every batch): the largest launch batch on the eight-wave, one-block-per-CU row
+// kernel; above it row2_kernel (two blocks per CU, bit-identical).  Measured on one box (fp32, B = 256,
+// profiles/r5d): row8 everywhere 9.04 ms per forward (row A 0.282, row B 0.386 ms), row2 above 32
+// images 9.61 ms (0.318, 0.440): row2's second round of transposes and its register spills cost more
+// than its second block per CU gains
 static int row8_maxb() {
   static const int v = [] {
     const char* e = std::getenv("MP_ROW8_MAXB");
-    return e ? std::atoi(e) : 32;
+    return e ? std::atoi(e) : (1 << 30);
   }();
   return v;
 }

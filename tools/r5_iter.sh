@@ -11,8 +11,8 @@ timeout -k 10 300 python tools/fft4_check.py > "$out/fft4_check.log" 2>&1 || exi
 for dt in $DT; do
   timeout -k 10 300 python tools/fft4_check.py --dtype $dt > "$out/fft4_check_$dt.log" 2>&1 || exit 1
 done
-for kv in $AB; do
-  env "$kv" timeout -k 10 300 python tools/fft4_check.py > "$out/fft4_check_$kv.log" 2>&1 || exit 1
+for kv in $AB; do   # one A/B setting per word; several variables joined by commas
+  env $(echo "$kv" | tr ',' ' ') timeout -k 10 300 python tools/fft4_check.py > "$out/fft4_check_$kv.log" 2>&1 || exit 1
 done
 if [ $# -gt 0 ]; then
   timeout -k 10 900 python -u -m pytest -x -v --timeout 120 --timeout-method thread "$@" > "$out/gpu_tests.log" 2>&1 || exit 1
