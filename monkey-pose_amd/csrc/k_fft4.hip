@@ -667,11 +667,19 @@ __global__ __launch_bounds__(RK_NT, 2) void row2_kernel(void* __restrict__ Z, Co
 constexpr int R8_NT = 512;
 constexpr int R8_NIT = (RK_ITEMS + R8_NT - 1) / R8_NT;   // 5
 
+// LDS of row8_kernel: T[n1][fx][c] (151.5 KB) for the two transposes; during the epilogue its first
+// 69.6 KB hold one 32-pixel staging segment per wave and the next 32 KB the two gates' packed weights
+// (read from L2 once per block instead of once per segment and wave: 0.5 MB less L2 traffic a block)
+// (ROW_FINAL, one gate: a whole 64-pixel row per wave, so no row stays in registers across the epilogue)
+constexpr int R8_GATE = 2 * 4 * 2 * 64;                  // f16x8 of one gate's f16x3 pack (gate_x3_bytes / 16)
+constexpr int R8_T = (8 * 64 * RK_SP * 4 + R8_GATE * 16) / 8;   // 155,648 B: T grown by 512 B for FINAL
+static_assert(R8_T >= RK_T && (8 * 32 * RK_SP * 4 + 2 * R8_GATE * 16) <= R8_T * 8, "staging + gate weights fit");
+
 template <int MODE, bool BF = false>
 __global__ __launch_bounds__(R8_NT, 1) void row8_kernel(void* __restrict__ Z, ConvArgs p, const void* __restrict__ or_x3,
                                                         float or_us, const void* __restrict__ ir_x3, float ir_us,
                                                         const float* __restrict__ O0) {
-  __shared__ cpx T[RK_T];
+  __shared__ cpx T[R8_T];
   __shared__ float vsh[V_COUNT * 64];
   const int b = blockIdx.x >> 3, n2 = blockIdx.x & 7;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
@@ -680,7 +688,11 @@ __global__ __launch_bounds__(R8_NT, 1) void row8_kernel(void* __restrict__ Z, Co
   const int y = 8 * w + n2;
   const bool live = y < H;
   cpx* slot = T + w * FX * 64;
-  float* stg = reinterpret_cast<float*>(slot);
+  constexpr int SPIX = MODE == ROW_FINAL ? 64 : 32;                        // staged pixels per wave
+  float* stg = reinterpret_cast<float*>(T) + w * SPIX * RK_SP;             // epilogue staging (after Ib)
+  uint4* gsh = reinterpret_cast<uint4*>(reinterpret_cast<float*>(T) + 8 * SPIX * RK_SP);   // gate weights
+  constexpr bool OR = MODE == ROW_B || MODE == ROW_FINAL, IR = MODE == ROW_B || MODE == ROW_INIT;
+  constexpr int GN = BF ? R8_GATE / 2 : R8_GATE;   // uint4 per gate (bf16: one product, no lo plane)
   float P[64];
   if constexpr (MODE != ROW_INIT) {
     {
@@ -710,34 +722,58 @@ __global__ __launch_bounds__(R8_NT, 1) void row8_kernel(void* __restrict__ Z, Co
       for (int k = 0; k < FX; ++k) A[k] = slot[k * 64 + lane];
       rfft72_inv(A, P);
     }
+  }
+  lds_barrier();   // every wave has read its row of T (and vsh is in): T becomes staging + gate weights
+  if constexpr (OR || IR) {
+    const uint4* ow = static_cast<const uint4*>(or_x3);
+    const uint4* iw = static_cast<const uint4*>(ir_x3);
+    for (int i = tid; i < GN; i += R8_NT) {
+      if constexpr (OR) gsh[i] = ow[i];
+      if constexpr (IR) gsh[GN + i] = iw[i];
+    }
+    lds_barrier();
+  }
+  if constexpr (MODE == ROW_FINAL) {
     if (live) {
 #pragma unroll
-      for (int x = 0; x < 64; ++x)
-        if (x < W) stg[x * RK_SP + lane] = P[x];   // (in-wave order: after the reads above)
-    }
-  } else {
-    lds_barrier();   // vsh
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  if (live) {
+      for (int x = 0; x < 64; ++x) stg[x * RK_SP + lane] = P[x];
 #pragma unroll 1
+      for (int sg = 0; sg < 2; ++sg) {
+        const int xs = 32 * sg;
+        if (xs >= W) continue;   // wave-uniform
+        SegIn L;
+        rk_load_seg<MODE, true, BF>(p, O0, b, y, xs, lane, L);
+        rk_segment<MODE, true, true, BF>(p, stg + xs * RK_SP, b, y, xs, lane, L, gsh, or_us, gsh, ir_us, vsh);
+      }
+    }
+    return;
+  }
+  if (live) {
+#pragma unroll
     for (int sg = 0; sg < 2; ++sg) {
       const int xs = 32 * sg;
       if (xs >= W) continue;   // wave-uniform
       SegIn L;
       rk_load_seg<MODE, true, BF>(p, O0, b, y, xs, lane, L);
-      rk_segment<MODE, true, true, BF>(p, stg + xs * RK_SP, b, y, xs, lane, L, or_x3, or_us, ir_x3, ir_us, vsh);
+      if constexpr (MODE != ROW_INIT) {
+#pragma unroll
+        for (int q = 0; q < 32; ++q) stg[q * RK_SP + lane] = P[xs + q];
+      }
+      rk_segment<MODE, true, true, BF>(p, stg, b, y, xs, lane, L, gsh, or_us, gsh + GN, ir_us, vsh);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+      for (int q = 0; q < 32; ++q) P[xs + q] = stg[q * RK_SP + lane];
     }
   }
-  if constexpr (MODE == ROW_FINAL) return;
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
-  for (int x = 0; x < 64; ++x) P[x] = (live && x < W) ? stg[x * RK_SP + lane] : 0.f;
+  for (int x = 0; x < 64; ++x) P[x] = (live && x < W) ? P[x] : 0.f;
   {
     cpx X[FX];
     rfft72_fwd(P, X);
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    lds_barrier();   // every wave is done with the staging and gate weights
 #pragma unroll
-    for (int k = 0; k < FX; ++k) slot[k * 64 + lane] = X[k];   // (in-wave order: after the reads above)
+    for (int k = 0; k < FX; ++k) slot[k * 64 + lane] = X[k];
   }
   lds_barrier();
   const int ts = opaque(tid);
