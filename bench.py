@@ -120,22 +120,27 @@ def fft_kernels(ctx, B, hw, steps, bf16=False):
 # per-kernel HBM bytes per launch from rocprofv3 PMC passes (FETCH_SIZE x2 on gfx950 + WRITE_SIZE,
 # MI355X_MICROARCH.md), collected with the full-batch single-stream launches of this workload by
 # tools/pmc_bytes.py and committed under profiles/ (bench cannot profile itself)
-PMC_TRAFFIC = {False: "profiles/r4z/pmc_traffic_fp32_b256.csv",
-               True: "profiles/r4z/pmc_traffic_bf16_b256.csv"}
+PMC_TRAFFIC = {False: "profiles/r5z/pmc_traffic_fp32_b256.csv",
+               True: "profiles/r5z/pmc_traffic_bf16_b256.csv"}
 PMC_KERNEL = {   # name: (fp32 path's kernel, bf16 path's kernel) as rocprofv3 names them
     "fft_fwd": ("fft_fwd3_kernel", "fft_fwd_kernel<true, true>"),
     "spec_gemm": ("spec_gemm_kernel<0, 32>", "spec_gemm_bf_kernel"),
     "inv_a_fwd": ("fft_inv_a_fwd_kernel<false, false>", "fft_inv_a_fwd_kernel<true, true>"),
     "fft_inv": ("fft_inv_kernel<false, false>", "fft_inv_kernel<true, true>"),
     "epi_b": ("spec_epi_b_kernel<false, false, false>", "spec_epi_b_kernel<true, true, false>"),
-    "col_gemm": ("col_gemm_kernel", None), "row_a": ("row_kernel<0>", None), "row_b": ("row_kernel<1>", None),
-    "row_final": ("row_kernel<2>", None), "row_init": ("row_kernel<3>", None)}
+    # the four-step loop's default kernels (k_fft4.hip: col8 / row8 forms)
+    "col_gemm": ("col8_kernel", "col8_bf_kernel"), "row_a": ("row8_kernel<0, false>", "row8_kernel<0, true>"),
+    "row_b": ("row8_kernel<1, false>", "row8_kernel<1, true>"),
+    "row_final": ("row8_kernel<2, false>", "row8_kernel<2, true>"),
+    "row_init": ("row8_kernel<3, false>", "row8_kernel<3, true>")}
 
 
 # MFMA utilisation per kernel from the committed PMC pass (tools/pmc_mfma.sh / .py: SQ_VALU_MFMA_BUSY_CYCLES
 # over GRBM_GUI_ACTIVE x 1024 SIMDs, the gfx950 MfmaUtil), same one-stream B = 256 workload
-PMC_MFMA = "profiles/r4p/mfma_util_pose_fp32_b256.csv"
-MFMA_KERNELS = {"fc_gemm_x3p (fc_1 on split planes, k_fc.hip)": "fc_gemm_x3p_kernel", "conv64x3 (conv_2/3, k_conv64x3.hip)": "conv64x3_kernel",
+PMC_MFMA = "profiles/r5z/mfma_util_pose_fp32_b256.csv"
+MFMA_KERNELS = {"col8 (four-step spectral GEMM, k_fft4.hip)": "col8_kernel",
+                "row8 B (gate GEMMs, k_fft4.hip)": "row8_kernel<1, false>",
+                "fc_gemm_x3p (fc_1 on split planes, k_fc.hip)": "fc_gemm_x3p_kernel", "conv64x3 (conv_2/3, k_conv64x3.hip)": "conv64x3_kernel",
                 "spec_gemm (k_fft.hip)": "spec_gemm_kernel", "spec_epi_b (gate GEMMs, k_fft.hip)": "spec_epi_b_kernel<false, false, false>",
                 "gate_init_x3 (k_fft.hip)": "gate_init_x3_kernel"}
 
@@ -178,7 +183,8 @@ def fft_roofline(kern, bf16=False, batch=256, hbm_meas=None):
     name = max(kern, key=lambda k: kern[k]["ms_per_step"])
     k = kern[name]
     traffic, src = pmc_traffic(name, bf16, batch)
-    r = {"kernel": name + " (k_fft.hip)", "avg_launch_ms": k["avg_launch_ms"], "launches": k["launches"],
+    src_file = "k_fft4.hip" if name in ("col_gemm", "row_a", "row_b", "row_final", "row_init") else "k_fft.hip"
+    r = {"kernel": f"{name} ({src_file})", "avg_launch_ms": k["avg_launch_ms"], "launches": k["launches"],
          "traffic": traffic, "traffic_source": src, "algo_bytes": k["algo_bytes"]}
     t_hbm = k["algo_bytes"] / (PEAK_HBM_GBPS * 1e9)
     peak = k.get("mfma_peak", round(PEAK_F16_TFLOPS / 3, 1))

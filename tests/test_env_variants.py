@@ -72,7 +72,8 @@ CASES = [
     ({"MP_FFT4": "0"}, "pose", "fp32_fft", 1e-4),
     ({"MP_FFT4": "0"}, "pose", "bf16", 5e-3),
     ({"MP_ROW2": "0", "MP_ROW8_MAXB": "0"}, "pose", "fp32_fft", 1e-4),
-    ({"MP_COLP": "0"}, "pose", "fp32_fft", 1e-4),
+    ({"MP_COLP": "1"}, "pose", "fp32_fft", 1e-4),
+    ({"MP_COLP": "1"}, "pose", "bf16", 5e-3),
     ({"MP_IGEMM_PW": "0", "MP_IGEMM_HALO_NARROW": "0"}, "dense", "fp32_split", 1e-4),
     ({"MP_IGEMM_PW": "0", "MP_IGEMM_HALO_NARROW": "0"}, "dense", "bf16", 5e-3),
     ({"MP_GRAPH_FUSE_1X1": "0"}, "dense", "fp32_split", 1e-4),
@@ -130,8 +131,8 @@ BITS_CASES = [
     # identically (under MP_COLP=0); the persistent column kernel gives the same bytes for any number
     # of image groups per block; the row2 B epilogue's O loads before / after the o_r gate move nothing
     # but timing; the eight-wave row kernel (gate weights in LDS) and row2 compute each value alike
-    ("pose80", "fp32_fft", "MP_COL8", ("0", "1"), {"MP_COLP": "0"}),
-    ("pose80", "fp32_fft", "MP_COLP_GPB", ("1", "2", "3"), {}),
+    ("pose80", "fp32_fft", "MP_COL8", ("0", "1"), {}),
+    ("pose80", "fp32_fft", "MP_COLP_GPB", ("1", "2", "3"), {"MP_COLP": "1"}),
     ("pose80", "fp32_fft", "MP_ROW2_PREO", ("0", "1"), {"MP_ROW8_MAXB": "0"}),
     ("pose80", "bf16", "MP_ROW2_PREO", ("0", "1"), {"MP_ROW8_MAXB": "0"}),
     ("pose80", "fp32_fft", "MP_ROW8_MAXB", ("0", "1000000"), {}),

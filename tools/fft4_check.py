@@ -21,6 +21,7 @@ p.add_argument("--batch", type=int, default=256)
 p.add_argument("--steps", type=int, default=20)
 p.add_argument("--child", default=None)
 p.add_argument("--dtype", default="f32_fft")
+p.add_argument("--quick", action="store_true", help="skip the six-launch comparison and the B = 256 timing")
 a = p.parse_args()
 dev = torch.device("cuda:0")
 T = 8
@@ -53,42 +54,48 @@ from oracle import hgru_ref as R  # noqa: E402  (test infrastructure: the checke
 r64 = R.hgru_pose_forward(d[:2], wts, o0[:2], T, np.float64)
 res["rel_err_fp64_oracle"] = float(np.abs(got[:2] - r64).max() / np.abs(r64).max())
 env = dict(os.environ, MP_FFT4="0")
+if a.quick:
+    print(json.dumps(res), flush=True)
 tmp = "/tmp/fft4_old.npy"
-r = subprocess.run([sys.executable, os.path.abspath(__file__), "--child", tmp, "--dtype", a.dtype], env=env, capture_output=True,
+r = None if a.quick else subprocess.run([sys.executable, os.path.abspath(__file__), "--child", tmp, "--dtype", a.dtype], env=env, capture_output=True,
                    text=True, timeout=300)
-if r.returncode == 0:
+if r is None:
+    pass
+elif r.returncode == 0:
     old = np.load(tmp)
     res["rel_err_vs_six_launch"] = float(np.abs(got - old).max() / np.abs(old).max())
     res["old_rel_err_fp64_oracle"] = float(np.abs(old[:2] - r64).max() / np.abs(r64).max())
 else:
     res["old_error"] = r.stderr[-2000:]
-print(json.dumps(res), flush=True)
+if not a.quick:
+    print(json.dumps(res), flush=True)
 
 B = a.batch
 depth = torch.from_numpy(W.synth_crops(B, seed=42, size=128)).to(dev)
 h0 = torch.from_numpy(W.synth_hidden((B, 64, 64, 64), seed=7)).to(dev)
-ob = torch.empty((B, 69), device=dev)
-for _ in range(3):
-    ctx.pose_fwd(depth, h0, ob, st)
-torch.cuda.synchronize()
-t0 = time.perf_counter()
-for _ in range(a.steps):
-    ctx.pose_fwd(depth, h0, ob, st)
-torch.cuda.synchronize()
-dt = (time.perf_counter() - t0) / a.steps
-print(json.dumps({"batch": B, "ms_per_step": round(dt * 1e3, 3), "crops_per_s": round(B / dt, 1)}), flush=True)
-ctx.profile(True)
-for _ in range(3):
-    ctx.pose_fwd(depth, h0, ob, st)
-torch.cuda.synchronize()
-ctx.profile(False)
-prof = {}
-for name in ("row_init", "col_gemm", "row_a", "row_b", "row_final", "fft_fwd", "spec_gemm", "inv_a_fwd", "fft_inv",
-             "epi_b", "conv15_a", "conv15_b", "fc1", "backbone"):
-    ms, n = ctx.profile_read(name)
-    if n:
-        prof[name] = {"avg_ms": round(ms / n, 4), "per_fwd_ms": round(ms / 3, 3), "launches_per_fwd": n / 3}
-print(json.dumps(prof), flush=True)
+if not a.quick:
+    ob = torch.empty((B, 69), device=dev)
+    for _ in range(3):
+        ctx.pose_fwd(depth, h0, ob, st)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        ctx.pose_fwd(depth, h0, ob, st)
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / a.steps
+    print(json.dumps({"batch": B, "ms_per_step": round(dt * 1e3, 3), "crops_per_s": round(B / dt, 1)}), flush=True)
+    ctx.profile(True)
+    for _ in range(3):
+        ctx.pose_fwd(depth, h0, ob, st)
+    torch.cuda.synchronize()
+    ctx.profile(False)
+    prof = {}
+    for name in ("row_init", "col_gemm", "row_a", "row_b", "row_final", "fft_fwd", "spec_gemm", "inv_a_fwd", "fft_inv",
+                 "epi_b", "conv15_a", "conv15_b", "fc1", "backbone"):
+        ms, n = ctx.profile_read(name)
+        if n:
+            prof[name] = {"avg_ms": round(ms / n, 4), "per_fwd_ms": round(ms / 3, 3), "launches_per_fwd": n / 3}
+    print(json.dumps(prof), flush=True)
 small = {}
 for bs in (1, 8, 32, 64, 128):
     d1 = depth[:bs].contiguous()
