@@ -1087,145 +1087,6 @@ __global__ __launch_bounds__(512, 2) void col8_kernel(cpx* __restrict__ Z, const
   }
 }
 
-// column kernel, persistent over image groups (colp_kernel; MP_COLP=1): block = (class, a chunk of
-// consecutive 16-image groups), one block per CU (eight waves, 256 registers each).  Wave k2 loads its
-// frequency's weights ONCE into 128 registers and keeps them for
-// every group of the chunk (col8 re-reads 256 KiB of weights from L2 per 16 images).  The compact
-// weights A = (gr, gi) pairs are used as stored; the S fragment supplies the two forms instead,
-// (sr, -si) for the real rows (gr sr - gi si) and (si, sr) for the imaginary ones (gr si + gi sr): one
-// sign flip or half swap per S dword instead of four weight forms per k-step.  The next group's partials
-// are loaded into registers before the current group's GEMM, so their HBM latency hides behind the
-// GEMM, the Y exchange and the inverse DFT.  Same DFTs, split and twiddles as col8_kernel; the
-// imaginary rows' k order within each (re, im) pair differs, so results agree with col8's to fp32
-// rounding, not bit for bit (batch-invariant and deterministic all the same).
-__global__ __launch_bounds__(512, 1) void colp_kernel(cpx* __restrict__ Z, const uint4* __restrict__ Gc, int B,
-                                                      int ngrp, int gpb, int nch, float unscale) {
-  __shared__ uint4 tile[2 * CG_HALF];   // 69,632 B
-  const int c8 = blockIdx.x / (8 * nch), rem = blockIdx.x - c8 * 8 * nch;
-  const int ch = rem >> 3, cls = c8 * 8 + (rem & 7);
-  if (cls >= Z_CLS) return;
-  const int g0 = ch * gpb, g1 = min(g0 + gpb, ngrp);
-  if (g0 >= g1) return;
-  const int fx = cls / 9, k1 = cls - fx * 9;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int bl = tid >> 5, a = tid & 31;
-  const int cq = a >> 1, hf = a & 1;
-  const int kq = lane >> 4, jj = lane & 15, k2 = wv;
-  const uint4 m = {0x80000000u, 0x80000000u, 0x80000000u, 0x80000000u};
-  // Z addressed as a uniform base + a 32-bit byte offset (the launcher checks B x 1.36 MB < 4 GiB), so
-  // each access needs one offset VGPR, not a 64-bit address pair held across the loop
-  char* const zb = reinterpret_cast<char*>(Z);
-  auto zoff = [&](int b, int n2) -> uint32_t {
-    return ((uint32_t)((b * 8 + n2) * FX + fx) * 9u + (uint32_t)k1) * 512u + (uint32_t)a * 16u;
-  };
-  f32x4 zin[8];
-  auto load_z = [&](int g) {
-    const int b = min(g * CG_NI + bl, B - 1);
-#pragma unroll
-    for (int n2 = 0; n2 < 8; ++n2) zin[n2] = *reinterpret_cast<const f32x4*>(zb + zoff(b, n2));
-  };
-  load_z(g0);
-  uint4 wr[4][4][2];
-  {
-    const uint4* gw = Gc + (size_t)(cls * 8 + k2) * 2 * 16 * 64;
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int mq = 0; mq < 4; ++mq) {
-        wr[t][mq][0] = gw[(0 * 16 + 4 * t + kq) * 64 + 16 * mq + jj];
-        wr[t][mq][1] = gw[(1 * 16 + 4 * t + kq) * 64 + 16 * mq + jj];
-      }
-  }
-  f32x4 yo[8];   // a group's output partials, stored during the next group's first phase
-  auto store_y = [&](int g) {
-    const int b = g * CG_NI + bl;
-    if (b < B) {
-#pragma unroll
-      for (int n2 = 0; n2 < 8; ++n2) *reinterpret_cast<f32x4*>(zb + zoff(b, n2)) = yo[n2];
-    }
-  };
-  constexpr int YLD = 16 * 8 * 2 + 1;
-  f32x4* ytile = reinterpret_cast<f32x4*>(tile);
-  for (int g = g0; g < g1; ++g) {
-    const bool live = g * CG_NI + bl < B;
-    {
-      cpx s[2][8];
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-#pragma unroll
-        for (int n2 = 0; n2 < 8; ++n2) s[e][n2] = twid<-1>(cpx{zin[n2][2 * e], zin[n2][2 * e + 1]}, n2 * k1);
-        dft8<-1>(s[e]);
-      }
-      typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
-      uint2* t2 = reinterpret_cast<uint2*>(tile);
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        f16x4 hv, lv;
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const float re = s[e][q].x * SPEC_SCALE, im = s[e][q].y * SPEC_SCALE;
-          const _Float16 hr = (_Float16)re, hm = (_Float16)im;
-          hv[2 * e] = hr;
-          hv[2 * e + 1] = hm;
-          lv[2 * e] = (_Float16)(re - (float)hr);
-          lv[2 * e + 1] = (_Float16)(im - (float)hm);
-        }
-        t2[cg_s(q, cq, 0, bl) * 2 + hf] = live ? __builtin_bit_cast(uint2, hv) : uint2{0, 0};
-        t2[cg_s(q, cq, 1, bl) * 2 + hf] = live ? __builtin_bit_cast(uint2, lv) : uint2{0, 0};
-      }
-    }
-    // the previous group's output goes out only now: vmcnt counts stores and loads together and the
-    // loop head's wait for zin would otherwise wait for the stores too
-    if (g > g0) store_y(g - 1);
-    if (g + 1 < g1) load_z(g + 1);   // in flight across the GEMM (lds_barrier does not wait for it)
-    lds_barrier();
-    f32x4 acc[8] = {};
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const uint4 uh = tile[cg_s(k2, 4 * t + kq, 0, jj)], ul = tile[cg_s(k2, 4 * t + kq, 1, jj)];
-      const f16x8 sh = __builtin_bit_cast(f16x8, uh ^ m), sl = __builtin_bit_cast(f16x8, ul ^ m);
-      const f16x8 sh2 = __builtin_bit_cast(f16x8, (uh >> 16) | (uh << 16));
-      const f16x8 sl2 = __builtin_bit_cast(f16x8, (ul >> 16) | (ul << 16));
-#pragma unroll
-      for (int mq = 0; mq < 4; ++mq) {
-        const f16x8 ah = __builtin_bit_cast(f16x8, wr[t][mq][0]), al = __builtin_bit_cast(f16x8, wr[t][mq][1]);
-        acc[mq] = mfma16x16(al, sh, acc[mq]);
-        acc[mq] = mfma16x16(ah, sl, acc[mq]);
-        acc[mq] = mfma16x16(ah, sh, acc[mq]);
-        acc[4 + mq] = mfma16x16(al, sh2, acc[4 + mq]);
-        acc[4 + mq] = mfma16x16(ah, sl2, acc[4 + mq]);
-        acc[4 + mq] = mfma16x16(ah, sh2, acc[4 + mq]);
-      }
-    }
-    lds_barrier();   // every wave has read the S tile
-#pragma unroll
-    for (int mq = 0; mq < 4; ++mq) {
-      const int cqo = 4 * mq + kq;
-      const f32x4 re = acc[mq], im = acc[4 + mq];
-      ytile[jj * YLD + (cqo * 8 + k2) * 2] = f32x4{re[0], im[0], re[1], im[1]} * unscale;
-      ytile[jj * YLD + (cqo * 8 + k2) * 2 + 1] = f32x4{re[2], im[2], re[3], im[3]} * unscale;
-    }
-    lds_barrier();
-    cpx yv[2][8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const f32x4 pv = ytile[bl * YLD + (cq * 8 + q) * 2 + hf];
-      yv[0][q] = cpx{pv[0], pv[1]};
-      yv[1][q] = cpx{pv[2], pv[3]};
-    }
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      dft8<1>(yv[e]);
-#pragma unroll
-      for (int n2 = 0; n2 < 8; ++n2) yv[e][n2] = twid<1>(yv[e][n2], n2 * k1);
-    }
-#pragma unroll
-    for (int n2 = 0; n2 < 8; ++n2) yo[n2] = f32x4{yv[0][n2].x, yv[0][n2].y, yv[1][n2].x, yv[1][n2].y};
-    lds_barrier();   // the Y tile is read before the next group's S tile goes over it
-  }
-  store_y(g1 - 1);
-}
-
 // column kernel, bf16 (MP_DTYPE_BF16): col8_kernel's blocking with bf16 Z partials (8-B reads of a
 // thread's two channels), a bf16 S tile (one (re, im) pair per channel, no lo plane: 34 KB), one
 // v_mfma_f32_16x16x32_bf16 product per (k-step, row block, re|im) against the class-major bf16
@@ -1316,114 +1177,6 @@ __global__ __launch_bounds__(512, 2) void col8_bf_kernel(void* __restrict__ Zv, 
   }
 }
 
-// bf16 persistent column kernel (colp_bf_kernel; MP_COLP=1 under MP_DTYPE_BF16): colp_kernel's chunked
-// blocks and prefetch over col8_bf_kernel's bf16 Z partials and one-product bf16 weights (16 KiB per
-// frequency: 64 registers a wave, held for the chunk); the S fragment supplies (sr, -si) and (si, sr)
-// as in colp_kernel.
-__global__ __launch_bounds__(512, 1) void colp_bf_kernel(void* __restrict__ Zv, const uint4* __restrict__ Gb, int B,
-                                                         int ngrp, int gpb, int nch) {
-  __shared__ uint4 tile[2 * CG_HALF];   // the Y tile (fp32) needs the fp32 kernel's space
-  const int c8 = blockIdx.x / (8 * nch), rem = blockIdx.x - c8 * 8 * nch;
-  const int ch = rem >> 3, cls = c8 * 8 + (rem & 7);
-  if (cls >= Z_CLS) return;
-  const int g0 = ch * gpb, g1 = min(g0 + gpb, ngrp);
-  if (g0 >= g1) return;
-  const int fx = cls / 9, k1 = cls - fx * 9;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int bl = tid >> 5, a = tid & 31;
-  const int cq = a >> 1, hf = a & 1;
-  const int kq = lane >> 4, jj = lane & 15, k2 = wv;
-  const uint4 m = {0x80000000u, 0x80000000u, 0x80000000u, 0x80000000u};
-  auto sidx = [](int q, int c, int img) { return (q >> 2) * CB_HALF + (c * 4 + (q & 3)) * CG_SLD + img; };
-  char* const zb = static_cast<char*>(Zv);
-  auto zoff = [&](int b, int n2) -> uint32_t {
-    return ((uint32_t)((b * 8 + n2) * FX + fx) * 9u + (uint32_t)k1) * 256u + (uint32_t)a * 8u;
-  };
-  uint2 zin[8];
-  auto load_z = [&](int g) {
-    const int b = min(g * CG_NI + bl, B - 1);
-#pragma unroll
-    for (int n2 = 0; n2 < 8; ++n2) zin[n2] = *reinterpret_cast<const uint2*>(zb + zoff(b, n2));
-  };
-  load_z(g0);
-  uint4 wr[4][4];
-  {
-    const uint4* gw = Gb + (size_t)(cls * 8 + k2) * 16 * 64;
-#pragma unroll
-    for (int t = 0; t < 4; ++t)
-#pragma unroll
-      for (int mq = 0; mq < 4; ++mq) wr[t][mq] = gw[(4 * t + kq) * 64 + 16 * mq + jj];
-  }
-  uint2 yo[8];
-  auto store_y = [&](int g) {
-    const int b = g * CG_NI + bl;
-    if (b < B) {
-#pragma unroll
-      for (int n2 = 0; n2 < 8; ++n2) *reinterpret_cast<uint2*>(zb + zoff(b, n2)) = yo[n2];
-    }
-  };
-  constexpr int YLD = 16 * 8 * 2 + 1;
-  f32x4* ytile = reinterpret_cast<f32x4*>(tile);
-  for (int g = g0; g < g1; ++g) {
-    const bool live = g * CG_NI + bl < B;
-    {
-      cpx s[2][8];
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-#pragma unroll
-        for (int n2 = 0; n2 < 8; ++n2) s[e][n2] = twid<-1>(unpack_bf2(e ? zin[n2].y : zin[n2].x), n2 * k1);
-        dft8<-1>(s[e]);
-      }
-      uint2* t2 = reinterpret_cast<uint2*>(tile);
-#pragma unroll
-      for (int q = 0; q < 8; ++q)
-        t2[sidx(q, cq, bl) * 2 + hf] =
-            live ? uint2{pack_bf2(s[0][q].x, s[0][q].y), pack_bf2(s[1][q].x, s[1][q].y)} : uint2{0, 0};
-    }
-    if (g > g0) store_y(g - 1);
-    if (g + 1 < g1) load_z(g + 1);
-    lds_barrier();
-    f32x4 acc[8] = {};
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const uint4 us = tile[sidx(k2, 4 * t + kq, jj)];
-      const bf16x8 sre = __builtin_bit_cast(bf16x8, us ^ m), sim = __builtin_bit_cast(bf16x8, (us >> 16) | (us << 16));
-#pragma unroll
-      for (int mq = 0; mq < 4; ++mq) {
-        const bf16x8 g = __builtin_bit_cast(bf16x8, wr[t][mq]);
-        acc[mq] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(g, sre, acc[mq], 0, 0, 0);
-        acc[4 + mq] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(g, sim, acc[4 + mq], 0, 0, 0);
-      }
-    }
-    lds_barrier();
-#pragma unroll
-    for (int mq = 0; mq < 4; ++mq) {
-      const int cqo = 4 * mq + kq;
-      const f32x4 re = acc[mq], im = acc[4 + mq];
-      ytile[jj * YLD + (cqo * 8 + k2) * 2] = f32x4{re[0], im[0], re[1], im[1]};
-      ytile[jj * YLD + (cqo * 8 + k2) * 2 + 1] = f32x4{re[2], im[2], re[3], im[3]};
-    }
-    lds_barrier();
-    cpx yv[2][8];
-#pragma unroll
-    for (int q = 0; q < 8; ++q) {
-      const f32x4 pv = ytile[bl * YLD + (cq * 8 + q) * 2 + hf];
-      yv[0][q] = cpx{pv[0], pv[1]};
-      yv[1][q] = cpx{pv[2], pv[3]};
-    }
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-      dft8<1>(yv[e]);
-#pragma unroll
-      for (int n2 = 0; n2 < 8; ++n2) yv[e][n2] = twid<1>(yv[e][n2], n2 * k1);
-    }
-#pragma unroll
-    for (int n2 = 0; n2 < 8; ++n2) yo[n2] = uint2{pack_bf2(yv[0][n2].x, yv[0][n2].y), pack_bf2(yv[1][n2].x, yv[1][n2].y)};
-    lds_barrier();
-  }
-  store_y(g1 - 1);
-}
-
 // ------------------------------------------------------------------------------------ launchers
 bool fft4_enabled() {
   static const bool v = [] {
@@ -1473,38 +1226,6 @@ static bool row2_preo() {
   return v;
 }
 
-// MP_COLP (default 0): 1 = the persistent column kernels (colp_kernel, colp_bf_kernel) instead of
-// col8_kernel / col_gemm_kernel (MP_COL8) / col8_bf_kernel.
-// MP_COLP_GPB (default: chosen below): 16-image groups per colp block
-static int colp_gpb_env() {
-  static const int v = [] {
-    const char* e = std::getenv("MP_COLP");
-    if (!e || std::atoi(e) == 0) return -1;
-    const char* g = std::getenv("MP_COLP_GPB");
-    return g ? std::max(1, std::atoi(g)) : 0;
-  }();
-  return v;
-}
-
-// groups per colp block: blocks run one per CU in rounds of the CU count, so the launch costs about
-// ceil(blocks / CUs) x (groups per block + the block's weight fill, ~half a group's time)
-static int colp_gpb(int ngrp) {
-  static const int cus = [] {
-    int dev = 0, n = 256;
-    if (hipGetDevice(&dev) == hipSuccess) hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev);
-    return std::max(1, n);
-  }();
-  int best = ngrp;
-  double bc = 1e30;
-  for (int gpb = 1; gpb <= ngrp; ++gpb) {
-    const int nch = (ngrp + gpb - 1) / gpb;
-    if (gpb > 1 && (nch - 1) * gpb >= ngrp) continue;
-    const double c = (double)((CG_NC8 * 8 * nch + cus - 1) / cus) * (gpb + 0.5);
-    if (c < bc - 1e-9) bc = c, best = gpb;
-  }
-  return best;
-}
-
 // MP_COL8 (default 1): the eight-wave column kernel; 0: the four-wave one (two frequencies per wave)
 static bool col8_enabled() {
   static const bool v = [] {
@@ -1517,20 +1238,10 @@ static bool col8_enabled() {
 hipError_t launch_col_gemm(void* Z, const void* Gc, int B, float unscale, hipStream_t st, bool bf) {
   if (B <= 0) return hipSuccess;
   const int ngrp = (B + CG_NI - 1) / CG_NI;
-  const int pe = colp_gpb_env();
-  const bool colp = pe >= 0 && (size_t)B * 8 * Z_CLS * 64 * sizeof(cpx) < ((size_t)1 << 32);   // 32-bit offsets
-  if (bf && colp) {
-    const int gpb = pe > 0 ? std::min(pe, ngrp) : colp_gpb(ngrp), nch = (ngrp + gpb - 1) / gpb;
-    hipLaunchKernelGGL(colp_bf_kernel, dim3(CG_NC8 * 8 * nch), dim3(512), 0, st, Z, static_cast<const uint4*>(Gc), B,
-                       ngrp, gpb, nch);
-  } else if (bf)
+  if (bf)
     hipLaunchKernelGGL(col8_bf_kernel, dim3(CG_NC8 * 8 * ngrp), dim3(512), 0, st, Z, static_cast<const uint4*>(Gc), B,
                        ngrp);
-  else if (colp) {
-    const int gpb = pe > 0 ? std::min(pe, ngrp) : colp_gpb(ngrp), nch = (ngrp + gpb - 1) / gpb;
-    hipLaunchKernelGGL(colp_kernel, dim3(CG_NC8 * 8 * nch), dim3(512), 0, st, static_cast<cpx*>(Z),
-                       static_cast<const uint4*>(Gc), B, ngrp, gpb, nch, unscale);
-  } else if (col8_enabled())
+  else if (col8_enabled())
     hipLaunchKernelGGL(col8_kernel, dim3(CG_NC8 * 8 * ngrp), dim3(512), 0, st, static_cast<cpx*>(Z),
                        static_cast<const uint4*>(Gc), B, ngrp, unscale);
   else
