@@ -675,14 +675,10 @@ constexpr int R8_GATE = 2 * 4 * 2 * 64;                  // f16x8 of one gate's 
 constexpr int R8_T = (8 * 64 * RK_SP * 4 + R8_GATE * 16) / 8;   // 155,648 B: T grown by 512 B for FINAL
 static_assert(R8_T >= RK_T && (8 * 32 * RK_SP * 4 + 2 * R8_GATE * 16) <= R8_T * 8, "staging + gate weights fit");
 
-// PF: the first segment's map loads are issued before the inverse row transforms (after Ia), so their
-// latency hides behind Ib and the gate-weight fill instead of stalling the epilogue (MP_ROW8_PF)
-// (not in ROW_FINAL: the whole staged row and L0 together spill)
-template <int MODE, bool BF = false, bool PFR = true>
+template <int MODE, bool BF = false>
 __global__ __launch_bounds__(R8_NT, 1) void row8_kernel(void* __restrict__ Z, ConvArgs p, const void* __restrict__ or_x3,
                                                         float or_us, const void* __restrict__ ir_x3, float ir_us,
                                                         const float* __restrict__ O0) {
-  constexpr bool PF = PFR && MODE != ROW_FINAL;
   __shared__ cpx T[R8_T];
   __shared__ float vsh[V_COUNT * 64];
   const int b = blockIdx.x >> 3, n2 = blockIdx.x & 7;
@@ -698,9 +694,6 @@ __global__ __launch_bounds__(R8_NT, 1) void row8_kernel(void* __restrict__ Z, Co
   constexpr bool OR = MODE == ROW_B || MODE == ROW_FINAL, IR = MODE == ROW_B || MODE == ROW_INIT;
   constexpr int GN = BF ? R8_GATE / 2 : R8_GATE;   // uint4 per gate (bf16: one product, no lo plane)
   float P[64];
-  SegIn L0;
-  if constexpr (PF && MODE == ROW_INIT)
-    if (live) rk_load_seg<MODE, true, BF>(p, O0, b, y, 0, lane, L0);
   if constexpr (MODE != ROW_INIT) {
     {
       cpx u[R8_NIT][9];
@@ -722,8 +715,6 @@ __global__ __launch_bounds__(R8_NT, 1) void row8_kernel(void* __restrict__ Z, Co
         }
       }
     }
-    if constexpr (PF)
-      if (live) rk_load_seg<MODE, true, BF>(p, O0, b, y, 0, lane, L0);
     lds_barrier();
     {
       cpx A[FX];
@@ -751,9 +742,8 @@ __global__ __launch_bounds__(R8_NT, 1) void row8_kernel(void* __restrict__ Z, Co
         const int xs = 32 * sg;
         if (xs >= W) continue;   // wave-uniform
         SegIn L;
-        if (!PF || sg) rk_load_seg<MODE, true, BF>(p, O0, b, y, xs, lane, L);
-        rk_segment<MODE, true, true, BF>(p, stg + xs * RK_SP, b, y, xs, lane, (PF && !sg) ? L0 : L, gsh, or_us, gsh,
-                                         ir_us, vsh);
+        rk_load_seg<MODE, true, BF>(p, O0, b, y, xs, lane, L);
+        rk_segment<MODE, true, true, BF>(p, stg + xs * RK_SP, b, y, xs, lane, L, gsh, or_us, gsh, ir_us, vsh);
       }
     }
     return;
@@ -764,13 +754,12 @@ __global__ __launch_bounds__(R8_NT, 1) void row8_kernel(void* __restrict__ Z, Co
       const int xs = 32 * sg;
       if (xs >= W) continue;   // wave-uniform
       SegIn L;
-      if (!PF || sg) rk_load_seg<MODE, true, BF>(p, O0, b, y, xs, lane, L);
+      rk_load_seg<MODE, true, BF>(p, O0, b, y, xs, lane, L);
       if constexpr (MODE != ROW_INIT) {
 #pragma unroll
         for (int q = 0; q < 32; ++q) stg[q * RK_SP + lane] = P[xs + q];
       }
-      rk_segment<MODE, true, true, BF>(p, stg, b, y, xs, lane, (PF && !sg) ? L0 : L, gsh, or_us, gsh + GN, ir_us,
-                                       vsh);
+      rk_segment<MODE, true, true, BF>(p, stg, b, y, xs, lane, L, gsh, or_us, gsh + GN, ir_us, vsh);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
       for (int q = 0; q < 32; ++q) P[xs + q] = stg[q * RK_SP + lane];
@@ -1208,15 +1197,6 @@ static int row8_maxb() {
   return v;
 }
 
-// MP_ROW8_PF (default 1): row8_kernel issues its first epilogue segment's map loads before Ib
-static bool row8_pf() {
-  static const bool v = [] {
-    const char* e = std::getenv("MP_ROW8_PF");
-    return e ? std::atoi(e) != 0 : true;
-  }();
-  return v;
-}
-
 // MP_ROW2_PREO (default 1): B epilogue segments load O with I, before the o_r gate; 0: after it
 static bool row2_preo() {
   static const bool v = [] {
@@ -1257,11 +1237,7 @@ hipError_t launch_row(int mode, void* Z, const ConvArgs& a, const void* or_x3, f
   cpx* z = static_cast<cpx*>(Z);
   const dim3 g(B * 8), t(RK_NT);
   if (B <= row8_maxb()) {
-#define MP_ROW8(M, BFV)                                                                                       \
-  if (row8_pf())                                                                                              \
-    hipLaunchKernelGGL((row8_kernel<M, BFV, true>), g, dim3(R8_NT), 0, st, Z, a, or_x3, or_us, ir_x3, ir_us, O0); \
-  else                                                                                                        \
-    hipLaunchKernelGGL((row8_kernel<M, BFV, false>), g, dim3(R8_NT), 0, st, Z, a, or_x3, or_us, ir_x3, ir_us, O0)
+#define MP_ROW8(M, BFV) hipLaunchKernelGGL((row8_kernel<M, BFV>), g, dim3(R8_NT), 0, st, Z, a, or_x3, or_us, ir_x3, ir_us, O0)
 #define MP_ROW8S(BFV)                          \
   switch (mode) {                              \
     case ROW_A: MP_ROW8(ROW_A, BFV); break;         \

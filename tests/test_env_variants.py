@@ -133,7 +133,6 @@ BITS_CASES = [
     ("pose80", "bf16", "MP_ROW2_PREO", ("0", "1"), {"MP_ROW8_MAXB": "0"}),
     ("pose80", "fp32_fft", "MP_ROW8_MAXB", ("0", "1000000"), {}),
     ("pose80", "bf16", "MP_ROW8_MAXB", ("0", "1000000"), {}),
-    ("pose80", "fp32_fft", "MP_ROW8_PF", ("0", "1"), {}),
 ]
 
 
