@@ -27,12 +27,9 @@
 namespace mp {
 
 constexpr int Z_CLS = FX * 9;                        // 333 (fx, k1) column classes
-constexpr int RK_NT = 256;                           // row kernel: 4 waves, wave w = rows n1 = 2w, 2w + 1
 constexpr int RK_ITEMS = FX * 64;                    // (fx, channel) columns of the 9-point passes: 2368
-constexpr int RK_NIT = (RK_ITEMS + RK_NT - 1) / RK_NT;   // 10 per thread
 constexpr int RK_T = 8 * FX * 64;                    // T[n1][fx][c] complex: 151,552 B of LDS
 constexpr int RK_SP = 68;                            // staging pitch (floats) per pixel (16-B fragment reads)
-static_assert(128 * RK_SP * 4 <= 2 * FX * 64 * 8, "a wave's staging fits its two rows of T");
 
 // complex index of channel 0 of Z[b][n2][fx][k1]
 __device__ __forceinline__ size_t z_off(int b, int n2, int fx, int k1) {
@@ -40,92 +37,6 @@ __device__ __forceinline__ size_t z_off(int b, int n2, int fx, int k1) {
 }
 
 enum { ROW_A = 0, ROW_B = 1, ROW_FINAL = 2, ROW_INIT = 3 };
-
-// ---------------------------------------------------------------------------------------------
-// row kernel.  Block = (image b, row class n2), 256 threads; lane c of wave w owns channel c of rows
-// n1 = 2w (real part of its packed transforms) and 2w + 1 (imaginary part).
-//   Ia  (all threads) inverse 9-point sums over k1 of Z'[b][n2][fx][.][c] -> T[n1][fx][c]
-//   Ib  (lane c)      inverse row transform (Hermitian-extended, rows 2w / 2w+1 packed) -> P[x][c]
-//   II  (wave)        the half-step's epilogue on 32-pixel segments in the MFMA accumulator layout,
-//                     P staged through the wave's own rows of T ([pixel][68 floats])
-//   III (lane c)      forward row transform of the epilogue's output -> T[n1][fx][c]
-//   IIIb(all)         forward 9-point sums over n1 -> Z[b][n2][fx][k1][c]
-// ---------------------------------------------------------------------------------------------
-
-// Ia: thread i = (fx, c), c fastest: a wave reads 9 runs of 512 B per item, all items' loads issued
-// before the first transform
-__device__ __forceinline__ void rk_inv9(const cpx* __restrict__ Z, int b, int n2, int tid, cpx* T) {
-  cpx v[RK_NIT][9];
-#pragma unroll
-  for (int it = 0; it < RK_NIT; ++it) {
-    const int i = min(it * RK_NT + tid, RK_ITEMS - 1);
-    const cpx* src = Z + z_off(b, n2, i >> 6, 0) + (i & 63);
-#pragma unroll
-    for (int k1 = 0; k1 < 9; ++k1) v[it][k1] = src[k1 * 64];
-  }
-#pragma unroll
-  for (int it = 0; it < RK_NIT; ++it) {
-    const int i = it * RK_NT + tid;
-    if (i < RK_ITEMS) {
-      dft9<1>(v[it]);
-      const int fx = i >> 6, c = i & 63;
-#pragma unroll
-      for (int n1 = 0; n1 < 8; ++n1) T[(n1 * FX + fx) * 64 + c] = v[it][n1];   // n1 = 8: row 64 + n2, unused
-    }
-  }
-}
-
-// Ib: the half spectra A (row 2w) and B (row 2w + 1) of channel c packed as C = A + iB, extended
-// Hermitian, one inverse 72-point transform: v[x] = (P[row 2w][x][c], P[row 2w + 1][x][c])
-__device__ __forceinline__ void rk_inv_row(const cpx* T, int w, int c, cpx (&v)[72]) {
-  const int ta = (2 * w) * FX * 64 + c, tb = ta + FX * 64;
-#pragma unroll
-  for (int k = 0; k < FX; ++k) {
-    const cpx A = T[ta + k * 64], B = T[tb + k * 64];
-    v[k] = cfma(swp(B), cpx{-1.f, 1.f}, A);                                 // (A.x - B.y, A.y + B.x)
-    if (k > 0 && k < FX - 1) v[72 - k] = cfma(A, cpx{1.f, -1.f}, swp(B));   // (A.x + B.y, B.x - A.y)
-  }
-  fft72<1>(v);
-}
-
-// III: the staged rows (zero outside the map) -> forward 72-point transform of the packed pair ->
-// the two half spectra into the wave's rows of T.  The wave's staging IS those rows: every lane reads
-// its 128 staged values before any lane of the wave writes (one wave's LDS operations run in order).
-__device__ __forceinline__ void rk_fwd_row(cpx* T, const float* stg, int w, int c, bool la, bool lb, int W) {
-  cpx v[72];
-#pragma unroll
-  for (int x = 0; x < 72; ++x) {
-    const bool in = x < 64 && x < W;
-    v[x] = cpx{(in && la) ? stg[x * RK_SP + c] : 0.f, (in && lb) ? stg[(64 + x) * RK_SP + c] : 0.f};
-  }
-  fft72<-1>(v);
-  const int ta = (2 * w) * FX * 64 + c, tb = ta + FX * 64;
-#pragma unroll
-  for (int k = 0; k < FX; ++k) {   // Z = FFT(a + ib): A[k] = (Z[k] + conj Z[-k]) / 2, B[k] = (Z[k] - conj Z[-k]) / 2i
-    const cpx zk = v[k], zm = v[(72 - k) % 72];
-    T[ta + k * 64] = cfma(zm, cpx{1.f, -1.f}, zk) * 0.5f;
-    T[tb + k * 64] = cfma(swp(zk), cpx{1.f, -1.f}, swp(zm)) * 0.5f;
-  }
-}
-
-// IIIb: thread i = (fx, c): the 8 rows' half spectra (row 64 + n2 is zero padding) -> 9-point sums
-// over n1 -> Z[b][n2][fx][k1][c], a wave storing 9 runs of 512 B
-__device__ __forceinline__ void rk_fwd9(cpx* __restrict__ Z, int b, int n2, int tid, const cpx* T) {
-#pragma unroll 2
-  for (int it = 0; it < RK_NIT; ++it) {
-    const int i = it * RK_NT + tid;
-    if (i >= RK_ITEMS) break;
-    const int fx = i >> 6, c = i & 63;
-    cpx u[9];
-#pragma unroll
-    for (int n1 = 0; n1 < 8; ++n1) u[n1] = T[(n1 * FX + fx) * 64 + c];
-    u[8] = cpx{0.f, 0.f};
-    dft9<-1>(u);
-    cpx* dst = Z + z_off(b, n2, fx, 0) + c;
-#pragma unroll
-    for (int k1 = 0; k1 < 9; ++k1) dst[k1 * 64] = u[k1];
-  }
-}
 
 // a value the compiler cannot see through: index math re-derived from it in a later phase is not
 // CSE'd with an earlier phase's (which would hold 64-bit item addresses live across the whole kernel),
@@ -140,23 +51,29 @@ __device__ __forceinline__ P* opaque_ptr(P* p) {
   return p;
 }
 
-// II: the wave's four 32-pixel segments (s: row 2w + (s >> 1), columns 32 (s & 1) + j), lane (h, j),
-// register r of block n = channel 32 n + 8 (r >> 2) + 4 h + (r & 3) -- k_fft.hip spec_epi_b_kernel's
-// layout and expressions, P read from (and the epilogue's output written back to) the staging.
-// The segment's map loads (A: X, O; B: I, O; INIT: O0) are issued one segment ahead, segment 0's at
-// the kernel's start: with one block per CU nothing else hides their latency.
+// Packed-FP32 forms of the epilogues' elementwise math: two channels per v_pk_{add,mul,fma}_f32, the
+// transcendentals (v_exp_f32, v_rcp_f32) per channel as in fsigmoid / ftanh.  Same operations and
+// contractions per channel as the scalar expressions.
+typedef float f2v __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ f2v pr2(const f32x4& v, int i) { return f2v{v[2 * i], v[2 * i + 1]}; }
+__device__ __forceinline__ f2v pr16(const f32x16& v, int i) { return f2v{v[2 * i], v[2 * i + 1]}; }
+__device__ __forceinline__ f2v rcp2(f2v x) { return f2v{__builtin_amdgcn_rcpf(x[0]), __builtin_amdgcn_rcpf(x[1])}; }
+__device__ __forceinline__ f2v exp2v(f2v x) { return f2v{__builtin_amdgcn_exp2f(x[0]), __builtin_amdgcn_exp2f(x[1])}; }
+constexpr float LOG2E = 1.44269504088896340736f;
+__device__ __forceinline__ f2v fsigmoid2(f2v x) { return rcp2(1.f + exp2v(-x * LOG2E)); }
+__device__ __forceinline__ f2v ftanh2(f2v x) { return 1.f - 2.f * rcp2(1.f + exp2v((2.f * x) * LOG2E)); }
+
+// II: a wave's 32-pixel segments (columns xs + j of its row), lane (h, j), register r of block n =
+// channel 32 n + 8 (r >> 2) + 4 h + (r & 3) -- k_fft.hip spec_epi_b_kernel's layout and expressions,
+// P read from (and the epilogue's output written back to) the staging.  The segment's map loads
+// (A: X, O; B: I, O; INIT: O0) in SegIn.
 struct SegIn {
   f32x4 a[2][4], o[2][4];
 };
 
-__device__ __forceinline__ bool seg_live(int s, int w, int n2, int H, int W) {
-  return 8 * (2 * w + (s >> 1)) + n2 < H && 32 * (s & 1) < W;
-}
-
-// the segment at map row y, columns xs .. xs + 31 (lane (h, j): pixel xs + j)
-// PREO: O is loaded here with the other map (B modes: 32 more live registers across the o_r gate,
-// against eight dependent loads after it)
-template <int MODE, bool PREO = true, bool BM = false>
+// the segment at map row y, columns xs .. xs + 31 (lane (h, j): pixel xs + j); O is loaded here with
+// the other map (B modes: before the o_r gate rather than eight dependent loads after it)
+template <int MODE, bool BM = false>
 __device__ __forceinline__ void rk_load_seg(const ConvArgs& p, const float* __restrict__ O0, int b, int y, int xs,
                                             int lane, SegIn& L) {
   const int H = p.H, W = p.W;
@@ -170,23 +87,22 @@ __device__ __forceinline__ void rk_load_seg(const ConvArgs& p, const float* __re
       } else {
         L.a[n][g] = MODE == ROW_A ? map_ld4<BM>(p.X, xx_index(b, 4 * n + g, y, x, 4 * h, H, W))
                                   : map_ld4<BM>(p.I, ii_index(b, 4 * n + g, y, x, 4 * h, H, W));
-        if constexpr (MODE == ROW_A || PREO) L.o[n][g] = map_ld4<BM>(p.O, oo_index(b, 4 * n + g, y, x, 4 * h, H, W));
+        L.o[n][g] = map_ld4<BM>(p.O, oo_index(b, 4 * n + g, y, x, 4 * h, H, W));
       }
     }
 }
 
 // seg: the segment's 32 staged pixels (pitch RK_SP floats); the output goes back over the input
 // LEAN: a scheduling fence after every 4-channel group, so the compiler does not hoist all eight groups'
-// loads and address math at once (row2_kernel's two-blocks-per-CU register budget)
-template <int MODE, bool LEAN = false, bool PREO = true, bool BM = false>
+// address math and LDS reads at once (the register budget next to the row's 64 values)
+template <int MODE, bool LEAN = false, bool BM = false>
 __device__ __forceinline__ void rk_segment(const ConvArgs& p, float* seg, int b, int y, int xs, int lane,
                                            const SegIn& L, const void* __restrict__ or_x3, float or_us,
                                            const void* __restrict__ ir_x3, float ir_us, const float* vec) {
   const int h = lane >> 5, j = lane & 31, H = p.H, W = p.W;
   const int x = xs + j;
   float* sp = seg + j * RK_SP;
-  // LEAN: the gate weights are re-read per segment (L1 / L2 hits) instead of 128 registers held across
-  // the kernel
+  // LEAN: the gate weights (LDS) are re-read per segment instead of 128 registers held across the kernel
   const void* orw = LEAN ? opaque_ptr(or_x3) : or_x3;
   const void* irw = LEAN ? opaque_ptr(ir_x3) : ir_x3;
   if constexpr (MODE == ROW_A) {
@@ -202,7 +118,12 @@ __device__ __forceinline__ void rk_segment(const ConvArgs& p, float* seg, int b,
         const f32x4 nu = *reinterpret_cast<const f32x4*>(vec + V_NU * 64 + c);
         f32x4 iv;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) iv[e] = atanh_f(epi_a(L.a[n][g][e], L.o[n][g][e], pv[e], be[e], nu[e], lat[e]));
+        for (int q = 0; q < 2; ++q) {
+          const f2v x = pr2(L.a[n][g], q), o = pr2(L.o[n][g], q);
+          const f2v t = ftanh2(-(pr2(be, q) * o + pr2(nu, q)) * (pr2(pv, q) + pr2(lat, q)) + x);
+          iv[2 * q] = t[0];
+          iv[2 * q + 1] = t[1];
+        }
         map_st4<BM>(p.dst, ii_index(b, 4 * n + g, y, x, 4 * h, H, W), iv);
         *reinterpret_cast<f32x4*>(sp + c) = iv;
         if constexpr (LEAN) __builtin_amdgcn_sched_barrier(0);
@@ -225,9 +146,12 @@ __device__ __forceinline__ void rk_segment(const ConvArgs& p, float* seg, int b,
         const f32x4 ib = *reinterpret_cast<const f32x4*>(vec + V_IB * 64 + c);
         f32x4 o, og;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          o[e] = V[n][4 * g + e];
-          og[e] = o[e] * fsigmoid(Y[n][4 * g + e] + ib[e]);
+        for (int q = 0; q < 2; ++q) {
+          const f2v ov = pr16(V[n], 2 * g + q), t = ov * fsigmoid2(pr16(Y[n], 2 * g + q) + pr2(ib, q));
+          o[2 * q] = ov[0];
+          o[2 * q + 1] = ov[1];
+          og[2 * q] = t[0];
+          og[2 * q + 1] = t[1];
         }
         map_st4<BM>(p.dst, oo_index(b, 4 * n + g, y, x, 4 * h, H, W), o);
         *reinterpret_cast<f32x4*>(sp + c) = og;
@@ -250,7 +174,7 @@ __device__ __forceinline__ void rk_segment(const ConvArgs& p, float* seg, int b,
       for (int g = 0; g < 4; ++g) {
         const int c = 32 * n + 8 * g + 4 * h;
         const f32x4 pv = *reinterpret_cast<const f32x4*>(sp + c);
-        const f32x4 ov = PREO ? L.o[n][g] : map_ld4<BM>(p.O, oo_index(b, 4 * n + g, y, x, 4 * h, H, W));
+        const f32x4 ov = L.o[n][g];
         const f32x4 lat = *reinterpret_cast<const f32x4*>(vec + V_LAT * 64 + c);
         const f32x4 ga = *reinterpret_cast<const f32x4*>(vec + V_GAMMA * 64 + c);
         const f32x4 ka = *reinterpret_cast<const f32x4*>(vec + V_KAPPA * 64 + c);
@@ -258,15 +182,17 @@ __device__ __forceinline__ void rk_segment(const ConvArgs& p, float* seg, int b,
         const f32x4 ob = *reinterpret_cast<const f32x4*>(vec + V_OB * 64 + c);
         f32x4 o;
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const int rr = 4 * g + e;
-          const float g2 = fsigmoid(Y[n][rr] + ob[e]);
-          const float iv = Iv[n][rr];
-          const float ee = ga[e] * (pv[e] + lat[e]);
-          const float S = ftanh(ka[e] * (iv + ee) + om[e] * (iv * ee));
-          const float on = (g2 * ov[e] + (1.f - g2) * S) * p.rho;
-          o[e] = on;
-          Iv[n][rr] = on;
+        for (int q = 0; q < 2; ++q) {
+          const int rr = 4 * g + 2 * q;
+          const f2v g2 = fsigmoid2(pr16(Y[n], 2 * g + q) + pr2(ob, q));
+          const f2v iv = pr16(Iv[n], 2 * g + q);
+          const f2v ee = pr2(ga, q) * (pr2(pv, q) + pr2(lat, q));
+          const f2v S = ftanh2(pr2(ka, q) * (iv + ee) + pr2(om, q) * (iv * ee));
+          const f2v on = (g2 * pr2(ov, q) + (1.f - g2) * S) * p.rho;
+          o[2 * q] = on[0];
+          o[2 * q + 1] = on[1];
+          Iv[n][rr] = on[0];
+          Iv[n][rr + 1] = on[1];
         }
         map_st4<BM>(p.dst, oo_index(b, 4 * n + g, y, x, 4 * h, H, W), o);
         if constexpr (LEAN) __builtin_amdgcn_sched_barrier(0);
@@ -282,7 +208,11 @@ __device__ __forceinline__ void rk_segment(const ConvArgs& p, float* seg, int b,
           const f32x4 ib = *reinterpret_cast<const f32x4*>(vec + V_IB * 64 + c);
           f32x4 o;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] = Ov[n][4 * g + e] * fsigmoid(Y[n][4 * g + e] + ib[e]);
+          for (int q = 0; q < 2; ++q) {
+            const f2v t = pr16(Ov[n], 2 * g + q) * fsigmoid2(pr16(Y[n], 2 * g + q) + pr2(ib, q));
+            o[2 * q] = t[0];
+            o[2 * q + 1] = t[1];
+          }
           *reinterpret_cast<f32x4*>(sp + c) = o;
           if constexpr (LEAN) __builtin_amdgcn_sched_barrier(0);
         }
@@ -299,7 +229,11 @@ __device__ __forceinline__ void rk_segment(const ConvArgs& p, float* seg, int b,
           const f32x4 tt = *reinterpret_cast<const f32x4*>(vec + V_OUTT * 64 + c);
           f32x4 o;
 #pragma unroll
-          for (int e = 0; e < 4; ++e) o[e] = Ov[n][4 * g + e] * ss[e] + tt[e];
+          for (int q = 0; q < 2; ++q) {
+            const f2v t = pr16(Ov[n], 2 * g + q) * pr2(ss, q) + pr2(tt, q);
+            o[2 * q] = t[0];
+            o[2 * q + 1] = t[1];
+          }
           *reinterpret_cast<f32x4*>(sp + c) = o;
         }
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -333,52 +267,8 @@ __device__ __forceinline__ void rk_segment(const ConvArgs& p, float* seg, int b,
   }
 }
 
-template <int MODE>
-__global__ __launch_bounds__(RK_NT, 1) void row_kernel(cpx* __restrict__ Z, ConvArgs p, const void* __restrict__ or_x3,
-                                                        float or_us, const void* __restrict__ ir_x3, float ir_us,
-                                                        const float* __restrict__ O0) {
-  __shared__ cpx T[RK_T];
-  const int b = blockIdx.x >> 3, n2 = blockIdx.x & 7;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  float* stg = reinterpret_cast<float*>(T + (2 * w) * FX * 64);   // the wave's own two rows of T
-  const int H = p.H, W = p.W;
-  const bool la = 8 * (2 * w) + n2 < H, lb = 8 * (2 * w + 1) + n2 < H;
-  SegIn L0, L1;
-  if (seg_live(0, w, n2, H, W)) rk_load_seg<MODE>(p, O0, b, 8 * (2 * w) + n2, 0, lane, L0);
-  if constexpr (MODE != ROW_INIT) {
-    rk_inv9(Z, b, n2, tid, T);
-    lds_barrier();
-    if (la || lb) {   // wave-uniform
-      cpx v[72];
-      rk_inv_row(T, w, lane, v);
-      // (in-wave order: the reads of T above precede these writes over the same rows)
-#pragma unroll
-      for (int x = 0; x < 64; ++x) {
-        if (x < W) {
-          stg[x * RK_SP + lane] = v[x].x;
-          stg[(64 + x) * RK_SP + lane] = v[x].y;
-        }
-      }
-    }
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-#pragma unroll
-  for (int s = 0; s < 4; ++s) {
-    if (s + 1 < 4 && seg_live(s + 1, w, n2, H, W))
-      rk_load_seg<MODE>(p, O0, b, 8 * (2 * w + ((s + 1) >> 1)) + n2, 32 * ((s + 1) & 1), lane, (s & 1) ? L0 : L1);
-    if (seg_live(s, w, n2, H, W))
-      rk_segment<MODE>(p, stg + ((s >> 1) * 64 + 32 * (s & 1)) * RK_SP, b, 8 * (2 * w + (s >> 1)) + n2, 32 * (s & 1),
-                       lane, (s & 1) ? L1 : L0, or_x3, or_us, ir_x3, ir_us, p.vecs);
-  }
-  if constexpr (MODE == ROW_FINAL) return;
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  rk_fwd_row(T, stg, w, lane, la, lb, W);
-  lds_barrier();
-  rk_fwd9(Z, b, n2, tid, T);
-}
-
 // ---------------------------------------------------------------------------------------------
-// one real row of 72 points per lane (row2_kernel): a 36-point complex transform of the even / odd
+// one real row of 72 points per lane: a 36-point complex transform of the even / odd
 // samples packed as z[m] = x[2m] + i x[2m+1] and the split by W72^k, half the registers of fft72 on a
 // packed pair of rows (72 instead of 144 values)
 // ---------------------------------------------------------------------------------------------
@@ -451,22 +341,6 @@ __device__ __forceinline__ void rfft72_inv(const cpx (&X)[FX], float (&x)[64]) {
   }
 }
 
-// ---------------------------------------------------------------------------------------------
-// row kernel, two blocks per CU (row2_kernel, the default; MP_ROW2=0 restores row_kernel above).
-// The same block (image b, row class n2), phases and arithmetic, with half the LDS: T holds 4 of the
-// 8 rows (75,776 B), so the two transposes run in two rounds.  Wave w owns rows n1 = w (the real part
-// of its packed transforms) and w + 4 (the imaginary part):
-//   Ia  items (fx, c): the 9-point inverse sums; rows 0-3 to T, rows 4-7 held in registers
-//   Ib  lane c reads its row w half spectrum (round 1); rows 4-7 replace rows 0-3 in T; it reads
-//       row w + 4 (round 2); one inverse transform of the packed pair: v[x] = (P[w][x], P[w+4][x])
-//   II  four 32-pixel segments per wave (rows w, w + 4): P staged through the wave's own row slot of
-//       T, the epilogue's output read back into v
-//   III one forward transform of the packed pair; row w's half spectrum to T (round 1), the items
-//       take rows 0-3 into registers; row w + 4's (round 2); the items' 9-point sums -> Z
-// ---------------------------------------------------------------------------------------------
-constexpr int R2_T = 4 * FX * 64;   // complex entries: 75,776 B
-static_assert(32 * RK_SP * 4 <= FX * 64 * 8, "a segment's staging fits the wave's row slot");
-
 // Z element access: complex64 (fp32 path) or one bf16 (re, im) pair (MP_DTYPE_BF16: round to nearest
 // even on store, exact on load), at the same complex index
 template <bool BF>
@@ -480,189 +354,18 @@ __device__ __forceinline__ void z_st(void* Z, size_t i, cpx v) {
   else static_cast<cpx*>(Z)[i] = v;
 }
 
-// BF: MP_DTYPE_BF16 -- Z and the hGRU maps in bf16, the gates one bf16 product (gate_bf); transforms,
-// epilogue math and the NHWC output fp32
-template <int MODE, bool PREO = true, bool BF = false>
-__global__ __launch_bounds__(RK_NT, 2) void row2_kernel(void* __restrict__ Z, ConvArgs p, const void* __restrict__ or_x3,
-                                                         float or_us, const void* __restrict__ ir_x3, float ir_us,
-                                                         const float* __restrict__ O0) {
-  __shared__ cpx T[R2_T];
-  // the epilogues' per-channel vectors in LDS: read per segment there, instead of ~100-200 registers of
-  // loop-invariant global loads held across the whole kernel
-  __shared__ float vsh[V_COUNT * 64];
-  const int b = blockIdx.x >> 3, n2 = blockIdx.x & 7;
-  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
-  for (int i = tid; i < V_COUNT * 64; i += RK_NT) vsh[i] = p.vecs[i];
-  if constexpr (MODE == ROW_INIT) lds_barrier();   // (the other modes pass Ia's barriers first)
-  const int H = p.H, W = p.W;
-  const int ya = 8 * w + n2, yb = 8 * (w + 4) + n2;   // the wave's two rows
-  const bool la = ya < H, lb = yb < H;
-  cpx* slot = T + w * FX * 64;                         // the wave's row slot of T
-  float* stg = reinterpret_cast<float*>(slot);
-  // Register budget (two waves per SIMD): no 64-value row is held across a transform; the row that
-  // waits sits in the wave's slot as staging instead.
-  float P0[64], P1[64];                                // rows w and w + 4 of this lane's channel
-  if constexpr (MODE != ROW_INIT) {
-    // ---- Ia: 9-point inverse sums over k1 (two batches of items); rows 0-3 to T, rows 4-7 kept ----
-    cpx keep[RK_NIT][4];
-#pragma unroll
-    for (int half = 0; half < 2; ++half) {
-      constexpr int NB = RK_NIT / 2;
-      cpx u[NB][9];
-#pragma unroll
-      for (int q = 0; q < NB; ++q) {
-        const int i = min((half * NB + q) * RK_NT + tid, RK_ITEMS - 1);
-        const size_t src = z_off(b, n2, i >> 6, 0) + (i & 63);
-#pragma unroll
-        for (int k1 = 0; k1 < 9; ++k1) u[q][k1] = z_ld<BF>(Z, src + k1 * 64);
-      }
-#pragma unroll
-      for (int q = 0; q < NB; ++q) {
-        const int it = half * NB + q, i = it * RK_NT + tid;
-        dft9<1>(u[q]);
-        if (i < RK_ITEMS) {
-          const int fx = i >> 6, c = i & 63;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) T[(r * FX + fx) * 64 + c] = u[q][r];
-        }
-#pragma unroll
-        for (int r = 0; r < 4; ++r) keep[it][r] = u[q][4 + r];
-      }
-    }
-    lds_barrier();
-#ifdef R2_MARK
-    asm volatile("; P_IB" ::: "memory");
-#endif
-    // ---- Ib round 1: row w's half spectrum; rows 4-7 replace rows 0-3; row w's inverse transform ----
-    {
-      cpx A[FX];
-#pragma unroll
-      for (int k = 0; k < FX; ++k) A[k] = slot[k * 64 + lane];
-      lds_barrier();
-      const int tk = opaque(tid);
-#pragma unroll
-      for (int it = 0; it < RK_NIT; ++it) {
-        const int i = it * RK_NT + tk;
-        if (i < RK_ITEMS) {
-          const int fx = i >> 6, c = i & 63;
-#pragma unroll
-          for (int r = 0; r < 4; ++r) T[(r * FX + fx) * 64 + c] = keep[it][r];
-        }
-      }
-      rfft72_inv(A, P0);
-    }
-    lds_barrier();
-    // ---- Ib round 2: row w + 4's half spectrum into registers, row w's P staged over it, inverse ----
-    {
-      cpx Bv[FX];
-#pragma unroll
-      for (int k = 0; k < FX; ++k) Bv[k] = slot[k * 64 + lane];
-      if (la) {
-#pragma unroll
-        for (int x = 0; x < 64; ++x)
-          if (x < W) stg[x * RK_SP + lane] = P0[x];   // (in-wave order: after the reads above)
-      }
-      __builtin_amdgcn_sched_barrier(0);
-      rfft72_inv(Bv, P1);
-    }
-  }
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-#ifdef R2_MARK
-  asm volatile("; P_II" ::: "memory");
-#endif
-  // ---- II: row w (staged), then row w + 4; two 32-pixel segments per row ----
-#pragma unroll
-  for (int rr = 0; rr < 2; ++rr) {
-    const bool live = rr ? lb : la;
-    const int y = rr ? yb : ya;
-    if (rr == 1) {
-      if constexpr (MODE != ROW_FINAL) {
-        // row w's output back into registers (zero outside the map) before row w + 4 is staged
-#pragma unroll
-        for (int x = 0; x < 64; ++x) P0[x] = (la && x < W) ? stg[x * RK_SP + lane] : 0.f;
-      }
-      if constexpr (MODE != ROW_INIT) {
-        if (live) {
-#pragma unroll
-          for (int x = 0; x < 64; ++x)
-            if (x < W) stg[x * RK_SP + lane] = P1[x];
-        }
-      }
-      __builtin_amdgcn_sched_barrier(0);
-    }
-    if (live) {
-#pragma unroll 1
-      for (int sg = 0; sg < 2; ++sg) {
-        const int xs = 32 * sg;
-        if (xs >= W) continue;   // wave-uniform
-        SegIn L;
-        rk_load_seg<MODE, PREO, BF>(p, O0, b, y, xs, lane, L);
-        rk_segment<MODE, true, PREO, BF>(p, stg + xs * RK_SP, b, y, xs, lane, L, or_x3, or_us, ir_x3, ir_us, vsh);
-      }
-    }
-  }
-  if constexpr (MODE == ROW_FINAL) return;
-  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-  __builtin_amdgcn_sched_barrier(0);
-#ifdef R2_MARK
-  asm volatile("; P_III" ::: "memory");
-#endif
-  // ---- III: row w's forward transform (row w + 4's output waits in the staging), then row w + 4's ----
-  cpx X1[FX];
-  {
-    cpx X0[FX];
-    rfft72_fwd(P0, X0);
-#pragma unroll
-    for (int x = 0; x < 64; ++x) P1[x] = (lb && x < W) ? stg[x * RK_SP + lane] : 0.f;
-#pragma unroll
-    for (int k = 0; k < FX; ++k) slot[k * 64 + lane] = X0[k];   // (in-wave order: after the reads above)
-    __builtin_amdgcn_sched_barrier(0);
-    rfft72_fwd(P1, X1);
-  }
-  lds_barrier();   // round 1: rows 0-3 in T
-  cpx got[RK_NIT][4];
-  const int tg = opaque(tid);
-#pragma unroll
-  for (int it = 0; it < RK_NIT; ++it) {
-    const int i = min(it * RK_NT + tg, RK_ITEMS - 1);
-#pragma unroll
-    for (int r = 0; r < 4; ++r) got[it][r] = T[(r * FX + (i >> 6)) * 64 + (i & 63)];
-  }
-  lds_barrier();
-#pragma unroll
-  for (int k = 0; k < FX; ++k) slot[k * 64 + lane] = X1[k];   // round 2: rows 4-7
-  lds_barrier();
-#ifdef R2_MARK
-  asm volatile("; P_IIIB" ::: "memory");
-#endif
-  // ---- IIIb: 9-point forward sums over n1 (row 64 + n2 is zero padding) -> Z ----
-  const int ts = opaque(tid);
-#pragma unroll
-  for (int it = 0; it < RK_NIT; ++it) {
-    const int i = it * RK_NT + ts;
-    if (i >= RK_ITEMS) break;
-    const int fx = i >> 6, c = i & 63;
-    cpx u[9];
-#pragma unroll
-    for (int r = 0; r < 4; ++r) {
-      u[r] = got[it][r];
-      u[4 + r] = T[(r * FX + fx) * 64 + c];
-    }
-    u[8] = cpx{0.f, 0.f};
-    dft9<-1>(u);
-    const size_t dst = z_off(b, n2, fx, 0) + c;
-#pragma unroll
-    for (int k1 = 0; k1 < 9; ++k1) z_st<BF>(Z, dst + k1 * 64, u[k1]);
-  }
-}
-
 // ---------------------------------------------------------------------------------------------
-// row kernel, eight waves (row8_kernel; small batches, MP_ROW8_MAXB): row2_kernel's block, phases and
-// per-element arithmetic re-parallelised for a full chip at few images -- 512 threads, wave w owns
-// row n1 = w alone, the whole T (151.5 KB, one block per CU) so both transposes run in one round.
-// Every value is produced by the same dft9 / rfft72 / rk_segment code as in row2_kernel: the two are
-// bit-identical (tests/test_gpu_parity.py batch invariance across the switch).
+// row kernel (row8_kernel).  Block = (image b, row class n2), 512 threads; wave w owns row n1 = w
+// (map row y = 8 w + n2), lane c its channel c; one block per CU (the whole T, 151.5 KB):
+//   Ia  items (fx, c): inverse 9-point sums over k1 of Z'[b][n2][fx][.][c] -> T[n1][fx][c]
+//   Ib  lane c: its row's inverse real transform (rfft72_inv) -> P[x]
+//   II  the half-step's epilogue on two 32-pixel segments in the MFMA accumulator layout (rk_segment),
+//       P staged through LDS, the 1x1 gates' weights read from LDS
+//   III lane c: forward real transform of the epilogue's output -> T; items (fx, c): forward 9-point
+//       sums over n1 -> Z[b][n2][fx][k1][c]
+// Round 5 measured two other forms and removed them: a four-wave block with the whole T (one row
+// pair per wave) and a two-blocks-per-CU block with half of T (two transpose rounds; register
+// spills): B = 256 fp32 9.61 ms per forward against this kernel's 9.04 (profiles/r5d).
 // ---------------------------------------------------------------------------------------------
 constexpr int R8_NT = 512;
 constexpr int R8_NIT = (RK_ITEMS + R8_NT - 1) / R8_NT;   // 5
@@ -675,6 +378,8 @@ constexpr int R8_GATE = 2 * 4 * 2 * 64;                  // f16x8 of one gate's 
 constexpr int R8_T = (8 * 64 * RK_SP * 4 + R8_GATE * 16) / 8;   // 155,648 B: T grown by 512 B for FINAL
 static_assert(R8_T >= RK_T && (8 * 32 * RK_SP * 4 + 2 * R8_GATE * 16) <= R8_T * 8, "staging + gate weights fit");
 
+// BF: MP_DTYPE_BF16 -- Z and the hGRU maps in bf16, the gates one bf16 product (gate_bf); transforms,
+// epilogue math and the NHWC output fp32
 template <int MODE, bool BF = false>
 __global__ __launch_bounds__(R8_NT, 1) void row8_kernel(void* __restrict__ Z, ConvArgs p, const void* __restrict__ or_x3,
                                                         float or_us, const void* __restrict__ ir_x3, float ir_us,
@@ -742,8 +447,8 @@ __global__ __launch_bounds__(R8_NT, 1) void row8_kernel(void* __restrict__ Z, Co
         const int xs = 32 * sg;
         if (xs >= W) continue;   // wave-uniform
         SegIn L;
-        rk_load_seg<MODE, true, BF>(p, O0, b, y, xs, lane, L);
-        rk_segment<MODE, true, true, BF>(p, stg + xs * RK_SP, b, y, xs, lane, L, gsh, or_us, gsh, ir_us, vsh);
+        rk_load_seg<MODE, BF>(p, O0, b, y, xs, lane, L);
+        rk_segment<MODE, true, BF>(p, stg + xs * RK_SP, b, y, xs, lane, L, gsh, or_us, gsh, ir_us, vsh);
       }
     }
     return;
@@ -754,12 +459,12 @@ __global__ __launch_bounds__(R8_NT, 1) void row8_kernel(void* __restrict__ Z, Co
       const int xs = 32 * sg;
       if (xs >= W) continue;   // wave-uniform
       SegIn L;
-      rk_load_seg<MODE, true, BF>(p, O0, b, y, xs, lane, L);
+      rk_load_seg<MODE, BF>(p, O0, b, y, xs, lane, L);
       if constexpr (MODE != ROW_INIT) {
 #pragma unroll
         for (int q = 0; q < 32; ++q) stg[q * RK_SP + lane] = P[xs + q];
       }
-      rk_segment<MODE, true, true, BF>(p, stg, b, y, xs, lane, L, gsh, or_us, gsh + GN, ir_us, vsh);
+      rk_segment<MODE, true, BF>(p, stg, b, y, xs, lane, L, gsh, or_us, gsh + GN, ir_us, vsh);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
       for (int q = 0; q < 32; ++q) P[xs + q] = stg[q * RK_SP + lane];
@@ -821,150 +526,12 @@ __device__ __forceinline__ f32x4 mfma16x16(f16x8 a, f16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
 
-__global__ __launch_bounds__(256, 2) void col_gemm_kernel(cpx* __restrict__ Z, const uint4* __restrict__ Gc, int B,
-                                                          int ngrp, float unscale) {
-  __shared__ uint4 tile[2 * CG_HALF];   // 69,632 B
-  const int c8 = blockIdx.x / (8 * ngrp), rem = blockIdx.x - c8 * 8 * ngrp;
-  const int grp = rem >> 3, cls = c8 * 8 + (rem & 7);
-  if (cls >= Z_CLS) return;
-  const int fx = cls / 9, k1 = cls - fx * 9;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int img0 = grp * CG_NI;
-  const int bl = tid >> 4, a = tid & 15;   // DFT role: image bl, channels 2a, 2a + 1, 32 + 2a, 33 + 2a
-  const bool live = img0 + bl < B;
-  const int b = min(img0 + bl, B - 1);
-  const int cq0 = a >> 1, cq1 = 8 + (a >> 1), hf = a & 1;   // their channel groups, half of the group
-  // ---- the thread's 8 row-class partials (unconditional, clamped) ----
-  f32x4 zin[8][2];
-#pragma unroll
-  for (int n2 = 0; n2 < 8; ++n2) {
-    const f32x4* src = reinterpret_cast<const f32x4*>(Z + z_off(b, n2, fx, k1));
-    zin[n2][0] = src[a];
-    zin[n2][1] = src[a + 16];
-  }
-  // ---- twiddle W72^{n2 k1}, 8-point DFT over n2 -> k2; scale and split into the S tile ----
-  {
-    cpx s[4][8];
-#pragma unroll
-    for (int e = 0; e < 4; ++e) {
-#pragma unroll
-      for (int n2 = 0; n2 < 8; ++n2) {
-        const f32x4 zz = zin[n2][e >> 1];
-        s[e][n2] = twid<-1>(cpx{zz[2 * (e & 1)], zz[2 * (e & 1) + 1]}, n2 * k1);
-      }
-      dft8<-1>(s[e]);
-    }
-    typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
-    uint2* t2 = reinterpret_cast<uint2*>(tile);
-#pragma unroll
-    for (int k2 = 0; k2 < 8; ++k2) {
-#pragma unroll
-      for (int pr = 0; pr < 2; ++pr) {   // channel pair 0: (2a, 2a+1) of group cq0; 1: of group cq1
-        f16x4 hv, lv;
-#pragma unroll
-        for (int e = 0; e < 2; ++e) {
-          const cpx z = s[2 * pr + e][k2];
-          const float re = z.x * SPEC_SCALE, im = z.y * SPEC_SCALE;
-          const _Float16 hr = (_Float16)re, hm = (_Float16)im;
-          hv[2 * e] = hr;
-          hv[2 * e + 1] = hm;
-          lv[2 * e] = (_Float16)(re - (float)hr);
-          lv[2 * e + 1] = (_Float16)(im - (float)hm);
-        }
-        const int cq = pr ? cq1 : cq0;
-        t2[cg_s(k2, cq, 0, bl) * 2 + hf] = live ? __builtin_bit_cast(uint2, hv) : uint2{0, 0};
-        t2[cg_s(k2, cq, 1, bl) * 2 + hf] = live ? __builtin_bit_cast(uint2, lv) : uint2{0, 0};
-      }
-    }
-  }
-  // ---- GEMM role: lane (kq = lane >> 4, jj = lane & 15); k-step t covers groups 4t .. 4t + 3 ----
-  const int kq = lane >> 4, jj = lane & 15;
-  constexpr int TW = 2;   // k-steps per weight batch (64 VGPRs)
-  uint4 wr[TW][4][2];
-  auto load_w = [&](int k2, int t0) {
-    const uint4* gw = Gc + (size_t)(cls * 8 + k2) * 2 * 16 * 64;
-#pragma unroll
-    for (int t = 0; t < TW; ++t)
-#pragma unroll
-      for (int mq = 0; mq < 4; ++mq) {
-        wr[t][mq][0] = gw[(0 * 16 + 4 * (t0 + t) + kq) * 64 + 16 * mq + jj];
-        wr[t][mq][1] = gw[(1 * 16 + 4 * (t0 + t) + kq) * 64 + 16 * mq + jj];
-      }
-  };
-  load_w(wv, 0);   // after the partials are consumed (register budget), in flight across the tile barrier
-  lds_barrier();
-  const uint4 m = {0x80000000u, 0x80000000u, 0x80000000u, 0x80000000u};
-#pragma unroll
-  for (int half = 0; half < 2; ++half) {
-    const int k2 = wv + 4 * half;
-    if (half) load_w(k2, 0);
-    f32x4 acc[8] = {};   // [mq] rows co = 16 mq + .. (re), [4 + mq] the same co (im)
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      if (t > 0 && t % TW == 0) load_w(k2, t);
-      const f16x8 sh = __builtin_bit_cast(f16x8, tile[cg_s(k2, 4 * t + kq, 0, jj)]);
-      const f16x8 sl = __builtin_bit_cast(f16x8, tile[cg_s(k2, 4 * t + kq, 1, jj)]);
-#pragma unroll
-      for (int mq = 0; mq < 4; ++mq) {
-        const uint4 gh = wr[t % TW][mq][0], gl = wr[t % TW][mq][1];
-        // re rows: (gr, -gi) pairs; im rows: (gi, gr) pairs
-        const f16x8 ah0 = __builtin_bit_cast(f16x8, gh ^ m), al0 = __builtin_bit_cast(f16x8, gl ^ m);
-        const f16x8 ah1 = __builtin_bit_cast(f16x8, (gh >> 16) | (gh << 16));
-        const f16x8 al1 = __builtin_bit_cast(f16x8, (gl >> 16) | (gl << 16));
-        acc[mq] = mfma16x16(al0, sh, acc[mq]);
-        acc[mq] = mfma16x16(ah0, sl, acc[mq]);
-        acc[mq] = mfma16x16(ah0, sh, acc[mq]);
-        acc[4 + mq] = mfma16x16(al1, sh, acc[4 + mq]);
-        acc[4 + mq] = mfma16x16(ah1, sl, acc[4 + mq]);
-        acc[4 + mq] = mfma16x16(ah1, sh, acc[4 + mq]);
-      }
-    }
-    lds_barrier();   // every wave has read this half of the S tile
-    // ---- Y of the half, [image][cq][k2 % 4] over its S: lane (kq, jj) holds rows 4 kq + r of each
-    // 16-row block, i.e. channels 4 (4 mq + kq) + r -- group cqo = 4 mq + kq, all four channels ----
-    f32x4* ytile = reinterpret_cast<f32x4*>(tile + half * CG_HALF);
-#pragma unroll
-    for (int mq = 0; mq < 4; ++mq) {
-      const int cqo = 4 * mq + kq;
-      const f32x4 re = acc[mq], im = acc[4 + mq];
-      ytile[jj * CG_YLD + (cqo * 4 + wv) * 2] = f32x4{re[0], im[0], re[1], im[1]} * unscale;
-      ytile[jj * CG_YLD + (cqo * 4 + wv) * 2 + 1] = f32x4{re[2], im[2], re[3], im[3]} * unscale;
-    }
-  }
-  lds_barrier();
-  // ---- 8-point inverse DFT over k2 -> n2, twiddle W72^{-n2 k1}, written over the inputs ----
-  cpx yv[4][8];
-#pragma unroll
-  for (int k2 = 0; k2 < 8; ++k2) {
-    const f32x4* yt = reinterpret_cast<const f32x4*>(tile + (k2 >> 2) * CG_HALF);
-    const f32x4 p0 = yt[bl * CG_YLD + (cq0 * 4 + (k2 & 3)) * 2 + hf];
-    const f32x4 p1 = yt[bl * CG_YLD + (cq1 * 4 + (k2 & 3)) * 2 + hf];
-    yv[0][k2] = cpx{p0[0], p0[1]};
-    yv[1][k2] = cpx{p0[2], p0[3]};
-    yv[2][k2] = cpx{p1[0], p1[1]};
-    yv[3][k2] = cpx{p1[2], p1[3]};
-  }
-#pragma unroll
-  for (int e = 0; e < 4; ++e) {
-    dft8<1>(yv[e]);
-#pragma unroll
-    for (int n2 = 0; n2 < 8; ++n2) yv[e][n2] = twid<1>(yv[e][n2], n2 * k1);
-  }
-  if (live) {
-#pragma unroll
-    for (int n2 = 0; n2 < 8; ++n2) {
-      f32x4* dst = reinterpret_cast<f32x4*>(Z + z_off(b, n2, fx, k1));
-      dst[a] = f32x4{yv[0][n2].x, yv[0][n2].y, yv[1][n2].x, yv[1][n2].y};
-      dst[a + 16] = f32x4{yv[2][n2].x, yv[2][n2].y, yv[3][n2].x, yv[3][n2].y};
-    }
-  }
-}
-
-// column kernel, eight waves (col8_kernel; MP_COL8=1): the same block (class, 16 images) and
-// arithmetic with 512 threads, so the per-thread DFT / split work halves (thread = image x channel
-// pair, one contiguous 512-B run of Z per image and n2 per wave instruction pair) and each wave
-// computes ONE frequency (k2 = wave): no second GEMM pass behind a weight reload.  Two blocks per
-// CU (16 waves) leave 128 VGPRs per wave.
+// col8_kernel: 512 threads, thread = image x channel pair (one contiguous 512-B run of Z per image
+// and n2 per wave instruction pair) for the DFTs and the split; each wave computes ONE frequency
+// (k2 = wave).  Two blocks per CU (16 waves) leave 128 VGPRs per wave.  Round 5 also measured a
+// four-wave form (two frequencies per wave behind a weight reload: 0.212 vs 0.192 ms at B = 256) and
+// a persistent form holding each wave's weights in registers over several image groups, one block
+// per CU (0.207 ms; batch-1 forward 1.06 vs 0.98 ms): both removed.
 __global__ __launch_bounds__(512, 2) void col8_kernel(cpx* __restrict__ Z, const uint4* __restrict__ Gc, int B,
                                                       int ngrp, float unscale) {
   __shared__ uint4 tile[2 * CG_HALF];   // 69,632 B
@@ -1175,57 +742,14 @@ bool fft4_enabled() {
   return v;
 }
 
-// MP_ROW2 (default 1): the two-blocks-per-CU row kernel; 0: row_kernel (one block per CU), for A/B
-static bool row2_enabled() {
-  static const bool v = [] {
-    const char* e = std::getenv("MP_ROW2");
-    return e ? std::atoi(e) != 0 : true;
-  }();
-  return v;
-}
-
-// MP_ROW8_MAXB (default: every batch): the largest launch batch on the eight-wave, one-block-per-CU row
-// kernel; above it row2_kernel (two blocks per CU, bit-identical).  Measured on one box (fp32, B = 256,
-// profiles/r5d): row8 everywhere 9.04 ms per forward (row A 0.282, row B 0.386 ms), row2 above 32
-// images 9.61 ms (0.318, 0.440): row2's second round of transposes and its register spills cost more
-// than its second block per CU gains
-static int row8_maxb() {
-  static const int v = [] {
-    const char* e = std::getenv("MP_ROW8_MAXB");
-    return e ? std::atoi(e) : (1 << 30);
-  }();
-  return v;
-}
-
-// MP_ROW2_PREO (default 1): B epilogue segments load O with I, before the o_r gate; 0: after it
-static bool row2_preo() {
-  static const bool v = [] {
-    const char* e = std::getenv("MP_ROW2_PREO");
-    return e ? std::atoi(e) != 0 : true;
-  }();
-  return v;
-}
-
-// MP_COL8 (default 1): the eight-wave column kernel; 0: the four-wave one (two frequencies per wave)
-static bool col8_enabled() {
-  static const bool v = [] {
-    const char* e = std::getenv("MP_COL8");
-    return e ? std::atoi(e) != 0 : true;
-  }();
-  return v;
-}
-
 hipError_t launch_col_gemm(void* Z, const void* Gc, int B, float unscale, hipStream_t st, bool bf) {
   if (B <= 0) return hipSuccess;
   const int ngrp = (B + CG_NI - 1) / CG_NI;
   if (bf)
     hipLaunchKernelGGL(col8_bf_kernel, dim3(CG_NC8 * 8 * ngrp), dim3(512), 0, st, Z, static_cast<const uint4*>(Gc), B,
                        ngrp);
-  else if (col8_enabled())
-    hipLaunchKernelGGL(col8_kernel, dim3(CG_NC8 * 8 * ngrp), dim3(512), 0, st, static_cast<cpx*>(Z),
-                       static_cast<const uint4*>(Gc), B, ngrp, unscale);
   else
-    hipLaunchKernelGGL(col_gemm_kernel, dim3(CG_NC8 * 8 * ngrp), dim3(256), 0, st, static_cast<cpx*>(Z),
+    hipLaunchKernelGGL(col8_kernel, dim3(CG_NC8 * 8 * ngrp), dim3(512), 0, st, static_cast<cpx*>(Z),
                        static_cast<const uint4*>(Gc), B, ngrp, unscale);
   return hipGetLastError();
 }
@@ -1234,63 +758,23 @@ hipError_t launch_row(int mode, void* Z, const ConvArgs& a, const void* or_x3, f
                       float ir_us, const float* O0, int B, hipStream_t st, bool bf) {
   if (B <= 0) return hipSuccess;
   if (a.H < 1 || a.H > 64 || (a.W != 32 && a.W != 64)) return hipErrorInvalidValue;
-  cpx* z = static_cast<cpx*>(Z);
-  const dim3 g(B * 8), t(RK_NT);
-  if (B <= row8_maxb()) {
-#define MP_ROW8(M, BFV) hipLaunchKernelGGL((row8_kernel<M, BFV>), g, dim3(R8_NT), 0, st, Z, a, or_x3, or_us, ir_x3, ir_us, O0)
-#define MP_ROW8S(BFV)                          \
-  switch (mode) {                              \
+  const dim3 g(B * 8), t(R8_NT);
+#define MP_ROW8(M, BFV) hipLaunchKernelGGL((row8_kernel<M, BFV>), g, t, 0, st, Z, a, or_x3, or_us, ir_x3, ir_us, O0)
+#define MP_ROW8S(BFV)                               \
+  switch (mode) {                                   \
     case ROW_A: MP_ROW8(ROW_A, BFV); break;         \
     case ROW_B: MP_ROW8(ROW_B, BFV); break;         \
     case ROW_FINAL: MP_ROW8(ROW_FINAL, BFV); break; \
     case ROW_INIT: MP_ROW8(ROW_INIT, BFV); break;   \
-    default: return hipErrorInvalidValue;      \
-  }
-    if (bf) {
-      MP_ROW8S(true)
-    } else {
-      MP_ROW8S(false)
-    }
-#undef MP_ROW8S
-#undef MP_ROW8
-    return hipGetLastError();
+    default: return hipErrorInvalidValue;           \
   }
   if (bf) {
-#define MP_ROW2BF(M) hipLaunchKernelGGL((row2_kernel<M, true, true>), g, t, 0, st, Z, a, or_x3, or_us, ir_x3, ir_us, O0)
-    switch (mode) {
-      case ROW_A: MP_ROW2BF(ROW_A); break;
-      case ROW_B: MP_ROW2BF(ROW_B); break;
-      case ROW_FINAL: MP_ROW2BF(ROW_FINAL); break;
-      case ROW_INIT: MP_ROW2BF(ROW_INIT); break;
-      default: return hipErrorInvalidValue;
-    }
-#undef MP_ROW2BF
-    return hipGetLastError();
+    MP_ROW8S(true)
+  } else {
+    MP_ROW8S(false)
   }
-  if (row2_enabled()) {
-    const bool pre = row2_preo();
-    switch (mode) {
-      case ROW_A: hipLaunchKernelGGL(row2_kernel<ROW_A>, g, t, 0, st, z, a, or_x3, or_us, ir_x3, ir_us, O0); break;
-      case ROW_B:
-        if (pre) hipLaunchKernelGGL((row2_kernel<ROW_B, true>), g, t, 0, st, z, a, or_x3, or_us, ir_x3, ir_us, O0);
-        else hipLaunchKernelGGL((row2_kernel<ROW_B, false>), g, t, 0, st, z, a, or_x3, or_us, ir_x3, ir_us, O0);
-        break;
-      case ROW_FINAL:
-        if (pre) hipLaunchKernelGGL((row2_kernel<ROW_FINAL, true>), g, t, 0, st, z, a, or_x3, or_us, ir_x3, ir_us, O0);
-        else hipLaunchKernelGGL((row2_kernel<ROW_FINAL, false>), g, t, 0, st, z, a, or_x3, or_us, ir_x3, ir_us, O0);
-        break;
-      case ROW_INIT: hipLaunchKernelGGL(row2_kernel<ROW_INIT>, g, t, 0, st, z, a, or_x3, or_us, ir_x3, ir_us, O0); break;
-      default: return hipErrorInvalidValue;
-    }
-    return hipGetLastError();
-  }
-  switch (mode) {
-    case ROW_A: hipLaunchKernelGGL(row_kernel<ROW_A>, g, t, 0, st, z, a, or_x3, or_us, ir_x3, ir_us, O0); break;
-    case ROW_B: hipLaunchKernelGGL(row_kernel<ROW_B>, g, t, 0, st, z, a, or_x3, or_us, ir_x3, ir_us, O0); break;
-    case ROW_FINAL: hipLaunchKernelGGL(row_kernel<ROW_FINAL>, g, t, 0, st, z, a, or_x3, or_us, ir_x3, ir_us, O0); break;
-    case ROW_INIT: hipLaunchKernelGGL(row_kernel<ROW_INIT>, g, t, 0, st, z, a, or_x3, or_us, ir_x3, ir_us, O0); break;
-    default: return hipErrorInvalidValue;
-  }
+#undef MP_ROW8S
+#undef MP_ROW8
   return hipGetLastError();
 }
 

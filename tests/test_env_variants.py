@@ -71,7 +71,6 @@ CASES = [
     # the six-launch FFT loop and the one-block-per-CU row kernel (A/B forms of the four-step loop)
     ({"MP_FFT4": "0"}, "pose", "fp32_fft", 1e-4),
     ({"MP_FFT4": "0"}, "pose", "bf16", 5e-3),
-    ({"MP_ROW2": "0", "MP_ROW8_MAXB": "0"}, "pose", "fp32_fft", 1e-4),
     ({"MP_IGEMM_PW": "0", "MP_IGEMM_HALO_NARROW": "0"}, "dense", "fp32_split", 1e-4),
     ({"MP_IGEMM_PW": "0", "MP_IGEMM_HALO_NARROW": "0"}, "dense", "bf16", 5e-3),
     ({"MP_GRAPH_FUSE_1X1": "0"}, "dense", "fp32_split", 1e-4),
@@ -125,14 +124,6 @@ BITS_CASES = [
     # 32-image tiles; the B epilogue's image order
     ("pose", "fp32_fft", "MP_SPEC_SMALLB", ("8", "32"), {"MP_FFT4": "0"}),
     ("pose80", "fp32_fft", "MP_EPI_REV", ("0", "1"), {"MP_FFT4": "0"}),
-    # four-step loop: the four- and eight-wave column kernels run each output's MFMA and DFT sequence
-    # identically; the row2 B epilogue's O loads before / after the o_r gate move nothing
-    # but timing; the eight-wave row kernel (gate weights in LDS) and row2 compute each value alike
-    ("pose80", "fp32_fft", "MP_COL8", ("0", "1"), {}),
-    ("pose80", "fp32_fft", "MP_ROW2_PREO", ("0", "1"), {"MP_ROW8_MAXB": "0"}),
-    ("pose80", "bf16", "MP_ROW2_PREO", ("0", "1"), {"MP_ROW8_MAXB": "0"}),
-    ("pose80", "fp32_fft", "MP_ROW8_MAXB", ("0", "1000000"), {}),
-    ("pose80", "bf16", "MP_ROW8_MAXB", ("0", "1000000"), {}),
 ]
 
 

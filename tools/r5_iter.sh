@@ -1,6 +1,6 @@
 #!/bin/bash
 # one iteration on the box: four-step loop check + timing + per-kernel profile (default, then each
-# MP_* A/B setting given in $AB, e.g. AB="MP_ROW2=0"; DT="bf16" adds that dtype's check), then the
+# MP_* A/B setting given in $AB, e.g. AB="MP_FFT4=0"; DT="bf16" adds that dtype's check), then the
 # given pytest files
 #   usage: [AB="K=V ..."] [DT="bf16"] bash tools/r5_iter.sh <tag> [pytest files...]
 set -o pipefail
