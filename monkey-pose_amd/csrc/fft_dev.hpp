@@ -81,8 +81,10 @@ __device__ __forceinline__ uint32_t pack_bf2(float a, float b) {
 
 
 // complex fp32: a 2-float vector, so a complex add is one v_pk_add_f32 and a twiddle product two
-// v_pk_fma_f32 / v_pk_mul_f32.  The re/im half swap of swp() is two plain v_mov_b32 in inline asm, so
-// the compiler cannot fold it into an op_sel half-select of a packed-FP32 source.  The folded form
+// v_pk_fma_f32 / v_pk_mul_f32.  The re/im half swap of swp() is one v_pk_mov_b32 (op_sel:[1,0], a
+// plain 64-bit move with its halves exchanged) in inline asm, so the compiler cannot fold it into an
+// op_sel half-select of a packed-FP32 source (round 5: it replaced two v_mov_b32 per swap, -11 % of
+// the row kernels' VALU instructions, same bits).  The folded form
 // (round 3's FFT_PACKED = 1: 7,902 such instructions in this file) gave results that differed from
 // the scalar build's and, under the two-stream hGRU schedule, from run to run (13-19 of 256 crops,
 // up to 2.1e-5, all in the batch's head / tail, where one slice runs alone:
@@ -97,9 +99,9 @@ __device__ __forceinline__ uint32_t pack_bf2(float a, float b) {
 typedef float cpx __attribute__((ext_vector_type(2)));
 __device__ __forceinline__ cpx cfma(cpx a, cpx b, cpx c) { return __builtin_elementwise_fma(a, b, c); }
 __device__ __forceinline__ cpx swp(cpx a) {
-  float x, y;
-  asm("v_mov_b32 %0, %2\n\tv_mov_b32 %1, %3" : "=&v"(x), "=&v"(y) : "v"(a.y), "v"(a.x));
-  return cpx{x, y};
+  cpx r;
+  asm("v_pk_mov_b32 %0, %1, %1 op_sel:[1,0]" : "=v"(r) : "v"(a));
+  return r;
 }
 
 // streaming (non-temporal) access to the once-written, once-read spectra and P2 (A/B switches)
