@@ -161,6 +161,18 @@ def pmc_mfma_busy():
     return {"source": PMC_MFMA, "mfma_busy": out}
 
 
+PMC_FORWARD = "profiles/r5z/pmc_forward_bytes.json"
+
+
+def pmc_forward_bytes(dtype, batch):
+    """Summed PMC HBM bytes of one whole pose forward (every kernel, B = 256) from the committed pass."""
+    full = os.path.join(os.path.dirname(os.path.abspath(__file__)), PMC_FORWARD)
+    if batch != 256 or not os.path.exists(full):
+        return None
+    d = json.load(open(full))
+    return dict(d.get(dtype, {}), source=d["source"]) if dtype in d else None
+
+
 def pmc_traffic(name, bf16, batch):
     """(bytes per launch, source) of kernel `name` from the committed PMC summary, or (None, why)."""
     import csv
@@ -718,6 +730,9 @@ def main():
             rec["roofline"]["mfma_busy_pmc"] = mb
     if kern:
         rec["fft_kernels"] = kern
+        pf = pmc_forward_bytes(args.dtype, B)
+        if pf:
+            rec["pmc_hbm_bytes_per_forward"] = pf
         # the direct 15x15 conv's FLOPs over the FFT path's time: a speed-up figure for the algorithm,
         # NOT an executed rate (the FFT path executes ~50x fewer FLOPs), so never read it against a peak
         rec["eCRF_direct_conv_flops_over_fft_time"] = {
