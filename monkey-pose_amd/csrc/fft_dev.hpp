@@ -246,6 +246,32 @@ __device__ __forceinline__ void dft8(cpx (&x)[8]) {
   x[7] = cfma(u7, cpx{-H, -H}, b3);
 }
 
+// FOLD: a +- rotq(v) as one fma each on swp(v) (3 instructions fewer; the same bits).  k_fft.hip's
+// 72-point transforms keep the unfolded form: folded, fft_inv_a_fwd_kernel spills (336 B / lane)
+template <int S>
+__device__ __forceinline__ void dft8_fold(cpx (&x)[8]) {
+  constexpr float H = 0.70710678118654752f;
+  constexpr cpx RP = {(float)-S, (float)S}, RM = {(float)S, (float)-S};
+  const cpx a0 = x[0] + x[4], a1 = x[0] - x[4], a2 = x[2] + x[6], v3 = swp(x[2] - x[6]);
+  const cpx a4 = x[1] + x[5], a5 = x[1] - x[5], a6 = x[3] + x[7], v7 = swp(x[3] - x[7]);
+  const cpx b0 = a0 + a2, b2 = a0 - a2, b1 = cfma(v3, RP, a1), b3 = cfma(v3, RM, a1);
+  const cpx b4 = a4 + a6, b6 = a4 - a6, b5 = cfma(v7, RP, a5), b7 = cfma(v7, RM, a5);
+  const cpx v6 = swp(b6);
+  // b5 * W8^1 = H (b5 + rotq b5), b7 * W8^3 = H (rotq b7 - b7): the products by H fused into the
+  // butterflies explicitly (contraction left to the compiler was decided per call site: the same
+  // transform rounded differently in the batched and the small-batch kernels)
+  const cpx u5 = cfma(swp(b5), cpx{(float)-S, (float)S}, b5);
+  const cpx u7 = cfma(swp(b7), cpx{(float)-S, (float)S}, -b7);
+  x[0] = b0 + b4;
+  x[4] = b0 - b4;
+  x[2] = cfma(v6, RP, b2);
+  x[6] = cfma(v6, RM, b2);
+  x[1] = cfma(u5, cpx{H, H}, b1);
+  x[5] = cfma(u5, cpx{-H, -H}, b1);
+  x[3] = cfma(u7, cpx{H, H}, b3);
+  x[7] = cfma(u7, cpx{-H, -H}, b3);
+}
+
 template <int S>
 __device__ __forceinline__ void dft3(cpx& z0, cpx& z1, cpx& z2) {
   constexpr float R3 = 0.86602540378443865f;
@@ -315,15 +341,23 @@ constexpr float GATE_VSCALE = 256.0f;   // activations entering a gate: |v| < 25
 // Y[n2] = sum_cin G[cin][32 n2 + row] V[cin][pixel], f16x3; gpk = [n2][s][hi|lo][lane] f16x8
 __device__ __forceinline__ void gate_x3(const f16x8* __restrict__ gpk, const f32x16 (&V)[2], f32x16 (&Y)[2],
                                         int lane, float unscale) {
+  // the split in channel pairs: one v_pk_mul_f32, v_cvt_pk_f16_f32 for hi and lo, one v_pk_add_f32
+  // (round to nearest even as (_Float16); v - hi is exact)
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  typedef _Float16 h2 __attribute__((ext_vector_type(2)));
   f16x8 bh[4], bl[4];
 #pragma unroll
   for (int s = 0; s < 4; ++s)
 #pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      const float v = V[s >> 1][8 * (s & 1) + e] * GATE_VSCALE;
-      const _Float16 hv = (_Float16)v;
-      bh[s][e] = hv;
-      bl[s][e] = (_Float16)(v - (float)hv);
+    for (int e = 0; e < 8; e += 2) {
+      const int r = 8 * (s & 1) + e;
+      const f2 v = f2{V[s >> 1][r], V[s >> 1][r + 1]} * GATE_VSCALE;
+      const h2 hv = __builtin_convertvector(v, h2);
+      const h2 lv = __builtin_convertvector(v - __builtin_convertvector(hv, f2), h2);
+      bh[s][e] = hv[0];
+      bh[s][e + 1] = hv[1];
+      bl[s][e] = lv[0];
+      bl[s][e + 1] = lv[1];
     }
 #pragma unroll
   for (int n2 = 0; n2 < 2; ++n2) {

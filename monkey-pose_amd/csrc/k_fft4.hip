@@ -274,11 +274,11 @@ __device__ __forceinline__ void rk_segment(const ConvArgs& p, float* seg, int b,
 // ---------------------------------------------------------------------------------------------
 template <int S>
 __device__ __forceinline__ void dft4(cpx (&x)[4]) {
-  const cpx a0 = x[0] + x[2], a1 = x[0] - x[2], a2 = x[1] + x[3], a3 = rotq<S>(x[1] - x[3]);
+  const cpx a0 = x[0] + x[2], a1 = x[0] - x[2], a2 = x[1] + x[3], v3 = swp(x[1] - x[3]);
   x[0] = a0 + a2;
   x[2] = a0 - a2;
-  x[1] = a1 + a3;
-  x[3] = a1 - a3;
+  x[1] = cfma(v3, cpx{(float)-S, (float)S}, a1);   // a1 + rotq(x1 - x3), one fma (exact product)
+  x[3] = cfma(v3, cpx{(float)S, (float)-S}, a1);
 }
 
 // 36-point DFT, X[k] = sum_n v[n] e^{S 2 pi i n k / 36}: Good-Thomas 36 = 4 x 9 (gcd 1),
@@ -315,10 +315,13 @@ __device__ __forceinline__ void rfft72_fwd(const float (&x)[64], cpx (&X)[FX]) {
 #pragma unroll
   for (int k = 0; k < FX; ++k) {
     // E[k] = (Z[k] + conj Z[36-k]) / 2, O[k] = (Z[k] - conj Z[36-k]) / 2i, X[k] = E[k] + W72^k O[k]
+    // = E + d w with d = Z[k] - conj Z[36-k] and w = W72^k / 2i = (-sin / 2, -cos / 2) (k 2 pi / 72):
+    // two fmas on d and swp(d) after E, no separate twiddle product
     const cpx zk = z[k % 36], zm = z[(36 - k) % 36];
-    const cpx E = cfma(zm, cpx{1.f, -1.f}, zk) * 0.5f;               // (zk.x + zm.x, zk.y - zm.y) / 2
-    const cpx O = cfma(swp(zk), cpx{1.f, -1.f}, swp(zm)) * 0.5f;     // (zk.y + zm.y, zm.x - zk.x) / 2
-    X[k] = E + twid<-1>(O, k);
+    const cpx E = cfma(zm, cpx{0.5f, -0.5f}, zk * 0.5f);             // (zk + conj zm) / 2, exact halving
+    const cpx d = cfma(zm, cpx{-1.f, 1.f}, zk);                       // zk - conj zm
+    const float wc = 0.5f * TW72_COS[k], ws = 0.5f * TW72_SIN[k];
+    X[k] = cfma(swp(d), cpx{wc, -wc}, cfma(d, cpx{-ws, -ws}, E));
   }
 }
 
@@ -328,10 +331,12 @@ __device__ __forceinline__ void rfft72_inv(const cpx (&X)[FX], float (&x)[64]) {
 #pragma unroll
   for (int k = 0; k < 36; ++k) {
     // x[2m] = IDFT36(E), x[2m+1] = IDFT36(O): E[k] = X[k] + conj X[36-k], O[k] = (X[k] - conj X[36-k]) W72^{-k}
+    // E + i O = E + D (i W72^{-k}), D = a - conj c, i W72^{-k} = (-sin, cos) (k 2 pi / 72)
     const cpx a = X[k], c = X[36 - k];
     const cpx E = cfma(c, cpx{1.f, -1.f}, a);                         // (a.x + c.x, a.y - c.y)
-    const cpx O = twid<1>(cfma(c, cpx{-1.f, 1.f}, a), k);            // (a.x - c.x, a.y + c.y) W72^{-k}
-    z[k] = cfma(swp(O), cpx{-1.f, 1.f}, E);                           // E + i O
+    const cpx D = cfma(c, cpx{-1.f, 1.f}, a);                         // (a.x - c.x, a.y + c.y)
+    const float wc = TW72_COS[k], ws = TW72_SIN[k];
+    z[k] = cfma(swp(D), cpx{-wc, wc}, cfma(D, cpx{-ws, -ws}, E));
   }
   fft36<1>(z);
 #pragma unroll
@@ -554,7 +559,7 @@ __global__ __launch_bounds__(512, 2) void col8_kernel(cpx* __restrict__ Z, const
     for (int e = 0; e < 2; ++e) {
 #pragma unroll
       for (int n2 = 0; n2 < 8; ++n2) s[e][n2] = twid<-1>(cpx{zin[n2][2 * e], zin[n2][2 * e + 1]}, n2 * k1);
-      dft8<-1>(s[e]);
+      dft8_fold<-1>(s[e]);
     }
     typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
     uint2* t2 = reinterpret_cast<uint2*>(tile);
@@ -632,7 +637,7 @@ __global__ __launch_bounds__(512, 2) void col8_kernel(cpx* __restrict__ Z, const
   }
 #pragma unroll
   for (int e = 0; e < 2; ++e) {
-    dft8<1>(yv[e]);
+    dft8_fold<1>(yv[e]);
 #pragma unroll
     for (int n2 = 0; n2 < 8; ++n2) yv[e][n2] = twid<1>(yv[e][n2], n2 * k1);
   }
@@ -672,7 +677,7 @@ __global__ __launch_bounds__(512, 2) void col8_bf_kernel(void* __restrict__ Zv, 
     for (int e = 0; e < 2; ++e) {
 #pragma unroll
       for (int n2 = 0; n2 < 8; ++n2) s[e][n2] = twid<-1>(unpack_bf2(e ? zin[n2].y : zin[n2].x), n2 * k1);
-      dft8<-1>(s[e]);
+      dft8_fold<-1>(s[e]);
     }
     uint2* t2 = reinterpret_cast<uint2*>(tile);
 #pragma unroll
@@ -721,7 +726,7 @@ __global__ __launch_bounds__(512, 2) void col8_bf_kernel(void* __restrict__ Zv, 
   }
 #pragma unroll
   for (int e = 0; e < 2; ++e) {
-    dft8<1>(yv[e]);
+    dft8_fold<1>(yv[e]);
 #pragma unroll
     for (int n2 = 0; n2 < 8; ++n2) yv[e][n2] = twid<1>(yv[e][n2], n2 * k1);
   }
