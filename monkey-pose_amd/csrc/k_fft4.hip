@@ -561,22 +561,24 @@ __global__ __launch_bounds__(512, 2) void col8_kernel(cpx* __restrict__ Z, const
       for (int n2 = 0; n2 < 8; ++n2) s[e][n2] = twid<-1>(cpx{zin[n2][2 * e], zin[n2][2 * e + 1]}, n2 * k1);
       dft8_fold<-1>(s[e]);
     }
-    typedef _Float16 f16x4 __attribute__((ext_vector_type(4)));
+    // the f16 hi / lo split of each (re, im) pair: v_pk_mul_f32, v_cvt_pk_f16_f32 for hi and lo (round to
+    // nearest even, as (_Float16)), v_pk_add_f32 (re - hi is exact).  Columns of images past B are not
+    // zeroed: an MFMA output column depends on its own S column only, and theirs are never stored.
+    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
     uint2* t2 = reinterpret_cast<uint2*>(tile);
 #pragma unroll
     for (int k2 = 0; k2 < 8; ++k2) {
-      f16x4 hv, lv;
+      uint32_t hv[2], lv[2];
 #pragma unroll
       for (int e = 0; e < 2; ++e) {
-        const float re = s[e][k2].x * SPEC_SCALE, im = s[e][k2].y * SPEC_SCALE;
-        const _Float16 hr = (_Float16)re, hm = (_Float16)im;
-        hv[2 * e] = hr;
-        hv[2 * e + 1] = hm;
-        lv[2 * e] = (_Float16)(re - (float)hr);
-        lv[2 * e + 1] = (_Float16)(im - (float)hm);
+        const cpx v = s[e][k2] * SPEC_SCALE;
+        const h2 hi = __builtin_convertvector(v, h2);
+        const h2 lo = __builtin_convertvector(v - __builtin_convertvector(hi, cpx), h2);
+        hv[e] = __builtin_bit_cast(uint32_t, hi);
+        lv[e] = __builtin_bit_cast(uint32_t, lo);
       }
-      t2[cg_s(k2, cq, 0, bl) * 2 + hf] = live ? __builtin_bit_cast(uint2, hv) : uint2{0, 0};
-      t2[cg_s(k2, cq, 1, bl) * 2 + hf] = live ? __builtin_bit_cast(uint2, lv) : uint2{0, 0};
+      t2[cg_s(k2, cq, 0, bl) * 2 + hf] = uint2{hv[0], hv[1]};
+      t2[cg_s(k2, cq, 1, bl) * 2 + hf] = uint2{lv[0], lv[1]};
     }
   }
   const int kq = lane >> 4, jj = lane & 15, k2 = wv;
@@ -594,25 +596,27 @@ __global__ __launch_bounds__(512, 2) void col8_kernel(cpx* __restrict__ Z, const
   };
   load_w(0);
   lds_barrier();
+  // the compact weights A = (gr, gi) pairs as stored; the S fragment supplies the two forms, (sr, -si)
+  // for the real rows (gr sr - gi si) and (si, sr) for the imaginary rows (gr si + gi sr): a sign flip
+  // and a half swap per S dword (16 VALU per k-step) instead of four weight forms (64)
   const uint4 m = {0x80000000u, 0x80000000u, 0x80000000u, 0x80000000u};
   f32x4 acc[8] = {};
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
     if (t > 0 && t % TW == 0) load_w(t);
-    const f16x8 sh = __builtin_bit_cast(f16x8, tile[cg_s(k2, 4 * t + kq, 0, jj)]);
-    const f16x8 sl = __builtin_bit_cast(f16x8, tile[cg_s(k2, 4 * t + kq, 1, jj)]);
+    const uint4 uh = tile[cg_s(k2, 4 * t + kq, 0, jj)], ul = tile[cg_s(k2, 4 * t + kq, 1, jj)];
+    const f16x8 sh = __builtin_bit_cast(f16x8, uh ^ m), sl = __builtin_bit_cast(f16x8, ul ^ m);
+    const f16x8 sh2 = __builtin_bit_cast(f16x8, (uh >> 16) | (uh << 16));
+    const f16x8 sl2 = __builtin_bit_cast(f16x8, (ul >> 16) | (ul << 16));
 #pragma unroll
     for (int mq = 0; mq < 4; ++mq) {
-      const uint4 gh = wr[t % TW][mq][0], gl = wr[t % TW][mq][1];
-      const f16x8 ah0 = __builtin_bit_cast(f16x8, gh ^ m), al0 = __builtin_bit_cast(f16x8, gl ^ m);
-      const f16x8 ah1 = __builtin_bit_cast(f16x8, (gh >> 16) | (gh << 16));
-      const f16x8 al1 = __builtin_bit_cast(f16x8, (gl >> 16) | (gl << 16));
-      acc[mq] = mfma16x16(al0, sh, acc[mq]);
-      acc[mq] = mfma16x16(ah0, sl, acc[mq]);
-      acc[mq] = mfma16x16(ah0, sh, acc[mq]);
-      acc[4 + mq] = mfma16x16(al1, sh, acc[4 + mq]);
-      acc[4 + mq] = mfma16x16(ah1, sl, acc[4 + mq]);
-      acc[4 + mq] = mfma16x16(ah1, sh, acc[4 + mq]);
+      const f16x8 ah = __builtin_bit_cast(f16x8, wr[t % TW][mq][0]), al = __builtin_bit_cast(f16x8, wr[t % TW][mq][1]);
+      acc[mq] = mfma16x16(al, sh, acc[mq]);
+      acc[mq] = mfma16x16(ah, sl, acc[mq]);
+      acc[mq] = mfma16x16(ah, sh, acc[mq]);
+      acc[4 + mq] = mfma16x16(al, sh2, acc[4 + mq]);
+      acc[4 + mq] = mfma16x16(ah, sl2, acc[4 + mq]);
+      acc[4 + mq] = mfma16x16(ah, sh2, acc[4 + mq]);
     }
   }
   lds_barrier();   // every wave has read the S tile
@@ -681,9 +685,8 @@ __global__ __launch_bounds__(512, 2) void col8_bf_kernel(void* __restrict__ Zv, 
     }
     uint2* t2 = reinterpret_cast<uint2*>(tile);
 #pragma unroll
-    for (int k2 = 0; k2 < 8; ++k2)
-      t2[sidx(k2, cq, bl) * 2 + hf] =
-          live ? uint2{pack_bf2(s[0][k2].x, s[0][k2].y), pack_bf2(s[1][k2].x, s[1][k2].y)} : uint2{0, 0};
+    for (int k2 = 0; k2 < 8; ++k2)   // (columns past B unmasked, as in col8_kernel)
+      t2[sidx(k2, cq, bl) * 2 + hf] = uint2{pack_bf2(s[0][k2].x, s[0][k2].y), pack_bf2(s[1][k2].x, s[1][k2].y)};
   }
   const int kq = lane >> 4, jj = lane & 15, k2 = wv;
   uint4 wr[4][4];
@@ -696,14 +699,14 @@ __global__ __launch_bounds__(512, 2) void col8_bf_kernel(void* __restrict__ Zv, 
   const uint4 m = {0x80000000u, 0x80000000u, 0x80000000u, 0x80000000u};
   f32x4 acc[8] = {};
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {
-    const bf16x8 sb = __builtin_bit_cast(bf16x8, tile[sidx(k2, 4 * t + kq, jj)]);
+  for (int t = 0; t < 4; ++t) {   // S-side forms as in col8_kernel
+    const uint4 us = tile[sidx(k2, 4 * t + kq, jj)];
+    const bf16x8 sre = __builtin_bit_cast(bf16x8, us ^ m), sim = __builtin_bit_cast(bf16x8, (us >> 16) | (us << 16));
 #pragma unroll
     for (int mq = 0; mq < 4; ++mq) {
-      const uint4 g = wr[t][mq];
-      acc[mq] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, g ^ m), sb, acc[mq], 0, 0, 0);
-      acc[4 + mq] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, (g >> 16) | (g << 16)), sb,
-                                                            acc[4 + mq], 0, 0, 0);
+      const bf16x8 g = __builtin_bit_cast(bf16x8, wr[t][mq]);
+      acc[mq] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(g, sre, acc[mq], 0, 0, 0);
+      acc[4 + mq] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(g, sim, acc[4 + mq], 0, 0, 0);
     }
   }
   lds_barrier();
