@@ -537,6 +537,7 @@ __device__ __forceinline__ f32x4 mfma16x16(f16x8 a, f16x8 b, f32x4 c) {
 // four-wave form (two frequencies per wave behind a weight reload: 0.212 vs 0.192 ms at B = 256) and
 // a persistent form holding each wave's weights in registers over several image groups, one block
 // per CU (0.207 ms; batch-1 forward 1.06 vs 0.98 ms): both removed.
+template <bool RING>
 __global__ __launch_bounds__(512, 2) void col8_kernel(cpx* __restrict__ Z, const uint4* __restrict__ Gc, int B,
                                                       int ngrp, float unscale) {
   __shared__ uint4 tile[2 * CG_HALF];   // 69,632 B
@@ -582,17 +583,22 @@ __global__ __launch_bounds__(512, 2) void col8_kernel(cpx* __restrict__ Z, const
     }
   }
   const int kq = lane >> 4, jj = lane & 15, k2 = wv;
+  // weights of two k-steps in registers (64 VGPRs).  RING: k-step t + 2's loads go into step t's slot
+  // right after step t's MFMAs, so step t + 1's MFMAs cover part of their latency; otherwise steps 2
+  // and 3 are loaded together after step 1
   constexpr int TW = 2;
   uint4 wr[TW][4][2];
   const uint4* gw = Gc + (size_t)(cls * 8 + k2) * 2 * 16 * 64;
+  auto load_1 = [&](int slot, int t) {
+#pragma unroll
+    for (int mq = 0; mq < 4; ++mq) {
+      wr[slot][mq][0] = gw[(0 * 16 + 4 * t + kq) * 64 + 16 * mq + jj];
+      wr[slot][mq][1] = gw[(1 * 16 + 4 * t + kq) * 64 + 16 * mq + jj];
+    }
+  };
   auto load_w = [&](int t0) {
 #pragma unroll
-    for (int t = 0; t < TW; ++t)
-#pragma unroll
-      for (int mq = 0; mq < 4; ++mq) {
-        wr[t][mq][0] = gw[(0 * 16 + 4 * (t0 + t) + kq) * 64 + 16 * mq + jj];
-        wr[t][mq][1] = gw[(1 * 16 + 4 * (t0 + t) + kq) * 64 + 16 * mq + jj];
-      }
+    for (int t = 0; t < TW; ++t) load_1(t, t0 + t);
   };
   load_w(0);
   lds_barrier();
@@ -603,7 +609,7 @@ __global__ __launch_bounds__(512, 2) void col8_kernel(cpx* __restrict__ Z, const
   f32x4 acc[8] = {};
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
-    if (t > 0 && t % TW == 0) load_w(t);
+    if (!RING && t > 0 && t % TW == 0) load_w(t);
     const uint4 uh = tile[cg_s(k2, 4 * t + kq, 0, jj)], ul = tile[cg_s(k2, 4 * t + kq, 1, jj)];
     const f16x8 sh = __builtin_bit_cast(f16x8, uh ^ m), sl = __builtin_bit_cast(f16x8, ul ^ m);
     const f16x8 sh2 = __builtin_bit_cast(f16x8, (uh >> 16) | (uh << 16));
@@ -618,6 +624,7 @@ __global__ __launch_bounds__(512, 2) void col8_kernel(cpx* __restrict__ Z, const
       acc[4 + mq] = mfma16x16(ah, sl2, acc[4 + mq]);
       acc[4 + mq] = mfma16x16(ah, sh2, acc[4 + mq]);
     }
+    if (RING && t + 2 < 4) load_1(t % 2, t + 2);
   }
   lds_barrier();   // every wave has read the S tile
   // Y tile over the whole S tile: [image][cq][k2] (16-B units, pitch 16 * 8 * 2 + 1 per image)
@@ -750,14 +757,26 @@ bool fft4_enabled() {
   return v;
 }
 
+// MP_COL8_RING (default 1): col8_kernel's weight loads one k-step ring slot ahead; 0: two steps at a time
+static bool col8_ring() {
+  static const bool v = [] {
+    const char* e = std::getenv("MP_COL8_RING");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  return v;
+}
+
 hipError_t launch_col_gemm(void* Z, const void* Gc, int B, float unscale, hipStream_t st, bool bf) {
   if (B <= 0) return hipSuccess;
   const int ngrp = (B + CG_NI - 1) / CG_NI;
   if (bf)
     hipLaunchKernelGGL(col8_bf_kernel, dim3(CG_NC8 * 8 * ngrp), dim3(512), 0, st, Z, static_cast<const uint4*>(Gc), B,
                        ngrp);
+  else if (col8_ring())
+    hipLaunchKernelGGL(col8_kernel<true>, dim3(CG_NC8 * 8 * ngrp), dim3(512), 0, st, static_cast<cpx*>(Z),
+                       static_cast<const uint4*>(Gc), B, ngrp, unscale);
   else
-    hipLaunchKernelGGL(col8_kernel, dim3(CG_NC8 * 8 * ngrp), dim3(512), 0, st, static_cast<cpx*>(Z),
+    hipLaunchKernelGGL(col8_kernel<false>, dim3(CG_NC8 * 8 * ngrp), dim3(512), 0, st, static_cast<cpx*>(Z),
                        static_cast<const uint4*>(Gc), B, ngrp, unscale);
   return hipGetLastError();
 }
