@@ -537,7 +537,9 @@ __device__ __forceinline__ f32x4 mfma16x16(f16x8 a, f16x8 b, f32x4 c) {
 // four-wave form (two frequencies per wave behind a weight reload: 0.212 vs 0.192 ms at B = 256) and
 // a persistent form holding each wave's weights in registers over several image groups, one block
 // per CU (0.207 ms; batch-1 forward 1.06 vs 0.98 ms): both removed.
-template <bool RING>
+// ZNT: the partials Z read and written non-temporal (the weights, re-read by the other batch slice's
+// launch of the same convolution, keep the cache)
+template <bool RING, bool ZNT>
 __global__ __launch_bounds__(512, 2) void col8_kernel(cpx* __restrict__ Z, const uint4* __restrict__ Gc, int B,
                                                       int ngrp, float unscale) {
   __shared__ uint4 tile[2 * CG_HALF];   // 69,632 B
@@ -554,7 +556,10 @@ __global__ __launch_bounds__(512, 2) void col8_kernel(cpx* __restrict__ Z, const
   {
     f32x4 zin[8];
 #pragma unroll
-    for (int n2 = 0; n2 < 8; ++n2) zin[n2] = reinterpret_cast<const f32x4*>(Z + z_off(b, n2, fx, k1))[a];
+    for (int n2 = 0; n2 < 8; ++n2) {
+      const f32x4* zp = reinterpret_cast<const f32x4*>(Z + z_off(b, n2, fx, k1)) + a;
+      zin[n2] = ZNT ? __builtin_nontemporal_load(zp) : *zp;
+    }
     cpx s[2][8];
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
@@ -655,7 +660,12 @@ __global__ __launch_bounds__(512, 2) void col8_kernel(cpx* __restrict__ Z, const
   if (live) {
 #pragma unroll
     for (int n2 = 0; n2 < 8; ++n2)
-      reinterpret_cast<f32x4*>(Z + z_off(b, n2, fx, k1))[a] = f32x4{yv[0][n2].x, yv[0][n2].y, yv[1][n2].x, yv[1][n2].y};
+    {
+      f32x4* zp = reinterpret_cast<f32x4*>(Z + z_off(b, n2, fx, k1)) + a;
+      const f32x4 v = f32x4{yv[0][n2].x, yv[0][n2].y, yv[1][n2].x, yv[1][n2].y};
+      if constexpr (ZNT) __builtin_nontemporal_store(v, zp);
+      else *zp = v;
+    }
   }
 }
 
@@ -766,18 +776,32 @@ static bool col8_ring() {
   return v;
 }
 
+// MP_COL8_ZNT (default 0): col8_kernel's Z loads and stores non-temporal
+static bool col8_znt() {
+  static const bool v = [] {
+    const char* e = std::getenv("MP_COL8_ZNT");
+    return e ? std::atoi(e) != 0 : false;
+  }();
+  return v;
+}
+
 hipError_t launch_col_gemm(void* Z, const void* Gc, int B, float unscale, hipStream_t st, bool bf) {
   if (B <= 0) return hipSuccess;
   const int ngrp = (B + CG_NI - 1) / CG_NI;
   if (bf)
     hipLaunchKernelGGL(col8_bf_kernel, dim3(CG_NC8 * 8 * ngrp), dim3(512), 0, st, Z, static_cast<const uint4*>(Gc), B,
                        ngrp);
-  else if (col8_ring())
-    hipLaunchKernelGGL(col8_kernel<true>, dim3(CG_NC8 * 8 * ngrp), dim3(512), 0, st, static_cast<cpx*>(Z),
-                       static_cast<const uint4*>(Gc), B, ngrp, unscale);
-  else
-    hipLaunchKernelGGL(col8_kernel<false>, dim3(CG_NC8 * 8 * ngrp), dim3(512), 0, st, static_cast<cpx*>(Z),
-                       static_cast<const uint4*>(Gc), B, ngrp, unscale);
+  else {
+#define MP_COL8(R, N)                                                                                       \
+  hipLaunchKernelGGL((col8_kernel<R, N>), dim3(CG_NC8 * 8 * ngrp), dim3(512), 0, st, static_cast<cpx*>(Z), \
+                     static_cast<const uint4*>(Gc), B, ngrp, unscale)
+    const bool r = col8_ring(), n = col8_znt();
+    if (r && n) MP_COL8(true, true);
+    else if (r) MP_COL8(true, false);
+    else if (n) MP_COL8(false, true);
+    else MP_COL8(false, false);
+#undef MP_COL8
+  }
   return hipGetLastError();
 }
 
