@@ -434,26 +434,6 @@ void fft4_circuit_range(mp_ctx* c, int b0, int n, int H, int W, int T, const flo
   }
 }
 
-// MP_WAVE = n (default 0 = off): a stream's images go through the whole four-step hGRU loop in
-// sequential waves of n, so that a wave's in-place Z buffer and maps (~2.1 MB per image at fp32)
-// can stay in the 256 MiB Infinity Cache between the loop's launches
-int wave_images() {
-  static const int v = [] {
-    const char* e = std::getenv("MP_WAVE");
-    return e ? std::max(0, std::atoi(e)) : 0;
-  }();
-  return v;
-}
-void fft4_waves(mp_ctx* c, int b0, int n, int H, int W, int T, const float* o0_nhwc, float* final_dst2,
-                const StateOut* so, const SplitOut* sp, hipStream_t st) {
-  const int wv = wave_images();
-  if (wv <= 0 || wv >= n) {
-    fft4_circuit_range(c, b0, n, H, W, T, o0_nhwc, final_dst2, so, sp, st);
-    return;
-  }
-  for (int w0 = 0; w0 < n; w0 += wv)
-    fft4_circuit_range(c, b0 + w0, std::min(wv, n - w0), H, W, T, o0_nhwc, final_dst2, so, sp, st);
-}
 
 // fc_1 on pre-split activation planes (MP_FC_PRESPLIT=0: the fp32 map + in-loop split, for A/B)
 bool fc_presplit() {
@@ -488,7 +468,7 @@ void run_circuit(mp_ctx* c, int64_t n, int H, int W, int T, const float* o0_nhwc
   // their latency-bound kernels overlap (the per-kernel HIP-event profile keeps one stream)
   const int ns = std::min<int>(stream_count(), (int)(n / slice_min()));
   if (c->fft4 && (c->prof || ns < 2)) {
-    fft4_waves(c, 0, (int)n, H, W, T, o0_nhwc, final_dst2, so, sp, st);
+    fft4_circuit_range(c, 0, (int)n, H, W, T, o0_nhwc, final_dst2, so, sp, st);
     return;
   }
   if (is_fft(c->dtype) && !c->prof && ns >= 2) {
@@ -516,7 +496,7 @@ void run_circuit(mp_ctx* c, int64_t n, int H, int W, int T, const float* o0_nhwc
       hipStream_t s = k == 0 ? st : c->sides[k - 1];
       if (k > 0) hip_check(hipStreamWaitEvent(s, c->ev_fork, 0), "hipStreamWaitEvent");
       if (c->fft4)
-        fft4_waves(c, b0, cnt, H, W, T, o0_nhwc, final_dst2, so, sp, s);
+        fft4_circuit_range(c, b0, cnt, H, W, T, o0_nhwc, final_dst2, so, sp, s);
       else
         fft_circuit_range(c, b0, cnt, H, W, T, final_dst2, so, sp, s);
       b0 += cnt;
