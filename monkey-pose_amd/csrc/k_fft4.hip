@@ -539,7 +539,7 @@ __device__ __forceinline__ f32x4 mfma16x16(f16x8 a, f16x8 b, f32x4 c) {
 // per CU (0.207 ms; batch-1 forward 1.06 vs 0.98 ms): both removed.
 // ZNT: the partials Z read and written non-temporal (the weights, re-read by the other batch slice's
 // launch of the same convolution, keep the cache)
-template <bool RING, bool ZNT>
+template <bool ZNT>
 __global__ __launch_bounds__(512, 2) void col8_kernel(cpx* __restrict__ Z, const uint4* __restrict__ Gc, int B,
                                                       int ngrp, float unscale) {
   __shared__ uint4 tile[2 * CG_HALF];   // 69,632 B
@@ -588,9 +588,9 @@ __global__ __launch_bounds__(512, 2) void col8_kernel(cpx* __restrict__ Z, const
     }
   }
   const int kq = lane >> 4, jj = lane & 15, k2 = wv;
-  // weights of two k-steps in registers (64 VGPRs).  RING: k-step t + 2's loads go into step t's slot
-  // right after step t's MFMAs, so step t + 1's MFMAs cover part of their latency; otherwise steps 2
-  // and 3 are loaded together after step 1
+  // weights of two k-steps in registers (64 VGPRs), a two-slot ring: k-step t + 2's loads go into step
+  // t's slot right after step t's MFMAs, so step t + 1's MFMAs cover part of their latency (col8 0.196 ->
+  // 0.185 ms against loading steps 2 and 3 together after step 1; profiles/r5l)
   constexpr int TW = 2;
   uint4 wr[TW][4][2];
   const uint4* gw = Gc + (size_t)(cls * 8 + k2) * 2 * 16 * 64;
@@ -614,7 +614,6 @@ __global__ __launch_bounds__(512, 2) void col8_kernel(cpx* __restrict__ Z, const
   f32x4 acc[8] = {};
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
-    if (!RING && t > 0 && t % TW == 0) load_w(t);
     const uint4 uh = tile[cg_s(k2, 4 * t + kq, 0, jj)], ul = tile[cg_s(k2, 4 * t + kq, 1, jj)];
     const f16x8 sh = __builtin_bit_cast(f16x8, uh ^ m), sl = __builtin_bit_cast(f16x8, ul ^ m);
     const f16x8 sh2 = __builtin_bit_cast(f16x8, (uh >> 16) | (uh << 16));
@@ -629,7 +628,7 @@ __global__ __launch_bounds__(512, 2) void col8_kernel(cpx* __restrict__ Z, const
       acc[4 + mq] = mfma16x16(ah, sl2, acc[4 + mq]);
       acc[4 + mq] = mfma16x16(ah, sh2, acc[4 + mq]);
     }
-    if (RING && t + 2 < 4) load_1(t % 2, t + 2);
+    if (t + 2 < 4) load_1(t % 2, t + 2);
   }
   lds_barrier();   // every wave has read the S tile
   // Y tile over the whole S tile: [image][cq][k2] (16-B units, pitch 16 * 8 * 2 + 1 per image)
@@ -674,6 +673,7 @@ __global__ __launch_bounds__(512, 2) void col8_kernel(cpx* __restrict__ Z, const
 // v_mfma_f32_16x16x32_bf16 product per (k-step, row block, re|im) against the class-major bf16
 // weights Gb[f][cq][co] (16 KiB per frequency), fp32 accumulation, DFTs and twiddles in fp32.
 constexpr int CB_HALF = 16 * 4 * CG_SLD;             // one frequency half of the bf16 S tile (16-B units)
+template <bool ZNT>
 __global__ __launch_bounds__(512, 2) void col8_bf_kernel(void* __restrict__ Zv, const uint4* __restrict__ Gb, int B,
                                                          int ngrp) {
   __shared__ uint4 tile[2 * CG_HALF];   // the Y tile (fp32) needs the fp32 kernel's space
@@ -692,7 +692,12 @@ __global__ __launch_bounds__(512, 2) void col8_bf_kernel(void* __restrict__ Zv, 
   {
     uint2 zin[8];
 #pragma unroll
-    for (int n2 = 0; n2 < 8; ++n2) zin[n2] = reinterpret_cast<const uint2*>(Z + z_off(b, n2, fx, k1))[a];
+    for (int n2 = 0; n2 < 8; ++n2) {
+      typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+      const u2v* zp = reinterpret_cast<const u2v*>(Z + z_off(b, n2, fx, k1)) + a;
+      const u2v v = ZNT ? __builtin_nontemporal_load(zp) : *zp;
+      zin[n2] = uint2{v.x, v.y};
+    }
     cpx s[2][8];
 #pragma unroll
     for (int e = 0; e < 2; ++e) {
@@ -753,8 +758,13 @@ __global__ __launch_bounds__(512, 2) void col8_bf_kernel(void* __restrict__ Zv, 
   if (live) {
 #pragma unroll
     for (int n2 = 0; n2 < 8; ++n2)
-      reinterpret_cast<uint2*>(Z + z_off(b, n2, fx, k1))[a] =
-          uint2{pack_bf2(yv[0][n2].x, yv[0][n2].y), pack_bf2(yv[1][n2].x, yv[1][n2].y)};
+    {
+      typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+      u2v* zp = reinterpret_cast<u2v*>(Z + z_off(b, n2, fx, k1)) + a;
+      const u2v v = u2v{pack_bf2(yv[0][n2].x, yv[0][n2].y), pack_bf2(yv[1][n2].x, yv[1][n2].y)};
+      if constexpr (ZNT) __builtin_nontemporal_store(v, zp);
+      else *zp = v;
+    }
   }
 }
 
@@ -767,20 +777,12 @@ bool fft4_enabled() {
   return v;
 }
 
-// MP_COL8_RING (default 1): col8_kernel's weight loads one k-step ring slot ahead; 0: two steps at a time
-static bool col8_ring() {
-  static const bool v = [] {
-    const char* e = std::getenv("MP_COL8_RING");
-    return e ? std::atoi(e) != 0 : true;
-  }();
-  return v;
-}
-
-// MP_COL8_ZNT (default 0): col8_kernel's Z loads and stores non-temporal
+// MP_COL8_ZNT (default 1): col8_kernel's Z loads and stores non-temporal (one box: 8.52 -> 8.40 ms per
+// B = 256 forward, col8 0.185 -> 0.184 ms, the same PMC bytes; profiles/r5l); 0: default policy
 static bool col8_znt() {
   static const bool v = [] {
     const char* e = std::getenv("MP_COL8_ZNT");
-    return e ? std::atoi(e) != 0 : false;
+    return e ? std::atoi(e) != 0 : true;
   }();
   return v;
 }
@@ -788,18 +790,19 @@ static bool col8_znt() {
 hipError_t launch_col_gemm(void* Z, const void* Gc, int B, float unscale, hipStream_t st, bool bf) {
   if (B <= 0) return hipSuccess;
   const int ngrp = (B + CG_NI - 1) / CG_NI;
-  if (bf)
-    hipLaunchKernelGGL(col8_bf_kernel, dim3(CG_NC8 * 8 * ngrp), dim3(512), 0, st, Z, static_cast<const uint4*>(Gc), B,
-                       ngrp);
-  else {
-#define MP_COL8(R, N)                                                                                       \
-  hipLaunchKernelGGL((col8_kernel<R, N>), dim3(CG_NC8 * 8 * ngrp), dim3(512), 0, st, static_cast<cpx*>(Z), \
+  if (bf) {
+#define MP_COL8B(N)                                                                                          \
+  hipLaunchKernelGGL((col8_bf_kernel<N>), dim3(CG_NC8 * 8 * ngrp), dim3(512), 0, st, Z, static_cast<const uint4*>(Gc), \
+                     B, ngrp)
+    if (col8_znt()) MP_COL8B(true);
+    else MP_COL8B(false);
+#undef MP_COL8B
+  } else {
+#define MP_COL8(N)                                                                                       \
+  hipLaunchKernelGGL((col8_kernel<N>), dim3(CG_NC8 * 8 * ngrp), dim3(512), 0, st, static_cast<cpx*>(Z), \
                      static_cast<const uint4*>(Gc), B, ngrp, unscale)
-    const bool r = col8_ring(), n = col8_znt();
-    if (r && n) MP_COL8(true, true);
-    else if (r) MP_COL8(true, false);
-    else if (n) MP_COL8(false, true);
-    else MP_COL8(false, false);
+    if (col8_znt()) MP_COL8(true);
+    else MP_COL8(false);
 #undef MP_COL8
   }
   return hipGetLastError();
