@@ -348,15 +348,29 @@ __device__ __forceinline__ void rfft72_inv(const cpx (&X)[FX], float (&x)[64]) {
 
 // Z element access: complex64 (fp32 path) or one bf16 (re, im) pair (MP_DTYPE_BF16: round to nearest
 // even on store, exact on load), at the same complex index
-template <bool BF>
+// NT: non-temporal (streaming) access
+template <bool BF, bool NT = false>
 __device__ __forceinline__ cpx z_ld(const void* Z, size_t i) {
-  if constexpr (BF) return unpack_bf2(static_cast<const uint32_t*>(Z)[i]);
-  else return static_cast<const cpx*>(Z)[i];
+  if constexpr (BF) {
+    const uint32_t* p = static_cast<const uint32_t*>(Z) + i;
+    return unpack_bf2(NT ? __builtin_nontemporal_load(p) : *p);
+  } else {
+    const cpx* p = static_cast<const cpx*>(Z) + i;
+    return NT ? __builtin_nontemporal_load(p) : *p;
+  }
 }
-template <bool BF>
+template <bool BF, bool NT = false>
 __device__ __forceinline__ void z_st(void* Z, size_t i, cpx v) {
-  if constexpr (BF) static_cast<uint32_t*>(Z)[i] = pack_bf2(v.x, v.y);
-  else static_cast<cpx*>(Z)[i] = v;
+  if constexpr (BF) {
+    uint32_t* p = static_cast<uint32_t*>(Z) + i;
+    const uint32_t u = pack_bf2(v.x, v.y);
+    if constexpr (NT) __builtin_nontemporal_store(u, p);
+    else *p = u;
+  } else {
+    cpx* p = static_cast<cpx*>(Z) + i;
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+  }
 }
 
 // ---------------------------------------------------------------------------------------------
@@ -385,7 +399,8 @@ static_assert(R8_T >= RK_T && (8 * 32 * RK_SP * 4 + 2 * R8_GATE * 16) <= R8_T * 
 
 // BF: MP_DTYPE_BF16 -- Z and the hGRU maps in bf16, the gates one bf16 product (gate_bf); transforms,
 // epilogue math and the NHWC output fp32
-template <int MODE, bool BF = false>
+// ZNT: Z read and written non-temporal (MP_ROW8_ZNT)
+template <int MODE, bool BF = false, bool ZNT = false>
 __global__ __launch_bounds__(R8_NT, 1) void row8_kernel(void* __restrict__ Z, ConvArgs p, const void* __restrict__ or_x3,
                                                         float or_us, const void* __restrict__ ir_x3, float ir_us,
                                                         const float* __restrict__ O0) {
@@ -412,7 +427,7 @@ __global__ __launch_bounds__(R8_NT, 1) void row8_kernel(void* __restrict__ Z, Co
         const int i = min(it * R8_NT + tid, RK_ITEMS - 1);
         const size_t src = z_off(b, n2, i >> 6, 0) + (i & 63);
 #pragma unroll
-        for (int k1 = 0; k1 < 9; ++k1) u[it][k1] = z_ld<BF>(Z, src + k1 * 64);
+        for (int k1 = 0; k1 < 9; ++k1) u[it][k1] = z_ld<BF, ZNT>(Z, src + k1 * 64);
       }
 #pragma unroll
       for (int it = 0; it < R8_NIT; ++it) {
@@ -499,7 +514,7 @@ __global__ __launch_bounds__(R8_NT, 1) void row8_kernel(void* __restrict__ Z, Co
     dft9<-1>(u);
     const size_t dst = z_off(b, n2, fx, 0) + c;
 #pragma unroll
-    for (int k1 = 0; k1 < 9; ++k1) z_st<BF>(Z, dst + k1 * 64, u[k1]);
+    for (int k1 = 0; k1 < 9; ++k1) z_st<BF, ZNT>(Z, dst + k1 * 64, u[k1]);
   }
 }
 
@@ -808,12 +823,25 @@ hipError_t launch_col_gemm(void* Z, const void* Gc, int B, float unscale, hipStr
   return hipGetLastError();
 }
 
+// MP_ROW8_ZNT (default 0): row8_kernel's Z loads and stores non-temporal
+static bool row8_znt() {
+  static const bool v = [] {
+    const char* e = std::getenv("MP_ROW8_ZNT");
+    return e ? std::atoi(e) != 0 : false;
+  }();
+  return v;
+}
+
 hipError_t launch_row(int mode, void* Z, const ConvArgs& a, const void* or_x3, float or_us, const void* ir_x3,
                       float ir_us, const float* O0, int B, hipStream_t st, bool bf) {
   if (B <= 0) return hipSuccess;
   if (a.H < 1 || a.H > 64 || (a.W != 32 && a.W != 64)) return hipErrorInvalidValue;
   const dim3 g(B * 8), t(R8_NT);
-#define MP_ROW8(M, BFV) hipLaunchKernelGGL((row8_kernel<M, BFV>), g, t, 0, st, Z, a, or_x3, or_us, ir_x3, ir_us, O0)
+#define MP_ROW8(M, BFV)                                                                            \
+  if (row8_znt())                                                                                  \
+    hipLaunchKernelGGL((row8_kernel<M, BFV, true>), g, t, 0, st, Z, a, or_x3, or_us, ir_x3, ir_us, O0); \
+  else                                                                                             \
+    hipLaunchKernelGGL((row8_kernel<M, BFV, false>), g, t, 0, st, Z, a, or_x3, or_us, ir_x3, ir_us, O0)
 #define MP_ROW8S(BFV)                               \
   switch (mode) {                                   \
     case ROW_A: MP_ROW8(ROW_A, BFV); break;         \
