@@ -124,6 +124,10 @@ BITS_CASES = [
     # 32-image tiles; the B epilogue's image order
     ("pose", "fp32_fft", "MP_SPEC_SMALLB", ("8", "32"), {"MP_FFT4": "0"}),
     ("pose80", "fp32_fft", "MP_EPI_REV", ("0", "1"), {"MP_FFT4": "0"}),
+    # four-step loop: non-temporal or default cache policy for the partials moves no value
+    ("pose80", "fp32_fft", "MP_COL8_ZNT", ("0", "1"), {}),
+    ("pose80", "bf16", "MP_COL8_ZNT", ("0", "1"), {}),
+    ("pose80", "fp32_fft", "MP_ROW8_ZNT", ("0", "1"), {}),
 ]
 
 
