@@ -452,6 +452,15 @@ int stream_count() {
   return v;
 }
 
+// MP_BB_PIPE (default 1): the backbone per batch slice on the slice's stream; 0: whole batch first
+bool bb_pipeline() {
+  static const bool v = [] {
+    const char* e = std::getenv("MP_BB_PIPE");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  return v;
+}
+
 // smallest batch slice worth a stream of its own (MP_SLICE_MIN, A/B knob)
 int slice_min() {
   static const int v = [] {
@@ -461,17 +470,22 @@ int slice_min() {
   return v;
 }
 
+// pre (optional): work a batch slice needs before its hGRU loop (the backbone of its images), run on the
+// slice's stream so that one slice's backbone overlaps another's loop
+using SliceFn = std::function<void(int b0, int cnt, hipStream_t s)>;
 void run_circuit(mp_ctx* c, int64_t n, int H, int W, int T, const float* o0_nhwc, float* final_dst2,
-                 const StateOut* so, hipStream_t st, const SplitOut* sp = nullptr) {
+                 const StateOut* so, hipStream_t st, const SplitOut* sp = nullptr, const SliceFn* pre = nullptr) {
   if (sp && !is_fft(c->dtype)) fail(MP_ERR_STATE, "split fc_1 planes are an FFT-path output");
   // FFT path, not profiling: batch slices are independent, so they run on separate streams and
   // their latency-bound kernels overlap (the per-kernel HIP-event profile keeps one stream)
   const int ns = std::min<int>(stream_count(), (int)(n / slice_min()));
-  if (c->fft4 && (c->prof || ns < 2)) {
+  const bool multi = is_fft(c->dtype) && !c->prof && ns >= 2;
+  if (pre && !multi) (*pre)(0, (int)n, st);
+  if (c->fft4 && !multi) {
     fft4_circuit_range(c, 0, (int)n, H, W, T, o0_nhwc, final_dst2, so, sp, st);
     return;
   }
-  if (is_fft(c->dtype) && !c->prof && ns >= 2) {
+  if (multi) {
     if (!c->fft4)
       hip_check(launch_gate_init_x3(o0_nhwc, c->O.f(), c->Og.f(), c->ir_x3.p, c->ir_us, c->vecs.f(), (int)n, H, W,
                                   st, c->dtype == MP_DTYPE_BF16),
@@ -495,6 +509,7 @@ void run_circuit(mp_ctx* c, int64_t n, int H, int W, int T, const float* o0_nhwc
       const int cnt = std::min<int>(g * gs, (int)n - b0);
       hipStream_t s = k == 0 ? st : c->sides[k - 1];
       if (k > 0) hip_check(hipStreamWaitEvent(s, c->ev_fork, 0), "hipStreamWaitEvent");
+      if (pre) (*pre)(b0, cnt, s);
       if (c->fft4)
         fft4_circuit_range(c, b0, cnt, H, W, T, o0_nhwc, final_dst2, so, sp, s);
       else
@@ -830,38 +845,48 @@ int pose_fwd(mp_ctx* ctx, const float* depth, int64_t n, int64_t h, int64_t w, c
       g.relu = 1;
       hip_check(launch_igemm_conv(g, st), "conv_1 tap");
     }
-    {
-      ProfScope ps(ctx, st, "backbone");
-      hip_check(launch_conv1_pool_bn(depth, ctx->conv1_w.f(), ctx->conv1_b.f(), ctx->bn0_s.f(), ctx->bn0_t.f(),
-                                     ctx->bufA.f(), N, (int)h, (int)w, st),
+    // the backbone of images b0 .. b0 + cnt on stream s (every buffer is image-major)
+    const bool x3 = ctx->dtype != MP_DTYPE_F32 && H % TH3 == 0;
+    const int np = ctx->dtype == MP_DTYPE_BF16 ? 1 : 3;   // bf16: one f16 product per MAC
+    const size_t px = (size_t)H * W * 64;                  // elements of one image's 64-channel map
+    const SliceFn backbone = [&](int b0, int cnt, hipStream_t s) {
+      ProfScope ps(ctx, s, "backbone");
+      float* bA = ctx->bufA.f() + b0 * px;
+      float* bB = ctx->bufB.f() + b0 * px;
+      float* xm = bf16_maps(ctx) ? reinterpret_cast<float*>(reinterpret_cast<uint16_t*>(ctx->X.p) + b0 * px)
+                                 : ctx->X.f() + b0 * px;
+      hip_check(launch_conv1_pool_bn(depth + (size_t)b0 * h * w, ctx->conv1_w.f(), ctx->conv1_b.f(), ctx->bn0_s.f(),
+                                     ctx->bn0_t.f(), bA, cnt, (int)h, (int)w, s),
                 "conv_1");
       ConvArgs a{};
       a.H = H;
       a.W = W;
-      a.src = ctx->bufA.f();
+      a.src = bA;
       a.wpk = ctx->conv2_pk.v4();
-      a.dst = ctx->bufB.f();
+      a.dst = bB;
       a.bias = ctx->conv2_b.f();
       a.bn_s = ctx->bn1_s.f();
       a.bn_t = ctx->bn1_t.f();
-      const bool x3 = ctx->dtype != MP_DTYPE_F32 && H % TH3 == 0;
       if (x3) a.ascale = BB_ASCALE;
-      const int np = ctx->dtype == MP_DTYPE_BF16 ? 1 : 3;   // bf16: one f16 product per MAC
-      hip_check(x3 ? launch_conv64x3(3, EPI_BB, a, ctx->conv2_pk.p, ctx->conv2_us, N, st, np)
-                   : launch_conv64(3, EPI_BB, a, N, st),
+      hip_check(x3 ? launch_conv64x3(3, EPI_BB, a, ctx->conv2_pk.p, ctx->conv2_us, cnt, s, np)
+                   : launch_conv64(3, EPI_BB, a, cnt, s),
                 "conv_2");
-      a.src = ctx->bufB.f();
+      a.src = bB;
       a.wpk = ctx->conv3_pk.v4();
-      a.dst = ctx->X.f();
+      a.dst = xm;
       a.dst_bf16 = bf16_maps(ctx) ? 1 : 0;
       a.dst_c4 = x_c4(ctx) ? 1 : 0;
       a.bias = ctx->conv3_b.f();
       a.bn_s = ctx->bn2_s.f();
       a.bn_t = ctx->bn2_t.f();
-      hip_check(x3 ? launch_conv64x3(3, EPI_BB, a, ctx->conv3_pk.p, ctx->conv3_us, N, st, np)
-                   : launch_conv64(3, EPI_BB, a, N, st),
+      hip_check(x3 ? launch_conv64x3(3, EPI_BB, a, ctx->conv3_pk.p, ctx->conv3_us, cnt, s, np)
+                   : launch_conv64(3, EPI_BB, a, cnt, s),
                 "conv_3");
-    }
+    };
+    // the backbone runs per batch slice on the slice's stream (MP_BB_PIPE) unless a tap needs its
+    // intermediate maps; otherwise whole-batch on the caller's stream first
+    const bool bb_pipe = bb_pipeline() && !tp.pool1 && !tp.conv2 && !tp.conv3;
+    if (!bb_pipe) backbone(0, N, st);
     if (tp.pool1) hip_check(launch_c8_to_nhwc(ctx->bufA.f(), tp.pool1, N, H, W, st), "pool1 tap");
     if (tp.conv2) hip_check(launch_c8_to_nhwc(ctx->bufB.f(), tp.conv2, N, H, W, st), "conv2 tap");
     if (tp.conv3) hip_check(launch_c8_to_nhwc(ctx->X.f(), tp.conv3, N, H, W, st, bf16_maps(ctx), 0, x_c4(ctx)), "conv3 tap");
@@ -881,7 +906,7 @@ int pose_fwd(mp_ctx* ctx, const float* depth, int64_t n, int64_t h, int64_t w, c
       sp.lo = fc_np == 3 ? sp.hi + (size_t)N * ctx->fc1_in : nullptr;
     }
     run_circuit(ctx, n, H, W, ctx->timesteps, h0, ctx->fcin.f(), (so.O || so.I) ? &so : nullptr, st,
-                presplit ? &sp : nullptr);
+                presplit ? &sp : nullptr, bb_pipe ? &backbone : nullptr);
     if (tp.hgru)
       hip_check(hipMemcpyAsync(tp.hgru, ctx->fcin.f(), (size_t)N * ctx->fc1_in * sizeof(float),
                                hipMemcpyDeviceToDevice, st),
