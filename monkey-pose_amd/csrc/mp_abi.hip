@@ -461,6 +461,15 @@ bool bb_pipeline() {
   return v;
 }
 
+// MP_BB_STAGGER (default 0): a slice's backbone waits for the previous slice's
+bool bb_stagger() {
+  static const bool v = [] {
+    const char* e = std::getenv("MP_BB_STAGGER");
+    return e ? std::atoi(e) != 0 : false;
+  }();
+  return v;
+}
+
 // smallest batch slice worth a stream of its own (MP_SLICE_MIN, A/B knob)
 int slice_min() {
   static const int v = [] {
@@ -509,7 +518,15 @@ void run_circuit(mp_ctx* c, int64_t n, int H, int W, int T, const float* o0_nhwc
       const int cnt = std::min<int>(g * gs, (int)n - b0);
       hipStream_t s = k == 0 ? st : c->sides[k - 1];
       if (k > 0) hip_check(hipStreamWaitEvent(s, c->ev_fork, 0), "hipStreamWaitEvent");
+      if (pre && bb_stagger() && k > 0) {   // slice k's backbone after slice k - 1's
+        if (!c->ev_pre) hip_check(hipEventCreateWithFlags(&c->ev_pre, hipEventDisableTiming), "hipEventCreate");
+        hip_check(hipStreamWaitEvent(s, c->ev_pre, 0), "hipStreamWaitEvent");
+      }
       if (pre) (*pre)(b0, cnt, s);
+      if (pre && bb_stagger() && k + 1 < ns) {
+        if (!c->ev_pre) hip_check(hipEventCreateWithFlags(&c->ev_pre, hipEventDisableTiming), "hipEventCreate");
+        hip_check(hipEventRecord(c->ev_pre, s), "hipEventRecord");
+      }
       if (c->fft4)
         fft4_circuit_range(c, b0, cnt, H, W, T, o0_nhwc, final_dst2, so, sp, s);
       else

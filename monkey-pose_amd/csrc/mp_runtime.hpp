@@ -166,11 +166,13 @@ struct mp_ctx {
   // ---- batch slices on extra streams (FFT circuit; MP_STREAMS=1 disables) ----
   std::vector<hipStream_t> sides;
   hipEvent_t ev_fork = nullptr;
+  hipEvent_t ev_pre = nullptr;   // a slice's backbone done (MP_BB_STAGGER)
   std::vector<hipEvent_t> ev_join;
 
   ~mp_ctx() {
     for (auto s : sides) (void)hipStreamDestroy(s);
     if (ev_fork) (void)hipEventDestroy(ev_fork);
+    if (ev_pre) (void)hipEventDestroy(ev_pre);
     for (auto e : ev_join) (void)hipEventDestroy(e);
     for (auto& e : events) {
       (void)hipEventDestroy(e.a);
