@@ -129,17 +129,18 @@ PMC_KERNEL = {   # name: (fp32 path's kernel, bf16 path's kernel) as rocprofv3 n
     "fft_inv": ("fft_inv_kernel<false, false>", "fft_inv_kernel<true, true>"),
     "epi_b": ("spec_epi_b_kernel<false, false, false>", "spec_epi_b_kernel<true, true, false>"),
     # the four-step loop's default kernels (k_fft4.hip: col8 / row8 forms)
-    "col_gemm": ("col8_kernel", "col8_bf_kernel"), "row_a": ("row8_kernel<0, false>", "row8_kernel<0, true>"),
-    "row_b": ("row8_kernel<1, false>", "row8_kernel<1, true>"),
-    "row_final": ("row8_kernel<2, false>", "row8_kernel<2, true>"),
-    "row_init": ("row8_kernel<3, false>", "row8_kernel<3, true>")}
+    # (prefixes: the template arguments after the dtype flag are cache-policy switches)
+    "col_gemm": ("col8_kernel", "col8_bf_kernel"), "row_a": ("row8_kernel<0, false", "row8_kernel<0, true"),
+    "row_b": ("row8_kernel<1, false", "row8_kernel<1, true"),
+    "row_final": ("row8_kernel<2, false", "row8_kernel<2, true"),
+    "row_init": ("row8_kernel<3, false", "row8_kernel<3, true")}
 
 
 # MFMA utilisation per kernel from the committed PMC pass (tools/pmc_mfma.sh / .py: SQ_VALU_MFMA_BUSY_CYCLES
 # over GRBM_GUI_ACTIVE x 1024 SIMDs, the gfx950 MfmaUtil), same one-stream B = 256 workload
 PMC_MFMA = "profiles/r5z/mfma_util_pose_fp32_b256.csv"
 MFMA_KERNELS = {"col8 (four-step spectral GEMM, k_fft4.hip)": "col8_kernel",
-                "row8 B (gate GEMMs, k_fft4.hip)": "row8_kernel<1, false>",
+                "row8 B (gate GEMMs, k_fft4.hip)": "row8_kernel<1, false",
                 "fc_gemm_x3p (fc_1 on split planes, k_fc.hip)": "fc_gemm_x3p_kernel", "conv64x3 (conv_2/3, k_conv64x3.hip)": "conv64x3_kernel",
                 "spec_gemm (k_fft.hip)": "spec_gemm_kernel", "spec_epi_b (gate GEMMs, k_fft.hip)": "spec_epi_b_kernel<false, false, false>",
                 "gate_init_x3 (k_fft.hip)": "gate_init_x3_kernel"}
