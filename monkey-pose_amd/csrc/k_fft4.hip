@@ -554,7 +554,7 @@ __device__ __forceinline__ f32x4 mfma16x16(f16x8 a, f16x8 b, f32x4 c) {
 // per CU (0.207 ms; batch-1 forward 1.06 vs 0.98 ms): both removed.
 // ZNT: the partials Z read and written non-temporal (the weights, re-read by the other batch slice's
 // launch of the same convolution, keep the cache)
-template <bool ZNT>
+template <bool ZNT, bool EW>
 __global__ __launch_bounds__(512, 2) void col8_kernel(cpx* __restrict__ Z, const uint4* __restrict__ Gc, int B,
                                                       int ngrp, float unscale) {
   __shared__ uint4 tile[2 * CG_HALF];   // 69,632 B
@@ -568,6 +568,21 @@ __global__ __launch_bounds__(512, 2) void col8_kernel(cpx* __restrict__ Z, const
   const bool live = img0 + bl < B;
   const int b = min(img0 + bl, B - 1);
   const int cq = a >> 1, hf = a & 1;
+  const int kq = lane >> 4, jj = lane & 15, k2 = wv;
+  // weights of two k-steps in registers (64 VGPRs), a two-slot ring: k-step t + 2's loads go into step
+  // t's slot right after step t's MFMAs, so step t + 1's MFMAs cover part of their latency (col8 0.196 ->
+  // 0.185 ms against loading steps 2 and 3 together after step 1; profiles/r5l).  EW: step 0's weights
+  // are requested before the partials, so they have landed when the GEMM starts
+  uint4 wr[2][4][2];
+  const uint4* gw = Gc + (size_t)(cls * 8 + k2) * 2 * 16 * 64;
+  auto load_1 = [&](int slot, int t) {
+#pragma unroll
+    for (int mq = 0; mq < 4; ++mq) {
+      wr[slot][mq][0] = gw[(0 * 16 + 4 * t + kq) * 64 + 16 * mq + jj];
+      wr[slot][mq][1] = gw[(1 * 16 + 4 * t + kq) * 64 + 16 * mq + jj];
+    }
+  };
+  if constexpr (EW) load_1(0, 0);
   {
     f32x4 zin[8];
 #pragma unroll
@@ -602,25 +617,8 @@ __global__ __launch_bounds__(512, 2) void col8_kernel(cpx* __restrict__ Z, const
       t2[cg_s(k2, cq, 1, bl) * 2 + hf] = uint2{lv[0], lv[1]};
     }
   }
-  const int kq = lane >> 4, jj = lane & 15, k2 = wv;
-  // weights of two k-steps in registers (64 VGPRs), a two-slot ring: k-step t + 2's loads go into step
-  // t's slot right after step t's MFMAs, so step t + 1's MFMAs cover part of their latency (col8 0.196 ->
-  // 0.185 ms against loading steps 2 and 3 together after step 1; profiles/r5l)
-  constexpr int TW = 2;
-  uint4 wr[TW][4][2];
-  const uint4* gw = Gc + (size_t)(cls * 8 + k2) * 2 * 16 * 64;
-  auto load_1 = [&](int slot, int t) {
-#pragma unroll
-    for (int mq = 0; mq < 4; ++mq) {
-      wr[slot][mq][0] = gw[(0 * 16 + 4 * t + kq) * 64 + 16 * mq + jj];
-      wr[slot][mq][1] = gw[(1 * 16 + 4 * t + kq) * 64 + 16 * mq + jj];
-    }
-  };
-  auto load_w = [&](int t0) {
-#pragma unroll
-    for (int t = 0; t < TW; ++t) load_1(t, t0 + t);
-  };
-  load_w(0);
+  if constexpr (!EW) load_1(0, 0);
+  load_1(1, 1);
   lds_barrier();
   // the compact weights A = (gr, gi) pairs as stored; the S fragment supplies the two forms, (sr, -si)
   // for the real rows (gr sr - gi si) and (si, sr) for the imaginary rows (gr si + gi sr): a sign flip
@@ -635,7 +633,7 @@ __global__ __launch_bounds__(512, 2) void col8_kernel(cpx* __restrict__ Z, const
     const f16x8 sl2 = __builtin_bit_cast(f16x8, (ul >> 16) | (ul << 16));
 #pragma unroll
     for (int mq = 0; mq < 4; ++mq) {
-      const f16x8 ah = __builtin_bit_cast(f16x8, wr[t % TW][mq][0]), al = __builtin_bit_cast(f16x8, wr[t % TW][mq][1]);
+      const f16x8 ah = __builtin_bit_cast(f16x8, wr[t % 2][mq][0]), al = __builtin_bit_cast(f16x8, wr[t % 2][mq][1]);
       acc[mq] = mfma16x16(al, sh, acc[mq]);
       acc[mq] = mfma16x16(ah, sl, acc[mq]);
       acc[mq] = mfma16x16(ah, sh, acc[mq]);
@@ -792,6 +790,15 @@ bool fft4_enabled() {
   return v;
 }
 
+// MP_COL8_EW (default 0): col8_kernel requests its first k-step's weights before the partials
+static bool col8_early_w() {
+  static const bool v = [] {
+    const char* e = std::getenv("MP_COL8_EW");
+    return e ? std::atoi(e) != 0 : false;
+  }();
+  return v;
+}
+
 // MP_COL8_ZNT (default 1): col8_kernel's Z loads and stores non-temporal (one box: 8.52 -> 8.40 ms per
 // B = 256 forward, col8 0.185 -> 0.184 ms, the same PMC bytes; profiles/r5l); 0: default policy
 static bool col8_znt() {
@@ -813,11 +820,14 @@ hipError_t launch_col_gemm(void* Z, const void* Gc, int B, float unscale, hipStr
     else MP_COL8B(false);
 #undef MP_COL8B
   } else {
-#define MP_COL8(N)                                                                                       \
-  hipLaunchKernelGGL((col8_kernel<N>), dim3(CG_NC8 * 8 * ngrp), dim3(512), 0, st, static_cast<cpx*>(Z), \
+#define MP_COL8(N, E)                                                                                       \
+  hipLaunchKernelGGL((col8_kernel<N, E>), dim3(CG_NC8 * 8 * ngrp), dim3(512), 0, st, static_cast<cpx*>(Z), \
                      static_cast<const uint4*>(Gc), B, ngrp, unscale)
-    if (col8_znt()) MP_COL8(true);
-    else MP_COL8(false);
+    const bool ew = col8_early_w();
+    if (col8_znt() && ew) MP_COL8(true, true);
+    else if (col8_znt()) MP_COL8(true, false);
+    else if (ew) MP_COL8(false, true);
+    else MP_COL8(false, false);
 #undef MP_COL8
   }
   return hipGetLastError();
