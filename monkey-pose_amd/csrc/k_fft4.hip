@@ -799,14 +799,15 @@ static bool col8_early_w() {
   return v;
 }
 
-// MP_COL8_ZNT (default 1): col8_kernel's Z loads and stores non-temporal (one box: 8.52 -> 8.40 ms per
-// B = 256 forward, col8 0.185 -> 0.184 ms, the same PMC bytes; profiles/r5l); 0: default policy
-static bool col8_znt() {
-  static const bool v = [] {
+// MP_COL8_ZNT: the column kernels' Z loads and stores non-temporal (1) or default policy (0).  Default:
+// on for fp32 (same box: 8.51 -> 8.38 ms per B = 256 forward, the same PMC bytes; profiles/r5l, r5m), off
+// for bf16 (col8_bf 0.0995 -> 0.1085 ms with it; profiles/r5m_bf16)
+static bool col8_znt(bool bf) {
+  static const int v = [] {
     const char* e = std::getenv("MP_COL8_ZNT");
-    return e ? std::atoi(e) != 0 : true;
+    return e ? (std::atoi(e) != 0 ? 1 : 0) : -1;
   }();
-  return v;
+  return v < 0 ? !bf : v != 0;
 }
 
 hipError_t launch_col_gemm(void* Z, const void* Gc, int B, float unscale, hipStream_t st, bool bf) {
@@ -816,7 +817,7 @@ hipError_t launch_col_gemm(void* Z, const void* Gc, int B, float unscale, hipStr
 #define MP_COL8B(N)                                                                                          \
   hipLaunchKernelGGL((col8_bf_kernel<N>), dim3(CG_NC8 * 8 * ngrp), dim3(512), 0, st, Z, static_cast<const uint4*>(Gc), \
                      B, ngrp)
-    if (col8_znt()) MP_COL8B(true);
+    if (col8_znt(true)) MP_COL8B(true);
     else MP_COL8B(false);
 #undef MP_COL8B
   } else {
@@ -824,8 +825,9 @@ hipError_t launch_col_gemm(void* Z, const void* Gc, int B, float unscale, hipStr
   hipLaunchKernelGGL((col8_kernel<N, E>), dim3(CG_NC8 * 8 * ngrp), dim3(512), 0, st, static_cast<cpx*>(Z), \
                      static_cast<const uint4*>(Gc), B, ngrp, unscale)
     const bool ew = col8_early_w();
-    if (col8_znt() && ew) MP_COL8(true, true);
-    else if (col8_znt()) MP_COL8(true, false);
+    const bool zn = col8_znt(false);
+    if (zn && ew) MP_COL8(true, true);
+    else if (zn) MP_COL8(true, false);
     else if (ew) MP_COL8(false, true);
     else MP_COL8(false, false);
 #undef MP_COL8
