@@ -461,11 +461,12 @@ bool bb_pipeline() {
   return v;
 }
 
-// MP_BB_STAGGER (default 0): a slice's backbone waits for the previous slice's
+// MP_BB_STAGGER (default 1): a slice's backbone waits for the previous slice's, so that it overlaps that
+// slice's hGRU loop instead of the other backbone (same box, B = 256: 8.40 -> 8.28 ms; profiles/r5n)
 bool bb_stagger() {
   static const bool v = [] {
     const char* e = std::getenv("MP_BB_STAGGER");
-    return e ? std::atoi(e) != 0 : false;
+    return e ? std::atoi(e) != 0 : true;
   }();
   return v;
 }

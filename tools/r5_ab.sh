@@ -7,9 +7,11 @@ set -o pipefail
 R=$(pwd)
 out=$R/gpurun_out/$1
 mkdir -p "$out"
-for kv in $AB; do
+i=0
+for kv in $AB; do   # (a setting may repeat: interleaved repeats, logs numbered in run order)
+  i=$((i + 1))
   vars=$( [ "$kv" = "-" ] || echo "$kv" | tr ',' ' ')
-  env $vars timeout -k 10 300 python tools/fft4_check.py ${DT:+--dtype $DT} > "$out/ab_$kv.log" 2>&1 || exit 1
+  env $vars timeout -k 10 300 python tools/fft4_check.py ${DT:+--dtype $DT} ${QUICK:+--quick} > "$out/ab_${i}_$kv.log" 2>&1 || exit 1
 done
 cd /tmp && export TMPDIR=/tmp
 for kv in $PMC; do
