@@ -554,7 +554,7 @@ __device__ __forceinline__ f32x4 mfma16x16(f16x8 a, f16x8 b, f32x4 c) {
 // per CU (0.207 ms; batch-1 forward 1.06 vs 0.98 ms): both removed.
 // ZNT: the partials Z read and written non-temporal (the weights, re-read by the other batch slice's
 // launch of the same convolution, keep the cache)
-template <bool ZNT, bool EW>
+template <bool ZNT>
 __global__ __launch_bounds__(512, 2) void col8_kernel(cpx* __restrict__ Z, const uint4* __restrict__ Gc, int B,
                                                       int ngrp, float unscale) {
   __shared__ uint4 tile[2 * CG_HALF];   // 69,632 B
@@ -571,8 +571,8 @@ __global__ __launch_bounds__(512, 2) void col8_kernel(cpx* __restrict__ Z, const
   const int kq = lane >> 4, jj = lane & 15, k2 = wv;
   // weights of two k-steps in registers (64 VGPRs), a two-slot ring: k-step t + 2's loads go into step
   // t's slot right after step t's MFMAs, so step t + 1's MFMAs cover part of their latency (col8 0.196 ->
-  // 0.185 ms against loading steps 2 and 3 together after step 1; profiles/r5l).  EW: step 0's weights
-  // are requested before the partials, so they have landed when the GEMM starts
+  // 0.185 ms against loading steps 2 and 3 together after step 1; profiles/r5l).  Requesting step 0's
+  // weights before the partials measured slower (8.27 -> 8.33 ms per forward; profiles/r5o)
   uint4 wr[2][4][2];
   const uint4* gw = Gc + (size_t)(cls * 8 + k2) * 2 * 16 * 64;
   auto load_1 = [&](int slot, int t) {
@@ -582,7 +582,6 @@ __global__ __launch_bounds__(512, 2) void col8_kernel(cpx* __restrict__ Z, const
       wr[slot][mq][1] = gw[(1 * 16 + 4 * t + kq) * 64 + 16 * mq + jj];
     }
   };
-  if constexpr (EW) load_1(0, 0);
   {
     f32x4 zin[8];
 #pragma unroll
@@ -617,7 +616,7 @@ __global__ __launch_bounds__(512, 2) void col8_kernel(cpx* __restrict__ Z, const
       t2[cg_s(k2, cq, 1, bl) * 2 + hf] = uint2{lv[0], lv[1]};
     }
   }
-  if constexpr (!EW) load_1(0, 0);
+  load_1(0, 0);
   load_1(1, 1);
   lds_barrier();
   // the compact weights A = (gr, gi) pairs as stored; the S fragment supplies the two forms, (sr, -si)
@@ -790,15 +789,6 @@ bool fft4_enabled() {
   return v;
 }
 
-// MP_COL8_EW (default 0): col8_kernel requests its first k-step's weights before the partials
-static bool col8_early_w() {
-  static const bool v = [] {
-    const char* e = std::getenv("MP_COL8_EW");
-    return e ? std::atoi(e) != 0 : false;
-  }();
-  return v;
-}
-
 // MP_COL8_ZNT: the column kernels' Z loads and stores non-temporal (1) or default policy (0).  Default:
 // on for fp32 (same box: 8.51 -> 8.38 ms per B = 256 forward, the same PMC bytes; profiles/r5l, r5m), off
 // for bf16 (col8_bf 0.0995 -> 0.1085 ms with it; profiles/r5m_bf16)
@@ -821,27 +811,25 @@ hipError_t launch_col_gemm(void* Z, const void* Gc, int B, float unscale, hipStr
     else MP_COL8B(false);
 #undef MP_COL8B
   } else {
-#define MP_COL8(N, E)                                                                                       \
-  hipLaunchKernelGGL((col8_kernel<N, E>), dim3(CG_NC8 * 8 * ngrp), dim3(512), 0, st, static_cast<cpx*>(Z), \
+#define MP_COL8(N)                                                                                       \
+  hipLaunchKernelGGL((col8_kernel<N>), dim3(CG_NC8 * 8 * ngrp), dim3(512), 0, st, static_cast<cpx*>(Z), \
                      static_cast<const uint4*>(Gc), B, ngrp, unscale)
-    const bool ew = col8_early_w();
-    const bool zn = col8_znt(false);
-    if (zn && ew) MP_COL8(true, true);
-    else if (zn) MP_COL8(true, false);
-    else if (ew) MP_COL8(false, true);
-    else MP_COL8(false, false);
+    if (col8_znt(false)) MP_COL8(true);
+    else MP_COL8(false);
 #undef MP_COL8
   }
   return hipGetLastError();
 }
 
-// MP_ROW8_ZNT (default 0): row8_kernel's Z loads and stores non-temporal
-static bool row8_znt() {
-  static const bool v = [] {
+// MP_ROW8_ZNT: row8_kernel's Z loads and stores non-temporal (1) or default policy (0).  Default: on for
+// fp32 (interleaved same-box timing 8.27 -> 8.21 ms per B = 256 forward; profiles/r5o), off for bf16
+// (5.080 vs 5.079 ms)
+static bool row8_znt(bool bf) {
+  static const int v = [] {
     const char* e = std::getenv("MP_ROW8_ZNT");
-    return e ? std::atoi(e) != 0 : false;
+    return e ? (std::atoi(e) != 0 ? 1 : 0) : -1;
   }();
-  return v;
+  return v < 0 ? !bf : v != 0;
 }
 
 hipError_t launch_row(int mode, void* Z, const ConvArgs& a, const void* or_x3, float or_us, const void* ir_x3,
@@ -850,7 +838,7 @@ hipError_t launch_row(int mode, void* Z, const ConvArgs& a, const void* or_x3, f
   if (a.H < 1 || a.H > 64 || (a.W != 32 && a.W != 64)) return hipErrorInvalidValue;
   const dim3 g(B * 8), t(R8_NT);
 #define MP_ROW8(M, BFV)                                                                            \
-  if (row8_znt())                                                                                  \
+  if (row8_znt(BFV))                                                                               \
     hipLaunchKernelGGL((row8_kernel<M, BFV, true>), g, t, 0, st, Z, a, or_x3, or_us, ir_x3, ir_us, O0); \
   else                                                                                             \
     hipLaunchKernelGGL((row8_kernel<M, BFV, false>), g, t, 0, st, Z, a, or_x3, or_us, ir_x3, ir_us, O0)
