@@ -21,13 +21,18 @@ def load(path, ctr):
 def main():
     f = load(sys.argv[1], "FETCH_SIZE")
     w = load(sys.argv[2], "WRITE_SIZE")
-    fwd, cur = [], None
+    fwd, cur, seen_fc = [], None, True
     for d in sorted(f):
         name, grid, fv = f[d]
-        if "conv1_pool_bn" in name:
+        # a forward starts at the first backbone kernel after the previous forward's fc_1 (with the
+        # backbone per batch slice, each slice's backbone starts with conv1_pool_bn)
+        if "conv1_pool_bn" in name and seen_fc:
             cur = collections.defaultdict(float)
             cur["_grids"] = set()
             fwd.append(cur)
+            seen_fc = False
+        if "fc_gemm" in name:
+            seen_fc = True
         if cur is None or any(t in name for t in ("probe_", "rocclr", "at::native")):
             continue
         mb = (2 * fv + (w[d][2] if d in w else 0.0)) / 1e3
