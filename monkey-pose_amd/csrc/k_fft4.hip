@@ -680,142 +680,6 @@ __global__ __launch_bounds__(512, 2) void col8_kernel(cpx* __restrict__ Z, const
   }
 }
 
-// column kernel, four waves over 8 images (col4_kernel; MP_COL4): half of col8_kernel's block, so four
-// blocks share a CU (36 KB of LDS, <= 128 VGPRs) and their load / DFT / GEMM / inverse phases interleave
-// across more independent blocks.  Thread (image bl < 8, channel pair a) as in col8_kernel; wave w
-// computes frequencies k2 = w, then w + 4, each against the S tile half that holds it (the MFMA's
-// 16 image columns carry the 8 images twice; the duplicate columns are never read back), and the
-// first half's Y goes into the S tile half it no longer needs while the second is computed.
-constexpr int C4_NI = 8;
-constexpr int C4_SLD = C4_NI + 1;
-constexpr int C4_HALF = 16 * 2 * 4 * C4_SLD;   // 1,152 x 16 B
-constexpr int C4_YLD = 16 * 4 * 2 + 1;         // Y pitch per image, one half
-static_assert(C4_NI * C4_YLD <= C4_HALF, "a half's Y tile fits the S half it replaces");
-__device__ __forceinline__ int c4_s(int k2, int cq, int part, int bl) {
-  return (k2 >> 2) * C4_HALF + ((cq * 2 + part) * 4 + (k2 & 3)) * C4_SLD + bl;
-}
-template <bool ZNT>
-__global__ __launch_bounds__(256, 4) void col4_kernel(cpx* __restrict__ Z, const uint4* __restrict__ Gc, int B,
-                                                      int ngrp, float unscale) {
-  __shared__ uint4 tile[2 * C4_HALF];   // 36,864 B
-  const int c8 = blockIdx.x / (8 * ngrp), rem = blockIdx.x - c8 * 8 * ngrp;
-  const int grp = rem >> 3, cls = c8 * 8 + (rem & 7);
-  if (cls >= Z_CLS) return;
-  const int fx = cls / 9, k1 = cls - fx * 9;
-  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int img0 = grp * C4_NI;
-  const int bl = tid >> 5, a = tid & 31;
-  const bool live = img0 + bl < B;
-  const int b = min(img0 + bl, B - 1);
-  const int cq = a >> 1, hf = a & 1;
-  const int kq = lane >> 4, jj = lane & 15;
-  uint4 wr[2][4][2];
-  auto load_1 = [&](int slot, int k2, int t) {
-    const uint4* gw = Gc + (size_t)(cls * 8 + k2) * 2 * 16 * 64;
-#pragma unroll
-    for (int mq = 0; mq < 4; ++mq) {
-      wr[slot][mq][0] = gw[(0 * 16 + 4 * t + kq) * 64 + 16 * mq + jj];
-      wr[slot][mq][1] = gw[(1 * 16 + 4 * t + kq) * 64 + 16 * mq + jj];
-    }
-  };
-  {
-    f32x4 zin[8];
-#pragma unroll
-    for (int n2 = 0; n2 < 8; ++n2) {
-      const f32x4* zp = reinterpret_cast<const f32x4*>(Z + z_off(b, n2, fx, k1)) + a;
-      zin[n2] = ZNT ? __builtin_nontemporal_load(zp) : *zp;
-    }
-    cpx sv[2][8];
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-#pragma unroll
-      for (int n2 = 0; n2 < 8; ++n2) sv[e][n2] = twid<-1>(cpx{zin[n2][2 * e], zin[n2][2 * e + 1]}, n2 * k1);
-      dft8_fold<-1>(sv[e]);
-    }
-    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
-    uint2* t2 = reinterpret_cast<uint2*>(tile);
-#pragma unroll
-    for (int k2 = 0; k2 < 8; ++k2) {
-      uint32_t hv[2], lv[2];
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const cpx v = sv[e][k2] * SPEC_SCALE;
-        const h2 hi = __builtin_convertvector(v, h2);
-        const h2 lo = __builtin_convertvector(v - __builtin_convertvector(hi, cpx), h2);
-        hv[e] = __builtin_bit_cast(uint32_t, hi);
-        lv[e] = __builtin_bit_cast(uint32_t, lo);
-      }
-      t2[c4_s(k2, cq, 0, bl) * 2 + hf] = uint2{hv[0], hv[1]};
-      t2[c4_s(k2, cq, 1, bl) * 2 + hf] = uint2{lv[0], lv[1]};
-    }
-  }
-  load_1(0, wv, 0);
-  load_1(1, wv, 1);
-  lds_barrier();
-  const uint4 m = {0x80000000u, 0x80000000u, 0x80000000u, 0x80000000u};
-  const int jc = jj & 7;   // the column's image (columns 8-15 repeat 0-7)
-#pragma unroll
-  for (int half = 0; half < 2; ++half) {
-    const int k2 = wv + 4 * half;
-    f32x4 acc[8] = {};
-#pragma unroll
-    for (int t = 0; t < 4; ++t) {
-      const uint4 uh = tile[c4_s(k2, 4 * t + kq, 0, jc)], ul = tile[c4_s(k2, 4 * t + kq, 1, jc)];
-      const f16x8 sh = __builtin_bit_cast(f16x8, uh ^ m), sl = __builtin_bit_cast(f16x8, ul ^ m);
-      const f16x8 sh2 = __builtin_bit_cast(f16x8, (uh >> 16) | (uh << 16));
-      const f16x8 sl2 = __builtin_bit_cast(f16x8, (ul >> 16) | (ul << 16));
-#pragma unroll
-      for (int mq = 0; mq < 4; ++mq) {
-        const f16x8 ah = __builtin_bit_cast(f16x8, wr[t % 2][mq][0]), al = __builtin_bit_cast(f16x8, wr[t % 2][mq][1]);
-        acc[mq] = mfma16x16(al, sh, acc[mq]);
-        acc[mq] = mfma16x16(ah, sl, acc[mq]);
-        acc[mq] = mfma16x16(ah, sh, acc[mq]);
-        acc[4 + mq] = mfma16x16(al, sh2, acc[4 + mq]);
-        acc[4 + mq] = mfma16x16(ah, sl2, acc[4 + mq]);
-        acc[4 + mq] = mfma16x16(ah, sh2, acc[4 + mq]);
-      }
-      // ring: the next k-step pair of this frequency, or the first two of the second frequency
-      if (t + 2 < 4) load_1(t % 2, k2, t + 2);
-      else if (half == 0) load_1(t % 2, k2 + 4, t - 2);
-    }
-    lds_barrier();   // every wave has read this half of the S tile
-    if (jj < C4_NI) {
-      f32x4* ytile = reinterpret_cast<f32x4*>(tile + half * C4_HALF);
-#pragma unroll
-      for (int mq = 0; mq < 4; ++mq) {
-        const int cqo = 4 * mq + kq;
-        const f32x4 re = acc[mq], im = acc[4 + mq];
-        ytile[jj * C4_YLD + (cqo * 4 + wv) * 2] = f32x4{re[0], im[0], re[1], im[1]} * unscale;
-        ytile[jj * C4_YLD + (cqo * 4 + wv) * 2 + 1] = f32x4{re[2], im[2], re[3], im[3]} * unscale;
-      }
-    }
-  }
-  lds_barrier();
-  cpx yv[2][8];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const f32x4* yt = reinterpret_cast<const f32x4*>(tile + (q >> 2) * C4_HALF);
-    const f32x4 pv = yt[bl * C4_YLD + (cq * 4 + (q & 3)) * 2 + hf];
-    yv[0][q] = cpx{pv[0], pv[1]};
-    yv[1][q] = cpx{pv[2], pv[3]};
-  }
-#pragma unroll
-  for (int e = 0; e < 2; ++e) {
-    dft8_fold<1>(yv[e]);
-#pragma unroll
-    for (int n2 = 0; n2 < 8; ++n2) yv[e][n2] = twid<1>(yv[e][n2], n2 * k1);
-  }
-  if (live) {
-#pragma unroll
-    for (int n2 = 0; n2 < 8; ++n2) {
-      f32x4* zp = reinterpret_cast<f32x4*>(Z + z_off(opaque(b), n2, fx, k1)) + a;
-      const f32x4 v = f32x4{yv[0][n2].x, yv[0][n2].y, yv[1][n2].x, yv[1][n2].y};
-      if constexpr (ZNT) __builtin_nontemporal_store(v, zp);
-      else *zp = v;
-    }
-  }
-}
-
 // column kernel, bf16 (MP_DTYPE_BF16): col8_kernel's blocking with bf16 Z partials (8-B reads of a
 // thread's two channels), a bf16 S tile (one (re, im) pair per channel, no lo plane: 34 KB), one
 // v_mfma_f32_16x16x32_bf16 product per (k-step, row block, re|im) against the class-major bf16
@@ -925,15 +789,6 @@ bool fft4_enabled() {
   return v;
 }
 
-// MP_COL4 (default 0): the four-wave, 8-image column kernel (fp32) instead of col8_kernel
-static bool col4_enabled() {
-  static const bool v = [] {
-    const char* e = std::getenv("MP_COL4");
-    return e ? std::atoi(e) != 0 : false;
-  }();
-  return v;
-}
-
 // MP_COL8_ZNT: the column kernels' Z loads and stores non-temporal (1) or default policy (0).  Default:
 // on for fp32 (same box: 8.51 -> 8.38 ms per B = 256 forward, the same PMC bytes; profiles/r5l, r5m), off
 // for bf16 (col8_bf 0.0995 -> 0.1085 ms with it; profiles/r5m_bf16)
@@ -955,14 +810,6 @@ hipError_t launch_col_gemm(void* Z, const void* Gc, int B, float unscale, hipStr
     if (col8_znt(true)) MP_COL8B(true);
     else MP_COL8B(false);
 #undef MP_COL8B
-  } else if (col4_enabled()) {
-    const int ng4 = (B + C4_NI - 1) / C4_NI;
-    if (col8_znt(false))
-      hipLaunchKernelGGL(col4_kernel<true>, dim3(CG_NC8 * 8 * ng4), dim3(256), 0, st, static_cast<cpx*>(Z),
-                         static_cast<const uint4*>(Gc), B, ng4, unscale);
-    else
-      hipLaunchKernelGGL(col4_kernel<false>, dim3(CG_NC8 * 8 * ng4), dim3(256), 0, st, static_cast<cpx*>(Z),
-                         static_cast<const uint4*>(Gc), B, ng4, unscale);
   } else {
 #define MP_COL8(N)                                                                                       \
   hipLaunchKernelGGL((col8_kernel<N>), dim3(CG_NC8 * 8 * ngrp), dim3(512), 0, st, static_cast<cpx*>(Z), \

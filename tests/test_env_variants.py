@@ -128,8 +128,6 @@ BITS_CASES = [
     ("pose80", "fp32_fft", "MP_COL8_ZNT", ("0", "1"), {}),
     ("pose80", "bf16", "MP_COL8_ZNT", ("0", "1"), {}),
     ("pose80", "fp32_fft", "MP_ROW8_ZNT", ("0", "1"), {}),
-    # the 8-image four-wave column kernel runs col8_kernel's per-output arithmetic
-    ("pose80", "fp32_fft", "MP_COL4", ("0", "1"), {}),
 ]
 
 
