@@ -1521,15 +1521,9 @@ hipError_t launch_fft_inv_a_fwd(const void* Y, const ConvArgs& a, void* S, int B
   return hipGetLastError();
 }
 
-// MP_SPEC_SMALLB: the largest batch whose spectral GEMM runs on 8-image tiles (spec_gemm_kernel<0, 8>,
-// ceil(B / 8) image groups; bit-identical to the 32-image tiles); default SPEC_SMALLB
-static int spec_smallb() {
-  static const int v = [] {
-    const char* e = std::getenv("MP_SPEC_SMALLB");
-    return e ? std::atoi(e) : SPEC_SMALLB;
-  }();
-  return v;
-}
+// batches up to SPEC_SMALLB run the spectral GEMM on 8-image tiles (spec_gemm_kernel<0, 8>, ceil(B / 8)
+// image groups; bit-identical to the 32-image tiles, which measured slower there)
+static int spec_smallb() { return SPEC_SMALLB; }
 
 hipError_t launch_spec_gemm(const void* S, const void* Gx, void* Y, int B, float unscale, hipStream_t st, bool bf) {
   const bool small = !bf && B <= spec_smallb();
@@ -1594,16 +1588,10 @@ hipError_t launch_gate_init_x3(const float* O0, float* O, float* Og, const void*
   return hipGetLastError();
 }
 
-// MP_EPI_REV (default 1): the B epilogue walks its images last to first, so its first blocks read the
-// P2 lines fft_inv wrote last and its last blocks write the Og lines the next fft_fwd reads first
-// (B = 256 fp32 10.43 -> 10.37 ms per forward, profiles/r4o; 0 restores ascending order)
-static int epi_rev() {
-  static const int v = [] {
-    const char* e = std::getenv("MP_EPI_REV");
-    return e ? std::atoi(e) : 1;
-  }();
-  return v;
-}
+// the B epilogue walks its images last to first, so its first blocks read the P2 lines fft_inv wrote
+// last and its last blocks write the Og lines the next fft_fwd reads first (B = 256 fp32 10.43 -> 10.37
+// ms per forward against ascending order, profiles/r4o)
+static int epi_rev() { return 1; }
 
 hipError_t launch_spec_epi_b(const ConvArgs& a, const float* P, const void* or_x3, float or_us, const void* ir_x3,
                              float ir_us, int B, hipStream_t st, bool bf) {

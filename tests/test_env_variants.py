@@ -120,10 +120,6 @@ BITS_CASES = [
     # output's MFMA sequence of igemm_x3pw_kernel: MP_IGEMM_PWN = 0 / 1 / 2 give the same bytes
     ("dense", "fp32_split", "MP_IGEMM_PWN", ("0", "1", "2", "3"), {}),
     ("dense", "bf16", "MP_IGEMM_PWN", ("0", "1", "2", "3"), {}),
-    # six-launch loop (MP_FFT4=0): the spectral GEMM on 8-image tiles (two groups at 12 crops) vs the
-    # 32-image tiles; the B epilogue's image order
-    ("pose", "fp32_fft", "MP_SPEC_SMALLB", ("8", "32"), {"MP_FFT4": "0"}),
-    ("pose80", "fp32_fft", "MP_EPI_REV", ("0", "1"), {"MP_FFT4": "0"}),
     # four-step loop: non-temporal or default cache policy for the partials moves no value
     ("pose80", "fp32_fft", "MP_COL8_ZNT", ("0", "1"), {}),
     ("pose80", "bf16", "MP_COL8_ZNT", ("0", "1"), {}),
