@@ -124,6 +124,10 @@ BITS_CASES = [
     ("pose80", "fp32_fft", "MP_COL8_ZNT", ("0", "1"), {}),
     ("pose80", "bf16", "MP_COL8_ZNT", ("0", "1"), {}),
     ("pose80", "fp32_fft", "MP_ROW8_ZNT", ("0", "1"), {}),
+    # the backbone per batch slice (two slices at 80 crops), staggered or not, or whole-batch first
+    ("pose80", "fp32_fft", "MP_BB_PIPE", ("0", "1"), {}),
+    ("pose80", "fp32_fft", "MP_BB_STAGGER", ("0", "1"), {}),
+    ("pose80", "bf16", "MP_BB_PIPE", ("0", "1"), {}),
 ]
 
 
