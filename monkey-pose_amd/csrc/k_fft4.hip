@@ -554,7 +554,7 @@ __device__ __forceinline__ f32x4 mfma16x16(f16x8 a, f16x8 b, f32x4 c) {
 // per CU (0.207 ms; batch-1 forward 1.06 vs 0.98 ms): both removed.
 // ZNT: the partials Z read and written non-temporal (the weights, re-read by the other batch slice's
 // launch of the same convolution, keep the cache)
-template <bool ZNT, bool PF>
+template <bool ZNT>
 __global__ __launch_bounds__(512, 2) void col8_kernel(cpx* __restrict__ Z, const uint4* __restrict__ Gc, int B,
                                                       int ngrp, float unscale) {
   __shared__ uint4 tile[2 * CG_HALF];   // 69,632 B
@@ -588,17 +588,6 @@ __global__ __launch_bounds__(512, 2) void col8_kernel(cpx* __restrict__ Z, const
     for (int n2 = 0; n2 < 8; ++n2) {
       const f32x4* zp = reinterpret_cast<const f32x4*>(Z + z_off(b, n2, fx, k1)) + a;
       zin[n2] = ZNT ? __builtin_nontemporal_load(zp) : *zp;
-    }
-    if constexpr (PF) {
-      // touch the next image group's partials of this class (one dword per 128-B line, thread t: line t of
-      // the group's 128 runs x 4 lines) so that they are in the XCD's L2 when that block -- dispatched 8
-      // blocks later onto the same XCD -- loads them; the dummy register is kept live until the wait
-      // before the DFT below (a load whose destination the compiler re-used would overwrite it)
-      const int bn = min((grp + 1) * CG_NI + ((tid >> 2) >> 3), B - 1);
-      const float* pp = reinterpret_cast<const float*>(Z + z_off(bn, (tid >> 2) & 7, fx, k1) + 16 * (tid & 3));
-      float dummy;
-      asm volatile("global_load_dword %0, %1, off" : "=v"(dummy) : "v"(pp) : "memory");
-      asm volatile("s_waitcnt vmcnt(0)" : "+v"(dummy) : : "memory");
     }
     cpx s[2][8];
 #pragma unroll
@@ -800,15 +789,6 @@ bool fft4_enabled() {
   return v;
 }
 
-// MP_COL8_PF (default 0): col8_kernel touches the next image group's partials into L2
-static bool col8_pf() {
-  static const bool v = [] {
-    const char* e = std::getenv("MP_COL8_PF");
-    return e ? std::atoi(e) != 0 : false;
-  }();
-  return v;
-}
-
 // MP_COL8_ZNT: the column kernels' Z loads and stores non-temporal (1) or default policy (0).  Default:
 // on for fp32 (same box: 8.51 -> 8.38 ms per B = 256 forward, the same PMC bytes; profiles/r5l, r5m), off
 // for bf16 (col8_bf 0.0995 -> 0.1085 ms with it; profiles/r5m_bf16)
@@ -831,14 +811,11 @@ hipError_t launch_col_gemm(void* Z, const void* Gc, int B, float unscale, hipStr
     else MP_COL8B(false);
 #undef MP_COL8B
   } else {
-#define MP_COL8(N, P)                                                                                       \
-  hipLaunchKernelGGL((col8_kernel<N, P>), dim3(CG_NC8 * 8 * ngrp), dim3(512), 0, st, static_cast<cpx*>(Z), \
+#define MP_COL8(N)                                                                                       \
+  hipLaunchKernelGGL((col8_kernel<N>), dim3(CG_NC8 * 8 * ngrp), dim3(512), 0, st, static_cast<cpx*>(Z), \
                      static_cast<const uint4*>(Gc), B, ngrp, unscale)
-    const bool zn = col8_znt(false), pf = col8_pf();
-    if (zn && pf) MP_COL8(true, true);
-    else if (zn) MP_COL8(true, false);
-    else if (pf) MP_COL8(false, true);
-    else MP_COL8(false, false);
+    if (col8_znt(false)) MP_COL8(true);
+    else MP_COL8(false);
 #undef MP_COL8
   }
   return hipGetLastError();
