@@ -31,10 +31,16 @@ constexpr int RK_ITEMS = FX * 64;                    // (fx, channel) columns of
 constexpr int RK_T = 8 * FX * 64;                    // T[n1][fx][c] complex: 151,552 B of LDS
 constexpr int RK_SP = 68;                            // staging pitch (floats) per pixel (16-B fragment reads)
 
-// complex index of channel 0 of Z[b][n2][fx][k1]
+// complex index of channel 0 of Z[b][n2][fx][k1] (ZLAYOUT 0: a row block's (b, n2) slice contiguous),
+// or of Z[b][fx][k1][n2] (ZLAYOUT 1: a column block's 8 row classes of one image contiguous)
+#ifndef ZLAYOUT
+#define ZLAYOUT 0
+#endif
 __device__ __forceinline__ size_t z_off(int b, int n2, int fx, int k1) {
+  if constexpr (ZLAYOUT == 1) return ((((size_t)b * FX + fx) * 9 + k1) * 8 + n2) * 64;
   return ((((size_t)b * 8 + n2) * FX + fx) * 9 + k1) * 64;
 }
+constexpr int Z_K1 = ZLAYOUT == 1 ? 8 * 64 : 64;   // complex stride between consecutive k1
 
 enum { ROW_A = 0, ROW_B = 1, ROW_FINAL = 2, ROW_INIT = 3 };
 
@@ -427,7 +433,7 @@ __global__ __launch_bounds__(R8_NT, 1) void row8_kernel(void* __restrict__ Z, Co
         const int i = min(it * R8_NT + tid, RK_ITEMS - 1);
         const size_t src = z_off(b, n2, i >> 6, 0) + (i & 63);
 #pragma unroll
-        for (int k1 = 0; k1 < 9; ++k1) u[it][k1] = z_ld<BF, ZNT>(Z, src + k1 * 64);
+        for (int k1 = 0; k1 < 9; ++k1) u[it][k1] = z_ld<BF, ZNT>(Z, src + k1 * Z_K1);
       }
 #pragma unroll
       for (int it = 0; it < R8_NIT; ++it) {
@@ -514,7 +520,7 @@ __global__ __launch_bounds__(R8_NT, 1) void row8_kernel(void* __restrict__ Z, Co
     dft9<-1>(u);
     const size_t dst = z_off(b, n2, fx, 0) + c;
 #pragma unroll
-    for (int k1 = 0; k1 < 9; ++k1) z_st<BF, ZNT>(Z, dst + k1 * 64, u[k1]);
+    for (int k1 = 0; k1 < 9; ++k1) z_st<BF, ZNT>(Z, dst + k1 * Z_K1, u[k1]);
   }
 }
 
