@@ -11,12 +11,12 @@
 //               transforms, the 9-point sums over n1, and every per-pixel channel mix (the 1x1 gates
 //               of hgru_module.py:696-711, 729-740), so the B half-step's epilogue runs between its
 //               inverse and the next step's forward transform without a map round trip;
-//   col kernel  (column fx, class k1, 32 images): the 8 frequencies fy = k1 + 9 k2 with all 64
+//   col kernel  (column fx, class k1, 16 images): the 8 frequencies fy = k1 + 9 k2 with all 64
 //               channels -- the twiddles W72^{n2 k1}, the 8-point sums over n2 and the per-frequency
 //               64 x 64 complex GEMM (f16x3, k_fft.hip spec_gemm_kernel's fragments).
 // One timestep is four launches (hgru_module.py:825-857):
 //   col: Z -> Z'   row_a: Z', X, O -> I, Z   col: Z -> Z'   row_b: Z', I, O -> O', Z
-// Z = [b][n2][fx][k1][64 channels] complex64 (1.36 MB per image, a spectrum's size) carries the
+// Z = [b][fx][k1][n2][64 channels] complex64 (1.36 MB per image, a spectrum's size) carries the
 // partial transforms between them IN PLACE: every block reads exactly the elements it writes.  Per
 // image and step: 8 spectra + 6 maps of traffic (17.2 MB) instead of the six-launch loop's 8 + 10
 // (22.1 MB): P2 and the gated state Og never reach HBM.  The numerics are the six-launch loop's (fp32
@@ -389,7 +389,7 @@ __device__ __forceinline__ void z_st(void* Z, size_t i, cpx v) {
 //   II  the half-step's epilogue on two 32-pixel segments in the MFMA accumulator layout (rk_segment),
 //       P staged through LDS, the 1x1 gates' weights read from LDS
 //   III lane c: forward real transform of the epilogue's output -> T; items (fx, c): forward 9-point
-//       sums over n1 -> Z[b][n2][fx][k1][c]
+//       sums over n1 -> Z[b][fx][k1][n2][c]
 // Round 5 measured two other forms and removed them: a four-wave block with the whole T (one row
 // pair per wave) and a two-blocks-per-CU block with half of T (two transpose rounds; register
 // spills): B = 256 fp32 9.61 ms per forward against this kernel's 9.04 (profiles/r5d).
@@ -530,7 +530,7 @@ __global__ __launch_bounds__(R8_NT, 1) void row8_kernel(void* __restrict__ Z, Co
 // column kernel (the spectral GEMM).  Block = (column class (fx, k1), 16 images), 256 threads, two
 // blocks per CU (68 KB of LDS).  Thread (image, channel pair a) holds channels 2a, 2a + 1 and
 // 32 + 2a, 33 + 2a of its image (each wave instruction reads / writes contiguous 256-B runs of Z) and
-// turns their 8 row-class partials Z[b][n2][fx][k1][.] into the class's 8 frequencies (twiddle, 8-point
+// turns their 8 row-class partials Z[b][fx][k1][n2][.] into the class's 8 frequencies (twiddle, 8-point
 // DFT, scale + f16 split into the S tile).  Wave w then computes frequency fy = k1 + 9 k2 for k2 = w and
 // w + 4:  Y[b][co] = sum_ci S[b][ci] G[ci][co]  (complex), as a real 128 x 16 x 128 product on
 // v_mfma_f32_16x16x32_f16 in the f16x3 split (k = 2 ci + re|im; rows n = 64 ro + co, the re / im rows'
