@@ -461,15 +461,6 @@ bool bb_pipeline() {
   return v;
 }
 
-// MP_FC1_SLICE (default 0): fc_1 per batch slice on the slice's stream after its hGRU loop
-bool fc1_per_slice() {
-  static const bool v = [] {
-    const char* e = std::getenv("MP_FC1_SLICE");
-    return e ? std::atoi(e) != 0 : false;
-  }();
-  return v;
-}
-
 // MP_BB_STAGGER (default 1): a slice's backbone waits for the previous slice's, so that it overlaps that
 // slice's hGRU loop instead of the other backbone (same box, B = 256: 8.40 -> 8.28 ms; profiles/r5n)
 bool bb_stagger() {
@@ -492,10 +483,8 @@ int slice_min() {
 // pre (optional): work a batch slice needs before its hGRU loop (the backbone of its images), run on the
 // slice's stream so that one slice's backbone overlaps another's loop
 using SliceFn = std::function<void(int b0, int cnt, hipStream_t s)>;
-// post (optional): work on a slice's rows after its hGRU loop, on the slice's stream (fc_1 per slice)
 void run_circuit(mp_ctx* c, int64_t n, int H, int W, int T, const float* o0_nhwc, float* final_dst2,
-                 const StateOut* so, hipStream_t st, const SplitOut* sp = nullptr, const SliceFn* pre = nullptr,
-                 const SliceFn* post = nullptr) {
+                 const StateOut* so, hipStream_t st, const SplitOut* sp = nullptr, const SliceFn* pre = nullptr) {
   if (sp && !is_fft(c->dtype)) fail(MP_ERR_STATE, "split fc_1 planes are an FFT-path output");
   // FFT path, not profiling: batch slices are independent, so they run on separate streams and
   // their latency-bound kernels overlap (the per-kernel HIP-event profile keeps one stream)
@@ -504,7 +493,6 @@ void run_circuit(mp_ctx* c, int64_t n, int H, int W, int T, const float* o0_nhwc
   if (pre && !multi) (*pre)(0, (int)n, st);
   if (c->fft4 && !multi) {
     fft4_circuit_range(c, 0, (int)n, H, W, T, o0_nhwc, final_dst2, so, sp, st);
-    if (post) (*post)(0, (int)n, st);
     return;
   }
   if (multi) {
@@ -544,7 +532,6 @@ void run_circuit(mp_ctx* c, int64_t n, int H, int W, int T, const float* o0_nhwc
         fft4_circuit_range(c, b0, cnt, H, W, T, o0_nhwc, final_dst2, so, sp, s);
       else
         fft_circuit_range(c, b0, cnt, H, W, T, final_dst2, so, sp, s);
-      if (post) (*post)(b0, cnt, s);
       b0 += cnt;
     }
     for (int k = 1; k < ns; ++k) {
@@ -936,30 +923,13 @@ int pose_fwd(mp_ctx* ctx, const float* depth, int64_t n, int64_t h, int64_t w, c
       sp.hi = reinterpret_cast<_Float16*>(ctx->fcin.p);
       sp.lo = fc_np == 3 ? sp.hi + (size_t)N * ctx->fc1_in : nullptr;
     }
-    // fc_1 of a slice's rows on the slice's stream as soon as its hGRU loop ends (MP_FC1_SLICE; each
-    // slice streams the weights again), or of the whole batch after the join
-    int fks;
-    const int fS = fc_choose_splits(N, ctx->fc1_in, ctx->fc1_out, &fks);
-    const int npad1 = (ctx->fc1_out + 31) / 32 * 32;
-    const SliceFn fc1_rows = [&](int b0, int cnt, hipStream_t s) {
-      ProfScope ps(ctx, s, "fc1");
-      float* part = ctx->part.f() + (size_t)fS * b0 * npad1;   // this slice's [S][cnt][Npad] slabs
-      hip_check(launch_fc_gemm_x3p(sp.hi + (size_t)b0 * ctx->fc1_in, sp.lo ? sp.lo + (size_t)b0 * ctx->fc1_in : nullptr,
-                                   ctx->fc1_in, ctx->fc1_pk.p, ctx->fc1_unscale, part, cnt, ctx->fc1_in, ctx->fc1_out,
-                                   fS, fks, s, fc_np),
-                "fc_1 gemm");
-      hip_check(launch_fc_reduce(part, fS, cnt, ctx->fc1_out, ctx->fc1_b.f(), 1, ctx->bn4_s.f(), ctx->bn4_t.f(),
-                                 ctx->h1.f() + (size_t)b0 * ctx->fc1_out, ctx->fc1_out, s),
-                "fc_1 reduce");
-    };
-    const bool fc1_slice = fc1_per_slice() && presplit && !tp.fc1 && ctx->fc1_in % 32 == 0;
     run_circuit(ctx, n, H, W, ctx->timesteps, h0, ctx->fcin.f(), (so.O || so.I) ? &so : nullptr, st,
-                presplit ? &sp : nullptr, bb_pipe ? &backbone : nullptr, fc1_slice && ctx->fft4 ? &fc1_rows : nullptr);
+                presplit ? &sp : nullptr, bb_pipe ? &backbone : nullptr);
     if (tp.hgru)
       hip_check(hipMemcpyAsync(tp.hgru, ctx->fcin.f(), (size_t)N * ctx->fc1_in * sizeof(float),
                                hipMemcpyDeviceToDevice, st),
                 "hgru tap");
-    if (!(fc1_slice && ctx->fft4)) {
+    {
       ProfScope ps(ctx, st, "fc1");
       int ks;
       const int S = fc_choose_splits(N, ctx->fc1_in, ctx->fc1_out, &ks);

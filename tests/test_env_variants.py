@@ -128,7 +128,6 @@ BITS_CASES = [
     ("pose80", "fp32_fft", "MP_BB_PIPE", ("0", "1"), {}),
     ("pose80", "fp32_fft", "MP_BB_STAGGER", ("0", "1"), {}),
     ("pose80", "bf16", "MP_BB_PIPE", ("0", "1"), {}),
-    ("pose80", "fp32_fft", "MP_FC1_SLICE", ("0", "1"), {}),
 ]
 
 
