@@ -120,8 +120,8 @@ def fft_kernels(ctx, B, hw, steps, bf16=False):
 # per-kernel HBM bytes per launch from rocprofv3 PMC passes (FETCH_SIZE x2 on gfx950 + WRITE_SIZE,
 # MI355X_MICROARCH.md), collected with the full-batch single-stream launches of this workload by
 # tools/pmc_bytes.py and committed under profiles/ (bench cannot profile itself)
-PMC_TRAFFIC = {False: "profiles/r5zz/pmc_traffic_fp32_b256.csv",
-               True: "profiles/r5zz/pmc_traffic_bf16_b256.csv"}
+PMC_TRAFFIC = {False: "profiles/r5fin/pmc_traffic_fp32_b256.csv",
+               True: "profiles/r5fin/pmc_traffic_bf16_b256.csv"}
 PMC_KERNEL = {   # name: (fp32 path's kernel, bf16 path's kernel) as rocprofv3 names them
     "fft_fwd": ("fft_fwd3_kernel", "fft_fwd_kernel<true, true>"),
     "spec_gemm": ("spec_gemm_kernel<0, 32>", "spec_gemm_bf_kernel"),
@@ -138,7 +138,7 @@ PMC_KERNEL = {   # name: (fp32 path's kernel, bf16 path's kernel) as rocprofv3 n
 
 # MFMA utilisation per kernel from the committed PMC pass (tools/pmc_mfma.sh / .py: SQ_VALU_MFMA_BUSY_CYCLES
 # over GRBM_GUI_ACTIVE x 1024 SIMDs, the gfx950 MfmaUtil), same one-stream B = 256 workload
-PMC_MFMA = "profiles/r5zz/mfma_util_pose_fp32_b256.csv"
+PMC_MFMA = "profiles/r5fin/mfma_util_pose_fp32_b256.csv"
 MFMA_KERNELS = {"col8 (four-step spectral GEMM, k_fft4.hip)": "col8_kernel",
                 "row8 B (gate GEMMs, k_fft4.hip)": "row8_kernel<1, false",
                 "fc_gemm_x3p (fc_1 on split planes, k_fc.hip)": "fc_gemm_x3p_kernel", "conv64x3 (conv_2/3, k_conv64x3.hip)": "conv64x3_kernel",
@@ -162,7 +162,7 @@ def pmc_mfma_busy():
     return {"source": PMC_MFMA, "mfma_busy": out}
 
 
-PMC_FORWARD = "profiles/r5zz/pmc_forward_bytes.json"
+PMC_FORWARD = "profiles/r5fin/pmc_forward_bytes.json"
 
 
 def pmc_forward_bytes(dtype, batch):
