@@ -20,7 +20,7 @@
 
 namespace mp {
 
-constexpr int FC_BM = 128, FC_BK = 32, FC_LDA = FC_BK + 4;
+constexpr int FC_BK = 32, FC_LDA = FC_BK + 4;
 
 __global__ void pack_fc_kernel(const float* __restrict__ W, f32x4* out, int K, int N, int K8, int N32) {
   const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
@@ -51,13 +51,17 @@ __device__ __forceinline__ FcTile fc_tile(int Mt, int Nt) {
 }
 inline int fc_grid(int Mt, int Nt, int S) { return 8 * ((S + 7) / 8) * Mt * Nt; }
 
+// MB: 32-row m-blocks per block (1 or 2 for M <= 32 / 64: a batch-1 fc_out 18.9 us with 4, the MFMAs
+// of 96 empty rows).  Each output row's K sum is the same MFMA chain whatever MB is (bit-identical)
+template <int MB>
 __global__ __launch_bounds__(256) void fc_gemm_kernel(const float* __restrict__ A, int lda,
                                                       const f32x4* __restrict__ Wpk,
                                                       float* __restrict__ part, int M, int K,
                                                       int N32, int kslice, int S) {
-  __shared__ float As[FC_BM * FC_LDA];
+  constexpr int BM = 32 * MB;
+  __shared__ float As[BM * FC_LDA];
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6, h = lane >> 5, col = lane & 31;
-  const FcTile tl = fc_tile((M + FC_BM - 1) / FC_BM, (N32 + 3) / 4);
+  const FcTile tl = fc_tile((M + BM - 1) / BM, (N32 + 3) / 4);
   if (tl.split >= S) return;
   const int mt = tl.mt, ntile = tl.nt, split = tl.split;
   const int K8 = (K + 7) / 8;
@@ -67,27 +71,39 @@ __global__ __launch_bounds__(256) void fc_gemm_kernel(const float* __restrict__ 
   const int kbeg = split * kslice;
   const int kend = min(K, kbeg + kslice);
 
-  f32x16 acc[4];
+  f32x16 acc[MB];
 #pragma unroll
-  for (int m = 0; m < 4; ++m) acc[m] = f32x16{};
+  for (int m = 0; m < MB; ++m) acc[m] = f32x16{};
 
+  const int nbc = min(nb, N32 - 1);
   for (int k0 = kbeg; k0 < kend; k0 += FC_BK) {
-    __syncthreads();
+    // the step's weight fragments requested with its activations (one memory latency per step, not
+    // two); k groups past K8 load group K8 - 1 and are not used.  With the MB tile: fc_out at batch 1
+    // 18.9 -> 7.2 us, at batch 32 13.7 -> 7.7 (profiles/r5_ab/r5y)
+    f32x4 wf[FC_BK / 8];
 #pragma unroll
-    for (int i = 0; i < 4; ++i) {
-      const int e = tid + i * 256;          // 0..1023 float4 slots: row = e / 8, k4 = e % 8
+    for (int g = 0; g < FC_BK / 8; ++g) wf[g] = Wpk[((size_t)min((k0 >> 3) + g, K8 - 1) * N32 + nbc) * 64 + lane];
+    f32x4 v[MB];
+#pragma unroll
+    for (int i = 0; i < MB; ++i) {
+      const int e = tid + i * 256;          // float4 slots: row = e / 8, k4 = e % 8
       const int row = e >> 3, k4 = (e & 7) * 4;
-      const int gm = mt * FC_BM + row, gk = k0 + k4;
-      f32x4 v = {0.f, 0.f, 0.f, 0.f};
+      const int gm = mt * BM + row, gk = k0 + k4;
+      v[i] = f32x4{0.f, 0.f, 0.f, 0.f};
       if (gm < M) {
         if (gk + 3 < kend) {
-          v = *reinterpret_cast<const f32x4*>(A + (size_t)gm * lda + gk);
+          v[i] = *reinterpret_cast<const f32x4*>(A + (size_t)gm * lda + gk);
         } else {
 #pragma unroll
-          for (int s = 0; s < 4; ++s) v[s] = (gk + s < kend) ? A[(size_t)gm * lda + gk + s] : 0.f;
+          for (int s = 0; s < 4; ++s) v[i][s] = (gk + s < kend) ? A[(size_t)gm * lda + gk + s] : 0.f;
         }
       }
-      *reinterpret_cast<f32x4*>(As + row * FC_LDA + k4) = v;
+    }
+    __syncthreads();
+#pragma unroll
+    for (int i = 0; i < MB; ++i) {
+      const int e = tid + i * 256;
+      *reinterpret_cast<f32x4*>(As + (e >> 3) * FC_LDA + (e & 7) * 4) = v[i];
     }
     __syncthreads();
     if (wave_on) {
@@ -95,20 +111,19 @@ __global__ __launch_bounds__(256) void fc_gemm_kernel(const float* __restrict__ 
       for (int g = 0; g < FC_BK / 8; ++g) {
         const int kb = (k0 >> 3) + g;
         if (kb >= K8) break;
-        const f32x4 wf = Wpk[((size_t)kb * N32 + nb) * 64 + lane];
 #pragma unroll
-        for (int m = 0; m < 4; ++m) {
+        for (int m = 0; m < MB; ++m) {
           const f32x4 a = *reinterpret_cast<const f32x4*>(As + (m * 32 + col) * FC_LDA + 8 * g + 4 * h);
 #pragma unroll
-          for (int s = 0; s < 4; ++s) acc[m] = mfma32(wf[s], a[s], acc[m]);
+          for (int s = 0; s < 4; ++s) acc[m] = mfma32(wf[g][s], a[s], acc[m]);
         }
       }
     }
   }
   if (!wave_on) return;
 #pragma unroll
-  for (int m = 0; m < 4; ++m) {
-    const int gm = mt * FC_BM + m * 32 + col;
+  for (int m = 0; m < MB; ++m) {
+    const int gm = mt * BM + m * 32 + col;
     if (gm >= M) continue;
     float* dst = part + ((size_t)split * M + gm) * Npad + 32 * nb + 4 * h;
 #pragma unroll
@@ -782,8 +797,14 @@ int fc_choose_splits(int M, int K, int N, int* kslice) {
 hipError_t launch_fc_gemm(const float* A, int lda, const f32x4* Wpk, float* part, int M, int K, int N,
                           int S, int kslice, hipStream_t st) {
   const int N32 = (N + 31) / 32;
-  const int grid = fc_grid((M + FC_BM - 1) / FC_BM, (N32 + 3) / 4, S);
-  hipLaunchKernelGGL(fc_gemm_kernel, dim3(grid), dim3(256), 0, st, A, lda, Wpk, part, M, K, N32, kslice, S);
+  const int mb = M <= 32 ? 1 : (M <= 64 ? 2 : 4);
+  const int grid = fc_grid((M + 32 * mb - 1) / (32 * mb), (N32 + 3) / 4, S);
+  if (mb == 1)
+    hipLaunchKernelGGL(fc_gemm_kernel<1>, dim3(grid), dim3(256), 0, st, A, lda, Wpk, part, M, K, N32, kslice, S);
+  else if (mb == 2)
+    hipLaunchKernelGGL(fc_gemm_kernel<2>, dim3(grid), dim3(256), 0, st, A, lda, Wpk, part, M, K, N32, kslice, S);
+  else
+    hipLaunchKernelGGL(fc_gemm_kernel<4>, dim3(grid), dim3(256), 0, st, A, lda, Wpk, part, M, K, N32, kslice, S);
   return hipGetLastError();
 }
 

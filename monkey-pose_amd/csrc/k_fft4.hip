@@ -799,30 +799,33 @@ bool fft4_enabled() {
 
 // MP_COL8_ZNT: the column kernels' Z loads and stores non-temporal (1) or default policy (0).  Default:
 // on for fp32 (same box: 8.51 -> 8.38 ms per B = 256 forward, the same PMC bytes; profiles/r5l, r5m), off
-// for bf16 (col8_bf 0.0995 -> 0.1085 ms with it; profiles/r5m_bf16)
-static bool col8_znt(bool bf) {
+// for bf16 (col8_bf 0.0995 -> 0.1085 ms with it; profiles/r5m_bf16).  `resident` (the forward's whole
+// batch <= 32: its Z, maps and spectral weights fit the 256 MB Infinity Cache): default policy, so the next kernel's reads hit there (interleaved same-box
+// timing, both Z switches off: B = 1 0.962 -> 0.945 ms, B = 32 1.445 -> 1.419, B = 64 2.41 -> 2.48;
+// profiles/r5_ab/r5w)
+static bool col8_znt(bool bf, bool resident) {
   static const int v = [] {
     const char* e = std::getenv("MP_COL8_ZNT");
     return e ? (std::atoi(e) != 0 ? 1 : 0) : -1;
   }();
-  return v < 0 ? !bf : v != 0;
+  return v < 0 ? !bf && !resident : v != 0;
 }
 
-hipError_t launch_col_gemm(void* Z, const void* Gc, int B, float unscale, hipStream_t st, bool bf) {
+hipError_t launch_col_gemm(void* Z, const void* Gc, int B, float unscale, hipStream_t st, bool bf, bool resident) {
   if (B <= 0) return hipSuccess;
   const int ngrp = (B + CG_NI - 1) / CG_NI;
   if (bf) {
 #define MP_COL8B(N)                                                                                          \
   hipLaunchKernelGGL((col8_bf_kernel<N>), dim3(CG_NC8 * 8 * ngrp), dim3(512), 0, st, Z, static_cast<const uint4*>(Gc), \
                      B, ngrp)
-    if (col8_znt(true)) MP_COL8B(true);
+    if (col8_znt(true, resident)) MP_COL8B(true);
     else MP_COL8B(false);
 #undef MP_COL8B
   } else {
 #define MP_COL8(N)                                                                                       \
   hipLaunchKernelGGL((col8_kernel<N>), dim3(CG_NC8 * 8 * ngrp), dim3(512), 0, st, static_cast<cpx*>(Z), \
                      static_cast<const uint4*>(Gc), B, ngrp, unscale)
-    if (col8_znt(false)) MP_COL8(true);
+    if (col8_znt(false, resident)) MP_COL8(true);
     else MP_COL8(false);
 #undef MP_COL8
   }
@@ -831,22 +834,22 @@ hipError_t launch_col_gemm(void* Z, const void* Gc, int B, float unscale, hipStr
 
 // MP_ROW8_ZNT: row8_kernel's Z loads and stores non-temporal (1) or default policy (0).  Default: on for
 // fp32 (interleaved same-box timing 8.27 -> 8.21 ms per B = 256 forward; profiles/r5o), off for bf16
-// (5.080 vs 5.079 ms)
-static bool row8_znt(bool bf) {
+// (5.080 vs 5.079 ms); off, as in col8_znt, when the batch is cache-resident
+static bool row8_znt(bool bf, bool resident) {
   static const int v = [] {
     const char* e = std::getenv("MP_ROW8_ZNT");
     return e ? (std::atoi(e) != 0 ? 1 : 0) : -1;
   }();
-  return v < 0 ? !bf : v != 0;
+  return v < 0 ? !bf && !resident : v != 0;
 }
 
 hipError_t launch_row(int mode, void* Z, const ConvArgs& a, const void* or_x3, float or_us, const void* ir_x3,
-                      float ir_us, const float* O0, int B, hipStream_t st, bool bf) {
+                      float ir_us, const float* O0, int B, hipStream_t st, bool bf, bool resident) {
   if (B <= 0) return hipSuccess;
   if (a.H < 1 || a.H > 64 || (a.W != 32 && a.W != 64)) return hipErrorInvalidValue;
   const dim3 g(B * 8), t(R8_NT);
 #define MP_ROW8(M, BFV)                                                                            \
-  if (row8_znt(BFV))                                                                               \
+  if (row8_znt(BFV, resident))                                                                             \
     hipLaunchKernelGGL((row8_kernel<M, BFV, true>), g, t, 0, st, Z, a, or_x3, or_us, ir_x3, ir_us, O0); \
   else                                                                                             \
     hipLaunchKernelGGL((row8_kernel<M, BFV, false>), g, t, 0, st, Z, a, or_x3, or_us, ir_x3, ir_us, O0)

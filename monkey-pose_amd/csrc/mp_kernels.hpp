@@ -90,9 +90,11 @@ hipError_t launch_spec_epi_b(const ConvArgs& a, const float* P, const void* or_x
 // 2 = the last B (O' and BN_3(O') to a.dst2 / a.dst3 per a.mode), 3 = INIT (O0 NHWC -> a.dst = O).
 bool fft4_enabled();
 // bf: MP_DTYPE_BF16 (bf16 Z, maps and spectral / gate products; class-major bf16 weights)
-hipError_t launch_col_gemm(void* Z, const void* Gc, int B, float unscale, hipStream_t st, bool bf = false);
+// resident: the forward's whole batch fits the Infinity Cache (Z accessed with the default cache policy)
+hipError_t launch_col_gemm(void* Z, const void* Gc, int B, float unscale, hipStream_t st, bool bf = false,
+                           bool resident = false);
 hipError_t launch_row(int mode, void* Z, const ConvArgs& a, const void* or_x3, float or_us, const void* ir_x3,
-                      float ir_us, const float* O0, int B, hipStream_t st, bool bf = false);
+                      float ir_us, const float* O0, int B, hipStream_t st, bool bf = false, bool resident = false);
 // k_igemm.hip (dense / hierarchical regressors)
 struct IgemmArgs {
   const float* x;      // input view: pixel (n,y,x) channel ci at x[((n*H+y)*W+x)*ldx + cix + ci]
