@@ -527,6 +527,114 @@ __global__ __launch_bounds__(R8_NT, 1) void row8_kernel(void* __restrict__ Z, Co
 }
 
 // ---------------------------------------------------------------------------------------------
+// row A on channel quarters (rowq_a_kernel, fp32, small batches).  Row A's math is channel-separable
+// (the 9-point sums and row transforms act per channel, the A epilogue per element: no gate), so a
+// block can take (image b, row class n2, 16 channels): 128 threads, thread (row n1 = tid / 16, channel
+// 16 q + tid % 16) for the transforms, T[n1][fx][16] (37.9 KB), four blocks per CU: four times the
+// blocks of row8_kernel, the same LDS (and so the same waves) per CU.  It pays where row8_kernel leaves
+// CUs idle: B = 1 0.941 -> 0.930 ms per forward, B = 4 0.968 -> 0.958, B = 8 0.994 -> 0.985; from B = 16
+// on it is slower (1.113 vs 1.098; B = 32 1.44 vs 1.41, B = 256 8.47 vs 8.17; profiles/r5_ab/rq).  The
+// same functions on the same values in the same order as row8_kernel<ROW_A>: bit-identical.
+// ---------------------------------------------------------------------------------------------
+constexpr int RQ_NT = 128;
+constexpr int RQ_ITEMS = FX * 16;                        // (fx, channel) items of the 9-point passes
+constexpr int RQ_NIT = (RQ_ITEMS + RQ_NT - 1) / RQ_NT;   // 5
+__device__ __forceinline__ int rq_stg(int r, int x, int c) { return (r * 64 + x) * 16 + c + 16 * r; }
+static_assert(8 * 64 * 16 + 16 * 8 <= 2 * 8 * FX * 16, "row A staging fits T");
+
+template <bool ZNT>
+__global__ __launch_bounds__(RQ_NT, 2) void rowq_a_kernel(void* __restrict__ Z, ConvArgs p) {
+  __shared__ cpx T[8 * FX * 16];
+  const int q = blockIdx.x & 3, n2 = (blockIdx.x >> 2) & 7, b = blockIdx.x >> 5;
+  const int tid = threadIdx.x, r = tid >> 4, cc = tid & 15, c0 = 16 * q;
+  const int H = p.H, W = p.W;
+  float P[64];
+  {
+    cpx u[RQ_NIT][9];
+#pragma unroll
+    for (int it = 0; it < RQ_NIT; ++it) {
+      const int i = min(it * RQ_NT + tid, RQ_ITEMS - 1);
+      const size_t src = z_off(b, n2, i >> 4, 0) + c0 + (i & 15);
+#pragma unroll
+      for (int k1 = 0; k1 < 9; ++k1) u[it][k1] = z_ld<false, ZNT>(Z, src + k1 * Z_K1);
+    }
+#pragma unroll
+    for (int it = 0; it < RQ_NIT; ++it) {
+      const int i = it * RQ_NT + tid;
+      dft9<1>(u[it]);
+      if (i < RQ_ITEMS) {
+#pragma unroll
+        for (int rr = 0; rr < 8; ++rr) T[(rr * FX + (i >> 4)) * 16 + (i & 15)] = u[it][rr];
+      }
+    }
+  }
+  lds_barrier();
+  {
+    cpx A[FX];
+#pragma unroll
+    for (int k = 0; k < FX; ++k) A[k] = T[(r * FX + k) * 16 + cc];
+    rfft72_inv(A, P);
+  }
+  lds_barrier();   // T becomes the epilogue staging [n1][x][16]
+  float* stg = reinterpret_cast<float*>(T);
+#pragma unroll
+  for (int x = 0; x < 64; ++x) stg[rq_stg(r, x, cc)] = P[x];
+  lds_barrier();
+  // the A epilogue (rk_segment<ROW_A>'s expression on the same 4-channel vectors): task (n1, x, 4 channels)
+  const float* vec = p.vecs;
+#pragma unroll 4
+  for (int k = 0; k < 8 * 64 * 4 / RQ_NT; ++k) {
+    const int t = k * RQ_NT + tid, g4 = t & 3, x = (t >> 2) & 63, rr = t >> 8;
+    const int y = 8 * rr + n2, c = c0 + 4 * g4;
+    if (y >= H || x >= W) continue;
+    float* sp = stg + rq_stg(rr, x, 4 * g4);
+    const f32x4 pv = *reinterpret_cast<const f32x4*>(sp);
+    const f32x4 lat = *reinterpret_cast<const f32x4*>(vec + V_LAT * 64 + c);
+    const f32x4 be = *reinterpret_cast<const f32x4*>(vec + V_BETA * 64 + c);
+    const f32x4 nu = *reinterpret_cast<const f32x4*>(vec + V_NU * 64 + c);
+    const f32x4 xv = map_ld4<false>(p.X, xx_index(b, c >> 3, y, x, c & 4, H, W));
+    const f32x4 ov = map_ld4<false>(p.O, oo_index(b, c >> 3, y, x, c & 4, H, W));
+    f32x4 iv;
+#pragma unroll
+    for (int qq = 0; qq < 2; ++qq) {
+      const f2v xx = pr2(xv, qq), o = pr2(ov, qq);
+      const f2v tt = ftanh2(-(pr2(be, qq) * o + pr2(nu, qq)) * (pr2(pv, qq) + pr2(lat, qq)) + xx);
+      iv[2 * qq] = tt[0];
+      iv[2 * qq + 1] = tt[1];
+    }
+    map_st4<false>(p.dst, ii_index(b, c >> 3, y, x, c & 4, H, W), iv);
+    *reinterpret_cast<f32x4*>(sp) = iv;
+  }
+  lds_barrier();
+  const bool live = 8 * r + n2 < H;
+#pragma unroll
+  for (int x = 0; x < 64; ++x) P[x] = (live && x < W) ? stg[rq_stg(r, x, cc)] : 0.f;
+  {
+    cpx X[FX];
+    rfft72_fwd(P, X);
+    lds_barrier();   // every thread has read its staged row
+#pragma unroll
+    for (int k = 0; k < FX; ++k) T[(r * FX + k) * 16 + cc] = X[k];
+  }
+  lds_barrier();
+  const int ts = opaque(tid);
+#pragma unroll
+  for (int it = 0; it < RQ_NIT; ++it) {
+    const int i = it * RQ_NT + ts;
+    if (i >= RQ_ITEMS) break;
+    const int fx = i >> 4, c = i & 15;
+    cpx u[9];
+#pragma unroll
+    for (int rr = 0; rr < 8; ++rr) u[rr] = T[(rr * FX + fx) * 16 + c];
+    u[8] = cpx{0.f, 0.f};
+    dft9<-1>(u);
+    const size_t dst = z_off(b, n2, fx, 0) + c0 + c;
+#pragma unroll
+    for (int k1 = 0; k1 < 9; ++k1) z_st<false, ZNT>(Z, dst + k1 * Z_K1, u[k1]);
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
 // column kernel (the spectral GEMM).  Block = (column class (fx, k1), 16 images), 256 threads, two
 // blocks per CU (68 KB of LDS).  Thread (image, channel pair a) holds channels 2a, 2a + 1 and
 // 32 + 2a, 33 + 2a of its image (each wave instruction reads / writes contiguous 256-B runs of Z) and
@@ -843,10 +951,26 @@ static bool row8_znt(bool bf, bool resident) {
   return v < 0 ? !bf && !resident : v != 0;
 }
 
+// MP_ROWQ_MAXB: batch slices up to this many images run row A as rowq_a_kernel (fp32; default 8)
+static int rowq_maxb() {
+  static const int v = [] {
+    const char* e = std::getenv("MP_ROWQ_MAXB");
+    return e ? std::atoi(e) : 8;
+  }();
+  return v;
+}
+
 hipError_t launch_row(int mode, void* Z, const ConvArgs& a, const void* or_x3, float or_us, const void* ir_x3,
                       float ir_us, const float* O0, int B, hipStream_t st, bool bf, bool resident) {
   if (B <= 0) return hipSuccess;
   if (a.H < 1 || a.H > 64 || (a.W != 32 && a.W != 64)) return hipErrorInvalidValue;
+  if (mode == ROW_A && !bf && B <= rowq_maxb()) {
+    if (row8_znt(false, resident))
+      hipLaunchKernelGGL(rowq_a_kernel<true>, dim3(B * 32), dim3(RQ_NT), 0, st, Z, a);
+    else
+      hipLaunchKernelGGL(rowq_a_kernel<false>, dim3(B * 32), dim3(RQ_NT), 0, st, Z, a);
+    return hipGetLastError();
+  }
   const dim3 g(B * 8), t(R8_NT);
 #define MP_ROW8(M, BFV)                                                                            \
   if (row8_znt(BFV, resident))                                                                             \

@@ -128,6 +128,11 @@ BITS_CASES = [
     ("pose80", "fp32_fft", "MP_BB_PIPE", ("0", "1"), {}),
     ("pose80", "fp32_fft", "MP_BB_STAGGER", ("0", "1"), {}),
     ("pose80", "bf16", "MP_BB_PIPE", ("0", "1"), {}),
+    # row A on channel quarters (rowq_a_kernel) or as row8_kernel<ROW_A>: one batch slice of 12, and
+    # two slices (64 + 16) all on rowq; and the cache policy of a cache-resident batch (12 crops)
+    ("pose12", "fp32_fft", "MP_ROWQ_MAXB", ("0", "16"), {}),
+    ("pose80", "fp32_fft", "MP_ROWQ_MAXB", ("0", "80"), {}),
+    ("pose12", "fp32_fft", "MP_ROW8_ZNT", ("0", "1"), {}),
 ]
 
 
