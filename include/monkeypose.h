@@ -283,7 +283,8 @@ int mp_crop3d_dev_ex(const mp_camera* cam, const float* frames, int64_t n, int64
                      double* Ms, double* coms_out, int32_t* status, void* stream);
 
 /* read a model property: "output_shape", "timesteps", "ssf", "finalized", "workspace_bytes",
- * "weight_bytes"; graph contexts also "graph_kernels" (kernel launches per forward),
+ * "weight_bytes", "fft_loop" (hGRU contexts: 4 = the four-step FFT loop, 6 = the six-launch FFT
+ * loop, 0 = a direct-convolution dtype, no FFT path); graph contexts also "graph_kernels" (kernel launches per forward),
  * "graph_streams" (streams the schedule uses), "graph_buffers" (activation buffers after concat placement), "graph_fused_pools" (2x2 max pools
  * computed inside their conv's kernel: MP_GRAPH_FUSE / MP_GRAPH_FUSE_POOL) -- as planned by the
  * last forward */

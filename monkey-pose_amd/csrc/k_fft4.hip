@@ -662,12 +662,119 @@ __device__ __forceinline__ f32x4 mfma16x16(f16x8 a, f16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
 
+// The three phases of one (class, 16-image group) item, shared by col8_kernel and col8p_kernel so
+// that both compute every output with the same operations in the same order (bit-identical).
+// Thread roles: DFT (image bl = tid / 32, channel pair a = tid % 32: channels 2a, 2a + 1); GEMM (wave
+// k2 = frequency fy = k1 + 9 k2, lane (kq, jj)).
+//
+// cg_forward: the thread's 8 row-class partials zin[n2] (channels 2a, 2a + 1) -> twiddle W72^{-n2 k1},
+// 8-point DFT over n2, scale + f16 hi / lo split into the S tile.  The split: v_pk_mul_f32,
+// v_cvt_pk_f16_f32 for hi and lo (round to nearest even, as (_Float16)), v_pk_add_f32 (re - hi is
+// exact).  Columns of images past B are not zeroed: an MFMA output column depends on its own S
+// column only, and theirs are never stored (col8p stores them: the same bytes as image B - 1's).
+__device__ __forceinline__ void cg_forward(const f32x4 (&zin)[8], int k1, uint4* tile, int cq, int hf, int bl) {
+  cpx s[2][8];
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+#pragma unroll
+    for (int n2 = 0; n2 < 8; ++n2) s[e][n2] = twid<-1>(cpx{zin[n2][2 * e], zin[n2][2 * e + 1]}, n2 * k1);
+    dft8_fold<-1>(s[e]);
+  }
+  typedef _Float16 h2 __attribute__((ext_vector_type(2)));
+  uint2* t2 = reinterpret_cast<uint2*>(tile);
+#pragma unroll
+  for (int k2 = 0; k2 < 8; ++k2) {
+    uint32_t hv[2], lv[2];
+#pragma unroll
+    for (int e = 0; e < 2; ++e) {
+      const cpx v = s[e][k2] * SPEC_SCALE;
+      const h2 hi = __builtin_convertvector(v, h2);
+      const h2 lo = __builtin_convertvector(v - __builtin_convertvector(hi, cpx), h2);
+      hv[e] = __builtin_bit_cast(uint32_t, hi);
+      lv[e] = __builtin_bit_cast(uint32_t, lo);
+    }
+    t2[cg_s(k2, cq, 0, bl) * 2 + hf] = uint2{hv[0], hv[1]};
+    t2[cg_s(k2, cq, 1, bl) * 2 + hf] = uint2{lv[0], lv[1]};
+  }
+}
+
+// cg_kstep: k-step t of wave k2's frequency, Y[b][co] = sum_ci S[b][ci] G[ci][co] (complex) as a real
+// 128 x 16 x 128 product on v_mfma_f32_16x16x32_f16 in the f16x3 split.  The compact weights A =
+// (gr, gi) pairs as stored; the S fragment supplies the two forms, (sr, -si) for the real rows
+// (gr sr - gi si) and (si, sr) for the imaginary rows (gr si + gi sr): a sign flip and a half swap per S
+// dword (16 VALU per k-step) instead of four weight forms (64).  w[mq][0 | 1] = the hi | lo planes.
+__device__ __forceinline__ void cg_kstep(const uint4* tile, int k2, int t, int kq, int jj, const uint4 (&w)[4][2],
+                                         f32x4 (&acc)[8]) {
+  const uint4 m = {0x80000000u, 0x80000000u, 0x80000000u, 0x80000000u};
+  const uint4 uh = tile[cg_s(k2, 4 * t + kq, 0, jj)], ul = tile[cg_s(k2, 4 * t + kq, 1, jj)];
+  const f16x8 sh = __builtin_bit_cast(f16x8, uh ^ m), sl = __builtin_bit_cast(f16x8, ul ^ m);
+  const f16x8 sh2 = __builtin_bit_cast(f16x8, (uh >> 16) | (uh << 16));
+  const f16x8 sl2 = __builtin_bit_cast(f16x8, (ul >> 16) | (ul << 16));
+#pragma unroll
+  for (int mq = 0; mq < 4; ++mq) {
+    const f16x8 ah = __builtin_bit_cast(f16x8, w[mq][0]), al = __builtin_bit_cast(f16x8, w[mq][1]);
+    acc[mq] = mfma16x16(al, sh, acc[mq]);
+    acc[mq] = mfma16x16(ah, sl, acc[mq]);
+    acc[mq] = mfma16x16(ah, sh, acc[mq]);
+    acc[4 + mq] = mfma16x16(al, sh2, acc[4 + mq]);
+    acc[4 + mq] = mfma16x16(ah, sl2, acc[4 + mq]);
+    acc[4 + mq] = mfma16x16(ah, sh2, acc[4 + mq]);
+  }
+}
+
+// weights of k-step t for wave k2 of class cls (both planes, the wave's four row blocks)
+__device__ __forceinline__ void cg_wload(const uint4* __restrict__ Gc, int cls, int k2, int t, int kq, int jj,
+                                         uint4 (&w)[4][2]) {
+  const uint4* gw = Gc + (size_t)(cls * 8 + k2) * 2 * 16 * 64;
+#pragma unroll
+  for (int mq = 0; mq < 4; ++mq) {
+    w[mq][0] = gw[(0 * 16 + 4 * t + kq) * 64 + 16 * mq + jj];
+    w[mq][1] = gw[(1 * 16 + 4 * t + kq) * 64 + 16 * mq + jj];
+  }
+}
+
+// the Y tile over the S tile's space: [image][cq][k2] (16-B units, pitch 16 * 8 * 2 + 1 per image)
+constexpr int CG_YP = 16 * 8 * 2 + 1;
+static_assert(CG_NI * CG_YP <= 2 * CG_HALF, "the Y tile fits the S tile's space");
+__device__ __forceinline__ void cg_ystore(uint4* tile, int k2, int kq, int jj, const f32x4 (&acc)[8], float unscale) {
+  f32x4* ytile = reinterpret_cast<f32x4*>(tile);
+#pragma unroll
+  for (int mq = 0; mq < 4; ++mq) {
+    const int cqo = 4 * mq + kq;
+    const f32x4 re = acc[mq], im = acc[4 + mq];
+    ytile[jj * CG_YP + (cqo * 8 + k2) * 2] = f32x4{re[0], im[0], re[1], im[1]} * unscale;
+    ytile[jj * CG_YP + (cqo * 8 + k2) * 2 + 1] = f32x4{re[2], im[2], re[3], im[3]} * unscale;
+  }
+}
+
+// cg_inverse: the thread's channels' 8 frequencies from the Y tile -> 8-point inverse DFT, twiddle
+// W72^{n2 k1} -> the row-class partials out[n2] (channels 2a, 2a + 1)
+__device__ __forceinline__ void cg_inverse(const uint4* tile, int k1, int cq, int hf, int bl, f32x4 (&out)[8]) {
+  const f32x4* ytile = reinterpret_cast<const f32x4*>(tile);
+  cpx yv[2][8];
+#pragma unroll
+  for (int q = 0; q < 8; ++q) {
+    const f32x4 pv = ytile[bl * CG_YP + (cq * 8 + q) * 2 + hf];
+    yv[0][q] = cpx{pv[0], pv[1]};
+    yv[1][q] = cpx{pv[2], pv[3]};
+  }
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+    dft8_fold<1>(yv[e]);
+#pragma unroll
+    for (int n2 = 0; n2 < 8; ++n2) yv[e][n2] = twid<1>(yv[e][n2], n2 * k1);
+  }
+#pragma unroll
+  for (int n2 = 0; n2 < 8; ++n2) out[n2] = f32x4{yv[0][n2].x, yv[0][n2].y, yv[1][n2].x, yv[1][n2].y};
+}
+
 // col8_kernel: 512 threads, thread = image x channel pair (one contiguous 512-B run of Z per image
 // and n2 per wave instruction pair) for the DFTs and the split; each wave computes ONE frequency
 // (k2 = wave).  Two blocks per CU (16 waves) leave 128 VGPRs per wave.  Round 5 also measured a
 // four-wave form (two frequencies per wave behind a weight reload: 0.212 vs 0.192 ms at B = 256) and
 // a persistent form holding each wave's weights in registers over several image groups, one block
-// per CU (0.207 ms; batch-1 forward 1.06 vs 0.98 ms): both removed.
+// per CU (0.207 ms; batch-1 forward 1.06 vs 0.98 ms): both removed.  Large batches run col8p_kernel
+// (below), the same arithmetic with the next item's partials in flight during this one's GEMM.
 // ZNT: the partials Z read and written non-temporal (the weights, re-read by the other batch slice's
 // launch of the same convolution, keep the cache)
 template <bool ZNT>
@@ -690,14 +797,6 @@ __global__ __launch_bounds__(512, 2) void col8_kernel(cpx* __restrict__ Z, const
   // 0.185 ms against loading steps 2 and 3 together after step 1; profiles/r5l).  Requesting step 0's
   // weights before the partials measured slower (8.27 -> 8.33 ms per forward; profiles/r5o)
   uint4 wr[2][4][2];
-  const uint4* gw = Gc + (size_t)(cls * 8 + k2) * 2 * 16 * 64;
-  auto load_1 = [&](int slot, int t) {
-#pragma unroll
-    for (int mq = 0; mq < 4; ++mq) {
-      wr[slot][mq][0] = gw[(0 * 16 + 4 * t + kq) * 64 + 16 * mq + jj];
-      wr[slot][mq][1] = gw[(1 * 16 + 4 * t + kq) * 64 + 16 * mq + jj];
-    }
-  };
   {
     f32x4 zin[8];
 #pragma unroll
@@ -705,93 +804,148 @@ __global__ __launch_bounds__(512, 2) void col8_kernel(cpx* __restrict__ Z, const
       const f32x4* zp = reinterpret_cast<const f32x4*>(Z + z_off(b, n2, fx, k1)) + a;
       zin[n2] = ZNT ? __builtin_nontemporal_load(zp) : *zp;
     }
-    cpx s[2][8];
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-#pragma unroll
-      for (int n2 = 0; n2 < 8; ++n2) s[e][n2] = twid<-1>(cpx{zin[n2][2 * e], zin[n2][2 * e + 1]}, n2 * k1);
-      dft8_fold<-1>(s[e]);
-    }
-    // the f16 hi / lo split of each (re, im) pair: v_pk_mul_f32, v_cvt_pk_f16_f32 for hi and lo (round to
-    // nearest even, as (_Float16)), v_pk_add_f32 (re - hi is exact).  Columns of images past B are not
-    // zeroed: an MFMA output column depends on its own S column only, and theirs are never stored.
-    typedef _Float16 h2 __attribute__((ext_vector_type(2)));
-    uint2* t2 = reinterpret_cast<uint2*>(tile);
-#pragma unroll
-    for (int k2 = 0; k2 < 8; ++k2) {
-      uint32_t hv[2], lv[2];
-#pragma unroll
-      for (int e = 0; e < 2; ++e) {
-        const cpx v = s[e][k2] * SPEC_SCALE;
-        const h2 hi = __builtin_convertvector(v, h2);
-        const h2 lo = __builtin_convertvector(v - __builtin_convertvector(hi, cpx), h2);
-        hv[e] = __builtin_bit_cast(uint32_t, hi);
-        lv[e] = __builtin_bit_cast(uint32_t, lo);
-      }
-      t2[cg_s(k2, cq, 0, bl) * 2 + hf] = uint2{hv[0], hv[1]};
-      t2[cg_s(k2, cq, 1, bl) * 2 + hf] = uint2{lv[0], lv[1]};
-    }
+    cg_forward(zin, k1, tile, cq, hf, bl);
   }
-  load_1(0, 0);
-  load_1(1, 1);
+  cg_wload(Gc, cls, k2, 0, kq, jj, wr[0]);
+  cg_wload(Gc, cls, k2, 1, kq, jj, wr[1]);
   lds_barrier();
-  // the compact weights A = (gr, gi) pairs as stored; the S fragment supplies the two forms, (sr, -si)
-  // for the real rows (gr sr - gi si) and (si, sr) for the imaginary rows (gr si + gi sr): a sign flip
-  // and a half swap per S dword (16 VALU per k-step) instead of four weight forms (64)
-  const uint4 m = {0x80000000u, 0x80000000u, 0x80000000u, 0x80000000u};
   f32x4 acc[8] = {};
 #pragma unroll
   for (int t = 0; t < 4; ++t) {
-    const uint4 uh = tile[cg_s(k2, 4 * t + kq, 0, jj)], ul = tile[cg_s(k2, 4 * t + kq, 1, jj)];
-    const f16x8 sh = __builtin_bit_cast(f16x8, uh ^ m), sl = __builtin_bit_cast(f16x8, ul ^ m);
-    const f16x8 sh2 = __builtin_bit_cast(f16x8, (uh >> 16) | (uh << 16));
-    const f16x8 sl2 = __builtin_bit_cast(f16x8, (ul >> 16) | (ul << 16));
-#pragma unroll
-    for (int mq = 0; mq < 4; ++mq) {
-      const f16x8 ah = __builtin_bit_cast(f16x8, wr[t % 2][mq][0]), al = __builtin_bit_cast(f16x8, wr[t % 2][mq][1]);
-      acc[mq] = mfma16x16(al, sh, acc[mq]);
-      acc[mq] = mfma16x16(ah, sl, acc[mq]);
-      acc[mq] = mfma16x16(ah, sh, acc[mq]);
-      acc[4 + mq] = mfma16x16(al, sh2, acc[4 + mq]);
-      acc[4 + mq] = mfma16x16(ah, sl2, acc[4 + mq]);
-      acc[4 + mq] = mfma16x16(ah, sh2, acc[4 + mq]);
-    }
-    if (t + 2 < 4) load_1(t % 2, t + 2);
+    cg_kstep(tile, k2, t, kq, jj, wr[t % 2], acc);
+    if (t + 2 < 4) cg_wload(Gc, cls, k2, t + 2, kq, jj, wr[t % 2]);
   }
   lds_barrier();   // every wave has read the S tile
-  // Y tile over the whole S tile: [image][cq][k2] (16-B units, pitch 16 * 8 * 2 + 1 per image)
-  constexpr int YLD = 16 * 8 * 2 + 1;
-  static_assert(CG_NI * YLD <= 2 * CG_HALF, "the Y tile fits the S tile's space");
-  f32x4* ytile = reinterpret_cast<f32x4*>(tile);
-#pragma unroll
-  for (int mq = 0; mq < 4; ++mq) {
-    const int cqo = 4 * mq + kq;
-    const f32x4 re = acc[mq], im = acc[4 + mq];
-    ytile[jj * YLD + (cqo * 8 + k2) * 2] = f32x4{re[0], im[0], re[1], im[1]} * unscale;
-    ytile[jj * YLD + (cqo * 8 + k2) * 2 + 1] = f32x4{re[2], im[2], re[3], im[3]} * unscale;
-  }
+  cg_ystore(tile, k2, kq, jj, acc, unscale);
   lds_barrier();
-  cpx yv[2][8];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const f32x4 pv = ytile[bl * YLD + (cq * 8 + q) * 2 + hf];
-    yv[0][q] = cpx{pv[0], pv[1]};
-    yv[1][q] = cpx{pv[2], pv[3]};
-  }
-#pragma unroll
-  for (int e = 0; e < 2; ++e) {
-    dft8_fold<1>(yv[e]);
-#pragma unroll
-    for (int n2 = 0; n2 < 8; ++n2) yv[e][n2] = twid<1>(yv[e][n2], n2 * k1);
-  }
+  f32x4 out[8];
+  cg_inverse(tile, k1, cq, hf, bl, out);
   if (live) {
 #pragma unroll
-    for (int n2 = 0; n2 < 8; ++n2)
-    {
+    for (int n2 = 0; n2 < 8; ++n2) {
       f32x4* zp = reinterpret_cast<f32x4*>(Z + z_off(b, n2, fx, k1)) + a;
-      const f32x4 v = f32x4{yv[0][n2].x, yv[0][n2].y, yv[1][n2].x, yv[1][n2].y};
-      if constexpr (ZNT) __builtin_nontemporal_store(v, zp);
-      else *zp = v;
+      if constexpr (ZNT) __builtin_nontemporal_store(out[n2], zp);
+      else *zp = out[n2];
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+// col8p_kernel: col8_kernel's items (class, 16-image group) with the HBM stream kept busy.  col8_kernel
+// runs each block's phases in series -- load the partials, DFT, GEMM, inverse DFT, store -- so with two
+// blocks per CU the partials stream idles while both are past their loads (waves parked 46 % of their
+// cycles, 0.53 of 8 TB/s).  Here a block (one per CU, 512 threads) walks a contiguous range of items and
+// keeps the NEXT item's 64 KiB of partials in flight during the current one's work: they go straight
+// into the second of two LDS slots by LDS-DMA (global_load_lds_dwordx4, 1 KiB per wave instruction, no
+// registers), and each slot serves an item as raw partials -> S tile -> Y tile in turn.  A wave's
+// weights (its frequency's 4 k-steps, 128 VGPRs) stay in registers while the range stays in one class
+// (an item range spans at most two or three classes), so no vector-memory load is waited for between
+// the DMA's issue and its use: vmcnt counts loads, stores and LDS-DMA together in issue order, and a
+// wait for a younger load would drain the prefetch.  The item math is cg_forward / cg_kstep /
+// cg_ystore / cg_inverse, as in col8_kernel: bit-identical outputs.
+// ---------------------------------------------------------------------------------------------
+constexpr int CP_SLOT = 2 * CG_HALF;                 // uint4 per LDS slot (69,632 B)
+static_assert(CG_NI * 8 * 64 * 8 <= CP_SLOT * 16, "an item's raw partials fit a slot");
+static_assert(ZLAYOUT == 1, "col8p DMA: an image's 8 row classes are one contiguous 4-KiB run of Z");
+
+// one LDS-DMA wave instruction: 64 lanes x 16 B from each lane's gsrc to LDS bytes [lds, lds + 1024)
+// (M0 = the wave-uniform LDS base, written and restored in the same statement)
+__device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds) {
+  unsigned keep;
+  asm volatile("s_mov_b32 %0, m0\n\ts_mov_b32 m0, %2\n\ts_nop 0\n\tglobal_load_lds_dwordx4 %1, off\n\ts_mov_b32 m0, %0"
+               : "=&s"(keep)
+               : "v"(gsrc), "s"(lds)
+               : "memory");
+}
+
+template <bool ZNT>
+__global__ __launch_bounds__(512, 1) void col8p_kernel(cpx* __restrict__ Z, const uint4* __restrict__ Gc, int B,
+                                                       int ngrp, int nitems, float unscale) {
+  __shared__ uint4 slots[2 * CP_SLOT];   // 139,264 B
+  // consecutive item ranges on one XCD (blockIdx % 8 under round-robin dispatch; a speed choice only):
+  // a class's weights are then read by one L2
+  const int nblk = gridDim.x, per = nblk / 8, r8 = nblk % 8, xg = blockIdx.x % 8, q = blockIdx.x / 8;
+  const int v = (xg < r8 ? xg * (per + 1) : r8 * (per + 1) + (xg - r8) * per) + q;
+  const int it0 = (int)((int64_t)v * nitems / nblk), it1 = (int)((int64_t)(v + 1) * nitems / nblk);
+  if (it0 >= it1) return;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int bl = tid >> 5, a = tid & 31, cq = a >> 1, hf = a & 1;
+  const int kq = lane >> 4, jj = lane & 15, k2 = wv;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)slots;
+  // item it -> slot s: wave wv moves images 2 wv, 2 wv + 1 of the group (four 1-KiB quarters each)
+  auto dma = [&](int it, int s) {
+    const int cls = it / ngrp, grp = it - cls * ngrp;
+    const int fx = cls / 9, k1 = cls - fx * 9;
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int il = 2 * wv + (i >> 2);
+      const int b = min(grp * CG_NI + il, B - 1);
+      const char* src = reinterpret_cast<const char*>(Z + z_off(b, 0, fx, k1)) + (i & 3) * 1024 + lane * 16;
+      const uint32_t dst = lds0 + (uint32_t)(s * CP_SLOT * 16 + il * 4096 + (i & 3) * 1024);
+      glds16(src, __builtin_amdgcn_readfirstlane(dst));
+    }
+  };
+  // the weight loads are waited for where they are issued (s_waitcnt vmcnt(0) through the builtin, so
+  // hipcc's wait bookkeeping sees them complete): otherwise every item's GEMM would carry hipcc's waits
+  // for them, which in issue order also wait for the next item's DMA
+  constexpr unsigned VMCNT0 = 0x0F70;   // vmcnt(0) expcnt(7) lgkmcnt(15)
+  uint4 w[4][4][2];
+  int wcls = it0 / ngrp;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) cg_wload(Gc, wcls, k2, t, kq, jj, w[t]);
+  __builtin_amdgcn_s_waitcnt(VMCNT0);
+  dma(it0, 0);
+  if (it0 + 1 < it1) dma(it0 + 1, 1);
+  for (int it = it0; it < it1; ++it) {
+    const int s = (it - it0) & 1;
+    uint4* tile = slots + s * CP_SLOT;
+    const int cls = it / ngrp, grp = it - cls * ngrp;
+    const int fx = cls / 9, k1 = cls - fx * 9;
+    // this item's DMA is older than: the previous item's 8 stores and the next item's 8 DMA pieces
+    // (and a class change's weight loads, which only make the wait longer)
+    if (it + 1 < it1) {
+      if (it == it0) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
+    } else {
+      if (it == it0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    }
+    lds_barrier();   // every wave's pieces have landed
+    {
+      f32x4 zin[8];
+      const f32x4* raw = reinterpret_cast<const f32x4*>(tile) + bl * 256 + a;   // [image][n2][64 complex]
+#pragma unroll
+      for (int n2 = 0; n2 < 8; ++n2) zin[n2] = raw[n2 * 32];
+      lds_barrier();   // the raw partials are read: the slot becomes the S tile
+      cg_forward(zin, k1, tile, cq, hf, bl);
+    }
+    if (cls != wcls) {   // block-uniform
+      wcls = cls;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) cg_wload(Gc, wcls, k2, t, kq, jj, w[t]);
+      __builtin_amdgcn_s_waitcnt(VMCNT0);
+    }
+    lds_barrier();
+    f32x4 acc[8] = {};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) cg_kstep(tile, k2, t, kq, jj, w[t], acc);
+    lds_barrier();   // every wave has read the S tile
+    cg_ystore(tile, k2, kq, jj, acc, unscale);
+    lds_barrier();
+    f32x4 out[8];
+    cg_inverse(tile, k1, cq, hf, bl, out);
+    // images past B (a partial last group) store image B - 1's values over it: the same bytes, since
+    // their DMA read image B - 1 too -- every item issues exactly 8 stores, as the counted waits assume
+    const int b = min(grp * CG_NI + bl, B - 1);
+#pragma unroll
+    for (int n2 = 0; n2 < 8; ++n2) {
+      f32x4* zp = reinterpret_cast<f32x4*>(Z + z_off(b, n2, fx, k1)) + a;
+      if constexpr (ZNT) __builtin_nontemporal_store(out[n2], zp);
+      else *zp = out[n2];
+    }
+    if (it + 2 < it1) {
+      lds_barrier();   // every thread has read its Y values: the slot takes item it + 2
+      dma(it + 2, s);
     }
   }
 }
@@ -919,9 +1073,40 @@ static bool col8_znt(bool bf, bool resident) {
   return v < 0 ? !bf && !resident : v != 0;
 }
 
+// MP_COL8P: slices of at least this many images run col8p_kernel (fp32; 0 = never); MP_COL8P_BLOCKS:
+// its grid (default: one block per CU)
+static int col8p_minb() {
+  static const int v = [] {
+    const char* e = std::getenv("MP_COL8P");
+    return e ? std::atoi(e) : 64;
+  }();
+  return v;
+}
+static int col8p_blocks() {
+  static const int v = [] {
+    const char* e = std::getenv("MP_COL8P_BLOCKS");
+    if (e) return std::max(1, std::atoi(e));
+    int dev = 0, ncu = 0;
+    if (hipGetDevice(&dev) != hipSuccess || hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      return 256;
+    return std::max(1, ncu);
+  }();
+  return v;
+}
+
 hipError_t launch_col_gemm(void* Z, const void* Gc, int B, float unscale, hipStream_t st, bool bf, bool resident) {
   if (B <= 0) return hipSuccess;
   const int ngrp = (B + CG_NI - 1) / CG_NI;
+  if (!bf && col8p_minb() > 0 && B >= col8p_minb()) {
+    const int nitems = Z_CLS * ngrp, nblk = std::min(nitems, col8p_blocks());
+    if (col8_znt(false, resident))
+      hipLaunchKernelGGL((col8p_kernel<true>), dim3(nblk), dim3(512), 0, st, static_cast<cpx*>(Z),
+                         static_cast<const uint4*>(Gc), B, ngrp, nitems, unscale);
+    else
+      hipLaunchKernelGGL((col8p_kernel<false>), dim3(nblk), dim3(512), 0, st, static_cast<cpx*>(Z),
+                         static_cast<const uint4*>(Gc), B, ngrp, nitems, unscale);
+    return hipGetLastError();
+  }
   if (bf) {
 #define MP_COL8B(N)                                                                                          \
   hipLaunchKernelGGL((col8_bf_kernel<N>), dim3(CG_NC8 * 8 * ngrp), dim3(512), 0, st, Z, static_cast<const uint4*>(Gc), \

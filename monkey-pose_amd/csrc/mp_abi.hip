@@ -97,6 +97,7 @@ void finalize_circuit(mp_ctx* c, const std::vector<float>* outs, const std::vect
     fail(MP_ERR_WEIGHT, "contextual_circuit/p_r must be [S,S,64,64] with S in {3,5,15}");
   c->ssf = (int)ps[0];
   c->p_pk.alloc((size_t)8 * c->ssf * c->ssf * 2 * 64 * 16);
+  c->fft4 = false;
   if (c->dtype == MP_DTYPE_F32_SPLIT) {
     pack_x3(it->second, c->p_pk, c->ssf, 1024.0f, &c->p_unscale, "pack p_r (f16x3)");
   } else if (is_fft(c->dtype)) {
@@ -203,11 +204,15 @@ void ensure_ws(mp_ctx* c, int64_t n, int64_t H, int64_t W) {
   c->X.alloc(st);
   c->O.alloc(st);
   c->I.alloc(st);
-  c->Og.alloc(st);
+  // the four-step loop (k_fft4.hip) keeps the gated state and P1 / P2 on chip and updates one
+  // spectrum-sized buffer Z (specS) in place: Og, specY and specP are six-launch-loop buffers only
+  if (!c->fft4) c->Og.alloc(st);
   if (is_fft(c->dtype)) {
     c->specS.alloc(fft_spec_bytes((int)nb));
-    c->specY.alloc(fft_spec_bytes((int)nb));
-    c->specP.alloc(st);
+    if (!c->fft4) {
+      c->specY.alloc(fft_spec_bytes((int)nb));
+      c->specP.alloc(st);
+    }
   }
   if (c->model == MP_MODEL_HGRU_POSE) {
     c->bufA.alloc(st);
@@ -904,8 +909,9 @@ int pose_fwd(mp_ctx* ctx, const float* depth, int64_t n, int64_t h, int64_t w, c
                 "conv_3");
     };
     // the backbone runs per batch slice on the slice's stream (MP_BB_PIPE) unless a tap needs its
-    // intermediate maps; otherwise whole-batch on the caller's stream first
-    const bool bb_pipe = bb_pipeline() && !tp.pool1 && !tp.conv2 && !tp.conv3;
+    // intermediate maps or hidden_init = identity needs X (O0 = X) before the loop; otherwise
+    // whole-batch on the caller's stream first
+    const bool bb_pipe = bb_pipeline() && !tp.pool1 && !tp.conv2 && !tp.conv3 && fo.hidden_init != MP_HIDDEN_IDENTITY;
     if (!bb_pipe) backbone(0, N, st);
     if (tp.pool1) hip_check(launch_c8_to_nhwc(ctx->bufA.f(), tp.pool1, N, H, W, st), "pool1 tap");
     if (tp.conv2) hip_check(launch_c8_to_nhwc(ctx->bufB.f(), tp.conv2, N, H, W, st), "conv2 tap");

@@ -106,12 +106,18 @@ if kind == "dense":
     out = model.build(torch.from_numpy(depth).cuda(), 69, train_mode=False).cpu().numpy()
 else:   # 12 crops: above the small-batch FFT kernels' B <= 8; pose80: three 32-image GEMM groups,
         # two hGRU slices (64 + 16 crops)
-    wts, depth, O0 = MG.pose_inputs(80 if kind == "pose80" else 12, 64, 8, 5, 6, 7)
+    wts, depth, O0 = MG.pose_inputs(12 if kind == "pose12" else 80, 64, 8, 5, 6, 7)
     model = P.hgru_pose.model()
     model.compute_dtype = dtype
     model.load_weights(wts)
-    out = model.build(torch.from_numpy(depth).cuda(), 69, train_mode=False,
-                      h2_init=torch.from_numpy(O0).cuda()).cpu().numpy()
+    if kind == "pose80id":   # O0 = X of this call, after a forward on other crops in the same context
+        model.build(torch.from_numpy(np.ascontiguousarray(depth[::-1])).cuda(), 69, train_mode=False,
+                    h2_init=torch.from_numpy(O0).cuda())
+        model.aux["hidden_init"] = "identity"
+        out = model.build(torch.from_numpy(depth).cuda(), 69, train_mode=False).cpu().numpy()
+    else:
+        out = model.build(torch.from_numpy(depth).cuda(), 69, train_mode=False,
+                          h2_init=torch.from_numpy(O0).cuda()).cpu().numpy()
 print(json.dumps({{"sha": hashlib.sha256(np.ascontiguousarray(out).tobytes()).hexdigest()}}))
 """
 
@@ -128,6 +134,12 @@ BITS_CASES = [
     ("pose80", "fp32_fft", "MP_BB_PIPE", ("0", "1"), {}),
     ("pose80", "fp32_fft", "MP_BB_STAGGER", ("0", "1"), {}),
     ("pose80", "bf16", "MP_BB_PIPE", ("0", "1"), {}),
+    # hidden_init = identity (O0 = X) keeps the whole-batch backbone first under either setting
+    ("pose80id", "fp32_fft", "MP_BB_PIPE", ("0", "1"), {}),
+    # the persistent column kernel (col8p_kernel, slices of >= MP_COL8P images) or col8_kernel: the
+    # same item arithmetic (64 + 16: col8p on the first slice only at 64; on both at 1)
+    ("pose80", "fp32_fft", "MP_COL8P", ("0", "64", "1"), {}),
+    ("pose12", "fp32_fft", "MP_COL8P", ("0", "1"), {}),
     # row A on channel quarters (rowq_a_kernel) or as row8_kernel<ROW_A>: one batch slice of 12, and
     # two slices (64 + 16) all on rowq; and the cache policy of a cache-resident batch (12 crops)
     ("pose12", "fp32_fft", "MP_ROWQ_MAXB", ("0", "16"), {}),

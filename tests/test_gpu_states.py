@@ -11,7 +11,7 @@ batch-1 runs."""
 import numpy as np
 import pytest
 
-from helpers import BF16_STATE_REL_TOL, FP32_REL_TOL, HGRU_POSE_AUX, MG, golden_meta, pkg, rel_inf
+from helpers import BF16_REL_TOL, BF16_STATE_REL_TOL, FP32_REL_TOL, HGRU_POSE_AUX, MG, golden_meta, pkg, rel_inf
 
 pytestmark = pytest.mark.gpu
 
@@ -114,6 +114,28 @@ def test_pose_hidden_init(hidden_init, dtype):
     assert rel_inf(m.states_O[:, 0].cpu().numpy(), inter["hgru_steps"][0]) <= FP32_REL_TOL
     with pytest.raises(ValueError):
         m.forward(_cuda(depth), h2_init=_cuda(np.zeros((2, 32, 32, 64))))
+
+
+@pytest.mark.parametrize("n", [2, 80])
+@pytest.mark.parametrize("dtype", ["fp32_fft", "bf16"])
+def test_pose_identity_after_other_forward(dtype, n):
+    """hidden_init='identity' sets O0 = X (hgru_module.py:888-892), so the backbone of THIS call has
+    to run before the loop starts: one context runs a forward on depth A first, then an identity
+    forward on depth B, which must match the oracle on B (80 crops: two batch slices on two
+    streams, the per-slice backbone schedule)."""
+    from oracle import hgru_ref as R
+    mp = pkg()
+    W = mp.weights
+    m, wts = _pose_ctx(dtype, crop=64)
+    a = W.synth_crops(n, seed=1, size=64)
+    b = W.synth_crops(n, seed=2, size=64)
+    m.build(_cuda(a), 69, h2_init=_cuda(W.synth_hidden((n, 32, 32, 64), seed=3)))
+    m.aux["hidden_init"] = "identity"
+    out = m.build(_cuda(b), 69).cpu().numpy()
+    k = [0, n - 1]
+    ref = R.hgru_pose_forward(b[k], wts, None, 8, np.float64, hidden_init="identity")
+    tol = BF16_REL_TOL if dtype == "bf16" else FP32_REL_TOL
+    assert rel_inf(out[k], ref) <= tol
 
 
 def test_pose_rejects_unknown_hidden_init_and_aux_store_states():
