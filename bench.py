@@ -120,8 +120,9 @@ def fft_kernels(ctx, B, hw, steps, bf16=False):
 # per-kernel HBM bytes per launch from rocprofv3 PMC passes (FETCH_SIZE x2 on gfx950 + WRITE_SIZE,
 # MI355X_MICROARCH.md), collected with the full-batch single-stream launches of this workload by
 # tools/pmc_bytes.py and committed under profiles/ (bench cannot profile itself)
-PMC_TRAFFIC = {False: "profiles/r5fin/pmc_traffic_fp32_b256.csv",
-               True: "profiles/r5fin/pmc_traffic_bf16_b256.csv"}
+PROFILE_DIR = "profiles/r6"
+PMC_TRAFFIC = {False: PROFILE_DIR + "/pmc_traffic_fp32_b256.csv",
+               True: PROFILE_DIR + "/pmc_traffic_bf16_b256.csv"}
 PMC_KERNEL = {   # name: (fp32 path's kernel, bf16 path's kernel) as rocprofv3 names them
     "fft_fwd": ("fft_fwd3_kernel", "fft_fwd_kernel<true, true>"),
     "spec_gemm": ("spec_gemm_kernel<0, 32>", "spec_gemm_bf_kernel"),
@@ -130,7 +131,7 @@ PMC_KERNEL = {   # name: (fp32 path's kernel, bf16 path's kernel) as rocprofv3 n
     "epi_b": ("spec_epi_b_kernel<false, false, false>", "spec_epi_b_kernel<true, true, false>"),
     # the four-step loop's default kernels (k_fft4.hip: col8 / row8 forms)
     # (prefixes: the template arguments after the dtype flag are cache-policy switches)
-    "col_gemm": ("col8_kernel", "col8_bf_kernel"), "row_a": ("row8_kernel<0, false", "row8_kernel<0, true"),
+    "col_gemm": ("col8p_kernel", "col8_bf_kernel"), "row_a": ("row8_kernel<0, false", "row8_kernel<0, true"),
     "row_b": ("row8_kernel<1, false", "row8_kernel<1, true"),
     "row_final": ("row8_kernel<2, false", "row8_kernel<2, true"),
     "row_init": ("row8_kernel<3, false", "row8_kernel<3, true")}
@@ -138,12 +139,42 @@ PMC_KERNEL = {   # name: (fp32 path's kernel, bf16 path's kernel) as rocprofv3 n
 
 # MFMA utilisation per kernel from the committed PMC pass (tools/pmc_mfma.sh / .py: SQ_VALU_MFMA_BUSY_CYCLES
 # over GRBM_GUI_ACTIVE x 1024 SIMDs, the gfx950 MfmaUtil), same one-stream B = 256 workload
-PMC_MFMA = "profiles/r5fin/mfma_util_pose_fp32_b256.csv"
-MFMA_KERNELS = {"col8 (four-step spectral GEMM, k_fft4.hip)": "col8_kernel",
+PMC_MFMA = PROFILE_DIR + "/mfma_util_pose_fp32_b256.csv"
+MFMA_KERNELS = {"col8p (four-step spectral GEMM, k_fft4.hip)": "col8p_kernel",
                 "row8 B (gate GEMMs, k_fft4.hip)": "row8_kernel<1, false",
                 "fc_gemm_x3p (fc_1 on split planes, k_fc.hip)": "fc_gemm_x3p_kernel", "conv64x3 (conv_2/3, k_conv64x3.hip)": "conv64x3_kernel",
                 "spec_gemm (k_fft.hip)": "spec_gemm_kernel", "spec_epi_b (gate GEMMs, k_fft.hip)": "spec_epi_b_kernel<false, false, false>",
                 "gate_init_x3 (k_fft.hip)": "gate_init_x3_kernel"}
+
+
+def tree_stamp():
+    """sha256 (16 hex digits) of the native sources libmonkeypose.so is built from (csrc/*.hip, *.hpp,
+    the Makefile, include/monkeypose.h): which kernels a profile or a bench line was measured on."""
+    import hashlib
+    h = hashlib.sha256()
+    csrc = os.path.join(ROOT, "monkey-pose_amd", "csrc")
+    files = sorted(f for f in os.listdir(csrc) if f.endswith((".hip", ".hpp")) or f == "Makefile")
+    for f in files + ["../../include/monkeypose.h"]:
+        with open(os.path.join(csrc, f), "rb") as fh:
+            h.update(f.encode() + b"\0" + fh.read())
+    return h.hexdigest()[:16]
+
+
+def profile_stamp():
+    """The STAMP.json of the committed profile directory the roofline's PMC figures come from (git
+    head and source hash of the tree they were collected on; tools/stamp_tree.py), with whether its
+    source hash equals this tree's."""
+    path = os.path.join(ROOT, PROFILE_DIR, "STAMP.json")
+    if not os.path.exists(path):
+        return {"dir": PROFILE_DIR, "stamp": None, "matches_this_tree": False}
+    st = json.load(open(path))
+    cur = tree_stamp()
+    ok = st.get("src_sha") == cur
+    if not ok:
+        sys.stderr.write(f"bench.py: WARNING the PMC figures in {PROFILE_DIR} were collected on sources "
+                         f"{st.get('src_sha')} (git {st.get('git_head')}), this tree is {cur}\n")
+    return {"dir": PROFILE_DIR, "git_head": st.get("git_head"), "src_sha": st.get("src_sha"),
+            "this_tree_src_sha": cur, "matches_this_tree": ok}
 
 
 def pmc_mfma_busy():
@@ -162,7 +193,7 @@ def pmc_mfma_busy():
     return {"source": PMC_MFMA, "mfma_busy": out}
 
 
-PMC_FORWARD = "profiles/r5fin/pmc_forward_bytes.json"
+PMC_FORWARD = PROFILE_DIR + "/pmc_forward_bytes.json"
 
 
 def pmc_forward_bytes(dtype, batch):
@@ -379,6 +410,48 @@ def extras(mp, dev, args):
     except Exception as e:  # noqa: BLE001
         out["attn_b256"] = {"error": repr(e)}
     return out
+
+
+def bf16_leg(mp, dev, wts, depth, o0, T, hbm_meas, steps=20):
+    """BASELINE config 4's dtype at the headline's per-GPU batch: the same crops and weights through a
+    bf16 context (bf16 spectra / maps / GEMM operands, fp32 accumulation and FFTs), timed like the
+    headline (default streams), with its own per-kernel profile and roofline, and its parity against
+    the float64 oracle on 2 crops under the stated bf16 gate."""
+    import torch
+    from oracle import hgru_ref as R
+    B = depth.shape[0]
+    ctx = mp._lib.Context(mp._lib.MP_MODEL_HGRU_POSE, dev.index)
+    for k, v in wts.items():
+        ctx.set_weight(k, v)
+    ctx.finalize(mp._lib.MP_DTYPE_BF16)
+    ctx.reserve(B)
+    out = torch.empty((B, 69), dtype=torch.float32, device=dev)
+    stream = mp._lib.current_stream(dev)
+    t = time_gpu(lambda: ctx.pose_fwd(depth, o0, out, stream), steps, 3)
+    got = out[:2].cpu().numpy().astype(np.float64)
+    prof_steps = 5
+    ctx.profile(True)
+    for _ in range(prof_steps):
+        ctx.pose_fwd(depth, o0, out, stream)
+    torch.cuda.synchronize()
+    ctx.profile(False)
+    px = (depth.shape[1] // 2) ** 2
+    kern = fft_kernels(ctx, B, px, prof_steps, True)
+    ms_fc, nfc = ctx.profile_read("fc1")
+    ms_bb, nbb = ctx.profile_read("backbone")
+    ms_fo, nfo = ctx.profile_read("fc_out")
+    ctx.close()
+    r64 = R.hgru_pose_forward(depth[:2].cpu().numpy(), wts, o0[:2].cpu().numpy(), T, np.float64)
+    err = float(np.abs(got - r64).max() / np.abs(r64).max())
+    one_stream = sum(k["ms_per_step"] for k in kern.values()) + (ms_fc + ms_bb + ms_fo) / prof_steps
+    return {"crops_per_s": round(B / t, 2), "ms_per_step": round(t * 1e3, 3), "batch": B, "steps": steps,
+            "dtype": "bf16 (bf16 spectra and hGRU maps, bf16 spectral / gate GEMMs, fp32 accumulate, fp32 FFTs "
+                     "and elementwise math)",
+            "roofline": fft_roofline(kern, True, B, hbm_meas), "fft_kernels": kern,
+            "one_stream_kernel_sum_ms": round(one_stream, 3),
+            "note": "ms_per_step runs two batch slices on two streams; one_stream_kernel_sum_ms is the "
+                    "profiled single-stream sum of every kernel (FFT loop + fc_1 + fc_out + backbone)",
+            "parity": {"rel_inf_err_fp64_oracle": err, "crops": 2, "gate": BF16_REL_TOL, "ok": err <= BF16_REL_TOL}}
 
 
 ATTN_GFLOP = 3.5421   # per frame: 5 convs at 128/64/32/16/8 px (one 5x5) + afc_1 (bench docstring)
@@ -725,6 +798,9 @@ def main():
     }
     if other:
         rec["other_scaling_row"] = other
+    rec["src_sha"] = tree_stamp()
+    if fft:
+        rec["roofline"]["traffic_stamp"] = profile_stamp()
     if args.dtype == "f32_fft":
         mb = pmc_mfma_busy()
         if mb:
@@ -745,10 +821,16 @@ def main():
             rec.update(cpu_baseline(depth, o0, out, wts, T, args))
         if not args.no_extras:
             head_rate = value
+            rec["extras"] = {}
+            if args.dtype == "f32_fft":
+                try:   # config 4's dtype (bf16) on the same crops at the same per-GPU batch
+                    rec["extras"]["bf16_b256"] = bf16_leg(mp, dev, wts, depth, o0, T, hbm_meas)
+                except Exception as e:  # noqa: BLE001
+                    rec["extras"]["bf16_b256"] = {"error": repr(e)}
             try:
-                rec["extras"] = {"e2e_batch1_latency": e2e_latency(mp, ctx, dev, T, wts, args.dtype)}
+                rec["extras"]["e2e_batch1_latency"] = e2e_latency(mp, ctx, dev, T, wts, args.dtype)
             except Exception as e:  # noqa: BLE001
-                rec["extras"] = {"e2e_batch1_latency": {"error": repr(e)}}
+                rec["extras"]["e2e_batch1_latency"] = {"error": repr(e)}
             ctx.close()
             rec["extras"].update(extras(mp, dev, args))
             sp = rec["extras"].get("strong_scaling_per_gpu")

@@ -655,9 +655,20 @@ constexpr int CG_YLD = 16 * 4 * 2 + 1;               // Y tile pitch (16-B units
 static_assert(CG_NI * CG_YLD <= CG_HALF, "a half's Y tile fits the S tile half it replaces");
 constexpr int CG_NC8 = (Z_CLS + 7) / 8;              // 42 groups of 8 classes (one per XCD)
 
+// CG_SWZ (default 1): rows of 16 units with image column bl ^ cq, so that a DFT thread group's S
+// writes (eight channel groups cq of one image at a 2,176-B stride: 4-way bank conflicts on the padded
+// rows) and the GEMM's fragment reads (16 images of a row, or two rows' halves) both spread over the 64
+// banks; and the Y tile's frequency slot rotated by the channel group, (q + cq) & 7, so the inverse
+// DFT's reads (one frequency of 16 channel groups, a 256-B stride: 8-way) do too.  Placement only: the
+// values and their arithmetic are unchanged.
+#ifndef CG_SWZ
+#define CG_SWZ 1
+#endif
 __device__ __forceinline__ int cg_s(int k2, int cq, int part, int bl) {   // S tile index (16-B units)
+  if constexpr (CG_SWZ) return (k2 >> 2) * CG_HALF + ((cq * 2 + part) * 4 + (k2 & 3)) * 16 + (bl ^ cq);
   return (k2 >> 2) * CG_HALF + ((cq * 2 + part) * 4 + (k2 & 3)) * CG_SLD + bl;
 }
+__device__ __forceinline__ int cg_yq(int q, int cq) { return CG_SWZ ? (q + cq) & 7 : q; }   // Y tile slot
 __device__ __forceinline__ f32x4 mfma16x16(f16x8 a, f16x8 b, f32x4 c) {
   return __builtin_amdgcn_mfma_f32_16x16x32_f16(a, b, c, 0, 0, 0);
 }
@@ -703,10 +714,31 @@ __device__ __forceinline__ void cg_forward(const f32x4 (&zin)[8], int k1, uint4*
 // (gr, gi) pairs as stored; the S fragment supplies the two forms, (sr, -si) for the real rows
 // (gr sr - gi si) and (si, sr) for the imaginary rows (gr si + gi sr): a sign flip and a half swap per S
 // dword (16 VALU per k-step) instead of four weight forms (64).  w[mq][0 | 1] = the hi | lo planes.
+template <bool LEAN = false>
 __device__ __forceinline__ void cg_kstep(const uint4* tile, int k2, int t, int kq, int jj, const uint4 (&w)[4][2],
                                          f32x4 (&acc)[8]) {
   const uint4 m = {0x80000000u, 0x80000000u, 0x80000000u, 0x80000000u};
   const uint4 uh = tile[cg_s(k2, 4 * t + kq, 0, jj)], ul = tile[cg_s(k2, 4 * t + kq, 1, jj)];
+  if constexpr (LEAN) {   // the real rows' MFMAs, then the imaginary rows' (fewer S forms live at once)
+    const f16x8 sh = __builtin_bit_cast(f16x8, uh ^ m), sl = __builtin_bit_cast(f16x8, ul ^ m);
+#pragma unroll
+    for (int mq = 0; mq < 4; ++mq) {
+      const f16x8 ah = __builtin_bit_cast(f16x8, w[mq][0]), al = __builtin_bit_cast(f16x8, w[mq][1]);
+      acc[mq] = mfma16x16(al, sh, acc[mq]);
+      acc[mq] = mfma16x16(ah, sl, acc[mq]);
+      acc[mq] = mfma16x16(ah, sh, acc[mq]);
+    }
+    const f16x8 sh2 = __builtin_bit_cast(f16x8, (uh >> 16) | (uh << 16));
+    const f16x8 sl2 = __builtin_bit_cast(f16x8, (ul >> 16) | (ul << 16));
+#pragma unroll
+    for (int mq = 0; mq < 4; ++mq) {
+      const f16x8 ah = __builtin_bit_cast(f16x8, w[mq][0]), al = __builtin_bit_cast(f16x8, w[mq][1]);
+      acc[4 + mq] = mfma16x16(al, sh2, acc[4 + mq]);
+      acc[4 + mq] = mfma16x16(ah, sl2, acc[4 + mq]);
+      acc[4 + mq] = mfma16x16(ah, sh2, acc[4 + mq]);
+    }
+    return;
+  }
   const f16x8 sh = __builtin_bit_cast(f16x8, uh ^ m), sl = __builtin_bit_cast(f16x8, ul ^ m);
   const f16x8 sh2 = __builtin_bit_cast(f16x8, (uh >> 16) | (uh << 16));
   const f16x8 sl2 = __builtin_bit_cast(f16x8, (ul >> 16) | (ul << 16));
@@ -742,21 +774,24 @@ __device__ __forceinline__ void cg_ystore(uint4* tile, int k2, int kq, int jj, c
   for (int mq = 0; mq < 4; ++mq) {
     const int cqo = 4 * mq + kq;
     const f32x4 re = acc[mq], im = acc[4 + mq];
-    ytile[jj * CG_YP + (cqo * 8 + k2) * 2] = f32x4{re[0], im[0], re[1], im[1]} * unscale;
-    ytile[jj * CG_YP + (cqo * 8 + k2) * 2 + 1] = f32x4{re[2], im[2], re[3], im[3]} * unscale;
+    ytile[jj * CG_YP + (cqo * 8 + cg_yq(k2, cqo)) * 2] = f32x4{re[0], im[0], re[1], im[1]} * unscale;
+    ytile[jj * CG_YP + (cqo * 8 + cg_yq(k2, cqo)) * 2 + 1] = f32x4{re[2], im[2], re[3], im[3]} * unscale;
   }
 }
 
 // cg_inverse: the thread's channels' 8 frequencies from the Y tile -> 8-point inverse DFT, twiddle
 // W72^{n2 k1} -> the row-class partials out[n2] (channels 2a, 2a + 1)
-__device__ __forceinline__ void cg_inverse(const uint4* tile, int k1, int cq, int hf, int bl, f32x4 (&out)[8]) {
+__device__ __forceinline__ void cg_yread(const uint4* tile, int cq, int hf, int bl, f32x4 (&y)[8]) {
   const f32x4* ytile = reinterpret_cast<const f32x4*>(tile);
+#pragma unroll
+  for (int q = 0; q < 8; ++q) y[q] = ytile[bl * CG_YP + (cq * 8 + cg_yq(q, cq)) * 2 + hf];
+}
+__device__ __forceinline__ void cg_inverse_regs(const f32x4 (&y)[8], int k1, f32x4 (&out)[8]) {
   cpx yv[2][8];
 #pragma unroll
   for (int q = 0; q < 8; ++q) {
-    const f32x4 pv = ytile[bl * CG_YP + (cq * 8 + q) * 2 + hf];
-    yv[0][q] = cpx{pv[0], pv[1]};
-    yv[1][q] = cpx{pv[2], pv[3]};
+    yv[0][q] = cpx{y[q][0], y[q][1]};
+    yv[1][q] = cpx{y[q][2], y[q][3]};
   }
 #pragma unroll
   for (int e = 0; e < 2; ++e) {
@@ -766,6 +801,11 @@ __device__ __forceinline__ void cg_inverse(const uint4* tile, int k1, int cq, in
   }
 #pragma unroll
   for (int n2 = 0; n2 < 8; ++n2) out[n2] = f32x4{yv[0][n2].x, yv[0][n2].y, yv[1][n2].x, yv[1][n2].y};
+}
+__device__ __forceinline__ void cg_inverse(const uint4* tile, int k1, int cq, int hf, int bl, f32x4 (&out)[8]) {
+  f32x4 y[8];
+  cg_yread(tile, cq, hf, bl, y);
+  cg_inverse_regs(y, k1, out);
 }
 
 // col8_kernel: 512 threads, thread = image x channel pair (one contiguous 512-B run of Z per image
@@ -950,6 +990,138 @@ __global__ __launch_bounds__(512, 1) void col8p_kernel(cpx* __restrict__ Z, cons
   }
 }
 
+// col8q_kernel: col8p_kernel's blocks and LDS-DMA prefetch, software-pipelined so that the matrix
+// cores and the vector ALUs work at the same time: item k's GEMM (MFMA, weights in registers, S from
+// the working slot) runs beside item k - 1's inverse DFT and stores (VALU on the thread's 8 Y values,
+// read from the Y tile into registers at the end of item k - 1).  Per item:
+//   GEMM(k) || inverse(k - 1) + stores(k - 1);  Y(k) -> W;  yv <- W;
+//   wait DMA(k + 1) in P;  raw(k + 1) -> DFT -> S(k + 1) over it in P;  DMA(k + 2) -> W;  swap W, P.
+// Item k + 2's DMA is issued one item ahead of its use.  The same item arithmetic (cg_*): bit-identical.
+template <bool ZNT>
+__global__ __launch_bounds__(512, 1) void col8q_kernel(cpx* __restrict__ Z, const uint4* __restrict__ Gc, int B,
+                                                       int ngrp, int nitems, float unscale) {
+  __shared__ uint4 slots[2 * CP_SLOT];   // 139,264 B
+  const int nblk = gridDim.x, per = nblk / 8, r8 = nblk % 8, xg = blockIdx.x % 8, q = blockIdx.x / 8;
+  const int v = (xg < r8 ? xg * (per + 1) : r8 * (per + 1) + (xg - r8) * per) + q;
+  const int it0 = (int)((int64_t)v * nitems / nblk), it1 = (int)((int64_t)(v + 1) * nitems / nblk);
+  if (it0 >= it1) return;
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int bl = tid >> 5, a = tid & 31, cq = a >> 1, hf = a & 1;
+  const int kq = lane >> 4, jj = lane & 15, k2 = wv;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)slots;
+  auto dma = [&](int it, int s) {
+    const int cls = it / ngrp, grp = it - cls * ngrp;
+    const int fx = cls / 9, k1 = cls - fx * 9;
+    const int lq = opaque(lane);   // (not hoisted out of the item loop)
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const int il = 2 * wv + (i >> 2);
+      const int b = min(grp * CG_NI + il, B - 1);
+      const char* src = reinterpret_cast<const char*>(Z + z_off(b, 0, fx, k1)) + (i & 3) * 1024 + lq * 16;
+      const uint32_t dst = lds0 + (uint32_t)(s * CP_SLOT * 16 + il * 4096 + (i & 3) * 1024);
+      glds16(src, __builtin_amdgcn_readfirstlane(dst));
+    }
+  };
+  // raw partials of the item in slot s -> S tile over them (two barriers)
+  auto forward = [&](int it, int s) {
+    // thread indices re-derived from an opaque tid: their address math is not hoisted out of the loop
+    // (held live, or spilled, across the GEMM)
+    const int tq = opaque(tid), bl = tq >> 5, a = tq & 31, cq = a >> 1, hf = a & 1;
+    uint4* tile = slots + s * CP_SLOT;
+    const int cls = it / ngrp, k1 = cls % 9;
+    f32x4 zin[8];
+    const f32x4* raw = reinterpret_cast<const f32x4*>(tile) + bl * 256 + a;
+#pragma unroll
+    for (int n2 = 0; n2 < 8; ++n2) zin[n2] = raw[n2 * 32];
+    lds_barrier();   // the raw partials are read: the slot becomes the S tile
+    cg_forward(zin, k1, tile, cq, hf, bl);
+  };
+  constexpr unsigned VMCNT0 = 0x0F70;   // vmcnt(0) expcnt(7) lgkmcnt(15), seen by hipcc's bookkeeping
+  uint4 w[4][4][2];
+  int wcls = it0 / ngrp;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) cg_wload(Gc, wcls, k2, t, kq, jj, w[t]);
+  __builtin_amdgcn_s_waitcnt(VMCNT0);
+  dma(it0, 0);
+  if (it0 + 1 < it1) {
+    dma(it0 + 1, 1);
+    asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+  } else {
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  }
+  lds_barrier();
+  forward(it0, 0);
+  lds_barrier();
+  f32x4 yv[8];   // the previous item's Y values of this thread's channels
+  // one item; WI: with the previous item's inverse DFT and stores beside the GEMM (every item but the
+  // first: a branch there would put them in a block of their own, after the MFMAs)
+  auto item = [&](int it, auto WI) {
+    const int s = (it - it0) & 1;
+    uint4* tile = slots + s * CP_SLOT;
+    const int cls = it / ngrp;
+    if (cls != wcls) {   // block-uniform: before this item's GEMM
+      wcls = cls;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) cg_wload(Gc, wcls, k2, t, kq, jj, w[t]);
+      __builtin_amdgcn_s_waitcnt(VMCNT0);
+    }
+    f32x4 acc[8] = {};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) cg_kstep<true>(tile, k2, t, kq, jj, w[t], acc);
+    if constexpr (decltype(WI)::value) {
+      const int pit = it - 1, pcls = pit / ngrp, pgrp = pit - pcls * ngrp;
+      const int pfx = pcls / 9, pk1 = pcls - pfx * 9;
+      f32x4 out[8];
+      cg_inverse_regs(yv, pk1, out);
+      const int tq = opaque(tid);
+      const int b = min(pgrp * CG_NI + (tq >> 5), B - 1);   // (images past B: image B - 1's bytes again)
+#pragma unroll
+      for (int n2 = 0; n2 < 8; ++n2) {
+        f32x4* zp = reinterpret_cast<f32x4*>(Z + z_off(b, n2, pfx, pk1)) + (tq & 31);
+        if constexpr (ZNT) __builtin_nontemporal_store(out[n2], zp);
+        else *zp = out[n2];
+      }
+    }
+    lds_barrier();   // every wave has read the S tile
+    {
+      const int lq = opaque(lane);
+      cg_ystore(tile, k2, lq >> 4, lq & 15, acc, unscale);
+    }
+    if (it + 1 < it1) {
+      // item it + 1's DMA (issued one item ago) is older than this item's 8 stores only
+      if constexpr (decltype(WI)::value) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      lds_barrier();   // every wave's pieces have landed; the Y tile is complete
+      forward(it + 1, s ^ 1);
+      {
+        const int tq = opaque(tid);   // after the forward DFT: fewer registers live beside it
+        cg_yread(tile, (tq & 31) >> 1, tq & 1, tq >> 5, yv);
+      }
+      lds_barrier();   // the S tile of item it + 1 is complete; every thread has read its Y values
+      if (it + 2 < it1) dma(it + 2, s);
+    } else {
+      lds_barrier();
+      const int tq = opaque(tid);
+      cg_yread(tile, (tq & 31) >> 1, tq & 1, tq >> 5, yv);
+    }
+  };
+  item(it0, std::false_type{});
+  for (int it = it0 + 1; it < it1; ++it) item(it, std::true_type{});
+  {   // the last item's inverse DFT and stores
+    const int pit = it1 - 1, pcls = pit / ngrp, pgrp = pit - pcls * ngrp;
+    const int pfx = pcls / 9, pk1 = pcls - pfx * 9;
+    f32x4 out[8];
+    cg_inverse_regs(yv, pk1, out);
+    const int b = min(pgrp * CG_NI + bl, B - 1);
+#pragma unroll
+    for (int n2 = 0; n2 < 8; ++n2) {
+      f32x4* zp = reinterpret_cast<f32x4*>(Z + z_off(b, n2, pfx, pk1)) + a;
+      if constexpr (ZNT) __builtin_nontemporal_store(out[n2], zp);
+      else *zp = out[n2];
+    }
+  }
+}
+
 // column kernel, bf16 (MP_DTYPE_BF16): col8_kernel's blocking with bf16 Z partials (8-B reads of a
 // thread's two channels), a bf16 S tile (one (re, im) pair per channel, no lo plane: 34 KB), one
 // v_mfma_f32_16x16x32_bf16 product per (k-step, row block, re|im) against the class-major bf16
@@ -970,7 +1142,11 @@ __global__ __launch_bounds__(512, 2) void col8_bf_kernel(void* __restrict__ Zv, 
   const int b = min(img0 + bl, B - 1);
   const int cq = a >> 1, hf = a & 1;
   uint32_t* Z = static_cast<uint32_t*>(Zv);
-  auto sidx = [](int k2, int c, int img) { return (k2 >> 2) * CB_HALF + (c * 4 + (k2 & 3)) * CG_SLD + img; };
+  // (CG_SWZ: rows of 16 units, image column img ^ c, as cg_s)
+  auto sidx = [](int k2, int c, int img) {
+    if constexpr (CG_SWZ) return (k2 >> 2) * CB_HALF + (c * 4 + (k2 & 3)) * 16 + (img ^ c);
+    return (k2 >> 2) * CB_HALF + (c * 4 + (k2 & 3)) * CG_SLD + img;
+  };
   {
     uint2 zin[8];
 #pragma unroll
@@ -1014,36 +1190,17 @@ __global__ __launch_bounds__(512, 2) void col8_bf_kernel(void* __restrict__ Zv, 
     }
   }
   lds_barrier();
-  constexpr int YLD = 16 * 8 * 2 + 1;
-  f32x4* ytile = reinterpret_cast<f32x4*>(tile);
-#pragma unroll
-  for (int mq = 0; mq < 4; ++mq) {
-    const int cqo = 4 * mq + kq;
-    const f32x4 re = acc[mq], im = acc[4 + mq];
-    ytile[jj * YLD + (cqo * 8 + k2) * 2] = f32x4{re[0], im[0], re[1], im[1]};
-    ytile[jj * YLD + (cqo * 8 + k2) * 2 + 1] = f32x4{re[2], im[2], re[3], im[3]};
-  }
+  cg_ystore(tile, k2, kq, jj, acc, 1.0f);   // (x 1.0f: exact)
   lds_barrier();
-  cpx yv[2][8];
-#pragma unroll
-  for (int q = 0; q < 8; ++q) {
-    const f32x4 pv = ytile[bl * YLD + (cq * 8 + q) * 2 + hf];
-    yv[0][q] = cpx{pv[0], pv[1]};
-    yv[1][q] = cpx{pv[2], pv[3]};
-  }
-#pragma unroll
-  for (int e = 0; e < 2; ++e) {
-    dft8_fold<1>(yv[e]);
-#pragma unroll
-    for (int n2 = 0; n2 < 8; ++n2) yv[e][n2] = twid<1>(yv[e][n2], n2 * k1);
-  }
+  f32x4 yo[8];
+  cg_inverse(tile, k1, cq, hf, bl, yo);
   if (live) {
 #pragma unroll
     for (int n2 = 0; n2 < 8; ++n2)
     {
       typedef uint32_t u2v __attribute__((ext_vector_type(2)));
       u2v* zp = reinterpret_cast<u2v*>(Z + z_off(b, n2, fx, k1)) + a;
-      const u2v v = u2v{pack_bf2(yv[0][n2].x, yv[0][n2].y), pack_bf2(yv[1][n2].x, yv[1][n2].y)};
+      const u2v v = u2v{pack_bf2(yo[n2][0], yo[n2][1]), pack_bf2(yo[n2][2], yo[n2][3])};
       if constexpr (ZNT) __builtin_nontemporal_store(v, zp);
       else *zp = v;
     }
@@ -1082,6 +1239,14 @@ static int col8p_minb() {
   }();
   return v;
 }
+// MP_COL8Q (default 1): the software-pipelined form col8q_kernel; 0: col8p_kernel
+static bool col8q_on() {
+  static const bool v = [] {
+    const char* e = std::getenv("MP_COL8Q");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  return v;
+}
 static int col8p_blocks() {
   static const int v = [] {
     const char* e = std::getenv("MP_COL8P_BLOCKS");
@@ -1099,6 +1264,15 @@ hipError_t launch_col_gemm(void* Z, const void* Gc, int B, float unscale, hipStr
   const int ngrp = (B + CG_NI - 1) / CG_NI;
   if (!bf && col8p_minb() > 0 && B >= col8p_minb()) {
     const int nitems = Z_CLS * ngrp, nblk = std::min(nitems, col8p_blocks());
+    if (col8q_on()) {
+      if (col8_znt(false, resident))
+        hipLaunchKernelGGL((col8q_kernel<true>), dim3(nblk), dim3(512), 0, st, static_cast<cpx*>(Z),
+                           static_cast<const uint4*>(Gc), B, ngrp, nitems, unscale);
+      else
+        hipLaunchKernelGGL((col8q_kernel<false>), dim3(nblk), dim3(512), 0, st, static_cast<cpx*>(Z),
+                           static_cast<const uint4*>(Gc), B, ngrp, nitems, unscale);
+      return hipGetLastError();
+    }
     if (col8_znt(false, resident))
       hipLaunchKernelGGL((col8p_kernel<true>), dim3(nblk), dim3(512), 0, st, static_cast<cpx*>(Z),
                          static_cast<const uint4*>(Gc), B, ngrp, nitems, unscale);

@@ -140,6 +140,9 @@ BITS_CASES = [
     # same item arithmetic (64 + 16: col8p on the first slice only at 64; on both at 1)
     ("pose80", "fp32_fft", "MP_COL8P", ("0", "64", "1"), {}),
     ("pose12", "fp32_fft", "MP_COL8P", ("0", "1"), {}),
+    # col8q_kernel (software-pipelined) or col8p_kernel: one item's arithmetic either way
+    ("pose80", "fp32_fft", "MP_COL8Q", ("0", "1"), {"MP_COL8P": "1"}),
+    ("pose12", "fp32_fft", "MP_COL8Q", ("0", "1"), {"MP_COL8P": "1"}),
     # row A on channel quarters (rowq_a_kernel) or as row8_kernel<ROW_A>: one batch slice of 12, and
     # two slices (64 + 16) all on rowq; and the cache policy of a cache-resident batch (12 crops)
     ("pose12", "fp32_fft", "MP_ROWQ_MAXB", ("0", "16"), {}),

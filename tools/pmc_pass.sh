@@ -10,7 +10,7 @@ dt=${3:-f32_fft}
 shift 3
 [ "$1" = "--" ] && shift
 mkdir -p "$out"
-cp -f "$R/profiles/HEAD_STAMP" "$out/head.txt" 2>/dev/null || true
+cp -f "$R/profiles/TREE_STAMP.json" "$out/STAMP.json" 2>/dev/null || true
 cd /tmp && export TMPDIR=/tmp
 [ -s "$base/avail.txt" ] || timeout -s KILL 60 rocprofv3 -L > "$base/avail.txt" 2>&1 || true
 CTRS=""

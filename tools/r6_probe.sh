@@ -14,6 +14,7 @@ for pass in ${PASSES:-tcc ta}; do
     ta) C="TA_TA_BUSY_sum TA_FLAT_READ_WAVEFRONTS_sum TD_TD_BUSY_sum TD_TC_STALL_sum" ;;
     bytes) C="FETCH_SIZE" ;;
     wbytes) C="WRITE_SIZE" ;;
+    lds) C="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_LDS SQ_WAIT_INST_LDS SQ_LDS_BANK_CONFLICT SQ_ACTIVE_INST_ANY" ;;
     sq) C="SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_ACTIVE_INST_VMEM SQ_ACTIVE_INST_LDS SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR" ;;
   esac
   bash tools/pmc_pass.sh "$out" "$pass" ${DT:-f32_fft} -- $C || exit 1
