@@ -53,6 +53,10 @@ __device__ __forceinline__ int opaque(int v) {
   asm volatile("" : "+v"(v));
   return v;
 }
+__device__ __forceinline__ int opaque_s(int v) {   // the same for a wave-uniform (SGPR) value
+  asm volatile("" : "+s"(v));
+  return v;
+}
 template <typename P>
 __device__ __forceinline__ P* opaque_ptr(P* p) {
   asm volatile("" : "+s"(p));
@@ -111,8 +115,11 @@ __device__ __forceinline__ void rk_segment(const ConvArgs& p, float* seg, int b,
   const int x = xs + j;
   float* sp = seg + j * RK_SP;
   // LEAN: the gate weights (LDS) are re-read per segment instead of 128 registers held across the kernel
-  const void* orw = LEAN ? opaque_ptr(or_x3) : or_x3;
-  const void* irw = LEAN ? opaque_ptr(ir_x3) : ir_x3;
+  // (an opaque OFFSET, not an opaque pointer: the pointer keeps its LDS provenance, so the loads stay
+  // ds_read_b128 -- through an opaque pointer they became flat loads, each followed by an
+  // s_waitcnt vmcnt(0) lgkmcnt(0) that drained the block's outstanding map loads and stores)
+  const void* orw = LEAN ? static_cast<const void*>(static_cast<const char*>(or_x3) + opaque_s(0)) : or_x3;
+  const void* irw = LEAN ? static_cast<const void*>(static_cast<const char*>(ir_x3) + opaque_s(0)) : ir_x3;
   if constexpr (MODE == ROW_A) {
     // hgru_module.py:797-799: I = tanh(X - (beta O + nu) (P1 + lateral_bias))
 #pragma unroll
@@ -957,7 +964,11 @@ __global__ __launch_bounds__(512, 1) void col8p_kernel(cpx* __restrict__ Z, cons
 #pragma unroll
       for (int n2 = 0; n2 < 8; ++n2) zin[n2] = raw[n2 * 32];
       lds_barrier();   // the raw partials are read: the slot becomes the S tile
+#ifndef COL8P_NODFT   // (timing-only A/B builds: tools/exp_lib.sh ... -DCOL8P_NODFT etc.)
       cg_forward(zin, k1, tile, cq, hf, bl);
+#else
+      if (zin[0][0] == 12345.f) tile[tid] = uint4{};
+#endif
     }
     if (cls != wcls) {   // block-uniform
       wcls = cls;
@@ -967,13 +978,19 @@ __global__ __launch_bounds__(512, 1) void col8p_kernel(cpx* __restrict__ Z, cons
     }
     lds_barrier();
     f32x4 acc[8] = {};
+#ifndef COL8P_NOGEMM
 #pragma unroll
     for (int t = 0; t < 4; ++t) cg_kstep(tile, k2, t, kq, jj, w[t], acc);
+#endif
     lds_barrier();   // every wave has read the S tile
     cg_ystore(tile, k2, kq, jj, acc, unscale);
     lds_barrier();
     f32x4 out[8];
+#ifndef COL8P_NOINV
     cg_inverse(tile, k1, cq, hf, bl, out);
+#else
+    cg_yread(tile, cq, hf, bl, out);
+#endif
     // images past B (a partial last group) store image B - 1's values over it: the same bytes, since
     // their DMA read image B - 1 too -- every item issues exactly 8 stores, as the counted waits assume
     const int b = min(grp * CG_NI + bl, B - 1);
@@ -1006,7 +1023,6 @@ __global__ __launch_bounds__(512, 1) void col8q_kernel(cpx* __restrict__ Z, cons
   const int it0 = (int)((int64_t)v * nitems / nblk), it1 = (int)((int64_t)(v + 1) * nitems / nblk);
   if (it0 >= it1) return;
   const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-  const int bl = tid >> 5, a = tid & 31, cq = a >> 1, hf = a & 1;
   const int kq = lane >> 4, jj = lane & 15, k2 = wv;
   const uint32_t lds0 = (uint32_t)(uintptr_t)slots;
   auto dma = [&](int it, int s) {
@@ -1112,10 +1128,10 @@ __global__ __launch_bounds__(512, 1) void col8q_kernel(cpx* __restrict__ Z, cons
     const int pfx = pcls / 9, pk1 = pcls - pfx * 9;
     f32x4 out[8];
     cg_inverse_regs(yv, pk1, out);
-    const int b = min(pgrp * CG_NI + bl, B - 1);
+    const int b = min(pgrp * CG_NI + (tid >> 5), B - 1);
 #pragma unroll
     for (int n2 = 0; n2 < 8; ++n2) {
-      f32x4* zp = reinterpret_cast<f32x4*>(Z + z_off(b, n2, pfx, pk1)) + a;
+      f32x4* zp = reinterpret_cast<f32x4*>(Z + z_off(b, n2, pfx, pk1)) + (tid & 31);
       if constexpr (ZNT) __builtin_nontemporal_store(out[n2], zp);
       else *zp = out[n2];
     }
@@ -1231,19 +1247,22 @@ static bool col8_znt(bool bf, bool resident) {
 }
 
 // MP_COL8P: slices of at least this many images run col8p_kernel (fp32; 0 = never); MP_COL8P_BLOCKS:
-// its grid (default: one block per CU)
+// its grid (default: one block per CU).  Same box (profiles/r6/ab_col8_batches.jsonl): B = 256 (two
+// slices of 128) 8.00 vs 8.05 ms per forward with col8_kernel; B = 128 (slices of 64) 4.35 vs 4.23 --
+// a persistent launch holding every CU keeps the other slice's kernels off the chip until it ends
 static int col8p_minb() {
   static const int v = [] {
     const char* e = std::getenv("MP_COL8P");
-    return e ? std::atoi(e) : 64;
+    return e ? std::atoi(e) : 128;
   }();
   return v;
 }
-// MP_COL8Q (default 1): the software-pipelined form col8q_kernel; 0: col8p_kernel
+// MP_COL8Q (default 0): 1 runs the software-pipelined form col8q_kernel instead of col8p_kernel (same
+// box, B = 256: 0.179 vs 0.170 ms; profiles/r6/ab_col8.jsonl)
 static bool col8q_on() {
   static const bool v = [] {
     const char* e = std::getenv("MP_COL8Q");
-    return e ? std::atoi(e) != 0 : true;
+    return e ? std::atoi(e) != 0 : false;
   }();
   return v;
 }
