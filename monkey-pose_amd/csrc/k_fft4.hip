@@ -412,6 +412,9 @@ constexpr int R8_GATE = 2 * 4 * 2 * 64;                  // f16x8 of one gate's 
 constexpr int R8_T = (8 * 64 * RK_SP * 4 + R8_GATE * 16) / 8;   // 155,648 B: T grown by 512 B for FINAL
 static_assert(R8_T >= RK_T && (8 * 32 * RK_SP * 4 + 2 * R8_GATE * 16) <= R8_T * 8, "staging + gate weights fit");
 
+#ifndef R8_SEGPF
+#define R8_SEGPF 0
+#endif
 // BF: MP_DTYPE_BF16 -- Z and the hGRU maps in bf16, the gates one bf16 product (gate_bf); transforms,
 // epilogue math and the NHWC output fp32
 // ZNT: Z read and written non-temporal (MP_ROW8_ZNT)
@@ -434,6 +437,8 @@ __global__ __launch_bounds__(R8_NT, 1) void row8_kernel(void* __restrict__ Z, Co
   constexpr bool OR = MODE == ROW_B || MODE == ROW_FINAL, IR = MODE == ROW_B || MODE == ROW_INIT;
   constexpr int GN = BF ? R8_GATE / 2 : R8_GATE;   // uint4 per gate (bf16: one product, no lo plane)
   float P[64];
+  constexpr bool SEGPF = R8_SEGPF && (MODE == ROW_A || MODE == ROW_B);
+  SegIn L0;
   if constexpr (MODE != ROW_INIT) {
     {
       cpx u[R8_NIT][9];
@@ -456,6 +461,12 @@ __global__ __launch_bounds__(R8_NT, 1) void row8_kernel(void* __restrict__ Z, Co
       }
     }
     lds_barrier();
+    // R8_SEGPF (A/B, default 0): the first epilogue segment's maps requested here, during the inverse
+    // row transforms instead of in front of the segment.  Same box, B = 256: row A 0.272 ms either
+    // way, row B 0.297 -> 0.312 (profiles/r6/ab_row_segpf.jsonl): not kept
+    if constexpr (SEGPF) {
+      if (live) rk_load_seg<MODE, BF>(p, O0, b, y, 0, lane, L0);
+    }
     {
       cpx A[FX];
 #pragma unroll
@@ -494,7 +505,8 @@ __global__ __launch_bounds__(R8_NT, 1) void row8_kernel(void* __restrict__ Z, Co
       const int xs = 32 * sg;
       if (xs >= W) continue;   // wave-uniform
       SegIn L;
-      rk_load_seg<MODE, BF>(p, O0, b, y, xs, lane, L);
+      if (SEGPF && sg == 0) L = L0;
+      else rk_load_seg<MODE, BF>(p, O0, b, y, xs, lane, L);
       if constexpr (MODE != ROW_INIT) {
 #pragma unroll
         for (int q = 0; q < 32; ++q) stg[q * RK_SP + lane] = P[xs + q];
