@@ -463,7 +463,7 @@ __global__ __launch_bounds__(R8_NT, 1) void row8_kernel(void* __restrict__ Z, Co
     lds_barrier();
     // R8_SEGPF (A/B, default 0): the first epilogue segment's maps requested here, during the inverse
     // row transforms instead of in front of the segment.  Same box, B = 256: row A 0.272 ms either
-    // way, row B 0.297 -> 0.312 (profiles/r6/ab_row_segpf.jsonl): not kept
+    // way, row B 0.297 -> 0.312 (profiles/r6/ab/ab_row.jsonl): not kept
     if constexpr (SEGPF) {
       if (live) rk_load_seg<MODE, BF>(p, O0, b, y, 0, lane, L0);
     }
@@ -917,6 +917,11 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds) {
                : "memory");
 }
 
+// COL8P_EARLY (A/B, default 0): item it + 2's DMA issued before item it's stores instead of after
+// them -- same box, B = 256: 0.186 vs 0.170 ms (profiles/r6/ab/ab_col8.jsonl)
+#ifndef COL8P_EARLY
+#define COL8P_EARLY 0
+#endif
 template <bool ZNT>
 __global__ __launch_bounds__(512, 1) void col8p_kernel(cpx* __restrict__ Z, const uint4* __restrict__ Gc, int B,
                                                        int ngrp, int nitems, float unscale) {
@@ -960,14 +965,20 @@ __global__ __launch_bounds__(512, 1) void col8p_kernel(cpx* __restrict__ Z, cons
     uint4* tile = slots + s * CP_SLOT;
     const int cls = it / ngrp, grp = it - cls * ngrp;
     const int fx = cls / 9, k1 = cls - fx * 9;
-    // this item's DMA is older than: the previous item's 8 stores and the next item's 8 DMA pieces
-    // (and a class change's weight loads, which only make the wait longer)
-    if (it + 1 < it1) {
-      if (it == it0) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
-    } else {
-      if (it == it0) asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    // this item's DMA is older than: the next item's 8 DMA pieces and the 8 stores of each item
+    // finished since it was issued (COL8P_EARLY: the previous two items' stores, the DMA being issued
+    // ahead of each item's stores; otherwise the previous item's) -- a class change's weight loads
+    // only make the wait longer
+    const bool nx = it + 1 < it1;
+    if (it == it0) {
+      if (nx) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else if (!COL8P_EARLY || it == it0 + 1) {
+      if (nx) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    } else {
+      if (nx) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     }
     lds_barrier();   // every wave's pieces have landed
     {
@@ -998,10 +1009,13 @@ __global__ __launch_bounds__(512, 1) void col8p_kernel(cpx* __restrict__ Z, cons
     cg_ystore(tile, k2, kq, jj, acc, unscale);
     lds_barrier();
     f32x4 out[8];
-#ifndef COL8P_NOINV
-    cg_inverse(tile, k1, cq, hf, bl, out);
-#else
     cg_yread(tile, cq, hf, bl, out);
+    if (COL8P_EARLY && it + 2 < it1) {
+      lds_barrier();   // every thread has read its Y values: the slot takes item it + 2 (before the stores)
+      dma(it + 2, s);
+    }
+#ifndef COL8P_NOINV
+    cg_inverse_regs(out, k1, out);
 #endif
     // images past B (a partial last group) store image B - 1's values over it: the same bytes, since
     // their DMA read image B - 1 too -- every item issues exactly 8 stores, as the counted waits assume
@@ -1012,7 +1026,7 @@ __global__ __launch_bounds__(512, 1) void col8p_kernel(cpx* __restrict__ Z, cons
       if constexpr (ZNT) __builtin_nontemporal_store(out[n2], zp);
       else *zp = out[n2];
     }
-    if (it + 2 < it1) {
+    if (!COL8P_EARLY && it + 2 < it1) {
       lds_barrier();   // every thread has read its Y values: the slot takes item it + 2
       dma(it + 2, s);
     }
@@ -1259,7 +1273,7 @@ static bool col8_znt(bool bf, bool resident) {
 }
 
 // MP_COL8P: slices of at least this many images run col8p_kernel (fp32; 0 = never); MP_COL8P_BLOCKS:
-// its grid (default: one block per CU).  Same box (profiles/r6/ab_col8_batches.jsonl): B = 256 (two
+// its grid (default: one block per CU).  Same box (profiles/r6/ab/ab_col8_batches.jsonl): B = 256 (two
 // slices of 128) 8.00 vs 8.05 ms per forward with col8_kernel; B = 128 (slices of 64) 4.35 vs 4.23 --
 // a persistent launch holding every CU keeps the other slice's kernels off the chip until it ends
 static int col8p_minb() {
@@ -1270,7 +1284,7 @@ static int col8p_minb() {
   return v;
 }
 // MP_COL8Q (default 0): 1 runs the software-pipelined form col8q_kernel instead of col8p_kernel (same
-// box, B = 256: 0.179 vs 0.170 ms; profiles/r6/ab_col8.jsonl)
+// box, B = 256: 0.179 vs 0.170 ms; profiles/r6/ab/ab_col8.jsonl)
 static bool col8q_on() {
   static const bool v = [] {
     const char* e = std::getenv("MP_COL8Q");
