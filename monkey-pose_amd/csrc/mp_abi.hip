@@ -224,6 +224,7 @@ void ensure_ws(mp_ctx* c, int64_t n, int64_t H, int64_t W) {
     const int S2 = fc_choose_splits((int)nb, c->fc1_out, c->nout, &ks);
     const size_t p2 = (size_t)S2 * nb * ((c->nout + 31) / 32 * 32) * sizeof(float);
     c->part.alloc(std::max(p1, p2));
+    c->part2.alloc(p2);
     c->h1.alloc((size_t)nb * c->fc1_out * sizeof(float));
   }
   (void)px;
@@ -451,6 +452,18 @@ bool fc_presplit() {
   return v;
 }
 
+// MP_FC_SLICE (A/B, default 0): 1 runs the pose head (fc_1, its reduce + BN_4, fc_out) per hGRU batch
+// slice on the slice's stream, right after that slice's loop, instead of once for the whole batch after
+// the join.  Bit-identical, but each slice streams fc_1's 1.07 GB of weights: same box, B = 256 8.16 vs
+// 7.97 ms, B = 64 2.60 vs 2.36 (profiles/r6/ab/ab_fc_slice.jsonl)
+bool fc_slice() {
+  static const bool v = [] {
+    const char* e = std::getenv("MP_FC_SLICE");
+    return e ? std::atoi(e) != 0 : false;
+  }();
+  return v;
+}
+
 int stream_count() {
   static const int v = [] {
     const char* e = std::getenv("MP_STREAMS");
@@ -490,8 +503,11 @@ int slice_min() {
 // pre (optional): work a batch slice needs before its hGRU loop (the backbone of its images), run on the
 // slice's stream so that one slice's backbone overlaps another's loop
 using SliceFn = std::function<void(int b0, int cnt, hipStream_t s)>;
+// post (optional): work a batch slice does after its hGRU loop (the pose head on its rows), on the
+// slice's stream, so that the first slice's head overlaps the last slice's loop
 void run_circuit(mp_ctx* c, int64_t n, int H, int W, int T, const float* o0_nhwc, float* final_dst2,
-                 const StateOut* so, hipStream_t st, const SplitOut* sp = nullptr, const SliceFn* pre = nullptr) {
+                 const StateOut* so, hipStream_t st, const SplitOut* sp = nullptr, const SliceFn* pre = nullptr,
+                 const SliceFn* post = nullptr) {
   if (sp && !is_fft(c->dtype)) fail(MP_ERR_STATE, "split fc_1 planes are an FFT-path output");
   // FFT path, not profiling: batch slices are independent, so they run on separate streams and
   // their latency-bound kernels overlap (the per-kernel HIP-event profile keeps one stream)
@@ -500,6 +516,7 @@ void run_circuit(mp_ctx* c, int64_t n, int H, int W, int T, const float* o0_nhwc
   if (pre && !multi) (*pre)(0, (int)n, st);
   if (c->fft4 && !multi) {
     fft4_circuit_range(c, 0, (int)n, (int)n, H, W, T, o0_nhwc, final_dst2, so, sp, st);
+    if (post) (*post)(0, (int)n, st);
     return;
   }
   if (multi) {
@@ -539,6 +556,7 @@ void run_circuit(mp_ctx* c, int64_t n, int H, int W, int T, const float* o0_nhwc
         fft4_circuit_range(c, b0, cnt, (int)n, H, W, T, o0_nhwc, final_dst2, so, sp, s);
       else
         fft_circuit_range(c, b0, cnt, H, W, T, final_dst2, so, sp, s);
+      if (post) (*post)(b0, cnt, s);
       b0 += cnt;
     }
     for (int k = 1; k < ns; ++k) {
@@ -590,6 +608,7 @@ void run_circuit(mp_ctx* c, int64_t n, int H, int W, int T, const float* o0_nhwc
     store_step(so, c->O.f(), c->I.f(), 0, (int)n, H, W, t, bf16_maps(c), st, is_fft(c->dtype) && fft_c4_maps(),
                is_fft(c->dtype) && fft_c4_state());
   }
+  if (post) (*post)(0, (int)n, st);
 }
 
 // the initial output state for hidden_init (hgru_module.py:875-892) as an NHWC fp32 pointer:
@@ -931,8 +950,39 @@ int pose_fwd(mp_ctx* ctx, const float* depth, int64_t n, int64_t h, int64_t w, c
       sp.hi = reinterpret_cast<_Float16*>(ctx->fcin.p);
       sp.lo = fc_np == 3 ? sp.hi + (size_t)N * ctx->fc1_in : nullptr;
     }
+    // the head of rows b0 .. b0 + cnt on stream s: fc_1 on the split planes (partials in the slice's own
+    // S x cnt x Npad region of part, so slices run at once), relu + BN_4 into h1, fc_out (part2), its
+    // reduce into out.  Each row's sums are the same MFMA chains whatever the rows' count (the split
+    // count and slice length are functions of K and N only): bit-identical to the whole-batch head
+    int ks1, ks2;
+    const int S1 = fc_choose_splits(N, ctx->fc1_in, ctx->fc1_out, &ks1);
+    const int S2 = fc_choose_splits(N, ctx->fc1_out, ctx->nout, &ks2);
+    const size_t np1 = (size_t)(ctx->fc1_out + 31) / 32 * 32, np2 = (size_t)(ctx->nout + 31) / 32 * 32;
+    const SliceFn head = [&](int b0, int cnt, hipStream_t s) {
+      float* h1 = ctx->h1.f() + (size_t)b0 * ctx->fc1_out;
+      {
+        ProfScope ps(ctx, s, "fc1");
+        float* p1 = ctx->part.f() + (size_t)S1 * b0 * np1;
+        hip_check(launch_fc_gemm_x3p(sp.hi + (size_t)b0 * ctx->fc1_in, sp.lo ? sp.lo + (size_t)b0 * ctx->fc1_in : nullptr,
+                                     ctx->fc1_in, ctx->fc1_pk.p, ctx->fc1_unscale, p1, cnt, ctx->fc1_in, ctx->fc1_out,
+                                     S1, ks1, s, fc_np),
+                  "fc_1 gemm");
+        hip_check(launch_fc_reduce(p1, S1, cnt, ctx->fc1_out, ctx->fc1_b.f(), 1, ctx->bn4_s.f(), ctx->bn4_t.f(), h1,
+                                   ctx->fc1_out, s),
+                  "fc_1 reduce");
+      }
+      ProfScope ps(ctx, s, "fc_out");
+      float* p2 = ctx->part2.f() + (size_t)S2 * b0 * np2;
+      hip_check(launch_fc_gemm(h1, ctx->fc1_out, ctx->fco_pk.v4(), p2, cnt, ctx->fc1_out, ctx->nout, S2, ks2, s),
+                "fc_out gemm");
+      hip_check(launch_fc_reduce(p2, S2, cnt, ctx->nout, ctx->fco_b.f(), 0, nullptr, nullptr, out + (size_t)b0 * ctx->nout,
+                                 ctx->nout, s),
+                "fc_out reduce");
+    };
+    const bool head_slices = presplit && fc_slice() && !tp.fc1 && !tp.relu1;
     run_circuit(ctx, n, H, W, ctx->timesteps, h0, ctx->fcin.f(), (so.O || so.I) ? &so : nullptr, st,
-                presplit ? &sp : nullptr, bb_pipe ? &backbone : nullptr);
+                presplit ? &sp : nullptr, bb_pipe ? &backbone : nullptr, head_slices ? &head : nullptr);
+    if (head_slices) return;
     if (tp.hgru)
       hip_check(hipMemcpyAsync(tp.hgru, ctx->fcin.f(), (size_t)N * ctx->fc1_in * sizeof(float),
                                hipMemcpyDeviceToDevice, st),
@@ -941,6 +991,8 @@ int pose_fwd(mp_ctx* ctx, const float* depth, int64_t n, int64_t h, int64_t w, c
       ProfScope ps(ctx, st, "fc1");
       int ks;
       const int S = fc_choose_splits(N, ctx->fc1_in, ctx->fc1_out, &ks);
+      (void)S1;
+      (void)S2;
       hip_check(ctx->dtype == MP_DTYPE_F32
                     ? launch_fc_gemm(ctx->fcin.f(), ctx->fc1_in, ctx->fc1_pk.v4(), ctx->part.f(), N, ctx->fc1_in,
                                      ctx->fc1_out, S, ks, st)

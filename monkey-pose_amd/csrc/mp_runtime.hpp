@@ -135,7 +135,7 @@ struct mp_ctx {
   // ---- workspace ----
   int64_t cap_batch = 0;
   int64_t cap_hw = 0;
-  DevBuf bufA, bufB, X, O, I, Og, fcin, part, h1;
+  DevBuf bufA, bufB, X, O, I, Og, fcin, part, part2, h1;   // part2: fc_out's partials (per-slice heads)
   DevBuf h0;                // hidden_init zeros / identity: the NHWC initial state (allocated on use)
   DevBuf specS, specY, specP;   // MP_DTYPE_F32_FFT: input / output spectra, spatial conv result
 

@@ -140,6 +140,9 @@ BITS_CASES = [
     # same item arithmetic (64 + 16: col8p on the first slice only at 64; on both at 1)
     ("pose80", "fp32_fft", "MP_COL8P", ("0", "64", "1"), {}),
     ("pose12", "fp32_fft", "MP_COL8P", ("0", "1"), {}),
+    # the pose head per batch slice on the slice's stream, or once after the join (64 + 16 crops)
+    ("pose80", "fp32_fft", "MP_FC_SLICE", ("0", "1"), {}),
+    ("pose80", "bf16", "MP_FC_SLICE", ("0", "1"), {}),
     # col8q_kernel (software-pipelined) or col8p_kernel: one item's arithmetic either way
     ("pose80", "fp32_fft", "MP_COL8Q", ("0", "1"), {"MP_COL8P": "1"}),
     ("pose12", "fp32_fft", "MP_COL8Q", ("0", "1"), {"MP_COL8P": "1"}),
