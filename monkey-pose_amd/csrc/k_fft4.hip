@@ -922,6 +922,12 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds) {
 #ifndef COL8P_EARLY
 #define COL8P_EARLY 0
 #endif
+// COL8P_DEFER (A/B, default 0): an item's stores held in registers and issued right before the next
+// item's GEMM -- same box, B = 256: 0.178 vs 0.169 ms (profiles/r6/ab/ab_col8.jsonl)
+#ifndef COL8P_DEFER
+#define COL8P_DEFER 0
+#endif
+static_assert(!(COL8P_EARLY && COL8P_DEFER), "one store placement");
 template <bool ZNT>
 __global__ __launch_bounds__(512, 1) void col8p_kernel(cpx* __restrict__ Z, const uint4* __restrict__ Gc, int B,
                                                        int ngrp, int nitems, float unscale) {
@@ -960,6 +966,18 @@ __global__ __launch_bounds__(512, 1) void col8p_kernel(cpx* __restrict__ Z, cons
   __builtin_amdgcn_s_waitcnt(VMCNT0);
   dma(it0, 0);
   if (it0 + 1 < it1) dma(it0 + 1, 1);
+  // COL8P_DEFER: an item's stores are issued right before the NEXT item's GEMM, so that HBM has work
+  // while the matrix cores run (the previous item's values held in registers until then)
+  f32x4 held[8];
+  f32x4* hz = reinterpret_cast<f32x4*>(Z);   // base of the held item's stores: this thread's image and class
+  auto store_item = [&](const f32x4 (&v)[8], f32x4* zb) {
+#pragma unroll
+    for (int n2 = 0; n2 < 8; ++n2) {
+      f32x4* zp = zb + n2 * 32;   // z_off(b, n2, fx, k1) - z_off(b, 0, fx, k1) = 64 n2 complex = 32 n2 f32x4
+      if constexpr (ZNT) __builtin_nontemporal_store(v[n2], zp);
+      else *zp = v[n2];
+    }
+  };
   for (int it = it0; it < it1; ++it) {
     const int s = (it - it0) & 1;
     uint4* tile = slots + s * CP_SLOT;
@@ -970,7 +988,7 @@ __global__ __launch_bounds__(512, 1) void col8p_kernel(cpx* __restrict__ Z, cons
     // ahead of each item's stores; otherwise the previous item's) -- a class change's weight loads
     // only make the wait longer
     const bool nx = it + 1 < it1;
-    if (it == it0) {
+    if (it == it0 || (COL8P_DEFER && it == it0 + 1)) {   // (DEFER: item it0's stores come after this wait)
       if (nx) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     } else if (!COL8P_EARLY || it == it0 + 1) {
@@ -1000,6 +1018,7 @@ __global__ __launch_bounds__(512, 1) void col8p_kernel(cpx* __restrict__ Z, cons
       __builtin_amdgcn_s_waitcnt(VMCNT0);
     }
     lds_barrier();
+    if (COL8P_DEFER && it > it0) store_item(held, hz);
     f32x4 acc[8] = {};
 #ifndef COL8P_NOGEMM
 #pragma unroll
@@ -1020,17 +1039,20 @@ __global__ __launch_bounds__(512, 1) void col8p_kernel(cpx* __restrict__ Z, cons
     // images past B (a partial last group) store image B - 1's values over it: the same bytes, since
     // their DMA read image B - 1 too -- every item issues exactly 8 stores, as the counted waits assume
     const int b = min(grp * CG_NI + bl, B - 1);
+    f32x4* zb = reinterpret_cast<f32x4*>(Z + z_off(b, 0, fx, k1)) + a;
+    if constexpr (COL8P_DEFER) {
 #pragma unroll
-    for (int n2 = 0; n2 < 8; ++n2) {
-      f32x4* zp = reinterpret_cast<f32x4*>(Z + z_off(b, n2, fx, k1)) + a;
-      if constexpr (ZNT) __builtin_nontemporal_store(out[n2], zp);
-      else *zp = out[n2];
+      for (int n2 = 0; n2 < 8; ++n2) held[n2] = out[n2];
+      hz = zb;
+    } else {
+      store_item(out, zb);
     }
     if (!COL8P_EARLY && it + 2 < it1) {
       lds_barrier();   // every thread has read its Y values: the slot takes item it + 2
       dma(it + 2, s);
     }
   }
+  if constexpr (COL8P_DEFER) store_item(held, hz);
 }
 
 // col8q_kernel: col8p_kernel's blocks and LDS-DMA prefetch, software-pipelined so that the matrix
