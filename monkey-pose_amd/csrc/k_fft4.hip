@@ -773,6 +773,25 @@ __device__ __forceinline__ void cg_kstep(const uint4* tile, int k2, int t, int k
   }
 }
 
+// cg_kstep on S fragments already read (uh / ul: the hi / lo fragment of k-step t): the same MFMAs in
+// the same order as cg_kstep
+__device__ __forceinline__ void cg_kstep_frag(uint4 uh, uint4 ul, const uint4 (&w)[4][2], f32x4 (&acc)[8]) {
+  const uint4 m = {0x80000000u, 0x80000000u, 0x80000000u, 0x80000000u};
+  const f16x8 sh = __builtin_bit_cast(f16x8, uh ^ m), sl = __builtin_bit_cast(f16x8, ul ^ m);
+  const f16x8 sh2 = __builtin_bit_cast(f16x8, (uh >> 16) | (uh << 16));
+  const f16x8 sl2 = __builtin_bit_cast(f16x8, (ul >> 16) | (ul << 16));
+#pragma unroll
+  for (int mq = 0; mq < 4; ++mq) {
+    const f16x8 ah = __builtin_bit_cast(f16x8, w[mq][0]), al = __builtin_bit_cast(f16x8, w[mq][1]);
+    acc[mq] = mfma16x16(al, sh, acc[mq]);
+    acc[mq] = mfma16x16(ah, sl, acc[mq]);
+    acc[mq] = mfma16x16(ah, sh, acc[mq]);
+    acc[4 + mq] = mfma16x16(al, sh2, acc[4 + mq]);
+    acc[4 + mq] = mfma16x16(ah, sl2, acc[4 + mq]);
+    acc[4 + mq] = mfma16x16(ah, sh2, acc[4 + mq]);
+  }
+}
+
 // weights of k-step t for wave k2 of class cls (both planes, the wave's four row blocks)
 __device__ __forceinline__ void cg_wload(const uint4* __restrict__ Gc, int cls, int k2, int t, int kq, int jj,
                                          uint4 (&w)[4][2]) {
@@ -927,6 +946,12 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds) {
 #ifndef COL8P_DEFER
 #define COL8P_DEFER 0
 #endif
+// COL8P_SFRAG (A/B, default 0): every k-step's S fragments read before the first MFMA (same box:
+// 0.1742 vs 0.1744 ms, 8 B of scratch).  Timing-only builds: COL8P_NOWAIT (no DMA wait: 0.169 vs
+// 0.174 ms) and COL8P_NOSTORE (no stores: 0.147) -- profiles/r6/ab/ab_col8.jsonl
+#ifndef COL8P_SFRAG
+#define COL8P_SFRAG 0
+#endif
 static_assert(!(COL8P_EARLY && COL8P_DEFER), "one store placement");
 template <bool ZNT>
 __global__ __launch_bounds__(512, 1) void col8p_kernel(cpx* __restrict__ Z, const uint4* __restrict__ Gc, int B,
@@ -971,6 +996,9 @@ __global__ __launch_bounds__(512, 1) void col8p_kernel(cpx* __restrict__ Z, cons
   f32x4 held[8];
   f32x4* hz = reinterpret_cast<f32x4*>(Z);   // base of the held item's stores: this thread's image and class
   auto store_item = [&](const f32x4 (&v)[8], f32x4* zb) {
+#ifdef COL8P_NOSTORE   // timing only: no stores
+    if (v[0][0] != 12345.f) return;
+#endif
 #pragma unroll
     for (int n2 = 0; n2 < 8; ++n2) {
       f32x4* zp = zb + n2 * 32;   // z_off(b, n2, fx, k1) - z_off(b, 0, fx, k1) = 64 n2 complex = 32 n2 f32x4
@@ -988,6 +1016,7 @@ __global__ __launch_bounds__(512, 1) void col8p_kernel(cpx* __restrict__ Z, cons
     // ahead of each item's stores; otherwise the previous item's) -- a class change's weight loads
     // only make the wait longer
     const bool nx = it + 1 < it1;
+#ifndef COL8P_NOWAIT   // (timing only when defined: no wait for the DMA, reads whatever has landed)
     if (it == it0 || (COL8P_DEFER && it == it0 + 1)) {   // (DEFER: item it0's stores come after this wait)
       if (nx) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
@@ -998,6 +1027,7 @@ __global__ __launch_bounds__(512, 1) void col8p_kernel(cpx* __restrict__ Z, cons
       if (nx) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     }
+#endif
     lds_barrier();   // every wave's pieces have landed
     {
       f32x4 zin[8];
@@ -1021,8 +1051,20 @@ __global__ __launch_bounds__(512, 1) void col8p_kernel(cpx* __restrict__ Z, cons
     if (COL8P_DEFER && it > it0) store_item(held, hz);
     f32x4 acc[8] = {};
 #ifndef COL8P_NOGEMM
+    if constexpr (COL8P_SFRAG) {   // every k-step's S fragments read before the first MFMA
+      uint4 fh[4], fl[4];
 #pragma unroll
-    for (int t = 0; t < 4; ++t) cg_kstep(tile, k2, t, kq, jj, w[t], acc);
+      for (int t = 0; t < 4; ++t) {
+        fh[t] = tile[cg_s(k2, 4 * t + kq, 0, jj)];
+        fl[t] = tile[cg_s(k2, 4 * t + kq, 1, jj)];
+      }
+      __builtin_amdgcn_sched_barrier(0);   // (hipcc would sink each read to just before its k-step)
+#pragma unroll
+      for (int t = 0; t < 4; ++t) cg_kstep_frag(fh[t], fl[t], w[t], acc);
+    } else {
+#pragma unroll
+      for (int t = 0; t < 4; ++t) cg_kstep(tile, k2, t, kq, jj, w[t], acc);
+    }
 #endif
     lds_barrier();   // every wave has read the S tile
     cg_ystore(tile, k2, kq, jj, acc, unscale);
