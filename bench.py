@@ -95,7 +95,7 @@ def fft_kernels(ctx, B, hw, steps, bf16=False):
         "col_gemm": (2 * spec + NF * ent * 1024, 8.0 * B * NF * 64 * 64),    # Z in, Z' out, weights
         "row_a": (2 * spec + 3 * sm, 0.0),             # Z', X, O in; I, Z out
         "row_b": (2 * spec + 3 * sm, 0.0),             # Z', I, O in; O', Z out
-        "row_final": (spec + 3 * sm + act, 0.0),       # Z', I, O in; O', BN_3(O_T) NHWC (fp32) out
+        "row_final": (spec + 2 * sm + act, 0.0),       # Z', I, O in; BN_3(O_T) NHWC (fp32 / split planes) out
         "row_init": (act + sm + spec, 0.0),            # O0 (NHWC fp32) in; O, Z out
     }
     out = {}

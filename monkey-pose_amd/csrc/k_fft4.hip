@@ -209,7 +209,9 @@ __device__ __forceinline__ void rk_segment(const ConvArgs& p, float* seg, int b,
           Iv[n][rr] = on[0];
           Iv[n][rr + 1] = on[1];
         }
-        map_st4<BM>(p.dst, oo_index(b, 4 * n + g, y, x, 4 * h, H, W), o);
+        // ROW_FINAL with p.dst == nullptr: O_T only feeds BN_3 (no per-step states asked for), so the
+        // C8 state map is not written (wave-uniform)
+        if (MODE != ROW_FINAL || p.dst) map_st4<BM>(p.dst, oo_index(b, 4 * n + g, y, x, 4 * h, H, W), o);
         if constexpr (LEAN) __builtin_amdgcn_sched_barrier(0);
       }
     f32x16 (&Ov)[2] = Iv;

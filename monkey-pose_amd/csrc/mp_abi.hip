@@ -418,7 +418,10 @@ void fft4_circuit_range(mp_ctx* c, int b0, int n, int ntot, int H, int W, int T,
     b.rho = c->rho[t];
     b.mode = 0;
     const bool last = t == T - 1;
-    if (last) final_out(b, final_dst2, sp, b0, H, W);
+    if (last) {
+      final_out(b, final_dst2, sp, b0, H, W);
+      if (!so) b.dst = nullptr;   // O_T is read by nothing but BN_3 (row FINAL): no C8 map write
+    }
     {
       ProfScope pa(c, st, "conv15_a");
       {
