@@ -96,7 +96,9 @@ def fft_kernels(ctx, B, hw, steps, bf16=False):
         "row_a": (2 * spec + 3 * sm, 0.0),             # Z', X, O in; I, Z out
         "row_b": (2 * spec + 3 * sm, 0.0),             # Z', I, O in; O', Z out
         "row_final": (spec + 2 * sm + act, 0.0),       # Z', I, O in; BN_3(O_T) NHWC (fp32 / split planes) out
-        "row_init": (act + sm + spec, 0.0),            # O0 (NHWC fp32) in; O, Z out
+        # O0 (NHWC fp32) in; Z out, and the C8 state map O under bf16 (the fp32 loop's step 0 reads O0
+        # itself: MP_O0_DIRECT)
+        "row_init": (act + spec + (sm if bf16 or os.environ.get("MP_O0_DIRECT", "1") == "0" else 0), 0.0),
     }
     out = {}
     # the fp32 path's spectral GEMM is f16x3 (three f16 MFMA products per fp32-accurate MAC): its

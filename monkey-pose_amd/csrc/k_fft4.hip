@@ -99,7 +99,10 @@ __device__ __forceinline__ void rk_load_seg(const ConvArgs& p, const float* __re
       } else {
         L.a[n][g] = MODE == ROW_A ? map_ld4<BM>(p.X, xx_index(b, 4 * n + g, y, x, 4 * h, H, W))
                                   : map_ld4<BM>(p.I, ii_index(b, 4 * n + g, y, x, 4 * h, H, W));
-        L.o[n][g] = map_ld4<BM>(p.O, oo_index(b, 4 * n + g, y, x, 4 * h, H, W));
+        if (!BM && p.o_nhwc)   // step 0: O0 as given (NHWC fp32), not copied into the C8 map first
+          L.o[n][g] = *reinterpret_cast<const f32x4*>(p.O + (((size_t)b * H + y) * W + x) * C + 32 * n + 8 * g + 4 * h);
+        else
+          L.o[n][g] = map_ld4<BM>(p.O, oo_index(b, 4 * n + g, y, x, 4 * h, H, W));
       }
     }
 }
@@ -168,7 +171,7 @@ __device__ __forceinline__ void rk_segment(const ConvArgs& p, float* seg, int b,
           og[2 * q] = t[0];
           og[2 * q + 1] = t[1];
         }
-        map_st4<BM>(p.dst, oo_index(b, 4 * n + g, y, x, 4 * h, H, W), o);
+        if (p.dst) map_st4<BM>(p.dst, oo_index(b, 4 * n + g, y, x, 4 * h, H, W), o);   // (null: O0 read directly)
         *reinterpret_cast<f32x4*>(sp + c) = og;
         if constexpr (LEAN) __builtin_amdgcn_sched_barrier(0);
       }
@@ -614,7 +617,8 @@ __global__ __launch_bounds__(RQ_NT, 2) void rowq_a_kernel(void* __restrict__ Z, 
     const f32x4 be = *reinterpret_cast<const f32x4*>(vec + V_BETA * 64 + c);
     const f32x4 nu = *reinterpret_cast<const f32x4*>(vec + V_NU * 64 + c);
     const f32x4 xv = map_ld4<false>(p.X, xx_index(b, c >> 3, y, x, c & 4, H, W));
-    const f32x4 ov = map_ld4<false>(p.O, oo_index(b, c >> 3, y, x, c & 4, H, W));
+    const f32x4 ov = p.o_nhwc ? *reinterpret_cast<const f32x4*>(p.O + (((size_t)b * H + y) * W + x) * C + c)
+                              : map_ld4<false>(p.O, oo_index(b, c >> 3, y, x, c & 4, H, W));
     f32x4 iv;
 #pragma unroll
     for (int qq = 0; qq < 2; ++qq) {

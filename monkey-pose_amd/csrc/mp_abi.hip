@@ -374,6 +374,16 @@ void fft_circuit_range(mp_ctx* c, int b0, int n, int H, int W, int T, float* fin
   }
 }
 
+// MP_O0_DIRECT (default 1): the fp32 four-step loop's first step reads O0 (NHWC) directly; 0: row(INIT)
+// copies it into the C8 state map first (1 MB per image more)
+bool o0_direct() {
+  static const bool v = [] {
+    const char* e = std::getenv("MP_O0_DIRECT");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  return v;
+}
+
 // the hGRU loop of images [b0, b0 + n) on stream st, four-step FFT path (k_fft4.hip): one row(INIT)
 // (hgru_module.py:696-711 on O0, and the forward transform of the gated state), then per timestep
 //   col -> row A (I = tanh(X - (beta O + nu) P1), hgru_module.py:797-799) -> col -> row B (O', the
@@ -390,11 +400,13 @@ void fft4_circuit_range(mp_ctx* c, int b0, int n, int ntot, int H, int W, int T,
   float* X = map(c->X);
   float* O = map(c->O);
   float* I = map(c->I);
+  // fp32: step 0's row A / B read O0 itself (NHWC) instead of a C8 copy that row(INIT) would write
+  const bool o0d = !bf && o0_direct();
   {
     ConvArgs a0{};
     a0.H = H;
     a0.W = W;
-    a0.dst = O;
+    a0.dst = o0d ? nullptr : O;
     a0.vecs = c->vecs.f();
     ProfScope pa(c, st, "conv15_a");
     ProfScope ps(c, st, "row_init");
@@ -414,6 +426,10 @@ void fft4_circuit_range(mp_ctx* c, int b0, int n, int ntot, int H, int W, int T,
     b.I = I;
     b.O = O;
     b.dst = O;
+    if (o0d && t == 0) {
+      a.O = b.O = o0_nhwc + m;
+      a.o_nhwc = b.o_nhwc = 1;
+    }
     b.vecs = c->vecs.f();
     b.rho = c->rho[t];
     b.mode = 0;

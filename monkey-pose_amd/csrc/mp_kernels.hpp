@@ -31,6 +31,7 @@ struct ConvArgs {
   float ascale;           // f16x3 kernel: activation split scale (0 = the hGRU default 2^10)
   int dst_bf16;           // BB: dst is a bf16 C8 map (MP_DTYPE_BF16's hGRU drive X)
   int dst_c4;             // BB: dst is a C4 map (the FFT loop's drive X, k_fft.hip FFT_C4 bit 3)
+  int o_nhwc;             // four-step row A / B (fp32): O is the NHWC fp32 initial state O0 (step 0)
 };
 
 // k_conv64.hip
