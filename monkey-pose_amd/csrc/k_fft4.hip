@@ -1239,6 +1239,48 @@ __global__ __launch_bounds__(512, 1) void col8q_kernel(cpx* __restrict__ Z, cons
 // v_mfma_f32_16x16x32_bf16 product per (k-step, row block, re|im) against the class-major bf16
 // weights Gb[f][cq][co] (16 KiB per frequency), fp32 accumulation, DFTs and twiddles in fp32.
 constexpr int CB_HALF = 16 * 4 * CG_SLD;             // one frequency half of the bf16 S tile (16-B units)
+// (CG_SWZ: rows of 16 units, image column img ^ c, as cg_s)
+__device__ __forceinline__ int cb_s(int k2, int c, int img) {
+  if constexpr (CG_SWZ) return (k2 >> 2) * CB_HALF + (c * 4 + (k2 & 3)) * 16 + (img ^ c);
+  return (k2 >> 2) * CB_HALF + (c * 4 + (k2 & 3)) * CG_SLD + img;
+}
+// the bf16 item phases, shared by col8_bf_kernel and col8p_bf_kernel (bit-identical): the thread's 8
+// bf16 row-class partials (channels 2a, 2a + 1) -> twiddle, 8-point DFT -> bf16 S tile
+__device__ __forceinline__ void cb_forward(const uint2 (&zin)[8], int k1, uint4* tile, int cq, int hf, int bl) {
+  cpx s[2][8];
+#pragma unroll
+  for (int e = 0; e < 2; ++e) {
+#pragma unroll
+    for (int n2 = 0; n2 < 8; ++n2) s[e][n2] = twid<-1>(unpack_bf2(e ? zin[n2].y : zin[n2].x), n2 * k1);
+    dft8_fold<-1>(s[e]);
+  }
+  uint2* t2 = reinterpret_cast<uint2*>(tile);
+#pragma unroll
+  for (int k2 = 0; k2 < 8; ++k2)   // (columns past B unmasked, as in col8_kernel)
+    t2[cb_s(k2, cq, bl) * 2 + hf] = uint2{pack_bf2(s[0][k2].x, s[0][k2].y), pack_bf2(s[1][k2].x, s[1][k2].y)};
+}
+// one k-step: S-side forms as in cg_kstep, one bf16 product per (row block, re | im)
+__device__ __forceinline__ void cb_kstep(const uint4* tile, int k2, int t, int kq, int jj, const uint4 (&w)[4],
+                                         f32x4 (&acc)[8]) {
+  const uint4 m = {0x80000000u, 0x80000000u, 0x80000000u, 0x80000000u};
+  const uint4 us = tile[cb_s(k2, 4 * t + kq, jj)];
+  const bf16x8 sre = __builtin_bit_cast(bf16x8, us ^ m), sim = __builtin_bit_cast(bf16x8, (us >> 16) | (us << 16));
+#pragma unroll
+  for (int mq = 0; mq < 4; ++mq) {
+    const bf16x8 g = __builtin_bit_cast(bf16x8, w[mq]);
+    acc[mq] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(g, sre, acc[mq], 0, 0, 0);
+    acc[4 + mq] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(g, sim, acc[4 + mq], 0, 0, 0);
+  }
+}
+__device__ __forceinline__ void cb_wload(const uint4* __restrict__ Gb, int cls, int k2, int t, int kq, int jj,
+                                         uint4 (&w)[4]) {
+  const uint4* gw = Gb + (size_t)(cls * 8 + k2) * 16 * 64;
+#pragma unroll
+  for (int mq = 0; mq < 4; ++mq) w[mq] = gw[(4 * t + kq) * 64 + 16 * mq + jj];
+}
+typedef uint32_t u2v_t __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ u2v_t cb_pack(f32x4 v) { return u2v_t{pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])}; }
+
 template <bool ZNT>
 __global__ __launch_bounds__(512, 2) void col8_bf_kernel(void* __restrict__ Zv, const uint4* __restrict__ Gb, int B,
                                                          int ngrp) {
@@ -1254,53 +1296,24 @@ __global__ __launch_bounds__(512, 2) void col8_bf_kernel(void* __restrict__ Zv, 
   const int b = min(img0 + bl, B - 1);
   const int cq = a >> 1, hf = a & 1;
   uint32_t* Z = static_cast<uint32_t*>(Zv);
-  // (CG_SWZ: rows of 16 units, image column img ^ c, as cg_s)
-  auto sidx = [](int k2, int c, int img) {
-    if constexpr (CG_SWZ) return (k2 >> 2) * CB_HALF + (c * 4 + (k2 & 3)) * 16 + (img ^ c);
-    return (k2 >> 2) * CB_HALF + (c * 4 + (k2 & 3)) * CG_SLD + img;
-  };
   {
     uint2 zin[8];
 #pragma unroll
     for (int n2 = 0; n2 < 8; ++n2) {
-      typedef uint32_t u2v __attribute__((ext_vector_type(2)));
-      const u2v* zp = reinterpret_cast<const u2v*>(Z + z_off(b, n2, fx, k1)) + a;
-      const u2v v = ZNT ? __builtin_nontemporal_load(zp) : *zp;
+      const u2v_t* zp = reinterpret_cast<const u2v_t*>(Z + z_off(b, n2, fx, k1)) + a;
+      const u2v_t v = ZNT ? __builtin_nontemporal_load(zp) : *zp;
       zin[n2] = uint2{v.x, v.y};
     }
-    cpx s[2][8];
-#pragma unroll
-    for (int e = 0; e < 2; ++e) {
-#pragma unroll
-      for (int n2 = 0; n2 < 8; ++n2) s[e][n2] = twid<-1>(unpack_bf2(e ? zin[n2].y : zin[n2].x), n2 * k1);
-      dft8_fold<-1>(s[e]);
-    }
-    uint2* t2 = reinterpret_cast<uint2*>(tile);
-#pragma unroll
-    for (int k2 = 0; k2 < 8; ++k2)   // (columns past B unmasked, as in col8_kernel)
-      t2[sidx(k2, cq, bl) * 2 + hf] = uint2{pack_bf2(s[0][k2].x, s[0][k2].y), pack_bf2(s[1][k2].x, s[1][k2].y)};
+    cb_forward(zin, k1, tile, cq, hf, bl);
   }
   const int kq = lane >> 4, jj = lane & 15, k2 = wv;
   uint4 wr[4][4];
-  const uint4* gw = Gb + (size_t)(cls * 8 + k2) * 16 * 64;
 #pragma unroll
-  for (int t = 0; t < 4; ++t)
-#pragma unroll
-    for (int mq = 0; mq < 4; ++mq) wr[t][mq] = gw[(4 * t + kq) * 64 + 16 * mq + jj];
+  for (int t = 0; t < 4; ++t) cb_wload(Gb, cls, k2, t, kq, jj, wr[t]);
   lds_barrier();
-  const uint4 m = {0x80000000u, 0x80000000u, 0x80000000u, 0x80000000u};
   f32x4 acc[8] = {};
 #pragma unroll
-  for (int t = 0; t < 4; ++t) {   // S-side forms as in col8_kernel
-    const uint4 us = tile[sidx(k2, 4 * t + kq, jj)];
-    const bf16x8 sre = __builtin_bit_cast(bf16x8, us ^ m), sim = __builtin_bit_cast(bf16x8, (us >> 16) | (us << 16));
-#pragma unroll
-    for (int mq = 0; mq < 4; ++mq) {
-      const bf16x8 g = __builtin_bit_cast(bf16x8, wr[t][mq]);
-      acc[mq] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(g, sre, acc[mq], 0, 0, 0);
-      acc[4 + mq] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(g, sim, acc[4 + mq], 0, 0, 0);
-    }
-  }
+  for (int t = 0; t < 4; ++t) cb_kstep(tile, k2, t, kq, jj, wr[t], acc);
   lds_barrier();
   cg_ystore(tile, k2, kq, jj, acc, 1.0f);   // (x 1.0f: exact)
   lds_barrier();
@@ -1308,13 +1321,100 @@ __global__ __launch_bounds__(512, 2) void col8_bf_kernel(void* __restrict__ Zv, 
   cg_inverse(tile, k1, cq, hf, bl, yo);
   if (live) {
 #pragma unroll
-    for (int n2 = 0; n2 < 8; ++n2)
+    for (int n2 = 0; n2 < 8; ++n2) {
+      u2v_t* zp = reinterpret_cast<u2v_t*>(Z + z_off(b, n2, fx, k1)) + a;
+      if constexpr (ZNT) __builtin_nontemporal_store(cb_pack(yo[n2]), zp);
+      else *zp = cb_pack(yo[n2]);
+    }
+  }
+}
+
+// col8p_bf_kernel: col8p_kernel's persistent LDS-DMA form for the bf16 path (32 KiB of bf16 partials per
+// item, 4 DMA pieces per wave; the weights of a wave's frequency, 64 VGPRs, resident), the item math
+// of col8_bf_kernel (cb_* / cg_ystore / cg_inverse): bit-identical to it
+template <bool ZNT>
+__global__ __launch_bounds__(512, 1) void col8p_bf_kernel(void* __restrict__ Zv, const uint4* __restrict__ Gb, int B,
+                                                          int ngrp, int nitems) {
+  __shared__ uint4 slots[2 * CP_SLOT];
+  const int nblk = gridDim.x, per = nblk / 8, r8 = nblk % 8, xg = blockIdx.x % 8, q = blockIdx.x / 8;
+  const int v = (xg < r8 ? xg * (per + 1) : r8 * (per + 1) + (xg - r8) * per) + q;
+  const int it0 = (int)((int64_t)v * nitems / nblk), it1 = (int)((int64_t)(v + 1) * nitems / nblk);
+  if (it0 >= it1) return;
+  uint32_t* Z = static_cast<uint32_t*>(Zv);
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const int bl = tid >> 5, a = tid & 31, cq = a >> 1, hf = a & 1;
+  const int kq = lane >> 4, jj = lane & 15, k2 = wv;
+  const uint32_t lds0 = (uint32_t)(uintptr_t)slots;
+  // item it -> slot s: wave wv moves images 2 wv, 2 wv + 1 (2 KiB each, two 1-KiB pieces)
+  auto dma = [&](int it, int s) {
+    const int cls = it / ngrp, grp = it - cls * ngrp;
+    const int fx = cls / 9, k1 = cls - fx * 9;
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int il = 2 * wv + (i >> 1);
+      const int b = min(grp * CG_NI + il, B - 1);
+      const char* src = reinterpret_cast<const char*>(Z + z_off(b, 0, fx, k1)) + (i & 1) * 1024 + lane * 16;
+      const uint32_t dst = lds0 + (uint32_t)(s * CP_SLOT * 16 + il * 2048 + (i & 1) * 1024);
+      glds16(src, __builtin_amdgcn_readfirstlane(dst));
+    }
+  };
+  constexpr unsigned VMCNT0 = 0x0F70;   // vmcnt(0) expcnt(7) lgkmcnt(15), seen by hipcc's bookkeeping
+  uint4 w[4][4];
+  int wcls = it0 / ngrp;
+#pragma unroll
+  for (int t = 0; t < 4; ++t) cb_wload(Gb, wcls, k2, t, kq, jj, w[t]);
+  __builtin_amdgcn_s_waitcnt(VMCNT0);
+  dma(it0, 0);
+  if (it0 + 1 < it1) dma(it0 + 1, 1);
+  for (int it = it0; it < it1; ++it) {
+    const int s = (it - it0) & 1;
+    uint4* tile = slots + s * CP_SLOT;
+    const int cls = it / ngrp, grp = it - cls * ngrp;
+    const int fx = cls / 9, k1 = cls - fx * 9;
+    // this item's DMA is older than the previous item's 8 stores and the next item's 4 DMA pieces
+    const bool nx = it + 1 < it1;
+    if (it == it0) {
+      if (nx) asm volatile("s_waitcnt vmcnt(4)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    } else {
+      if (nx) asm volatile("s_waitcnt vmcnt(12)" ::: "memory");
+      else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
+    }
+    lds_barrier();   // every wave's pieces have landed
     {
-      typedef uint32_t u2v __attribute__((ext_vector_type(2)));
-      u2v* zp = reinterpret_cast<u2v*>(Z + z_off(b, n2, fx, k1)) + a;
-      const u2v v = u2v{pack_bf2(yo[n2][0], yo[n2][1]), pack_bf2(yo[n2][2], yo[n2][3])};
-      if constexpr (ZNT) __builtin_nontemporal_store(v, zp);
-      else *zp = v;
+      uint2 zin[8];
+      const uint2* raw = reinterpret_cast<const uint2*>(tile) + bl * 256 + a;   // [image][n2][64 bf16 pairs]
+#pragma unroll
+      for (int n2 = 0; n2 < 8; ++n2) zin[n2] = raw[n2 * 32];
+      lds_barrier();   // the raw partials are read: the slot becomes the S tile
+      cb_forward(zin, k1, tile, cq, hf, bl);
+    }
+    if (cls != wcls) {   // block-uniform
+      wcls = cls;
+#pragma unroll
+      for (int t = 0; t < 4; ++t) cb_wload(Gb, wcls, k2, t, kq, jj, w[t]);
+      __builtin_amdgcn_s_waitcnt(VMCNT0);
+    }
+    lds_barrier();
+    f32x4 acc[8] = {};
+#pragma unroll
+    for (int t = 0; t < 4; ++t) cb_kstep(tile, k2, t, kq, jj, w[t], acc);
+    lds_barrier();   // every wave has read the S tile
+    cg_ystore(tile, k2, kq, jj, acc, 1.0f);
+    lds_barrier();
+    f32x4 yo[8];
+    cg_inverse(tile, k1, cq, hf, bl, yo);
+    // images past B: image B - 1's bytes again; exactly 8 stores per item, as the counted waits assume
+    const int b = min(grp * CG_NI + bl, B - 1);
+#pragma unroll
+    for (int n2 = 0; n2 < 8; ++n2) {
+      u2v_t* zp = reinterpret_cast<u2v_t*>(Z + z_off(b, n2, fx, k1)) + a;
+      if constexpr (ZNT) __builtin_nontemporal_store(cb_pack(yo[n2]), zp);
+      else *zp = cb_pack(yo[n2]);
+    }
+    if (it + 2 < it1) {
+      lds_barrier();   // every thread has read its Y values: the slot takes item it + 2
+      dma(it + 2, s);
     }
   }
 }
@@ -1362,6 +1462,14 @@ static bool col8q_on() {
   }();
   return v;
 }
+// MP_COL8P_BF (default 1): the bf16 path's slices of >= MP_COL8P images run col8p_bf_kernel
+static bool col8p_bf_on() {
+  static const bool v = [] {
+    const char* e = std::getenv("MP_COL8P_BF");
+    return e ? std::atoi(e) != 0 : true;
+  }();
+  return v;
+}
 static int col8p_blocks() {
   static const int v = [] {
     const char* e = std::getenv("MP_COL8P_BLOCKS");
@@ -1394,6 +1502,16 @@ hipError_t launch_col_gemm(void* Z, const void* Gc, int B, float unscale, hipStr
     else
       hipLaunchKernelGGL((col8p_kernel<false>), dim3(nblk), dim3(512), 0, st, static_cast<cpx*>(Z),
                          static_cast<const uint4*>(Gc), B, ngrp, nitems, unscale);
+    return hipGetLastError();
+  }
+  if (bf && col8p_minb() > 0 && B >= col8p_minb() && col8p_bf_on()) {
+    const int nitems = Z_CLS * ngrp, nblk = std::min(nitems, col8p_blocks());
+    if (col8_znt(true, resident))
+      hipLaunchKernelGGL((col8p_bf_kernel<true>), dim3(nblk), dim3(512), 0, st, Z, static_cast<const uint4*>(Gc), B,
+                         ngrp, nitems);
+    else
+      hipLaunchKernelGGL((col8p_bf_kernel<false>), dim3(nblk), dim3(512), 0, st, Z, static_cast<const uint4*>(Gc), B,
+                         ngrp, nitems);
     return hipGetLastError();
   }
   if (bf) {

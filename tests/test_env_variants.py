@@ -139,6 +139,7 @@ BITS_CASES = [
     # the persistent column kernel (col8p_kernel, slices of >= MP_COL8P images) or col8_kernel: the
     # same item arithmetic (64 + 16: col8p on the first slice only at 64; on both at 1)
     ("pose80", "fp32_fft", "MP_COL8P", ("0", "64", "1"), {}),
+    ("pose80", "bf16", "MP_COL8P", ("0", "64", "1"), {}),
     ("pose12", "fp32_fft", "MP_COL8P", ("0", "1"), {}),
     # step 0 reading O0 (NHWC) directly, or row(INIT) copying it into the C8 state map first
     ("pose80", "fp32_fft", "MP_O0_DIRECT", ("0", "1"), {}),
