@@ -942,23 +942,15 @@ __device__ __forceinline__ void glds16(const void* gsrc, uint32_t lds) {
                : "memory");
 }
 
-// COL8P_EARLY (A/B, default 0): item it + 2's DMA issued before item it's stores instead of after
-// them -- same box, B = 256: 0.186 vs 0.170 ms (profiles/r6/ab/ab_col8.jsonl)
-#ifndef COL8P_EARLY
-#define COL8P_EARLY 0
-#endif
-// COL8P_DEFER (A/B, default 0): an item's stores held in registers and issued right before the next
-// item's GEMM -- same box, B = 256: 0.178 vs 0.169 ms (profiles/r6/ab/ab_col8.jsonl)
-#ifndef COL8P_DEFER
-#define COL8P_DEFER 0
-#endif
-// COL8P_SFRAG (A/B, default 0): every k-step's S fragments read before the first MFMA (same box:
-// 0.1742 vs 0.1744 ms, 8 B of scratch).  Timing-only builds: COL8P_NOWAIT (no DMA wait: 0.169 vs
-// 0.174 ms) and COL8P_NOSTORE (no stores: 0.147) -- profiles/r6/ab/ab_col8.jsonl
-#ifndef COL8P_SFRAG
-#define COL8P_SFRAG 0
-#endif
-static_assert(!(COL8P_EARLY && COL8P_DEFER), "one store placement");
+// Measured and removed (same box, B = 256; profiles/r6/ab/ab_col8.jsonl): item it + 2's DMA issued
+// before item it's stores (0.186 vs 0.170 ms); an item's stores held in registers and issued before
+// the next item's GEMM (0.178 vs 0.169) or two after each of its k-steps (0.212); every k-step's S
+// fragments read before the first MFMA (0.1742 vs 0.1744).  Timing-only builds (tools/exp_lib.sh
+// -DCOL8P_NO...): no DMA wait 0.166 vs 0.171, no stores 0.147, no GEMM 0.129, no DMA and no stores
+// (the item arithmetic alone) 0.103 of which the GEMM phase is 0.053, every item on the first class's
+// weights 0.152 (the 85 MB of weights not read).  A class change's weights requested right after the
+// previous item's GEMM instead of behind a vmcnt(0) at the class's first item: 0.1687 vs 0.1676, not
+// kept (profiles/r6/ab/ab_col8_phases.jsonl).
 template <bool ZNT>
 __global__ __launch_bounds__(512, 1) void col8p_kernel(cpx* __restrict__ Z, const uint4* __restrict__ Gc, int B,
                                                        int ngrp, int nitems, float unscale) {
@@ -975,6 +967,9 @@ __global__ __launch_bounds__(512, 1) void col8p_kernel(cpx* __restrict__ Z, cons
   const uint32_t lds0 = (uint32_t)(uintptr_t)slots;
   // item it -> slot s: wave wv moves images 2 wv, 2 wv + 1 of the group (four 1-KiB quarters each)
   auto dma = [&](int it, int s) {
+#ifdef COL8P_NODMA   // timing only (with COL8P_NOWAIT): no partials loaded
+    if (it >= 0) return;
+#endif
     const int cls = it / ngrp, grp = it - cls * ngrp;
     const int fx = cls / 9, k1 = cls - fx * 9;
 #pragma unroll
@@ -997,41 +992,21 @@ __global__ __launch_bounds__(512, 1) void col8p_kernel(cpx* __restrict__ Z, cons
   __builtin_amdgcn_s_waitcnt(VMCNT0);
   dma(it0, 0);
   if (it0 + 1 < it1) dma(it0 + 1, 1);
-  // COL8P_DEFER: an item's stores are issued right before the NEXT item's GEMM, so that HBM has work
-  // while the matrix cores run (the previous item's values held in registers until then)
-  f32x4 held[8];
-  f32x4* hz = reinterpret_cast<f32x4*>(Z);   // base of the held item's stores: this thread's image and class
-  auto store_item = [&](const f32x4 (&v)[8], f32x4* zb) {
-#ifdef COL8P_NOSTORE   // timing only: no stores
-    if (v[0][0] != 12345.f) return;
-#endif
-#pragma unroll
-    for (int n2 = 0; n2 < 8; ++n2) {
-      f32x4* zp = zb + n2 * 32;   // z_off(b, n2, fx, k1) - z_off(b, 0, fx, k1) = 64 n2 complex = 32 n2 f32x4
-      if constexpr (ZNT) __builtin_nontemporal_store(v[n2], zp);
-      else *zp = v[n2];
-    }
-  };
   for (int it = it0; it < it1; ++it) {
     const int s = (it - it0) & 1;
     uint4* tile = slots + s * CP_SLOT;
     const int cls = it / ngrp, grp = it - cls * ngrp;
     const int fx = cls / 9, k1 = cls - fx * 9;
-    // this item's DMA is older than: the next item's 8 DMA pieces and the 8 stores of each item
-    // finished since it was issued (COL8P_EARLY: the previous two items' stores, the DMA being issued
-    // ahead of each item's stores; otherwise the previous item's) -- a class change's weight loads
-    // only make the wait longer
+    // this item's DMA is older than: the previous item's 8 stores and the next item's 8 DMA pieces (a
+    // class change's weight loads only make the wait longer)
     const bool nx = it + 1 < it1;
 #ifndef COL8P_NOWAIT   // (timing only when defined: no wait for the DMA, reads whatever has landed)
-    if (it == it0 || (COL8P_DEFER && it == it0 + 1)) {   // (DEFER: item it0's stores come after this wait)
+    if (it == it0) {
       if (nx) asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    } else if (!COL8P_EARLY || it == it0 + 1) {
+    } else {
       if (nx) asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
       else asm volatile("s_waitcnt vmcnt(8)" ::: "memory");
-    } else {
-      if (nx) asm volatile("s_waitcnt vmcnt(24)" ::: "memory");
-      else asm volatile("s_waitcnt vmcnt(16)" ::: "memory");
     }
 #endif
     lds_barrier();   // every wave's pieces have landed
@@ -1054,33 +1029,16 @@ __global__ __launch_bounds__(512, 1) void col8p_kernel(cpx* __restrict__ Z, cons
       __builtin_amdgcn_s_waitcnt(VMCNT0);
     }
     lds_barrier();
-    if (COL8P_DEFER && it > it0) store_item(held, hz);
     f32x4 acc[8] = {};
 #ifndef COL8P_NOGEMM
-    if constexpr (COL8P_SFRAG) {   // every k-step's S fragments read before the first MFMA
-      uint4 fh[4], fl[4];
 #pragma unroll
-      for (int t = 0; t < 4; ++t) {
-        fh[t] = tile[cg_s(k2, 4 * t + kq, 0, jj)];
-        fl[t] = tile[cg_s(k2, 4 * t + kq, 1, jj)];
-      }
-      __builtin_amdgcn_sched_barrier(0);   // (hipcc would sink each read to just before its k-step)
-#pragma unroll
-      for (int t = 0; t < 4; ++t) cg_kstep_frag(fh[t], fl[t], w[t], acc);
-    } else {
-#pragma unroll
-      for (int t = 0; t < 4; ++t) cg_kstep(tile, k2, t, kq, jj, w[t], acc);
-    }
+    for (int t = 0; t < 4; ++t) cg_kstep(tile, k2, t, kq, jj, w[t], acc);
 #endif
     lds_barrier();   // every wave has read the S tile
     cg_ystore(tile, k2, kq, jj, acc, unscale);
     lds_barrier();
     f32x4 out[8];
     cg_yread(tile, cq, hf, bl, out);
-    if (COL8P_EARLY && it + 2 < it1) {
-      lds_barrier();   // every thread has read its Y values: the slot takes item it + 2 (before the stores)
-      dma(it + 2, s);
-    }
 #ifndef COL8P_NOINV
     cg_inverse_regs(out, k1, out);
 #endif
@@ -1088,19 +1046,21 @@ __global__ __launch_bounds__(512, 1) void col8p_kernel(cpx* __restrict__ Z, cons
     // their DMA read image B - 1 too -- every item issues exactly 8 stores, as the counted waits assume
     const int b = min(grp * CG_NI + bl, B - 1);
     f32x4* zb = reinterpret_cast<f32x4*>(Z + z_off(b, 0, fx, k1)) + a;
-    if constexpr (COL8P_DEFER) {
+#ifndef COL8P_NOSTORE   // timing only: no stores
 #pragma unroll
-      for (int n2 = 0; n2 < 8; ++n2) held[n2] = out[n2];
-      hz = zb;
-    } else {
-      store_item(out, zb);
+    for (int n2 = 0; n2 < 8; ++n2) {
+      f32x4* zp = zb + n2 * 32;   // z_off(b, n2, fx, k1) - z_off(b, 0, fx, k1) = 64 n2 complex = 32 n2 f32x4
+      if constexpr (ZNT) __builtin_nontemporal_store(out[n2], zp);
+      else *zp = out[n2];
     }
-    if (!COL8P_EARLY && it + 2 < it1) {
+#else
+    if (out[0][0] == 12345.f) zb[0] = out[0];
+#endif
+    if (it + 2 < it1) {
       lds_barrier();   // every thread has read its Y values: the slot takes item it + 2
       dma(it + 2, s);
     }
   }
-  if constexpr (COL8P_DEFER) store_item(held, hz);
 }
 
 // col8q_kernel: col8p_kernel's blocks and LDS-DMA prefetch, software-pipelined so that the matrix
