@@ -165,20 +165,27 @@ __device__ __forceinline__ cpx unpack_bf2(uint32_t u) {   // bf16 -> fp32 is exa
 // hGRU maps of the FFT path (the drive X, the states O, I, Og and the B half-step's P2): fp32 C8,
 // or -- BM, the MP_DTYPE_BF16 default -- bf16 C8 at the same element index (half the bytes; round
 // to nearest even on store, exact on load).  The final NHWC output for fc_1 stays fp32.
-template <bool BM>
+// NT (fp32 maps only): non-temporal loads / stores -- the batch-streaming kernels of a batch that
+// does not fit the Infinity Cache, so that the maps do not evict what is re-read there (the spectral
+// weights, read by every column launch)
+template <bool BM, bool NT = false>
 __device__ __forceinline__ f32x4 map_ld4(const float* base, size_t idx) {
   if constexpr (BM) {
     const uint2 u = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(base) + idx);
     const cpx a = unpack_bf2(u.x), b = unpack_bf2(u.y);
     return f32x4{a.x, a.y, b.x, b.y};
+  } else if constexpr (NT) {
+    return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(base + idx));
   } else {
     return *reinterpret_cast<const f32x4*>(base + idx);
   }
 }
-template <bool BM>
+template <bool BM, bool NT = false>
 __device__ __forceinline__ void map_st4(float* base, size_t idx, f32x4 v) {
   if constexpr (BM)
     *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(base) + idx) = uint2{pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])};
+  else if constexpr (NT)
+    __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(base + idx));
   else
     *reinterpret_cast<f32x4*>(base + idx) = v;
 }

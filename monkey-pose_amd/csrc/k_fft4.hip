@@ -63,6 +63,13 @@ __device__ __forceinline__ P* opaque_ptr(P* p) {
   return p;
 }
 
+// an fp32 x4 load, non-temporal under NT (the maps' policy: fft_dev.hpp map_ld4)
+template <bool NT>
+__device__ __forceinline__ f32x4 ld4(const float* p) {
+  if constexpr (NT) return __builtin_nontemporal_load(reinterpret_cast<const f32x4*>(p));
+  else return *reinterpret_cast<const f32x4*>(p);
+}
+
 // Packed-FP32 forms of the epilogues' elementwise math: two channels per v_pk_{add,mul,fma}_f32, the
 // transcendentals (v_exp_f32, v_rcp_f32) per channel as in fsigmoid / ftanh.  Same operations and
 // contractions per channel as the scalar expressions.
@@ -85,7 +92,7 @@ struct SegIn {
 
 // the segment at map row y, columns xs .. xs + 31 (lane (h, j): pixel xs + j); O is loaded here with
 // the other map (B modes: before the o_r gate rather than eight dependent loads after it)
-template <int MODE, bool BM = false>
+template <int MODE, bool BM = false, bool NT = false>
 __device__ __forceinline__ void rk_load_seg(const ConvArgs& p, const float* __restrict__ O0, int b, int y, int xs,
                                             int lane, SegIn& L) {
   const int H = p.H, W = p.W;
@@ -95,14 +102,14 @@ __device__ __forceinline__ void rk_load_seg(const ConvArgs& p, const float* __re
 #pragma unroll
     for (int g = 0; g < 4; ++g) {
       if constexpr (MODE == ROW_INIT) {
-        L.a[n][g] = *reinterpret_cast<const f32x4*>(O0 + (((size_t)b * H + y) * W + x) * C + 32 * n + 8 * g + 4 * h);
+        L.a[n][g] = ld4<NT>(O0 + (((size_t)b * H + y) * W + x) * C + 32 * n + 8 * g + 4 * h);
       } else {
-        L.a[n][g] = MODE == ROW_A ? map_ld4<BM>(p.X, xx_index(b, 4 * n + g, y, x, 4 * h, H, W))
-                                  : map_ld4<BM>(p.I, ii_index(b, 4 * n + g, y, x, 4 * h, H, W));
+        L.a[n][g] = MODE == ROW_A ? map_ld4<BM, NT>(p.X, xx_index(b, 4 * n + g, y, x, 4 * h, H, W))
+                                  : map_ld4<BM, NT>(p.I, ii_index(b, 4 * n + g, y, x, 4 * h, H, W));
         if (!BM && p.o_nhwc)   // step 0: O0 as given (NHWC fp32), not copied into the C8 map first
-          L.o[n][g] = *reinterpret_cast<const f32x4*>(p.O + (((size_t)b * H + y) * W + x) * C + 32 * n + 8 * g + 4 * h);
+          L.o[n][g] = ld4<NT>(p.O + (((size_t)b * H + y) * W + x) * C + 32 * n + 8 * g + 4 * h);
         else
-          L.o[n][g] = map_ld4<BM>(p.O, oo_index(b, 4 * n + g, y, x, 4 * h, H, W));
+          L.o[n][g] = map_ld4<BM, NT>(p.O, oo_index(b, 4 * n + g, y, x, 4 * h, H, W));
       }
     }
 }
@@ -110,7 +117,7 @@ __device__ __forceinline__ void rk_load_seg(const ConvArgs& p, const float* __re
 // seg: the segment's 32 staged pixels (pitch RK_SP floats); the output goes back over the input
 // LEAN: a scheduling fence after every 4-channel group, so the compiler does not hoist all eight groups'
 // address math and LDS reads at once (the register budget next to the row's 64 values)
-template <int MODE, bool LEAN = false, bool BM = false>
+template <int MODE, bool LEAN = false, bool BM = false, bool NT = false>
 __device__ __forceinline__ void rk_segment(const ConvArgs& p, float* seg, int b, int y, int xs, int lane,
                                            const SegIn& L, const void* __restrict__ or_x3, float or_us,
                                            const void* __restrict__ ir_x3, float ir_us, const float* vec) {
@@ -142,7 +149,7 @@ __device__ __forceinline__ void rk_segment(const ConvArgs& p, float* seg, int b,
           iv[2 * q] = t[0];
           iv[2 * q + 1] = t[1];
         }
-        map_st4<BM>(p.dst, ii_index(b, 4 * n + g, y, x, 4 * h, H, W), iv);
+        map_st4<BM, NT>(p.dst, ii_index(b, 4 * n + g, y, x, 4 * h, H, W), iv);
         *reinterpret_cast<f32x4*>(sp + c) = iv;
         if constexpr (LEAN) __builtin_amdgcn_sched_barrier(0);
       }
@@ -171,7 +178,7 @@ __device__ __forceinline__ void rk_segment(const ConvArgs& p, float* seg, int b,
           og[2 * q] = t[0];
           og[2 * q + 1] = t[1];
         }
-        if (p.dst) map_st4<BM>(p.dst, oo_index(b, 4 * n + g, y, x, 4 * h, H, W), o);   // (null: O0 read directly)
+        if (p.dst) map_st4<BM, NT>(p.dst, oo_index(b, 4 * n + g, y, x, 4 * h, H, W), o);   // (null: O0 read directly)
         *reinterpret_cast<f32x4*>(sp + c) = og;
         if constexpr (LEAN) __builtin_amdgcn_sched_barrier(0);
       }
@@ -214,7 +221,7 @@ __device__ __forceinline__ void rk_segment(const ConvArgs& p, float* seg, int b,
         }
         // ROW_FINAL with p.dst == nullptr: O_T only feeds BN_3 (no per-step states asked for), so the
         // C8 state map is not written (wave-uniform)
-        if (MODE != ROW_FINAL || p.dst) map_st4<BM>(p.dst, oo_index(b, 4 * n + g, y, x, 4 * h, H, W), o);
+        if (MODE != ROW_FINAL || p.dst) map_st4<BM, NT>(p.dst, oo_index(b, 4 * n + g, y, x, 4 * h, H, W), o);
         if constexpr (LEAN) __builtin_amdgcn_sched_barrier(0);
       }
     f32x16 (&Ov)[2] = Iv;
@@ -422,8 +429,8 @@ static_assert(R8_T >= RK_T && (8 * 32 * RK_SP * 4 + 2 * R8_GATE * 16) <= R8_T * 
 #endif
 // BF: MP_DTYPE_BF16 -- Z and the hGRU maps in bf16, the gates one bf16 product (gate_bf); transforms,
 // epilogue math and the NHWC output fp32
-// ZNT: Z read and written non-temporal (MP_ROW8_ZNT)
-template <int MODE, bool BF = false, bool ZNT = false>
+// ZNT: Z read and written non-temporal (MP_ROW8_ZNT); MNT: the fp32 maps (X, O, I, O0) too (MP_MAP_NT)
+template <int MODE, bool BF = false, bool ZNT = false, bool MNT = false>
 __global__ __launch_bounds__(R8_NT, 1) void row8_kernel(void* __restrict__ Z, ConvArgs p, const void* __restrict__ or_x3,
                                                         float or_us, const void* __restrict__ ir_x3, float ir_us,
                                                         const float* __restrict__ O0) {
@@ -470,7 +477,7 @@ __global__ __launch_bounds__(R8_NT, 1) void row8_kernel(void* __restrict__ Z, Co
     // row transforms instead of in front of the segment.  Same box, B = 256: row A 0.272 ms either
     // way, row B 0.297 -> 0.312 (profiles/r6/ab/ab_row.jsonl): not kept
     if constexpr (SEGPF) {
-      if (live) rk_load_seg<MODE, BF>(p, O0, b, y, 0, lane, L0);
+      if (live) rk_load_seg<MODE, BF, MNT>(p, O0, b, y, 0, lane, L0);
     }
     {
       cpx A[FX];
@@ -498,8 +505,8 @@ __global__ __launch_bounds__(R8_NT, 1) void row8_kernel(void* __restrict__ Z, Co
         const int xs = 32 * sg;
         if (xs >= W) continue;   // wave-uniform
         SegIn L;
-        rk_load_seg<MODE, BF>(p, O0, b, y, xs, lane, L);
-        rk_segment<MODE, true, BF>(p, stg + xs * RK_SP, b, y, xs, lane, L, gsh, or_us, gsh, ir_us, vsh);
+        rk_load_seg<MODE, BF, MNT>(p, O0, b, y, xs, lane, L);
+        rk_segment<MODE, true, BF, MNT>(p, stg + xs * RK_SP, b, y, xs, lane, L, gsh, or_us, gsh, ir_us, vsh);
       }
     }
     return;
@@ -511,12 +518,12 @@ __global__ __launch_bounds__(R8_NT, 1) void row8_kernel(void* __restrict__ Z, Co
       if (xs >= W) continue;   // wave-uniform
       SegIn L;
       if (SEGPF && sg == 0) L = L0;
-      else rk_load_seg<MODE, BF>(p, O0, b, y, xs, lane, L);
+      else rk_load_seg<MODE, BF, MNT>(p, O0, b, y, xs, lane, L);
       if constexpr (MODE != ROW_INIT) {
 #pragma unroll
         for (int q = 0; q < 32; ++q) stg[q * RK_SP + lane] = P[xs + q];
       }
-      rk_segment<MODE, true, BF>(p, stg, b, y, xs, lane, L, gsh, or_us, gsh + GN, ir_us, vsh);
+      rk_segment<MODE, true, BF, MNT>(p, stg, b, y, xs, lane, L, gsh, or_us, gsh + GN, ir_us, vsh);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
       for (int q = 0; q < 32; ++q) P[xs + q] = stg[q * RK_SP + lane];
@@ -566,7 +573,7 @@ constexpr int RQ_NIT = (RQ_ITEMS + RQ_NT - 1) / RQ_NT;   // 5
 __device__ __forceinline__ int rq_stg(int r, int x, int c) { return (r * 64 + x) * 16 + c + 16 * r; }
 static_assert(8 * 64 * 16 + 16 * 8 <= 2 * 8 * FX * 16, "row A staging fits T");
 
-template <bool ZNT>
+template <bool ZNT, bool MNT>
 __global__ __launch_bounds__(RQ_NT, 2) void rowq_a_kernel(void* __restrict__ Z, ConvArgs p) {
   __shared__ cpx T[8 * FX * 16];
   const int q = blockIdx.x & 3, n2 = (blockIdx.x >> 2) & 7, b = blockIdx.x >> 5;
@@ -616,9 +623,9 @@ __global__ __launch_bounds__(RQ_NT, 2) void rowq_a_kernel(void* __restrict__ Z, 
     const f32x4 lat = *reinterpret_cast<const f32x4*>(vec + V_LAT * 64 + c);
     const f32x4 be = *reinterpret_cast<const f32x4*>(vec + V_BETA * 64 + c);
     const f32x4 nu = *reinterpret_cast<const f32x4*>(vec + V_NU * 64 + c);
-    const f32x4 xv = map_ld4<false>(p.X, xx_index(b, c >> 3, y, x, c & 4, H, W));
-    const f32x4 ov = p.o_nhwc ? *reinterpret_cast<const f32x4*>(p.O + (((size_t)b * H + y) * W + x) * C + c)
-                              : map_ld4<false>(p.O, oo_index(b, c >> 3, y, x, c & 4, H, W));
+    const f32x4 xv = map_ld4<false, MNT>(p.X, xx_index(b, c >> 3, y, x, c & 4, H, W));
+    const f32x4 ov = p.o_nhwc ? ld4<MNT>(p.O + (((size_t)b * H + y) * W + x) * C + c)
+                              : map_ld4<false, MNT>(p.O, oo_index(b, c >> 3, y, x, c & 4, H, W));
     f32x4 iv;
 #pragma unroll
     for (int qq = 0; qq < 2; ++qq) {
@@ -627,7 +634,7 @@ __global__ __launch_bounds__(RQ_NT, 2) void rowq_a_kernel(void* __restrict__ Z, 
       iv[2 * qq] = tt[0];
       iv[2 * qq + 1] = tt[1];
     }
-    map_st4<false>(p.dst, ii_index(b, c >> 3, y, x, c & 4, H, W), iv);
+    map_st4<false, MNT>(p.dst, ii_index(b, c >> 3, y, x, c & 4, H, W), iv);
     *reinterpret_cast<f32x4*>(sp) = iv;
   }
   lds_barrier();
@@ -799,13 +806,24 @@ __device__ __forceinline__ void cg_kstep_frag(uint4 uh, uint4 ul, const uint4 (&
 }
 
 // weights of k-step t for wave k2 of class cls (both planes, the wave's four row blocks)
+// CG_WNT (A/B, default 0): the weight loads non-temporal
+#ifndef CG_WNT
+#define CG_WNT 0
+#endif
 __device__ __forceinline__ void cg_wload(const uint4* __restrict__ Gc, int cls, int k2, int t, int kq, int jj,
                                          uint4 (&w)[4][2]) {
   const uint4* gw = Gc + (size_t)(cls * 8 + k2) * 2 * 16 * 64;
 #pragma unroll
   for (int mq = 0; mq < 4; ++mq) {
+#if CG_WNT
+    typedef unsigned u4v __attribute__((ext_vector_type(4)));
+    const u4v* gv = reinterpret_cast<const u4v*>(gw);
+    w[mq][0] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(gv + (0 * 16 + 4 * t + kq) * 64 + 16 * mq + jj));
+    w[mq][1] = __builtin_bit_cast(uint4, __builtin_nontemporal_load(gv + (1 * 16 + 4 * t + kq) * 64 + 16 * mq + jj));
+#else
     w[mq][0] = gw[(0 * 16 + 4 * t + kq) * 64 + 16 * mq + jj];
     w[mq][1] = gw[(1 * 16 + 4 * t + kq) * 64 + 16 * mq + jj];
+#endif
   }
 }
 
@@ -1442,8 +1460,9 @@ static int col8p_blocks() {
   return v;
 }
 
-hipError_t launch_col_gemm(void* Z, const void* Gc, int B, float unscale, hipStream_t st, bool bf, bool resident) {
+hipError_t launch_col_gemm(void* Z, const void* Gc, int B, float unscale, hipStream_t st, bool bf, int ntot) {
   if (B <= 0) return hipSuccess;
+  const bool resident = ntot <= 32;
   const int ngrp = (B + CG_NI - 1) / CG_NI;
   if (!bf && col8p_minb() > 0 && B >= col8p_minb()) {
     const int nitems = Z_CLS * ngrp, nblk = std::min(nitems, col8p_blocks());
@@ -1503,6 +1522,20 @@ static bool row8_znt(bool bf, bool resident) {
   return v < 0 ? !bf && !resident : v != 0;
 }
 
+// MP_MAP_NT: row8_kernel / rowq_a_kernel's fp32 map loads and stores (X, O, I and O0) non-temporal (1) or
+// default policy (0).  Default: on for fp32 forwards of >= 128 images, whose maps are far larger than the
+// 256 MB Infinity Cache: they then stop evicting the two convolutions' spectral weights (2 x 87 MB, read
+// by every column launch) from it.  Same box, bit-identical: B = 256 7.99 -> 7.78 ms per forward (col8p
+// 0.170 -> 0.154, row A 0.272 -> 0.264, row B 0.310 -> 0.305), B = 128 4.21 -> 4.10; B = 64 (slices of
+// 32) 2.364 -> 2.398, so not there (profiles/r6/ab/ab_map_nt.jsonl)
+static bool map_nt(bool bf, int ntot) {
+  static const int v = [] {
+    const char* e = std::getenv("MP_MAP_NT");
+    return e ? (std::atoi(e) != 0 ? 1 : 0) : -1;
+  }();
+  return bf ? false : v < 0 ? ntot >= 128 : v != 0;
+}
+
 // MP_ROWQ_MAXB: batch slices up to this many images run row A as rowq_a_kernel (fp32; default 8)
 static int rowq_maxb() {
   static const int v = [] {
@@ -1513,22 +1546,33 @@ static int rowq_maxb() {
 }
 
 hipError_t launch_row(int mode, void* Z, const ConvArgs& a, const void* or_x3, float or_us, const void* ir_x3,
-                      float ir_us, const float* O0, int B, hipStream_t st, bool bf, bool resident) {
+                      float ir_us, const float* O0, int B, hipStream_t st, bool bf, int ntot) {
   if (B <= 0) return hipSuccess;
   if (a.H < 1 || a.H > 64 || (a.W != 32 && a.W != 64)) return hipErrorInvalidValue;
+  const bool resident = ntot <= 32, znt = row8_znt(bf, resident), mnt = map_nt(bf, ntot);
   if (mode == ROW_A && !bf && B <= rowq_maxb()) {
-    if (row8_znt(false, resident))
-      hipLaunchKernelGGL(rowq_a_kernel<true>, dim3(B * 32), dim3(RQ_NT), 0, st, Z, a);
-    else
-      hipLaunchKernelGGL(rowq_a_kernel<false>, dim3(B * 32), dim3(RQ_NT), 0, st, Z, a);
+#define MP_ROWQ(ZV, MV) hipLaunchKernelGGL((rowq_a_kernel<ZV, MV>), dim3(B * 32), dim3(RQ_NT), 0, st, Z, a)
+    if (znt) {
+      if (mnt) MP_ROWQ(true, true);
+      else MP_ROWQ(true, false);
+    } else {
+      if (mnt) MP_ROWQ(false, true);
+      else MP_ROWQ(false, false);
+    }
+#undef MP_ROWQ
     return hipGetLastError();
   }
   const dim3 g(B * 8), t(R8_NT);
-#define MP_ROW8(M, BFV)                                                                            \
-  if (row8_znt(BFV, resident))                                                                             \
-    hipLaunchKernelGGL((row8_kernel<M, BFV, true>), g, t, 0, st, Z, a, or_x3, or_us, ir_x3, ir_us, O0); \
-  else                                                                                             \
-    hipLaunchKernelGGL((row8_kernel<M, BFV, false>), g, t, 0, st, Z, a, or_x3, or_us, ir_x3, ir_us, O0)
+#define MP_ROW8K(M, BFV, ZV, MV) \
+  hipLaunchKernelGGL((row8_kernel<M, BFV, ZV, MV>), g, t, 0, st, Z, a, or_x3, or_us, ir_x3, ir_us, O0)
+#define MP_ROW8(M, BFV)                            \
+  if (znt) {                                       \
+    if (!BFV && mnt) MP_ROW8K(M, BFV, true, true); \
+    else MP_ROW8K(M, BFV, true, false);            \
+  } else {                                         \
+    if (!BFV && mnt) MP_ROW8K(M, BFV, false, true); \
+    else MP_ROW8K(M, BFV, false, false);           \
+  }
 #define MP_ROW8S(BFV)                               \
   switch (mode) {                                   \
     case ROW_A: MP_ROW8(ROW_A, BFV); break;         \
@@ -1544,6 +1588,7 @@ hipError_t launch_row(int mode, void* Z, const ConvArgs& a, const void* or_x3, f
   }
 #undef MP_ROW8S
 #undef MP_ROW8
+#undef MP_ROW8K
   return hipGetLastError();
 }
 

@@ -389,11 +389,10 @@ bool o0_direct() {
 //   col -> row A (I = tanh(X - (beta O + nu) P1), hgru_module.py:797-799) -> col -> row B (O', the
 //   next gated state; the last step: O' and BN_3(O_T))
 // every launch in place on one spectrum-sized buffer Z
-// ntot: the forward's whole batch (at most 32 images: Z accessed cache-resident, k_fft4.hip col8_znt)
+// ntot: the forward's whole batch (its cache policy: k_fft4.hip col8_znt, row8_znt, map_nt)
 void fft4_circuit_range(mp_ctx* c, int b0, int n, int ntot, int H, int W, int T, const float* o0_nhwc,
                         float* final_dst2, const StateOut* so, const SplitOut* sp, hipStream_t st) {
   const size_t m = (size_t)b0 * 64 * H * W;
-  const bool res = ntot <= 32;
   const bool bf = c->dtype == MP_DTYPE_BF16;   // bf16 Z (half a spectrum's bytes per image) and maps
   void* Z = static_cast<char*>(c->specS.p) + fft_spec_bytes(b0) / (bf ? 2 : 1);
   auto map = [&](DevBuf& buf) { return bf ? reinterpret_cast<float*>(reinterpret_cast<uint16_t*>(buf.p) + m) : buf.f() + m; };
@@ -410,7 +409,7 @@ void fft4_circuit_range(mp_ctx* c, int b0, int n, int ntot, int H, int W, int T,
     a0.vecs = c->vecs.f();
     ProfScope pa(c, st, "conv15_a");
     ProfScope ps(c, st, "row_init");
-    hip_check(launch_row(3, Z, a0, c->or_x3.p, c->or_us, c->ir_x3.p, c->ir_us, o0_nhwc + m, n, st, bf, res), "row_init");
+    hip_check(launch_row(3, Z, a0, c->or_x3.p, c->or_us, c->ir_x3.p, c->ir_us, o0_nhwc + m, n, st, bf, ntot), "row_init");
   }
   for (int t = 0; t < T; ++t) {
     ConvArgs a{};
@@ -442,19 +441,19 @@ void fft4_circuit_range(mp_ctx* c, int b0, int n, int ntot, int H, int W, int T,
       ProfScope pa(c, st, "conv15_a");
       {
         ProfScope ps(c, st, "col_gemm");
-        hip_check(launch_col_gemm(Z, c->spec_g.p, n, c->p_unscale, st, bf, res), "col_gemm");
+        hip_check(launch_col_gemm(Z, c->spec_g.p, n, c->p_unscale, st, bf, ntot), "col_gemm");
       }
       ProfScope ps(c, st, "row_a");
-      hip_check(launch_row(0, Z, a, c->or_x3.p, c->or_us, c->ir_x3.p, c->ir_us, nullptr, n, st, bf, res), "row_a");
+      hip_check(launch_row(0, Z, a, c->or_x3.p, c->or_us, c->ir_x3.p, c->ir_us, nullptr, n, st, bf, ntot), "row_a");
     }
     {
       ProfScope pb(c, st, "conv15_b");
       {
         ProfScope ps(c, st, "col_gemm");
-        hip_check(launch_col_gemm(Z, c->spec_g.p, n, c->p_unscale, st, bf, res), "col_gemm");
+        hip_check(launch_col_gemm(Z, c->spec_g.p, n, c->p_unscale, st, bf, ntot), "col_gemm");
       }
       ProfScope ps(c, st, last ? "row_final" : "row_b");
-      hip_check(launch_row(last ? 2 : 1, Z, b, c->or_x3.p, c->or_us, c->ir_x3.p, c->ir_us, nullptr, n, st, bf, res),
+      hip_check(launch_row(last ? 2 : 1, Z, b, c->or_x3.p, c->or_us, c->ir_x3.p, c->ir_us, nullptr, n, st, bf, ntot),
                 last ? "row_final" : "row_b");
     }
     store_step(so, O, I, b0, n, H, W, t, bf, st, fft_c4_maps(), fft_c4_state());

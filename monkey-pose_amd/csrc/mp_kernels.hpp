@@ -91,11 +91,12 @@ hipError_t launch_spec_epi_b(const ConvArgs& a, const float* P, const void* or_x
 // 2 = the last B (O' and BN_3(O') to a.dst2 / a.dst3 per a.mode), 3 = INIT (O0 NHWC -> a.dst = O).
 bool fft4_enabled();
 // bf: MP_DTYPE_BF16 (bf16 Z, maps and spectral / gate products; class-major bf16 weights)
-// resident: the forward's whole batch fits the Infinity Cache (Z accessed with the default cache policy)
+// ntot: the forward's whole batch -- its cache policy: at most 32 images fit the Infinity Cache (Z and
+// the maps accessed with the default policy); from 128 on the maps are streamed non-temporal too
 hipError_t launch_col_gemm(void* Z, const void* Gc, int B, float unscale, hipStream_t st, bool bf = false,
-                           bool resident = false);
+                           int ntot = 1 << 30);
 hipError_t launch_row(int mode, void* Z, const ConvArgs& a, const void* or_x3, float or_us, const void* ir_x3,
-                      float ir_us, const float* O0, int B, hipStream_t st, bool bf = false, bool resident = false);
+                      float ir_us, const float* O0, int B, hipStream_t st, bool bf = false, int ntot = 1 << 30);
 // k_igemm.hip (dense / hierarchical regressors)
 struct IgemmArgs {
   const float* x;      // input view: pixel (n,y,x) channel ci at x[((n*H+y)*W+x)*ldx + cix + ci]

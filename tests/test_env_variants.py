@@ -130,6 +130,12 @@ BITS_CASES = [
     ("pose80", "fp32_fft", "MP_COL8_ZNT", ("0", "1"), {}),
     ("pose80", "bf16", "MP_COL8_ZNT", ("0", "1"), {}),
     ("pose80", "fp32_fft", "MP_ROW8_ZNT", ("0", "1"), {}),
+    # col8p_kernel's partials stored non-temporal or not (MP_COL8_ZNT under MP_COL8P = 1); the row
+    # kernels' fp32 maps non-temporal or not (MP_MAP_NT, default on from 128 images), row8_kernel and
+    # row A on channel quarters
+    ("pose80", "fp32_fft", "MP_COL8_ZNT", ("0", "1"), {"MP_COL8P": "1"}),
+    ("pose80", "fp32_fft", "MP_MAP_NT", ("0", "1"), {}),
+    ("pose80", "fp32_fft", "MP_MAP_NT", ("0", "1"), {"MP_ROWQ_MAXB": "80"}),
     # the backbone per batch slice (two slices at 80 crops), staggered or not, or whole-batch first
     ("pose80", "fp32_fft", "MP_BB_PIPE", ("0", "1"), {}),
     ("pose80", "fp32_fft", "MP_BB_STAGGER", ("0", "1"), {}),
@@ -159,7 +165,7 @@ BITS_CASES = [
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("kind,dtype,var,values,base", BITS_CASES, ids=[f"{c[2]}-{c[0]}-{c[1]}" for c in BITS_CASES])
+@pytest.mark.parametrize("kind,dtype,var,values,base", BITS_CASES, ids=[f"{c[2]}-{c[0]}-{c[1]}" + "".join(f"-{k}{v}" for k, v in c[4].items()) for c in BITS_CASES])
 def test_switch_is_bit_identical(kind, dtype, var, values, base):
     """Switches whose forms compute every output with the same operations in the same order: the
     model output is the same bytes under each setting (one child process per setting)."""
