@@ -165,13 +165,15 @@ __device__ __forceinline__ cpx unpack_bf2(uint32_t u) {   // bf16 -> fp32 is exa
 // hGRU maps of the FFT path (the drive X, the states O, I, Og and the B half-step's P2): fp32 C8,
 // or -- BM, the MP_DTYPE_BF16 default -- bf16 C8 at the same element index (half the bytes; round
 // to nearest even on store, exact on load).  The final NHWC output for fc_1 stays fp32.
-// NT (fp32 maps only): non-temporal loads / stores -- the batch-streaming kernels of a batch that
+// NT: non-temporal loads / stores -- the batch-streaming kernels of a batch that
 // does not fit the Infinity Cache, so that the maps do not evict what is re-read there (the spectral
 // weights, read by every column launch)
+typedef unsigned map_u2 __attribute__((ext_vector_type(2)));
 template <bool BM, bool NT = false>
 __device__ __forceinline__ f32x4 map_ld4(const float* base, size_t idx) {
   if constexpr (BM) {
-    const uint2 u = *reinterpret_cast<const uint2*>(reinterpret_cast<const uint16_t*>(base) + idx);
+    const map_u2* p = reinterpret_cast<const map_u2*>(reinterpret_cast<const uint16_t*>(base) + idx);
+    const map_u2 u = NT ? __builtin_nontemporal_load(p) : *p;
     const cpx a = unpack_bf2(u.x), b = unpack_bf2(u.y);
     return f32x4{a.x, a.y, b.x, b.y};
   } else if constexpr (NT) {
@@ -182,9 +184,12 @@ __device__ __forceinline__ f32x4 map_ld4(const float* base, size_t idx) {
 }
 template <bool BM, bool NT = false>
 __device__ __forceinline__ void map_st4(float* base, size_t idx, f32x4 v) {
-  if constexpr (BM)
-    *reinterpret_cast<uint2*>(reinterpret_cast<uint16_t*>(base) + idx) = uint2{pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])};
-  else if constexpr (NT)
+  if constexpr (BM) {
+    map_u2* p = reinterpret_cast<map_u2*>(reinterpret_cast<uint16_t*>(base) + idx);
+    const map_u2 u = {pack_bf2(v[0], v[1]), pack_bf2(v[2], v[3])};
+    if constexpr (NT) __builtin_nontemporal_store(u, p);
+    else *p = u;
+  } else if constexpr (NT)
     __builtin_nontemporal_store(v, reinterpret_cast<f32x4*>(base + idx));
   else
     *reinterpret_cast<f32x4*>(base + idx) = v;

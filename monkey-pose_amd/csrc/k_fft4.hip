@@ -424,6 +424,9 @@ constexpr int R8_GATE = 2 * 4 * 2 * 64;                  // f16x8 of one gate's 
 constexpr int R8_T = (8 * 64 * RK_SP * 4 + R8_GATE * 16) / 8;   // 155,648 B: T grown by 512 B for FINAL
 static_assert(R8_T >= RK_T && (8 * 32 * RK_SP * 4 + 2 * R8_GATE * 16) <= R8_T * 8, "staging + gate weights fit");
 
+#ifndef R8_INIT_MNT   // (A/B) row(INIT) follows the maps' policy too
+#define R8_INIT_MNT 0
+#endif
 #ifndef R8_SEGPF
 #define R8_SEGPF 0
 #endif
@@ -450,6 +453,7 @@ __global__ __launch_bounds__(R8_NT, 1) void row8_kernel(void* __restrict__ Z, Co
   constexpr int GN = BF ? R8_GATE / 2 : R8_GATE;   // uint4 per gate (bf16: one product, no lo plane)
   float P[64];
   constexpr bool SEGPF = R8_SEGPF && (MODE == ROW_A || MODE == ROW_B);
+  constexpr bool MNTM = MNT && (R8_INIT_MNT || MODE != ROW_INIT);   // this mode's map policy
   SegIn L0;
   if constexpr (MODE != ROW_INIT) {
     {
@@ -477,7 +481,7 @@ __global__ __launch_bounds__(R8_NT, 1) void row8_kernel(void* __restrict__ Z, Co
     // row transforms instead of in front of the segment.  Same box, B = 256: row A 0.272 ms either
     // way, row B 0.297 -> 0.312 (profiles/r6/ab/ab_row.jsonl): not kept
     if constexpr (SEGPF) {
-      if (live) rk_load_seg<MODE, BF, MNT>(p, O0, b, y, 0, lane, L0);
+      if (live) rk_load_seg<MODE, BF, MNTM>(p, O0, b, y, 0, lane, L0);
     }
     {
       cpx A[FX];
@@ -505,8 +509,8 @@ __global__ __launch_bounds__(R8_NT, 1) void row8_kernel(void* __restrict__ Z, Co
         const int xs = 32 * sg;
         if (xs >= W) continue;   // wave-uniform
         SegIn L;
-        rk_load_seg<MODE, BF, MNT>(p, O0, b, y, xs, lane, L);
-        rk_segment<MODE, true, BF, MNT>(p, stg + xs * RK_SP, b, y, xs, lane, L, gsh, or_us, gsh, ir_us, vsh);
+        rk_load_seg<MODE, BF, MNTM>(p, O0, b, y, xs, lane, L);
+        rk_segment<MODE, true, BF, MNTM>(p, stg + xs * RK_SP, b, y, xs, lane, L, gsh, or_us, gsh, ir_us, vsh);
       }
     }
     return;
@@ -518,12 +522,12 @@ __global__ __launch_bounds__(R8_NT, 1) void row8_kernel(void* __restrict__ Z, Co
       if (xs >= W) continue;   // wave-uniform
       SegIn L;
       if (SEGPF && sg == 0) L = L0;
-      else rk_load_seg<MODE, BF, MNT>(p, O0, b, y, xs, lane, L);
+      else rk_load_seg<MODE, BF, MNTM>(p, O0, b, y, xs, lane, L);
       if constexpr (MODE != ROW_INIT) {
 #pragma unroll
         for (int q = 0; q < 32; ++q) stg[q * RK_SP + lane] = P[xs + q];
       }
-      rk_segment<MODE, true, BF, MNT>(p, stg, b, y, xs, lane, L, gsh, or_us, gsh + GN, ir_us, vsh);
+      rk_segment<MODE, true, BF, MNTM>(p, stg, b, y, xs, lane, L, gsh, or_us, gsh + GN, ir_us, vsh);
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
 #pragma unroll
       for (int q = 0; q < 32; ++q) P[xs + q] = stg[q * RK_SP + lane];
@@ -1522,18 +1526,26 @@ static bool row8_znt(bool bf, bool resident) {
   return v < 0 ? !bf && !resident : v != 0;
 }
 
-// MP_MAP_NT: row8_kernel / rowq_a_kernel's fp32 map loads and stores (X, O, I and O0) non-temporal (1) or
-// default policy (0).  Default: on for fp32 forwards of >= 128 images, whose maps are far larger than the
-// 256 MB Infinity Cache: they then stop evicting the two convolutions' spectral weights (2 x 87 MB, read
-// by every column launch) from it.  Same box, bit-identical: B = 256 7.99 -> 7.78 ms per forward (col8p
-// 0.170 -> 0.154, row A 0.272 -> 0.264, row B 0.310 -> 0.305), B = 128 4.21 -> 4.10; B = 64 (slices of
-// 32) 2.364 -> 2.398, so not there (profiles/r6/ab/ab_map_nt.jsonl)
+// MP_MAP_NT: row8_kernel / rowq_a_kernel's map loads and stores (X, O, I; fp32 or bf16) non-temporal (1)
+// or default policy (0).  Default: on for forwards of >= 128 images, whose maps are far larger than the
+// 256 MB Infinity Cache: they then stop evicting the two convolutions' spectral weights (fp32 2 x 87 MB,
+// bf16 2 x 44 MB, read by every column launch) from it; row(INIT) keeps the default policy
+// (R8_INIT_MNT).  Same box, bit-identical (profiles/r6/ab/ab_map_nt.jsonl): fp32 B = 256 7.92 -> 7.70 ms
+// per forward (col8p 0.166 -> 0.151, row A 0.273 -> 0.266, row B 0.307 -> 0.304), B = 128 4.10 -> 4.05;
+// bf16 B = 256 4.98 -> 4.72, B = 128 2.555 -> 2.518.  Not below 128: fp32 B = 64 (slices of 32) 2.364 ->
+// 2.398, B = 32 1.40 -> 1.43; bf16 B = 64 1.495 -> 1.505
+#ifndef MAP_NT_MINB
+#define MAP_NT_MINB 128
+#endif
+#ifndef MAP_NT_MINB_BF
+#define MAP_NT_MINB_BF 128
+#endif
 static bool map_nt(bool bf, int ntot) {
   static const int v = [] {
     const char* e = std::getenv("MP_MAP_NT");
     return e ? (std::atoi(e) != 0 ? 1 : 0) : -1;
   }();
-  return bf ? false : v < 0 ? ntot >= 128 : v != 0;
+  return v < 0 ? ntot >= (bf ? MAP_NT_MINB_BF : MAP_NT_MINB) : v != 0;
 }
 
 // MP_ROWQ_MAXB: batch slices up to this many images run row A as rowq_a_kernel (fp32; default 8)
@@ -1567,10 +1579,10 @@ hipError_t launch_row(int mode, void* Z, const ConvArgs& a, const void* or_x3, f
   hipLaunchKernelGGL((row8_kernel<M, BFV, ZV, MV>), g, t, 0, st, Z, a, or_x3, or_us, ir_x3, ir_us, O0)
 #define MP_ROW8(M, BFV)                            \
   if (znt) {                                       \
-    if (!BFV && mnt) MP_ROW8K(M, BFV, true, true); \
+    if (mnt) MP_ROW8K(M, BFV, true, true);         \
     else MP_ROW8K(M, BFV, true, false);            \
   } else {                                         \
-    if (!BFV && mnt) MP_ROW8K(M, BFV, false, true); \
+    if (mnt) MP_ROW8K(M, BFV, false, true);        \
     else MP_ROW8K(M, BFV, false, false);           \
   }
 #define MP_ROW8S(BFV)                               \

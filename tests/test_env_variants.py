@@ -135,6 +135,7 @@ BITS_CASES = [
     # row A on channel quarters
     ("pose80", "fp32_fft", "MP_COL8_ZNT", ("0", "1"), {"MP_COL8P": "1"}),
     ("pose80", "fp32_fft", "MP_MAP_NT", ("0", "1"), {}),
+    ("pose80", "bf16", "MP_MAP_NT", ("0", "1"), {}),
     ("pose80", "fp32_fft", "MP_MAP_NT", ("0", "1"), {"MP_ROWQ_MAXB": "80"}),
     # the backbone per batch slice (two slices at 80 crops), staggered or not, or whole-batch first
     ("pose80", "fp32_fft", "MP_BB_PIPE", ("0", "1"), {}),
