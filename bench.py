@@ -231,7 +231,11 @@ def fft_roofline(kern, bf16=False, batch=256, hbm_meas=None):
     traffic, src = pmc_traffic(name, bf16, batch)
     src_file = "k_fft4.hip" if name in ("col_gemm", "row_a", "row_b", "row_final", "row_init") else "k_fft.hip"
     r = {"kernel": f"{name} ({src_file})", "avg_launch_ms": k["avg_launch_ms"], "launches": k["launches"],
-         "traffic": traffic, "traffic_source": src, "algo_bytes": k["algo_bytes"]}
+         "traffic": traffic, "traffic_source": src, "algo_bytes": k["algo_bytes"],
+         # FETCH_SIZE x 2 + WRITE_SIZE count L2 misses whether the Infinity Cache or HBM serves them:
+         # from 128 images the column launches' spectral weights are Infinity Cache hits (MP_MAP_NT,
+         # DESIGN.md section 8), so this figure includes them
+         "traffic_counts": "L2 misses (Infinity Cache hits included)"}
     t_hbm = k["algo_bytes"] / (PEAK_HBM_GBPS * 1e9)
     peak = k.get("mfma_peak", round(PEAK_F16_TFLOPS / 3, 1))
     t_mfma = k.get("algo_flop", 0.0) / (peak * 1e12)
