@@ -1410,18 +1410,44 @@ bool fft4_enabled() {
   return v;
 }
 
+// MP_MAP_NT: row8_kernel / rowq_a_kernel's map loads and stores (X, O, I; fp32 or bf16) non-temporal (1)
+// or default policy (0).  Default: on for forwards of >= 128 images, whose maps are far larger than the
+// 256 MB Infinity Cache: they then stop evicting the two convolutions' spectral weights (fp32 2 x 87 MB,
+// bf16 2 x 44 MB, read by every column launch) from it; row(INIT) keeps the default policy
+// (R8_INIT_MNT).  Same box, bit-identical (profiles/r6/ab/ab_map_nt.jsonl): fp32 B = 256 7.92 -> 7.70 ms
+// per forward (col8p 0.166 -> 0.151, row A 0.273 -> 0.266, row B 0.307 -> 0.304), B = 128 4.10 -> 4.05;
+// bf16 B = 256 4.98 -> 4.72, B = 128 2.555 -> 2.518.  Not below 128: fp32 B = 64 (slices of 32) 2.364 ->
+// 2.398, B = 32 1.40 -> 1.43; bf16 B = 64 1.495 -> 1.505
+#ifndef MAP_NT_MINB
+#define MAP_NT_MINB 128
+#endif
+#ifndef MAP_NT_MINB_BF
+#define MAP_NT_MINB_BF 128
+#endif
+static bool map_nt(bool bf, int ntot) {
+  static const int v = [] {
+    const char* e = std::getenv("MP_MAP_NT");
+    return e ? (std::atoi(e) != 0 ? 1 : 0) : -1;
+  }();
+  return v < 0 ? ntot >= (bf ? MAP_NT_MINB_BF : MAP_NT_MINB) : v != 0;
+}
+
 // MP_COL8_ZNT: the column kernels' Z loads and stores non-temporal (1) or default policy (0).  Default:
 // on for fp32 (same box: 8.51 -> 8.38 ms per B = 256 forward, the same PMC bytes; profiles/r5l, r5m), off
 // for bf16 (col8_bf 0.0995 -> 0.1085 ms with it; profiles/r5m_bf16).  `resident` (the forward's whole
 // batch <= 32: its Z, maps and spectral weights fit the 256 MB Infinity Cache): default policy, so the next kernel's reads hit there (interleaved same-box
 // timing, both Z switches off: B = 1 0.962 -> 0.945 ms, B = 32 1.445 -> 1.419, B = 64 2.41 -> 2.48;
-// profiles/r5_ab/r5w)
-static bool col8_znt(bool bf, bool resident) {
+// profiles/r5_ab/r5w).  Also default policy for slices of <= 64 images when the maps are streamed
+// (MP_MAP_NT): a slice's Z (<= 87 MB) then shares the Infinity Cache with the resident spectral weights
+// (B = 128, slices of 64: 4.048 -> 3.977 ms per forward, both Z switches; at B = 192 / 256 / 64 it loses:
+// 6.04 -> 6.15, 7.87 -> 8.11, 2.368 -> 2.429; profiles/r6/ab/ab_map_nt.jsonl)
+static bool z_default_policy(bool bf, int B, int ntot) { return ntot <= 32 || (map_nt(bf, ntot) && B <= 64); }
+static bool col8_znt(bool bf, int B, int ntot) {
   static const int v = [] {
     const char* e = std::getenv("MP_COL8_ZNT");
     return e ? (std::atoi(e) != 0 ? 1 : 0) : -1;
   }();
-  return v < 0 ? !bf && !resident : v != 0;
+  return v < 0 ? !bf && !z_default_policy(bf, B, ntot) : v != 0;
 }
 
 // MP_COL8P: slices of at least this many images run col8p_kernel (fp32; 0 = never); MP_COL8P_BLOCKS:
@@ -1466,12 +1492,11 @@ static int col8p_blocks() {
 
 hipError_t launch_col_gemm(void* Z, const void* Gc, int B, float unscale, hipStream_t st, bool bf, int ntot) {
   if (B <= 0) return hipSuccess;
-  const bool resident = ntot <= 32;
   const int ngrp = (B + CG_NI - 1) / CG_NI;
   if (!bf && col8p_minb() > 0 && B >= col8p_minb()) {
     const int nitems = Z_CLS * ngrp, nblk = std::min(nitems, col8p_blocks());
     if (col8q_on()) {
-      if (col8_znt(false, resident))
+      if (col8_znt(false, B, ntot))
         hipLaunchKernelGGL((col8q_kernel<true>), dim3(nblk), dim3(512), 0, st, static_cast<cpx*>(Z),
                            static_cast<const uint4*>(Gc), B, ngrp, nitems, unscale);
       else
@@ -1479,7 +1504,7 @@ hipError_t launch_col_gemm(void* Z, const void* Gc, int B, float unscale, hipStr
                            static_cast<const uint4*>(Gc), B, ngrp, nitems, unscale);
       return hipGetLastError();
     }
-    if (col8_znt(false, resident))
+    if (col8_znt(false, B, ntot))
       hipLaunchKernelGGL((col8p_kernel<true>), dim3(nblk), dim3(512), 0, st, static_cast<cpx*>(Z),
                          static_cast<const uint4*>(Gc), B, ngrp, nitems, unscale);
     else
@@ -1489,7 +1514,7 @@ hipError_t launch_col_gemm(void* Z, const void* Gc, int B, float unscale, hipStr
   }
   if (bf && col8p_minb() > 0 && B >= col8p_minb() && col8p_bf_on()) {
     const int nitems = Z_CLS * ngrp, nblk = std::min(nitems, col8p_blocks());
-    if (col8_znt(true, resident))
+    if (col8_znt(true, B, ntot))
       hipLaunchKernelGGL((col8p_bf_kernel<true>), dim3(nblk), dim3(512), 0, st, Z, static_cast<const uint4*>(Gc), B,
                          ngrp, nitems);
     else
@@ -1501,14 +1526,14 @@ hipError_t launch_col_gemm(void* Z, const void* Gc, int B, float unscale, hipStr
 #define MP_COL8B(N)                                                                                          \
   hipLaunchKernelGGL((col8_bf_kernel<N>), dim3(CG_NC8 * 8 * ngrp), dim3(512), 0, st, Z, static_cast<const uint4*>(Gc), \
                      B, ngrp)
-    if (col8_znt(true, resident)) MP_COL8B(true);
+    if (col8_znt(true, B, ntot)) MP_COL8B(true);
     else MP_COL8B(false);
 #undef MP_COL8B
   } else {
 #define MP_COL8(N)                                                                                       \
   hipLaunchKernelGGL((col8_kernel<N>), dim3(CG_NC8 * 8 * ngrp), dim3(512), 0, st, static_cast<cpx*>(Z), \
                      static_cast<const uint4*>(Gc), B, ngrp, unscale)
-    if (col8_znt(false, resident)) MP_COL8(true);
+    if (col8_znt(false, B, ntot)) MP_COL8(true);
     else MP_COL8(false);
 #undef MP_COL8
   }
@@ -1517,35 +1542,13 @@ hipError_t launch_col_gemm(void* Z, const void* Gc, int B, float unscale, hipStr
 
 // MP_ROW8_ZNT: row8_kernel's Z loads and stores non-temporal (1) or default policy (0).  Default: on for
 // fp32 (interleaved same-box timing 8.27 -> 8.21 ms per B = 256 forward; profiles/r5o), off for bf16
-// (5.080 vs 5.079 ms); off, as in col8_znt, when the batch is cache-resident
-static bool row8_znt(bool bf, bool resident) {
+// (5.080 vs 5.079 ms); off where col8_znt is (z_default_policy)
+static bool row8_znt(bool bf, int B, int ntot) {
   static const int v = [] {
     const char* e = std::getenv("MP_ROW8_ZNT");
     return e ? (std::atoi(e) != 0 ? 1 : 0) : -1;
   }();
-  return v < 0 ? !bf && !resident : v != 0;
-}
-
-// MP_MAP_NT: row8_kernel / rowq_a_kernel's map loads and stores (X, O, I; fp32 or bf16) non-temporal (1)
-// or default policy (0).  Default: on for forwards of >= 128 images, whose maps are far larger than the
-// 256 MB Infinity Cache: they then stop evicting the two convolutions' spectral weights (fp32 2 x 87 MB,
-// bf16 2 x 44 MB, read by every column launch) from it; row(INIT) keeps the default policy
-// (R8_INIT_MNT).  Same box, bit-identical (profiles/r6/ab/ab_map_nt.jsonl): fp32 B = 256 7.92 -> 7.70 ms
-// per forward (col8p 0.166 -> 0.151, row A 0.273 -> 0.266, row B 0.307 -> 0.304), B = 128 4.10 -> 4.05;
-// bf16 B = 256 4.98 -> 4.72, B = 128 2.555 -> 2.518.  Not below 128: fp32 B = 64 (slices of 32) 2.364 ->
-// 2.398, B = 32 1.40 -> 1.43; bf16 B = 64 1.495 -> 1.505
-#ifndef MAP_NT_MINB
-#define MAP_NT_MINB 128
-#endif
-#ifndef MAP_NT_MINB_BF
-#define MAP_NT_MINB_BF 128
-#endif
-static bool map_nt(bool bf, int ntot) {
-  static const int v = [] {
-    const char* e = std::getenv("MP_MAP_NT");
-    return e ? (std::atoi(e) != 0 ? 1 : 0) : -1;
-  }();
-  return v < 0 ? ntot >= (bf ? MAP_NT_MINB_BF : MAP_NT_MINB) : v != 0;
+  return v < 0 ? !bf && !z_default_policy(bf, B, ntot) : v != 0;
 }
 
 // MP_ROWQ_MAXB: batch slices up to this many images run row A as rowq_a_kernel (fp32; default 8)
@@ -1561,7 +1564,7 @@ hipError_t launch_row(int mode, void* Z, const ConvArgs& a, const void* or_x3, f
                       float ir_us, const float* O0, int B, hipStream_t st, bool bf, int ntot) {
   if (B <= 0) return hipSuccess;
   if (a.H < 1 || a.H > 64 || (a.W != 32 && a.W != 64)) return hipErrorInvalidValue;
-  const bool resident = ntot <= 32, znt = row8_znt(bf, resident), mnt = map_nt(bf, ntot);
+  const bool znt = row8_znt(bf, B, ntot), mnt = map_nt(bf, ntot);
   if (mode == ROW_A && !bf && B <= rowq_maxb()) {
 #define MP_ROWQ(ZV, MV) hipLaunchKernelGGL((rowq_a_kernel<ZV, MV>), dim3(B * 32), dim3(RQ_NT), 0, st, Z, a)
     if (znt) {
