@@ -349,6 +349,10 @@ __device__ __forceinline__ void fft72(cpx (&v)[72]) {
 
 constexpr float GATE_VSCALE = 256.0f;   // activations entering a gate: |v| < 255 stays in f16 range
 
+#ifndef GATE_IL
+#define GATE_IL 1   // gate_x3: the two output blocks' MFMA chains interleaved (0: one after the other, A/B)
+#endif
+
 
 // Y[n2] = sum_cin G[cin][32 n2 + row] V[cin][pixel], f16x3; gpk = [n2][s][hi|lo][lane] f16x8
 __device__ __forceinline__ void gate_x3(const f16x8* __restrict__ gpk, const f32x16 (&V)[2], f32x16 (&Y)[2],
@@ -371,6 +375,29 @@ __device__ __forceinline__ void gate_x3(const f16x8* __restrict__ gpk, const f32
       bl[s][e] = lv[0];
       bl[s][e + 1] = lv[1];
     }
+#if GATE_IL
+  // the two 32-channel output blocks' chains interleaved (each accumulator keeps its own product
+  // order: bit-identical to the sequential form): one block's MFMA covers the other's fragment
+  // reads, where the sequential second chain waited out an LDS read before each of its MFMAs
+  f32x16 acc[2] = {};
+#pragma unroll
+  for (int s = 0; s < 4; ++s) {
+    f16x8 ah[2], al[2];
+#pragma unroll
+    for (int n2 = 0; n2 < 2; ++n2) {
+      ah[n2] = gpk[((n2 * 4 + s) * 2) * 64 + lane];
+      al[n2] = gpk[((n2 * 4 + s) * 2 + 1) * 64 + lane];
+    }
+#pragma unroll
+    for (int n2 = 0; n2 < 2; ++n2) acc[n2] = mfma16(al[n2], bh[s], acc[n2]);
+#pragma unroll
+    for (int n2 = 0; n2 < 2; ++n2) acc[n2] = mfma16(ah[n2], bl[s], acc[n2]);
+#pragma unroll
+    for (int n2 = 0; n2 < 2; ++n2) acc[n2] = mfma16(ah[n2], bh[s], acc[n2]);
+  }
+#pragma unroll
+  for (int n2 = 0; n2 < 2; ++n2) Y[n2] = acc[n2] * unscale;
+#else
 #pragma unroll
   for (int n2 = 0; n2 < 2; ++n2) {
     f32x16 acc = {};
@@ -383,6 +410,7 @@ __device__ __forceinline__ void gate_x3(const f16x8* __restrict__ gpk, const f32
     }
     Y[n2] = acc * unscale;
   }
+#endif
 }
 
 // bf16 variant (MP_DTYPE_BF16): one product, gpk = [n2][s][lane] bf16x8 in the same K order
